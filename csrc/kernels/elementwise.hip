@@ -1,0 +1,575 @@
+// elementwise.hip - memory-bound kernels of the veles_amd library (gfx950).
+//
+// Reference kernels replaced: ocl/fullbatch_loader.cl
+// (fill_minibatch_data_labels / fill_minibatch_target), mean_disp_normalizer.cl,
+// matrix_reduce.cl (bias gradients), join.jcl (InputJoiner), random.cl
+// (xorshift1024*, xorshift128+), plus the Znicz evaluator / GD / dropout /
+// activation element-wise work.  Every kernel vectorises its bf16 traffic to
+// 8-16 B per lane (cdna_hip_programming.md Guideline 13) and grid-strides
+// over at most 2048 blocks (Guideline 11).
+#include "hvk_common.h"
+
+using namespace hvk;
+
+namespace {
+inline int grid_for(long long n, int per_block = 256) {
+  long long g = (n + per_block - 1) / per_block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// dtype codes shared with python (veles_amd/ops/_lib.py)
+enum DT { DT_F32 = 0, DT_BF16 = 1, DT_U8 = 2, DT_I32 = 3, DT_F16 = 4 };
+
+__device__ __forceinline__ float ld_any(const void* p, long long i, int dt) {
+  switch (dt) {
+    case DT_F32: return ((const float*)p)[i];
+    case DT_BF16: return bf2f(((const uint16_t*)p)[i]);
+    case DT_U8: return (float)((const uint8_t*)p)[i];
+    case DT_I32: return (float)((const int*)p)[i];
+    default: return (float)((const _Float16*)p)[i];
+  }
+}
+__device__ __forceinline__ void st_any(void* p, long long i, int dt, float v) {
+  switch (dt) {
+    case DT_F32: ((float*)p)[i] = v; break;
+    case DT_BF16: ((uint16_t*)p)[i] = f2bf(v); break;
+    case DT_U8: ((uint8_t*)p)[i] = (uint8_t)v; break;
+    case DT_I32: ((int*)p)[i] = (int)v; break;
+    default: ((_Float16*)p)[i] = (_Float16)v; break;
+  }
+}
+
+// ---------------------------------------------------------------- loader
+// out[i][:] = (in[idx[start+i]][:] - mean) * rdisp   (i < count), else 0
+// labels_out[i] = labels[idx[start+i]] or -1; indices_out[i] = idx or -1.
+__global__ void fill_minibatch_kernel(const void* src, int src_dt,
+                                      const int* shuffled, int start, int count,
+                                      int max_mb, long long sample_size,
+                                      const float* mean, const float* rdisp,
+                                      void* dst, int dst_dt, const int* labels,
+                                      int* labels_out, int* idx_out) {
+  long long total = (long long)max_mb * sample_size;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    int i = (int)(e / sample_size);
+    long long j = e - (long long)i * sample_size;
+    float v = 0.f;
+    if (i < count) {
+      int s = shuffled[start + i];
+      v = ld_any(src, (long long)s * sample_size + j, src_dt);
+      if (mean) v -= mean[j];
+      if (rdisp) v *= rdisp[j];
+    }
+    st_any(dst, e, dst_dt, v);
+    if (j == 0) {
+      int s = i < count ? shuffled[start + i] : -1;
+      if (labels_out) labels_out[i] = (s >= 0 && labels) ? labels[s] : -1;
+      if (idx_out) idx_out[i] = s;
+    }
+  }
+}
+
+// Vectorised special case: uint8 source, bf16 destination, sample_size % 16
+// == 0.  16 bytes in, 32 bytes out per lane.
+__global__ void fill_minibatch_u8_bf16_kernel(const uint8_t* src,
+                                              const int* shuffled, int start,
+                                              int count, int max_mb,
+                                              long long sample_size,
+                                              const float* mean,
+                                              const float* rdisp, uint16_t* dst,
+                                              const int* labels, int* labels_out,
+                                              int* idx_out) {
+  long long vecs = sample_size / 16;
+  long long total = (long long)max_mb * vecs;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    int i = (int)(e / vecs);
+    long long jv = e - (long long)i * vecs;
+    long long j0 = jv * 16;
+    uint16_t o[16];
+    if (i < count) {
+      int s = shuffled[start + i];
+      uint4 raw = *(const uint4*)(src + (long long)s * sample_size + j0);
+      const uint8_t* b = (const uint8_t*)&raw;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        float v = (float)b[q];
+        if (mean) v -= mean[j0 + q];
+        if (rdisp) v *= rdisp[j0 + q];
+        o[q] = f2bf(v);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) o[q] = 0;
+    }
+    uint4* d = (uint4*)(dst + (long long)i * sample_size + j0);
+    d[0] = *(uint4*)&o[0];
+    d[1] = *(uint4*)&o[8];
+    if (jv == 0) {
+      int s = i < count ? shuffled[start + i] : -1;
+      if (labels_out) labels_out[i] = (s >= 0 && labels) ? labels[s] : -1;
+      if (idx_out) idx_out[i] = s;
+    }
+  }
+}
+
+// out[b][j] = (in[b][j] - mean[j]) * rdisp[j]
+__global__ void mean_disp_kernel(const void* in, int in_dt, const float* mean,
+                                 const float* rdisp, void* out, int out_dt,
+                                 long long total, long long sample) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    long long j = e % sample;
+    st_any(out, e, out_dt, (ld_any(in, e, in_dt) - mean[j]) * rdisp[j]);
+  }
+}
+
+// ------------------------------------------------------------- evaluator
+// One wave per row: softmax of logits, then
+//   err[i][c] = (p[c] - (c == label)) * scale       (dL/dlogits of mean CE)
+//   probs (optional f32 output), per-row loss, argmax; block reductions of
+//   n_err and loss into metrics[0..1] (atomics, f32).
+__global__ void softmax_ce_kernel(const void* logits, int in_dt, int B, int C,
+                                  const int* labels, float scale, void* err,
+                                  int err_dt, float* probs, int* max_idx,
+                                  float* metrics, int* confusion) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  long long base = (long long)row * C;
+  float mx = -INFINITY;
+  int amax = 0;
+  for (int c = lane; c < C; c += 64) {
+    float v = ld_any(logits, base + c, in_dt);
+    if (v > mx) { mx = v; amax = c; }
+  }
+  // wave argmax (first index on ties)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float om = __shfl_xor(mx, o, 64);
+    int oa = __shfl_xor(amax, o, 64);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
+  float sum = 0.f;
+  for (int c = lane; c < C; c += 64) sum += __expf(ld_any(logits, base + c, in_dt) - mx);
+  sum = wave_sum(sum);
+  float inv = 1.f / sum;
+  int lab = labels ? labels[row] : -1;
+  for (int c = lane; c < C; c += 64) {
+    float p = __expf(ld_any(logits, base + c, in_dt) - mx) * inv;
+    if (probs) probs[base + c] = p;
+    if (err) {
+      float g = lab < 0 ? 0.f : (p - (c == lab ? 1.f : 0.f)) * scale;
+      st_any(err, base + c, err_dt, g);
+    }
+  }
+  if (lane == 0) {
+    if (max_idx) max_idx[row] = amax;
+    if (lab >= 0 && metrics) {
+      float pl = __expf(ld_any(logits, base + lab, in_dt) - mx) * inv;
+      atomicAdd(&metrics[0], amax != lab ? 1.f : 0.f);
+      atomicAdd(&metrics[1], -__logf(fmaxf(pl, 1e-30f)));
+      atomicAdd(&metrics[2], 1.f);
+      if (confusion) atomicAdd(&confusion[amax * C + lab], 1);
+    }
+  }
+}
+
+// MSE evaluator: err = (y - t) * scale; metrics[0] += sum sq, per-sample
+// max/min mse optional.
+__global__ void mse_kernel(const void* y, int y_dt, const void* t, int t_dt,
+                           int B, int D, float scale, void* err, int err_dt,
+                           float* mse_out, float* metrics, int valid_rows) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  long long base = (long long)row * D;
+  float s = 0.f;
+  bool valid = row < valid_rows;
+  for (int c = lane; c < D; c += 64) {
+    float d = ld_any(y, base + c, y_dt) - ld_any(t, base + c, t_dt);
+    if (!valid) d = 0.f;
+    s += d * d;
+    if (err) st_any(err, base + c, err_dt, d * scale);
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    float mse = s / D;
+    if (mse_out) mse_out[row] = mse;
+    if (metrics && valid) {
+      atomicAdd(&metrics[0], mse);
+      atomicAdd(&metrics[1], sqrtf(mse));
+      atomicAdd(&metrics[2], 1.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------- optimizer
+// Fused SGD with momentum and L1/L2 decay over a flat parameter buffer split
+// into segments with their own hyper-parameters (Znicz GD semantics,
+// docs/OPS.md):
+//   g = grad*gscale + decay*((1-l1)*w + l1*sign(w))
+//   v = moment*v - lr*g ;  w += v ; w_lp = bf16(w)
+struct SgdSeg {
+  long long begin, end;
+  float lr, decay, l1, moment;
+};
+__global__ void sgd_kernel(float* w, const float* grad, float* mom,
+                           uint16_t* w_lp, const SgdSeg* segs, int nseg,
+                           long long total, float gscale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    // segments are few and sorted: linear probe from a binary search
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (segs[mid].begin <= i) lo = mid; else hi = mid - 1;
+    }
+    const SgdSeg sg = segs[lo];
+    float wi = w[i];
+    float g = grad[i] * gscale;
+    if (sg.decay != 0.f)
+      g += sg.decay * ((1.f - sg.l1) * wi + sg.l1 * (wi > 0.f ? 1.f : (wi < 0.f ? -1.f : 0.f)));
+    float v = -sg.lr * g;
+    if (mom) {
+      v += sg.moment * mom[i];
+      mom[i] = v;
+    }
+    wi += v;
+    w[i] = wi;
+    if (w_lp) w_lp[i] = f2bf(wi);
+  }
+}
+
+// ------------------------------------------------------------ reductions
+// out[c] (+)= sum_r in[r][c]  for in [R][C] (bias gradients / column sums).
+// Block = 256 threads covering 256*VEC columns... simple form: each thread
+// owns one column and a slab of rows; atomics once per block-column.
+__global__ void col_sum_kernel(const void* in, int dt, int R, int C, float* out,
+                               int rows_per_block, float scale) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  int r0 = blockIdx.y * rows_per_block;
+  int r1 = min(R, r0 + rows_per_block);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += ld_any(in, (long long)r * C + c, dt);
+  atomicAdd(&out[c], s * scale);
+}
+
+// out[r] = sum_c in[r][c] * scale  (one wave per row)
+__global__ void row_sum_kernel(const void* in, int dt, int R, int C, float* out,
+                               float scale) {
+  int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += ld_any(in, (long long)r * C + c, dt);
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s * scale;
+}
+
+// --------------------------------------------------------- activations
+__global__ void act_fwd_kernel(const void* x, int xdt, void* y, int ydt,
+                               long long n, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    st_any(y, i, ydt, act_fwd(ld_any(x, i, xdt), act));
+}
+// dx = dy * act_bwd(y)
+__global__ void act_bwd_kernel(const void* dy, int dydt, const void* y, int ydt,
+                               void* dx, int dxdt, long long n, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    st_any(dx, i, dxdt, ld_any(dy, i, dydt) * act_bwd(ld_any(y, i, ydt), act));
+}
+// bf16 strict-relu backward, 8 elements per lane (the AlexNet hot case)
+__global__ void relu_bwd_bf16x8_kernel(const uint16_t* dy, const uint16_t* y,
+                                       uint16_t* dx, long long n8) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    uint4 a = ((const uint4*)dy)[i], b = ((const uint4*)y)[i];
+    uint32_t* pa = (uint32_t*)&a;
+    const uint32_t* pb = (const uint32_t*)&b;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t m = 0;
+      if ((pb[q] & 0x7fff) && !(pb[q] & 0x8000)) m |= 0xffff;
+      if ((pb[q] & 0x7fff0000) && !(pb[q] & 0x80000000)) m |= 0xffff0000;
+      pa[q] &= m;
+    }
+    ((uint4*)dx)[i] = a;
+  }
+}
+
+// --------------------------------------------------------------- dropout
+// Counter-based mask (no state; the backward pass regenerates it):
+//   keep(i) = hash(seed, i) >= p * 2^32 ; y = keep ? x / (1-p) : 0
+__device__ __forceinline__ uint32_t hash32(uint32_t x, uint32_t seed) {
+  x ^= seed * 0x9E3779B9u;
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__global__ void dropout_kernel(const void* x, int xdt, void* y, int ydt,
+                               long long n, uint32_t seed, uint32_t thresh,
+                               float scale, uint8_t* mask_out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    bool keep = hash32((uint32_t)i, seed) >= thresh;
+    st_any(y, i, ydt, keep ? ld_any(x, i, xdt) * scale : 0.f);
+    if (mask_out) mask_out[i] = keep;
+  }
+}
+
+// ------------------------------------------------------------------- RNG
+// xorshift1024*: bit-exact with veles_amd.prng.xorshift1024star (and with the
+// reference ocl/random.cl:42-70): out[round*16*n + i*n + id].
+__global__ void xorshift1024_kernel(uint64_t* states, int n_states, int rounds,
+                                    uint64_t* out) {
+  int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n_states) return;
+  uint64_t s[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[i] = states[id * 16 + i];
+  long long offs = id;
+  for (int r = 0; r < rounds; ++r) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      uint64_t s0 = s[i];
+      uint64_t s1 = s[(i + 1) & 15];
+      s1 ^= s1 << 31;
+      s1 ^= s1 >> 11;
+      s0 ^= s0 >> 30;
+      s[(i + 1) & 15] = s0 ^ s1;
+      out[offs] = s[(i + 1) & 15] * 1181783497276652981ull;
+      offs += n_states;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) states[id * 16 + i] = s[i];
+}
+
+__global__ void xorshift128p_kernel(uint64_t* states, int n, uint64_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t s1 = states[2 * i], s0 = states[2 * i + 1];
+  states[2 * i] = s0;
+  s1 ^= s1 << 23;
+  uint64_t ns = s1 ^ s0 ^ (s1 >> 17) ^ (s0 >> 26);
+  states[2 * i + 1] = ns;
+  out[i] = ns + s0;
+}
+
+// uniform floats in [lo, hi) from uint64 stream
+__global__ void u64_to_uniform_kernel(const uint64_t* in, float* out,
+                                      long long n, float lo, float hi) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = lo + (hi - lo) * ((float)(in[i] >> 40) * (1.0f / 16777216.0f));
+}
+
+// ---------------------------------------------------------------- concat
+// out[b][offs_k + j] = in_k[b][j]
+struct JoinArgs {
+  const void* in[16];
+  int len[16];
+  int offs[16];
+};
+__global__ void join_kernel(JoinArgs a, int nin, int dt, void* out, int B,
+                            int out_len) {
+  long long total = (long long)B * out_len;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    int b = (int)(e / out_len);
+    int j = (int)(e - (long long)b * out_len);
+    int k = 0;
+    while (k + 1 < nin && j >= a.offs[k + 1]) ++k;
+    int jj = j - a.offs[k];
+    float v = jj < a.len[k] ? ld_any(a.in[k], (long long)b * a.len[k] + jj, dt) : 0.f;
+    st_any(out, e, dt, v);
+  }
+}
+
+// ------------------------------------------------------------------ cast
+__global__ void cast_kernel(const void* in, int idt, void* out, int odt,
+                            long long n, float scale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    st_any(out, i, odt, ld_any(in, i, idt) * scale);
+}
+__global__ void f32_to_bf16x4_kernel(const float4* in, uint2* out, long long n4) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    float4 v = in[i];
+    uint2 o;
+    o.x = f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+    o.y = f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+    out[i] = o;
+  }
+}
+}  // namespace
+
+HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
+                               int start, int count, int max_mb,
+                               long long sample_size, const float* mean,
+                               const float* rdisp, void* dst, int dst_dt,
+                               const int* labels, int* labels_out, int* idx_out,
+                               hipStream_t s) {
+  if (src_dt == DT_U8 && dst_dt == DT_BF16 && sample_size % 16 == 0 &&
+      ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+    long long total = (long long)max_mb * (sample_size / 16);
+    hipLaunchKernelGGL(fill_minibatch_u8_bf16_kernel, dim3(grid_for(total)),
+                       dim3(256), 0, s, (const uint8_t*)src, shuffled, start,
+                       count, max_mb, sample_size, mean, rdisp, (uint16_t*)dst,
+                       labels, labels_out, idx_out);
+  } else {
+    long long total = (long long)max_mb * sample_size;
+    hipLaunchKernelGGL(fill_minibatch_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       s, src, src_dt, shuffled, start, count, max_mb,
+                       sample_size, mean, rdisp, dst, dst_dt, labels, labels_out,
+                       idx_out);
+  }
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_mean_disp_normalize(const void* in, int in_dt, const float* mean,
+                                    const float* rdisp, void* out, int out_dt,
+                                    long long total, long long sample,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(mean_disp_kernel, dim3(grid_for(total)), dim3(256), 0, s,
+                     in, in_dt, mean, rdisp, out, out_dt, total, sample);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_softmax_ce(const void* logits, int in_dt, int B, int C,
+                           const int* labels, float scale, void* err, int err_dt,
+                           float* probs, int* max_idx, float* metrics,
+                           int* confusion, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_ce_kernel, dim3((B + 3) / 4), dim3(256), 0, s,
+                     logits, in_dt, B, C, labels, scale, err, err_dt, probs,
+                     max_idx, metrics, confusion);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_mse(const void* y, int y_dt, const void* t, int t_dt, int B,
+                    int D, float scale, void* err, int err_dt, float* mse_out,
+                    float* metrics, int valid_rows, hipStream_t s) {
+  hipLaunchKernelGGL(mse_kernel, dim3((B + 3) / 4), dim3(256), 0, s, y, y_dt, t,
+                     t_dt, B, D, scale, err, err_dt, mse_out, metrics,
+                     valid_rows);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
+                    const void* segs, int nseg, long long total, float gscale,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(total)), dim3(256), 0, s, w,
+                     grad, mom, (uint16_t*)w_lp, (const SgdSeg*)segs, nseg,
+                     total, gscale);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
+                        float scale, hipStream_t s) {
+  int rpb = 256;
+  // aim for >= 1024 blocks in total
+  int cb = (C + 255) / 256;
+  int rb = (R + rpb - 1) / rpb;
+  while (rb * cb < 1024 && rpb > 16) { rpb >>= 1; rb = (R + rpb - 1) / rpb; }
+  hipLaunchKernelGGL(col_sum_kernel, dim3(cb, rb), dim3(256), 0, s, in, dt, R, C,
+                     out, rpb, scale);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_row_sum(const void* in, int dt, int R, int C, float* out,
+                        float scale, hipStream_t s) {
+  hipLaunchKernelGGL(row_sum_kernel, dim3((R + 3) / 4), dim3(256), 0, s, in, dt,
+                     R, C, out, scale);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_act_fwd(const void* x, int xdt, void* y, int ydt, long long n,
+                        int act, hipStream_t s) {
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
+                     y, ydt, n, act);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_act_bwd(const void* dy, int dydt, const void* y, int ydt,
+                        void* dx, int dxdt, long long n, int act, hipStream_t s) {
+  if (act == ACT_STRICT_RELU && dydt == DT_BF16 && ydt == DT_BF16 &&
+      dxdt == DT_BF16 && n % 8 == 0 && ((uintptr_t)dy & 15) == 0 &&
+      ((uintptr_t)y & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+    hipLaunchKernelGGL(relu_bwd_bf16x8_kernel, dim3(grid_for(n / 8)), dim3(256),
+                       0, s, (const uint16_t*)dy, (const uint16_t*)y,
+                       (uint16_t*)dx, n / 8);
+  } else {
+    hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, dy,
+                       dydt, y, ydt, dx, dxdt, n, act);
+  }
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_dropout(const void* x, int xdt, void* y, int ydt, long long n,
+                        unsigned seed, float p, void* mask_out, hipStream_t s) {
+  uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
+                     y, ydt, n, seed, thresh, scale, (uint8_t*)mask_out);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_xorshift1024star(void* states, int n_states, int rounds,
+                                 void* out, hipStream_t s) {
+  int bs = 64;
+  hipLaunchKernelGGL(xorshift1024_kernel, dim3((n_states + bs - 1) / bs),
+                     dim3(bs), 0, s, (uint64_t*)states, n_states, rounds,
+                     (uint64_t*)out);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_xorshift128plus(void* states, int n, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(xorshift128p_kernel, dim3((n + 255) / 256), dim3(256), 0, s,
+                     (uint64_t*)states, n, (uint64_t*)out);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_u64_to_uniform(const void* in, float* out, long long n, float lo,
+                               float hi, hipStream_t s) {
+  hipLaunchKernelGGL(u64_to_uniform_kernel, dim3(grid_for(n)), dim3(256), 0, s,
+                     (const uint64_t*)in, out, n, lo, hi);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_join(const void* const* ins, const int* lens, int nin, int dt,
+                     void* out, int B, hipStream_t s) {
+  if (nin > 16) return -1;
+  JoinArgs a;
+  int off = 0;
+  for (int k = 0; k < nin; ++k) {
+    a.in[k] = ins[k];
+    a.len[k] = lens[k];
+    a.offs[k] = off;
+    off += lens[k];
+  }
+  long long total = (long long)B * off;
+  hipLaunchKernelGGL(join_kernel, dim3(grid_for(total)), dim3(256), 0, s, a, nin,
+                     dt, out, B, off);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_cast(const void* in, int idt, void* out, int odt, long long n,
+                     float scale, hipStream_t s) {
+  if (idt == DT_F32 && odt == DT_BF16 && scale == 1.f && n % 4 == 0 &&
+      ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 7) == 0) {
+    hipLaunchKernelGGL(f32_to_bf16x4_kernel, dim3(grid_for(n / 4)), dim3(256), 0,
+                       s, (const float4*)in, (uint2*)out, n / 4);
+  } else {
+    hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, s, in, idt,
+                       out, odt, n, scale);
+  }
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,567 @@
+// gemm.hip - MFMA (v_mfma_f32_16x16x32_bf16) GEMM and implicit-GEMM
+// convolution for gfx950.
+//
+// One main loop, pluggable operand loaders and epilogues:
+//   * C[M][N] = alpha * op(A) * op(B) (+ beta*C) (+ bias) -> act -> store
+//   * conv forward   : A = im2col(X) gathered on the fly (NHWC), B = W
+//   * conv dgrad     : A = "transposed im2col" of dY, B = W rows gathered
+//   * conv wgrad     : A = dY^T, B = im2col(X), split over pixels, f32 atomics
+// Replaces the reference's ocl/gemm.cl + matrix_multiplication*.cl family and
+// the (absent) Znicz conv/all2all/gd kernels.
+//
+// Block tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 =
+// 4x4 MFMA 16x16 tiles.  Operands are register-staged global->LDS (async
+// STAGE split: next tile's global loads are issued before this tile's MFMAs,
+// written to the other LDS buffer after them), double buffered, one barrier
+// per K-tile.  LDS images:
+//   K-major  tile [128 rows][64 k]  128-B rows, 16-B chunk c stored at
+//            c ^ (row & 7)   -> ds_read_b128 fragment reads conflict-free
+//   MN-major tile [64 k][128 cols]  256-B rows, 32-B block b stored at
+//            b ^ h(k), h(k) = (k&3) | ((k>>3)&1)<<2 -> ds_read_b64_tr_b16
+//            transposed fragment reads conflict-free
+// Grid x is remapped so that consecutive output tiles share one XCD's L2.
+#include "hvk_common.h"
+
+using namespace hvk;
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NTHR = 256;
+constexpr int TILE = 128 * 64;  // elements per operand tile buffer
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
+
+__device__ __forceinline__ uint4 pack8(const uint16_t* e) {
+  uint4 v;
+  v.x = e[0] | ((uint32_t)e[1] << 16);
+  v.y = e[2] | ((uint32_t)e[3] << 16);
+  v.z = e[4] | ((uint32_t)e[5] << 16);
+  v.w = e[6] | ((uint32_t)e[7] << 16);
+  return v;
+}
+
+// ---------------------------------------------------------------- loaders
+// K-major loader: rows = M (or N) index, 8-element chunks along K.
+struct DenseK {
+  const uint16_t* p;
+  long long gstride;  // elements between groups
+  int rows, K, ld, vec;
+  struct Ctx { const uint16_t* row; int ok; };
+  __device__ void group(int g) { p += (long long)g * gstride; }
+  __device__ Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < rows;
+    c.row = p + (long long)(c.ok ? r : 0) * ld;
+    return c;
+  }
+  __device__ uint4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
+    if (vec && k + 8 <= K) return *(const uint4*)(c.row + k);
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = (k + j < K) ? c.row[k + j] : 0;
+    return pack8(e);
+  }
+};
+
+// MN-major loader: rows = K index, 8-element chunks along M (or N).
+struct DenseMN {
+  const uint16_t* p;
+  long long gstride;
+  int cols, K, ld, vec;
+  struct Ctx { int c; };
+  __device__ void group(int g) { p += (long long)g * gstride; }
+  __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
+  __device__ uint4 load(const Ctx& cx, int k) const {
+    if (k >= K || cx.c >= cols) return zero4();
+    const uint16_t* row = p + (long long)k * ld;
+    if (vec && cx.c + 8 <= cols) return *(const uint4*)(row + cx.c);
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = (cx.c + j < cols) ? row[cx.c + j] : 0;
+    return pack8(e);
+  }
+};
+
+struct ConvGeom {
+  int N, H, W, C, Cg;       // input NHWC, C total, Cg per group
+  int OH, OW, OC, OCg;      // output
+  int KH, KW, sy, sx, pt, pl;
+  FastDiv fOW, fOHOW, fW, fHW, fCg, fOCg, fKW;
+};
+
+// conv forward A: rows = output pixels (n,oh,ow), k = (kh,kw,c)
+struct ConvFwdA {
+  const uint16_t* x;
+  ConvGeom g;
+  int M, K, vec;
+  int coff;
+  struct Ctx { int base, ih0, iw0, ok; };
+  __device__ void group(int gi) { coff = gi * g.Cg; }
+  __device__ Ctx row_ctx(int m) const {
+    Ctx c;
+    c.ok = m < M;
+    uint32_t mm = c.ok ? m : 0, n, rem, oh, ow;
+    fdivmod(mm, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    c.base = n * g.H * g.W * g.C + coff;
+    c.ih0 = oh * g.sy - g.pt;
+    c.iw0 = ow * g.sx - g.pl;
+    return c;
+  }
+  __device__ __forceinline__ uint16_t elem(const Ctx& c, int k) const {
+    if (k >= K) return 0;
+    uint32_t t, ch, kh, kw;
+    fdivmod(k, g.fCg, t, ch);
+    fdivmod(t, g.fKW, kh, kw);
+    int ih = c.ih0 + (int)kh, iw = c.iw0 + (int)kw;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return 0;
+    return x[c.base + (ih * g.W + iw) * g.C + ch];
+  }
+  __device__ uint4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
+    if (vec) {  // Cg % 8 == 0: the 8 elements are 8 channels of one tap
+      uint32_t t, ch, kh, kw;
+      fdivmod(k, g.fCg, t, ch);
+      fdivmod(t, g.fKW, kh, kw);
+      int ih = c.ih0 + (int)kh, iw = c.iw0 + (int)kw;
+      if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
+        return zero4();
+      return *(const uint4*)(x + c.base + (ih * g.W + iw) * g.C + ch);
+    }
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = elem(c, k + j);
+    return pack8(e);
+  }
+};
+
+// conv dgrad A: rows = input pixels (n,h,w), k = (kh,kw,oc) over dY
+struct ConvDgradA {
+  const uint16_t* dy;
+  ConvGeom g;
+  int M, K, vec;
+  int coff;
+  struct Ctx { int base, hp, wp, ok; };
+  __device__ void group(int gi) { coff = gi * g.OCg; }
+  __device__ Ctx row_ctx(int m) const {
+    Ctx c;
+    c.ok = m < M;
+    uint32_t mm = c.ok ? m : 0, n, rem, h, w;
+    fdivmod(mm, g.fHW, n, rem);
+    fdivmod(rem, g.fW, h, w);
+    c.base = n * g.OH * g.OW * g.OC + coff;
+    c.hp = h + g.pt;
+    c.wp = w + g.pl;
+    return c;
+  }
+  __device__ __forceinline__ int tap(const Ctx& c, int k, uint32_t& oc) const {
+    uint32_t t, kh, kw;
+    fdivmod(k, g.fOCg, t, oc);
+    fdivmod(t, g.fKW, kh, kw);
+    int ohs = c.hp - (int)kh, ows = c.wp - (int)kw;
+    if (ohs < 0 || ows < 0) return -1;
+    int oh = ohs / g.sy, ow = ows / g.sx;
+    if (oh * g.sy != ohs || ow * g.sx != ows || oh >= g.OH || ow >= g.OW)
+      return -1;
+    return c.base + (oh * g.OW + ow) * g.OC;
+  }
+  __device__ uint4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
+    if (vec) {
+      uint32_t oc;
+      int off = tap(c, k, oc);
+      if (off < 0) return zero4();
+      return *(const uint4*)(dy + off + oc);
+    }
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      e[j] = 0;
+      if (k + j < K) {
+        uint32_t oc;
+        int off = tap(c, k + j, oc);
+        if (off >= 0) e[j] = dy[off + oc];
+      }
+    }
+    return pack8(e);
+  }
+};
+
+// conv dgrad B: MN-major, rows k = (kh,kw,oc) gathered from W[oc][kh][kw][c]
+struct ConvDgradB {
+  const uint16_t* w;
+  ConvGeom g;
+  int K, vec;
+  int ocoff;
+  struct Ctx { int c; };
+  __device__ void group(int gi) { ocoff = gi * g.OCg; }
+  __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
+  __device__ uint4 load(const Ctx& cx, int k) const {
+    if (k >= K || cx.c >= g.Cg) return zero4();
+    uint32_t t, oc, kh, kw;
+    fdivmod(k, g.fOCg, t, oc);
+    fdivmod(t, g.fKW, kh, kw);
+    const uint16_t* row =
+        w + (((long long)(ocoff + oc) * g.KH + kh) * g.KW + kw) * g.Cg;
+    if (vec && cx.c + 8 <= g.Cg) return *(const uint4*)(row + cx.c);
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = (cx.c + j < g.Cg) ? row[cx.c + j] : 0;
+    return pack8(e);
+  }
+};
+
+// conv wgrad B: MN-major, rows = output pixel p, cols kk = (kh,kw,c)
+struct ConvWgradB {
+  const uint16_t* x;
+  ConvGeom g;
+  int K /* pixels */, KK, vec;
+  int coff;
+  struct Ctx { int kh, kw, ch, ok; };
+  __device__ void group(int gi) { coff = gi * g.Cg; }
+  __device__ Ctx col_ctx(int kk) const {
+    Ctx c;
+    c.ok = kk < KK;
+    uint32_t t, ch, kh, kw;
+    fdivmod(c.ok ? kk : 0, g.fCg, t, ch);
+    fdivmod(t, g.fKW, kh, kw);
+    c.kh = kh; c.kw = kw; c.ch = ch;
+    return c;
+  }
+  __device__ uint4 load(const Ctx& cx, int p) const {
+    if (!cx.ok || p >= K) return zero4();
+    uint32_t n, rem, oh, ow;
+    fdivmod(p, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    int ih0 = oh * g.sy - g.pt, iw0 = ow * g.sx - g.pl;
+    long long base = (long long)n * g.H * g.W * g.C + coff;
+    if (vec) {
+      int ih = ih0 + cx.kh, iw = iw0 + cx.kw;
+      if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
+        return zero4();
+      return *(const uint4*)(x + base + (ih * g.W + iw) * g.C + cx.ch);
+    }
+    uint16_t e[8];
+    uint32_t kk0 = 0;
+    (void)kk0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      // element j is column kk+j: recompute its tap
+      int kk = (cx.kh * g.KW + cx.kw) * g.Cg + cx.ch + j;
+      e[j] = 0;
+      if (kk < KK) {
+        uint32_t t, ch, kh, kw;
+        fdivmod(kk, g.fCg, t, ch);
+        fdivmod(t, g.fKW, kh, kw);
+        int ih = ih0 + (int)kh, iw = iw0 + (int)kw;
+        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+          e[j] = x[base + (ih * g.W + iw) * g.C + ch];
+      }
+    }
+    return pack8(e);
+  }
+};
+
+// -------------------------------------------------------------- epilogue
+struct Epi {
+  void* c;
+  int ldc, M, N;
+  int out_f32;     // 1: float output, 0: bf16
+  int atomic;      // 1: f32 atomicAdd (split-K / accumulate)
+  float alpha, beta;
+  const float* bias;
+  int bias_mode;   // 0 none, 1 per column, 2 per row
+  int act;         // forward activation after bias
+  const uint16_t* aux;  // multiply by act_bwd(aux, aux_act)
+  int ld_aux, aux_act;
+  int grow, gcol;  // per-group row / column offsets
+  float* preact;   // optional f32 copy of the pre-activation (unused = null)
+  __device__ void store(int gi, int m, int n, float v) const {
+    if (m >= M || n >= N) return;
+    int gm = m + gi * grow, gn = n + gi * gcol;
+    long long idx = (long long)gm * ldc + gn;
+    v *= alpha;
+    if (bias_mode == 1) v += bias[gn];
+    else if (bias_mode == 2) v += bias[gm];
+    if (atomic) {
+      atomicAdd((float*)c + idx, v);
+      return;
+    }
+    if (beta != 0.f) {
+      float old = out_f32 ? ((float*)c)[idx] : bf2f(((uint16_t*)c)[idx]);
+      v += beta * old;
+    }
+    if (act) v = act_fwd(v, act);
+    if (aux) v *= act_bwd(bf2f(aux[(long long)gm * ld_aux + gn]), aux_act);
+    if (out_f32) ((float*)c)[idx] = v;
+    else ((uint16_t*)c)[idx] = f2bf(v);
+  }
+};
+
+__device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+template <class LA, bool AK, class LB, bool BKM>
+__global__ void __launch_bounds__(NTHR, 2)
+gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
+            int tiles_n) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[4 * TILE];
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  // bijective XCD remap (cdna_hip_programming.md T1)
+  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = wgid / tiles_n, tn = wgid - (wgid / tiles_n) * tiles_n;
+  const int gi = blockIdx.z;
+  const int kbeg = blockIdx.y * k_split;
+  const int kend = min(K, kbeg + k_split);
+  if (kbeg >= kend) return;
+  la.group(gi);
+  lb.group(gi);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  typename LA::Ctx ca[4];
+  typename LB::Ctx cb[4];
+  if constexpr (AK) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ca[i] = la.row_ctx(m0 + (t >> 3) + 32 * i);
+  } else {
+    ca[0] = la.col_ctx(m0 + (t & 15) * 8);
+  }
+  if constexpr (BKM) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cb[i] = lb.row_ctx(n0 + (t >> 3) + 32 * i);
+  } else {
+    cb[0] = lb.col_ctx(n0 + (t & 15) * 8);
+  }
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (AK) ra[i] = la.load(ca[i], k0 + (t & 7) * 8);
+      else ra[i] = la.load(ca[0], k0 + (t >> 4) + 16 * i);
+      if constexpr (BKM) rb[i] = lb.load(cb[i], k0 + (t & 7) * 8);
+      else rb[i] = lb.load(cb[0], k0 + (t >> 4) + 16 * i);
+    }
+  };
+  auto sstore = [&](uint16_t* sA, uint16_t* sB) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (AK) {
+        int row = (t >> 3) + 32 * i, c = t & 7;
+        *(uint4*)(sA + row * 64 + ((c ^ (row & 7)) << 3)) = ra[i];
+      } else {
+        int k = (t >> 4) + 16 * i, c = t & 15;
+        *(uint4*)(sA + k * 128 + (((c >> 1) ^ hk(k)) << 4) + ((c & 1) << 3)) = ra[i];
+      }
+      if constexpr (BKM) {
+        int row = (t >> 3) + 32 * i, c = t & 7;
+        *(uint4*)(sB + row * 64 + ((c ^ (row & 7)) << 3)) = rb[i];
+      } else {
+        int k = (t >> 4) + 16 * i, c = t & 15;
+        *(uint4*)(sB + k * 128 + (((c >> 1) ^ hk(k)) << 4) + ((c & 1) << 3)) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int trq = fr >> 2, trp = fr & 3;
+
+  auto frag_k = [&](const uint16_t* s, int rowbase, int ks) -> bf16x8 {
+    int row = rowbase + fr;
+    int c = ks * 4 + fq;
+    return *(const bf16x8*)(s + row * 64 + ((c ^ (row & 7)) << 3));
+  };
+  auto frag_mn = [&](const uint16_t* s, int colbase, int ks) -> bf16x8 {
+    int k = ks * 32 + fq * 8 + trq;
+    int b = colbase >> 4;  // 32-B block of this 16-col tile
+    const uint16_t* p0 = s + k * 128 + ((b ^ hk(k)) << 4) + trp * 4;
+    const uint16_t* p1 = s + (k + 4) * 128 + ((b ^ hk(k + 4)) << 4) + trp * 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  int nk = (kend - kbeg + BK - 1) / BK;
+  gload(kbeg);
+  sstore(smem, smem + 2 * TILE);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) gload(kbeg + (kt + 1) * BK);
+    const uint16_t* sA = smem + cur * TILE;
+    const uint16_t* sB = smem + (2 + cur) * TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (AK) af[i] = frag_k(sA, wm * 64 + i * 16, ks);
+        else af[i] = frag_mn(sA, wm * 64 + i * 16, ks);
+        if constexpr (BKM) bfv[i] = frag_k(sB, wn * 64 + i * 16, ks);
+        else bfv[i] = frag_mn(sB, wn * 64 + i * 16, ks);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
+                                                              acc[i][j], 0, 0, 0);
+    }
+    if (more) sstore(smem + (cur ^ 1) * TILE, smem + (2 + (cur ^ 1)) * TILE);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int mb = m0 + wm * 64 + i * 16 + fq * 4;
+      int n = n0 + wn * 64 + j * 16 + fr;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) epi.store(gi, mb + rr, n, acc[i][j][rr]);
+    }
+}
+
+template <class LA, bool AK, class LB, bool BKM>
+hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
+                  int K, int splits, int groups, hipStream_t s) {
+  int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  if (splits < 1) splits = 1;
+  int k_split = (K + splits - 1) / splits;
+  k_split = (k_split + BK - 1) / BK * BK;
+  splits = (K + k_split - 1) / k_split;
+  dim3 grid(tiles_m * tiles_n, splits, groups);
+  hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM>), grid, dim3(NTHR), 0, s,
+                     la, lb, epi, M, N, K, k_split, tiles_n);
+  return hipGetLastError();
+}
+
+ConvGeom make_geom(int N, int H, int W, int C, int OC, int KH, int KW, int sy,
+                   int sx, int pt, int pl, int OH, int OW, int groups) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.Cg = C / groups;
+  g.OH = OH; g.OW = OW; g.OC = OC; g.OCg = OC / groups;
+  g.KH = KH; g.KW = KW; g.sy = sy; g.sx = sx; g.pt = pt; g.pl = pl;
+  g.fOW = make_fastdiv(OW); g.fOHOW = make_fastdiv(OH * OW);
+  g.fW = make_fastdiv(W); g.fHW = make_fastdiv(H * W);
+  g.fCg = make_fastdiv(g.Cg); g.fOCg = make_fastdiv(g.OCg);
+  g.fKW = make_fastdiv(KW);
+  return g;
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
+             float alpha, float beta, const float* bias, int bias_mode,
+             int act, const void* aux, int ld_aux, int aux_act) {
+  Epi e;
+  e.c = c; e.ldc = ldc; e.M = M; e.N = N; e.out_f32 = out_f32;
+  e.atomic = atomic; e.alpha = alpha; e.beta = beta; e.bias = bias;
+  e.bias_mode = bias ? bias_mode : 0; e.act = act;
+  e.aux = (const uint16_t*)aux; e.ld_aux = ld_aux; e.aux_act = aux_act;
+  e.grow = 0; e.gcol = 0; e.preact = nullptr;
+  return e;
+}
+
+}  // namespace
+
+// C[M][N] = alpha*op(A)*op(B) + beta*C (+bias, act, aux-derivative mask)
+// transA=0: A is [M][K] (lda); transA=1: A is [K][M].
+// transB=0: B is [K][N] (ldb); transB=1: B is [N][K].
+HVK_API int hvk_gemm(int transA, int transB, int M, int N, int K,
+                     const void* A, int lda, const void* B, int ldb, void* C,
+                     int ldc, int out_f32, int atomic, float alpha, float beta,
+                     const float* bias, int bias_mode, int act, const void* aux,
+                     int ld_aux, int aux_act, int splits, hipStream_t s) {
+  Epi e = make_epi(C, ldc, M, N, out_f32, atomic, alpha, beta, bias,
+                   bias_mode, act, aux, ld_aux, aux_act);
+  const uint16_t* a = (const uint16_t*)A;
+  const uint16_t* b = (const uint16_t*)B;
+  int va = al16(a) && (lda % 8 == 0), vb = al16(b) && (ldb % 8 == 0);
+  hipError_t err;
+  if (!transA && transB) {
+    DenseK la{a, 0, M, K, lda, va};
+    DenseK lb{b, 0, N, K, ldb, vb};
+    err = launch<DenseK, true, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
+  } else if (!transA && !transB) {
+    DenseK la{a, 0, M, K, lda, va};
+    DenseMN lb{b, 0, N, K, ldb, vb};
+    err = launch<DenseK, true, DenseMN, false>(la, lb, e, M, N, K, splits, 1, s);
+  } else if (transA && !transB) {
+    DenseMN la{a, 0, M, K, lda, va};
+    DenseMN lb{b, 0, N, K, ldb, vb};
+    err = launch<DenseMN, false, DenseMN, false>(la, lb, e, M, N, K, splits, 1, s);
+  } else {
+    DenseMN la{a, 0, M, K, lda, va};
+    DenseK lb{b, 0, N, K, ldb, vb};
+    err = launch<DenseMN, false, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
+  }
+  return (int)err;
+}
+
+// Y[n][oh][ow][oc] = act(sum X*W + bias); X NHWC bf16, W [OC][KH][KW][C/g]
+HVK_API int hvk_conv_fwd(const void* X, const void* Wt, const float* bias,
+                         void* Y, int N, int H, int W, int C, int OC, int KH,
+                         int KW, int sy, int sx, int pt, int pl, int OH, int OW,
+                         int groups, int act, hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
+  int M = N * OH * OW, K = KH * KW * g.Cg;
+  ConvFwdA la{(const uint16_t*)X, g, M, K,
+              (g.Cg % 8 == 0 && C % 8 == 0 && al16(X)) ? 1 : 0, 0};
+  DenseK lb{(const uint16_t*)Wt, (long long)g.OCg * K, g.OCg, K, K,
+            (K % 8 == 0 && al16(Wt)) ? 1 : 0};
+  Epi e = make_epi(Y, OC, M, g.OCg, 0, 0, 1.f, 0.f, bias, 1, act, nullptr, 0, 0);
+  e.gcol = g.OCg;
+  return (int)launch<ConvFwdA, true, DenseK, true>(la, lb, e, M, g.OCg, K, 1,
+                                                   groups, s);
+}
+
+// dX = conv_transpose(dY, W); optional multiply by act_bwd(aux) (the
+// derivative of the previous layer's activation, aux = its output).
+HVK_API int hvk_conv_dgrad(const void* dY, const void* Wt, void* dX, int N,
+                           int H, int W, int C, int OC, int KH, int KW, int sy,
+                           int sx, int pt, int pl, int OH, int OW, int groups,
+                           const void* aux, int aux_act, hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
+  int M = N * H * W, K = KH * KW * g.OCg;
+  ConvDgradA la{(const uint16_t*)dY, g, M, K,
+                (g.OCg % 8 == 0 && OC % 8 == 0 && al16(dY)) ? 1 : 0, 0};
+  ConvDgradB lb{(const uint16_t*)Wt, g, K, (g.Cg % 8 == 0 && al16(Wt)) ? 1 : 0, 0};
+  Epi e = make_epi(dX, C, M, g.Cg, 0, 0, 1.f, 0.f, nullptr, 0, 0, aux, C, aux_act);
+  e.gcol = g.Cg;
+  return (int)launch<ConvDgradA, true, ConvDgradB, false>(la, lb, e, M, g.Cg, K,
+                                                          1, groups, s);
+}
+
+// dW[oc][kh][kw][c] (+)= sum_p dY[p][oc] * im2col(X)[p][kk]  (f32, atomics)
+HVK_API int hvk_conv_wgrad(const void* X, const void* dY, float* dW, int N,
+                           int H, int W, int C, int OC, int KH, int KW, int sy,
+                           int sx, int pt, int pl, int OH, int OW, int groups,
+                           int splits, hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
+  int P = N * OH * OW, KK = KH * KW * g.Cg;
+  DenseMN la{(const uint16_t*)dY, (long long)g.OCg, g.OCg, P, OC,
+             (OC % 8 == 0 && g.OCg % 8 == 0 && al16(dY)) ? 1 : 0};
+  ConvWgradB lb{(const uint16_t*)X, g, P, KK,
+                (g.Cg % 8 == 0 && C % 8 == 0 && al16(X)) ? 1 : 0, 0};
+  Epi e = make_epi(dW, KK, g.OCg, KK, 1, 1, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0);
+  e.grow = g.OCg;
+  return (int)launch<DenseMN, false, ConvWgradB, false>(la, lb, e, g.OCg, KK, P,
+                                                        splits, groups, s);
+}

@@ -1,0 +1,88 @@
+// hvk_common.h - shared device helpers for the veles_amd HIP kernel library
+// (gfx950 / CDNA4 only: wave64, MFMA, 160 KiB LDS).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HVK_API extern "C" __attribute__((visibility("default")))
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+namespace hvk {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+// Round-to-nearest-even; hipcc lowers the cast to v_cvt_pk_bf16_f32 which
+// keeps NaNs NaN (MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Fast unsigned division by a runtime-constant divisor (n < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.s = l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t hi = __umulhi(n, f.m);
+  return (hi + n) >> f.s;
+}
+__device__ __forceinline__ void fdivmod(uint32_t n, const FastDiv& f,
+                                        uint32_t& q, uint32_t& r) {
+  q = fdiv(n, f);
+  r = n - q * f.d;
+}
+
+// Activation codes (Znicz semantics, docs/OPS.md):
+//   0 linear, 1 tanh (1.7159*tanh(0.6666x)), 2 relu (softplus: log(1+e^x)),
+//   3 strict relu max(0,x), 4 sigmoid, 5 log (asinh-like, see OPS.md)
+enum Act { ACT_LINEAR = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_STRICT_RELU = 3,
+           ACT_SIGMOID = 4 };
+
+__device__ __forceinline__ float act_fwd(float x, int act) {
+  switch (act) {
+    case ACT_TANH: return 1.7159f * tanhf(0.6666f * x);
+    case ACT_RELU: return x > 15.f ? x : log1pf(__expf(x));
+    case ACT_STRICT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    default: return x;
+  }
+}
+// derivative expressed through the activation OUTPUT y
+__device__ __forceinline__ float act_bwd(float y, int act) {
+  switch (act) {
+    case ACT_TANH: return 0.6666f * 1.7159f - (0.6666f / 1.7159f) * y * y;
+    case ACT_RELU: return 1.f - __expf(-y);
+    case ACT_STRICT_RELU: return y > 0.f ? 1.f : 0.f;
+    case ACT_SIGMOID: return y * (1.f - y);
+    default: return 1.f;
+  }
+}
+
+}  // namespace hvk

@@ -1,0 +1,242 @@
+"""HIP kernel numerics: every kernel vs the float32 PyTorch reference of the
+same op (the CPU path of veles_amd.ops), plus the NaN-tail overflow guard of
+the reference test-suite (veles/tests/doubling_reset.py:41-64)."""
+import pytest
+import torch
+
+import veles_amd.ops as ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rnd(*shape, scale=1.0, dtype=BF, seed=0):
+    g = torch.Generator().manual_seed(seed + sum(shape))
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+def close(gpu, ref, tol):
+    gpu = gpu.float().cpu()
+    ref = ref.float().cpu()
+    err = (gpu - ref).abs().max().item()
+    mag = ref.abs().max().item() + 1e-6
+    assert err <= tol * mag, "max err %g vs scale %g (tol %g)" % (err, mag, tol)
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(17, 1999, 231), (7, 9, 8), (9, 7, 800),
+                                   (1, 1, 1), (256, 384, 512),
+                                   (1000, 100, 784)])
+def test_gemm_layouts(ta, tb, M, N, K):
+    a = rnd(K, M) if ta else rnd(M, K)
+    b = rnd(N, K, seed=1) if tb else rnd(K, N, seed=1)
+    ref = ops.gemm(a, b, trans_a=bool(ta), trans_b=bool(tb),
+                   out_dtype=torch.float32)
+    got = ops.gemm(a.to(DEV), b.to(DEV), trans_a=bool(ta), trans_b=bool(tb),
+                   out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    close(got, ref, 2e-3)
+
+
+def test_gemm_asymmetric_identity():
+    # A = I with an asymmetric B catches a transposed C-write
+    n = 128
+    a = torch.eye(n).to(BF)
+    b = (torch.arange(n * n).view(n, n) % 97).float().to(BF)
+    got = ops.gemm(a.to(DEV), b.to(DEV), trans_b=False, out_dtype=torch.float32)
+    assert torch.equal(got.cpu(), b.float())
+
+
+def test_gemm_epilogue_bias_act_aux():
+    M, N, K = 300, 260, 192
+    a, w = rnd(M, K), rnd(N, K, seed=2)
+    bias = torch.randn(N)
+    aux = rnd(M, N, seed=3)
+    for act in (0, 1, 2, 3, 4):
+        ref = ops.gemm(a, w, trans_b=True, bias=bias, act=act, aux=aux,
+                       aux_act=3, out_dtype=torch.float32)
+        got = ops.gemm(a.to(DEV), w.to(DEV), trans_b=True,
+                       bias=bias.to(DEV), act=act, aux=aux.to(DEV),
+                       aux_act=3, out_dtype=torch.float32)
+        close(got, ref, 5e-3)
+
+
+def test_gemm_splitk_accumulate():
+    M, N, K = 96, 200, 4096
+    a, b = rnd(K, M), rnd(K, N, seed=4)
+    ref = ops.gemm(a, b, trans_a=True, accumulate=True)
+    out = torch.zeros(M, N, device=DEV)
+    ops.gemm(a.to(DEV), b.to(DEV), trans_a=True, out=out, accumulate=True,
+             splits=8)
+    close(out, ref, 2e-3)
+
+
+def test_gemm_nan_tail_guard():
+    M, N, K = 33, 65, 64
+    a, b = rnd(M, K), rnd(N, K, seed=5)
+    big = torch.full((2 * M, N), float("nan"), device=DEV)
+    ops.gemm(a.to(DEV), b.to(DEV), trans_b=True, out=big[:M],
+             out_dtype=torch.float32)
+    assert torch.isnan(big[M:]).all()
+    assert not torch.isnan(big[:M]).any()
+
+
+CONVS = [
+    # N, H, W, C, OC, KH, KW, sliding(x,y), padding(l,t,r,b), groups
+    (2, 13, 13, 16, 24, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (2, 27, 27, 96, 256, 5, 5, (1, 1), (2, 2, 2, 2), 2),
+    (2, 35, 35, 3, 96, 11, 11, (4, 4), (0, 0, 0, 0), 1),
+    (3, 9, 11, 8, 16, 3, 2, (2, 1), (1, 0, 0, 1), 1),
+    (1, 7, 7, 5, 6, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (2, 14, 14, 64, 64, 3, 3, (1, 1), (1, 1, 1, 1), 4),
+]
+
+
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd(cfg):
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    x = rnd(N, H, W, C)
+    w = rnd(OC, KH, KW, C // g, seed=1, scale=0.1)
+    b = torch.randn(OC)
+    for act in (0, 3):
+        ref = ops.conv_fwd(x, w, b, sl, pad, g, act)
+        got = ops.conv_fwd(x.to(DEV), w.to(DEV), b.to(DEV), sl, pad, g, act)
+        close(got, ref, 1e-2)
+
+
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_dgrad(cfg):
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    w = rnd(OC, KH, KW, C // g, seed=1, scale=0.1)
+    OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
+    dy = rnd(N, OH, OW, OC, seed=2)
+    aux = rnd(N, H, W, C, seed=3)
+    ref = ops.conv_dgrad(dy, w, (N, H, W, C), sl, pad, g, aux=aux, aux_act=3)
+    got = ops.conv_dgrad(dy.to(DEV), w.to(DEV), (N, H, W, C), sl, pad, g,
+                         aux=aux.to(DEV), aux_act=3)
+    close(got, ref, 1e-2)
+
+
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_wgrad(cfg):
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    x = rnd(N, H, W, C)
+    OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
+    dy = rnd(N, OH, OW, OC, seed=2)
+    ref = torch.zeros(OC, KH, KW, C // g)
+    ops.conv_wgrad(x, dy, ref, sl, pad, g)
+    got = torch.zeros(OC, KH, KW, C // g, device=DEV)
+    ops.conv_wgrad(x.to(DEV), dy.to(DEV), got, sl, pad, g)
+    close(got, ref, 1e-2)
+
+
+@pytest.mark.parametrize("mode", ["max", "avg", "maxabs"])
+@pytest.mark.parametrize("shape,k,s", [((2, 55, 55, 96), 3, 2),
+                                       ((2, 13, 13, 5), 3, 2),
+                                       ((1, 8, 8, 16), 2, 2)])
+def test_pool(mode, shape, k, s):
+    x = rnd(*shape)
+    y, am = ops.pool_fwd(x, k, k, (s, s), mode)
+    yg, amg = ops.pool_fwd(x.to(DEV), k, k, (s, s), mode)
+    close(yg, y, 1e-6)
+    dy = rnd(*y.shape, seed=7)
+    aux = rnd(*shape, seed=8)
+    dx = ops.pool_bwd(dy, am, shape, k, k, (s, s), mode, aux=aux, aux_act=3)
+    dxg = ops.pool_bwd(dy.to(DEV), amg, shape, k, k, (s, s), mode,
+                       aux=aux.to(DEV), aux_act=3)
+    close(dxg, dx, 1e-2)
+
+
+@pytest.mark.parametrize("C", [96, 256, 13])
+def test_lrn(C):
+    x = rnd(3, 7, 5, C, scale=3.0)
+    y = ops.lrn_fwd(x, 5, 2e-4, 0.75, 2.0)
+    close(ops.lrn_fwd(x.to(DEV), 5, 2e-4, 0.75, 2.0), y, 1e-2)
+    dy = rnd(3, 7, 5, C, seed=3)
+    dx = ops.lrn_bwd(x, dy, 5, 2e-4, 0.75, 2.0)
+    close(ops.lrn_bwd(x.to(DEV), dy.to(DEV), 5, 2e-4, 0.75, 2.0), dx, 1e-2)
+
+
+def test_softmax_ce_and_mse():
+    B, C = 37, 1000
+    logits = rnd(B, C, scale=3.0, dtype=torch.float32)
+    labels = torch.randint(0, C, (B,), dtype=torch.int32)
+    labels[5] = -1
+    err = torch.empty(B, C)
+    m = torch.zeros(3)
+    ops.softmax_ce(logits, labels, err=err, metrics=m)
+    errg = torch.empty(B, C, device=DEV)
+    mg = torch.zeros(3, device=DEV)
+    ops.softmax_ce(logits.to(DEV), labels.to(DEV), err=errg, metrics=mg)
+    close(errg, err, 1e-4)
+    close(mg, m, 1e-4)
+    y, t = rnd(9, 33, dtype=torch.float32), rnd(9, 33, seed=1,
+                                               dtype=torch.float32)
+    e, mm = torch.empty(9, 33), torch.zeros(3)
+    ops.mse(y, t, scale=0.5, err=e, metrics=mm, valid_rows=7)
+    eg, mmg = torch.empty(9, 33, device=DEV), torch.zeros(3, device=DEV)
+    ops.mse(y.to(DEV), t.to(DEV), scale=0.5, err=eg, metrics=mmg,
+            valid_rows=7)
+    close(eg, e, 1e-5)
+    close(mmg, mm, 1e-4)
+
+
+def test_sgd_and_colsum():
+    n = 10007
+    w, g, m = torch.randn(n), torch.randn(n), torch.randn(n)
+    segs = [(0, 5000, 0.1, 0.01, 0.0, 0.9), (5000, n, 0.2, 0.001, 0.5, 0.5)]
+    wg, gg, mg = w.to(DEV), g.to(DEV), m.to(DEV)
+    lp = torch.empty(n, dtype=BF, device=DEV)
+    ops.sgd_update(w, g, m, segs, gscale=0.5)
+    ops.sgd_update(wg, gg, mg, segs, w_lp=lp, gscale=0.5)
+    close(wg, w, 1e-6)
+    close(mg, m, 1e-6)
+    close(lp, w, 1e-2)
+    x = rnd(5000, 300)
+    close(ops.col_sum(x.to(DEV)), ops.col_sum(x), 1e-4)
+
+
+def test_dropout_mask_matches_reference():
+    x = torch.randn(12345)
+    y = ops.dropout(x, 0.4, 1234)
+    yg = ops.dropout(x.to(DEV), 0.4, 1234)
+    close(yg, y, 1e-6)
+
+
+def test_xorshift_bit_exact():
+    g = torch.Generator().manual_seed(5)
+    st = torch.randint(-2 ** 62, 2 ** 62, (256, 16), generator=g,
+                       dtype=torch.int64)
+    stg = st.clone().to(DEV)
+    out = ops.xorshift1024star(st, 3)
+    outg = ops.xorshift1024star(stg, 3)
+    assert torch.equal(outg.cpu(), out)
+    assert torch.equal(stg.cpu(), st)
+
+
+def test_fill_minibatch_u8_bf16():
+    src = torch.randint(0, 256, (50, 3 * 16 * 16), dtype=torch.uint8)
+    lab = torch.randint(0, 10, (50,), dtype=torch.int32)
+    sh = torch.randperm(50).to(torch.int32)
+    mean = torch.rand(768) * 128
+    rd = torch.rand(768) * 0.02
+    d = torch.empty(16, 768, dtype=BF)
+    lo, io = torch.empty(16, dtype=torch.int32), torch.empty(16, dtype=torch.int32)
+    ops.fill_minibatch(src, sh, 3, 11, d, mean=mean, rdisp=rd, labels=lab,
+                       labels_out=lo, idx_out=io)
+    dg = torch.empty(16, 768, dtype=BF, device=DEV)
+    log, iog = torch.empty_like(lo, device=DEV), torch.empty_like(io, device=DEV)
+    ops.fill_minibatch(src.to(DEV), sh.to(DEV), 3, 11, dg, mean=mean.to(DEV),
+                       rdisp=rd.to(DEV), labels=lab.to(DEV), labels_out=log,
+                       idx_out=iog)
+    close(dg, d, 1e-2)
+    assert torch.equal(log.cpu(), lo) and torch.equal(iog.cpu(), io)
+
+
+def test_join_and_cast():
+    a, b = rnd(7, 5), rnd(7, 9, seed=1)
+    close(ops.join([a.to(DEV), b.to(DEV)]), ops.join([a, b]), 0)
+    x = torch.randn(1000)
+    close(ops.cast(x.to(DEV), BF), ops.cast(x, BF), 0)

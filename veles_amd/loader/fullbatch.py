@@ -1,0 +1,214 @@
+"""Whole dataset resident in (device) memory.
+
+Reference: veles/loader/fullbatch.py:78-566 (``FullBatchLoader``: original
+data/labels on the device, minibatch by a gather kernel, numpy fallback on
+OOM; ``FullBatchLoaderMSE`` for targets).
+
+MI355X design: the dataset stays in HBM as stored (uint8 images stay uint8 -
+288 GB per GPU holds ImageNet-scale synthetic sets), the shuffled index
+permutation lives on the device, and one ``hvk_fill_minibatch`` launch
+gathers the rank's rows, converts uint8 -> bf16 and applies the normalizer's
+per-feature affine map (mean / dispersion) in the same pass.  The CPU device
+runs the identical op through its float32 reference.
+"""
+from __future__ import annotations
+
+import numpy
+
+from veles_amd.loader.base import Loader, LoaderMSEMixin, TRAIN, VALID
+from veles_amd.memory import Array
+
+__all__ = ["FullBatchLoader", "FullBatchLoaderMSE", "IFullBatchLoader"]
+
+
+class IFullBatchLoader(object):
+    def load_data(self):
+        """Fill original_data, original_labels and class_lengths."""
+
+
+class FullBatchLoader(Loader, IFullBatchLoader):
+    hide_from_registry = True
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.original_data = Array()
+        self.original_labels = []
+        self.validation_ratio = kwargs.get("validation_ratio", None)
+        self.on_device = kwargs.get("on_device", True)
+        self._affine = None
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self._dev_labels_ = None
+        self._dev_mean_ = None
+        self._dev_rdisp_ = None
+        self._dev_shuffled_ = None
+
+    def __getstate__(self):
+        st = super().__getstate__()
+        # the dataset itself is regenerated / reloaded by load_data()
+        st["original_data"] = Array()
+        st["original_labels"] = []
+        return st
+
+    @property
+    def has_labels(self):
+        return len(self.original_labels) > 0
+
+    @has_labels.setter
+    def has_labels(self, value):
+        pass
+
+    @property
+    def sample_shape(self):
+        return tuple(self.original_data.shape[1:])
+
+    def _torch_dtype_for_minibatch(self):
+        import torch
+        dev = self.device
+        if dev is not None and getattr(dev, "is_gpu", False):
+            return dev.compute_dtype
+        return torch.float32
+
+    def create_minibatch_data(self):
+        import torch
+        n = self.local_minibatch_size
+        dev = self.device
+        shape = (n,) + self.sample_shape
+        tdev = dev.torch_device if dev is not None else torch.device("cpu")
+        t = torch.zeros(shape, dtype=self._torch_dtype_for_minibatch(),
+                        device=tdev)
+        self.minibatch_data.devmem = t
+        for arr in (self.minibatch_labels, self.minibatch_indices):
+            if arr.mem is not None:
+                arr.initialize(dev)
+
+    def _apply_validation_ratio(self):
+        if not self.validation_ratio:
+            return
+        n = int(self.class_lengths[TRAIN] * self.validation_ratio)
+        self.class_lengths[VALID] += n
+        self.class_lengths[TRAIN] -= n
+
+    def analyze_dataset(self):
+        """Analyse the TRAIN slice on the host, then either keep a
+        per-feature affine map for the device gather (uint8 / raw data) or
+        normalise the whole resident dataset once (reference
+        fullbatch.py:336-347)."""
+        if self.normalizer is None or self.normalization_type == "none":
+            self._affine = None
+            return
+        data = self.original_data.mem
+        train = data[self.class_end_offsets[VALID]:
+                     self.class_end_offsets[TRAIN]]
+        step = 4096
+        for i in range(0, len(train), step):
+            self.normalizer.analyze(train[i:i + step].astype(numpy.float32))
+        if not self.normalizer.is_initialized:
+            self.normalizer.analyze(train[:1].astype(numpy.float32))
+        aff = self.normalizer.affine()
+        if aff is not None:
+            mean, rdisp = aff
+            feat = int(numpy.prod(self.sample_shape))
+            mean = numpy.broadcast_to(numpy.asarray(mean, numpy.float32),
+                                      (feat,)).copy()
+            rdisp = numpy.broadcast_to(numpy.asarray(rdisp, numpy.float32),
+                                       (feat,)).copy()
+            self._affine = (mean, rdisp)
+        else:
+            # non-affine normalizer: normalise the resident data once
+            d = data.astype(numpy.float32)
+            for i in range(0, len(d), step):
+                self.normalizer.normalize(d[i:i + step])
+            self.original_data.reset(d)
+            self._affine = None
+
+    def normalize_minibatch(self):
+        pass  # folded into the gather
+
+    def on_initialized(self, **kwargs):
+        import torch
+        dev = self.device
+        tdev = dev.torch_device if dev is not None else torch.device("cpu")
+        if self.original_data.devmem is None or \
+                self.original_data.devmem.device != tdev:
+            self.original_data.initialize(dev)
+        lab = numpy.asarray(self.original_labels, dtype=numpy.int32) \
+            if self.has_labels else None
+        self._dev_labels_ = None if lab is None else torch.from_numpy(
+            lab).to(tdev)
+        if self._affine is not None:
+            self._dev_mean_ = torch.from_numpy(self._affine[0]).to(tdev)
+            self._dev_rdisp_ = torch.from_numpy(self._affine[1]).to(tdev)
+        self._upload_shuffled()
+
+    def on_shuffled(self):
+        if self._dev_labels_ is not None or self.original_data.devmem is not None:
+            self._upload_shuffled()
+
+    def _upload_shuffled(self):
+        import torch
+        dev = self.device
+        tdev = dev.torch_device if dev is not None else torch.device("cpu")
+        src = torch.from_numpy(self.shuffled_indices.mem)
+        if self._dev_shuffled_ is None or self._dev_shuffled_.device != tdev \
+                or self._dev_shuffled_.numel() != src.numel():
+            self._dev_shuffled_ = src.to(tdev).clone()
+        else:
+            self._dev_shuffled_.copy_(src, non_blocking=False)
+
+    def fill_indices(self, start_offset, count):
+        from veles_amd import ops
+        if self._dev_shuffled_ is None:
+            self.on_initialized()
+        data = self.original_data.devmem
+        ops.fill_minibatch(
+            data, self._dev_shuffled_, start_offset, count,
+            self.minibatch_data.devmem, mean=self._dev_mean_,
+            rdisp=self._dev_rdisp_, labels=self._dev_labels_,
+            labels_out=self.minibatch_labels.devmem
+            if self.has_labels else None,
+            idx_out=self.minibatch_indices.devmem)
+        return True
+
+    def fill_minibatch(self):
+        """Host path used by analysis helpers: fill by minibatch_indices."""
+        idx = self.minibatch_indices.to_numpy()[:self.minibatch_size]
+        self.minibatch_data.map_write()
+        self.minibatch_data.mem[:len(idx)] = self.original_data.mem[idx]
+        self.minibatch_data.unmap()
+
+
+class FullBatchLoaderMSE(LoaderMSEMixin, FullBatchLoader):
+    hide_from_registry = True
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.original_targets = Array()
+
+    def __getstate__(self):
+        st = super().__getstate__()
+        st["original_targets"] = Array()
+        return st
+
+    def create_minibatch_data(self):
+        import torch
+        super().create_minibatch_data()
+        dev = self.device
+        tdev = dev.torch_device if dev is not None else torch.device("cpu")
+        n = self.local_minibatch_size
+        tshape = (n,) + tuple(self.original_targets.shape[1:])
+        self.minibatch_targets.devmem = torch.zeros(
+            tshape, dtype=self._torch_dtype_for_minibatch(), device=tdev)
+
+    def on_initialized(self, **kwargs):
+        super().on_initialized(**kwargs)
+        if self.original_targets.devmem is None:
+            self.original_targets.initialize(self.device)
+
+    def fill_indices(self, start_offset, count):
+        from veles_amd import ops
+        super().fill_indices(start_offset, count)
+        ops.fill_minibatch(self.original_targets.devmem, self._dev_shuffled_,
+                           start_offset, count, self.minibatch_targets.devmem)
+        return True

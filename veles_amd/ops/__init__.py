@@ -1,0 +1,704 @@
+"""Functional ops: hand-written HIP kernels on the GPU, PyTorch-fp32 references
+on the CPU.
+
+One code path for units: every op takes torch tensors; CUDA (HIP) tensors go
+to ``libhvk.so`` (csrc/kernels, gfx950 MFMA / vectorised kernels) on the
+current stream, CPU tensors are evaluated by the float32 reference below -
+the numerics oracle of every kernel test (the reference's "numpy backend",
+veles/backends.py:917-948).  There is no silent fallback: a GPU tensor with a
+missing library raises ``KernelLibraryMissing``.
+
+Layout conventions (docs/OPS.md): activations NHWC, conv weights
+[OC][KH][KW][C/groups], fully-connected weights [out][in] (reference export
+fixture libVeles/tests/workflow_files/contents.json), padding (left, top,
+right, bottom), sliding (x, y).
+"""
+from __future__ import annotations
+
+import struct
+
+import torch
+import torch.nn.functional as F
+
+from veles_amd.ops import _lib
+from veles_amd.ops._lib import available, require_library  # noqa: F401
+
+__all__ = ["ACT", "gemm", "linear_fwd", "conv_out_size", "conv_fwd",
+           "conv_dgrad", "conv_wgrad", "col_sum", "row_sum", "act_fwd",
+           "act_bwd", "pool_fwd", "pool_bwd", "lrn_fwd", "lrn_bwd",
+           "softmax_ce", "mse", "sgd_update", "dropout", "xorshift1024star",
+           "xorshift128plus", "join", "cast", "fill_minibatch",
+           "mean_disp_normalize", "act_code"]
+
+DT = {torch.float32: 0, torch.bfloat16: 1, torch.uint8: 2, torch.int32: 3,
+      torch.float16: 4}
+ACT = {"linear": 0, None: 0, "tanh": 1, "relu": 2, "strict_relu": 3,
+       "str": 3, "sigmoid": 4}
+
+
+def act_code(act):
+    if isinstance(act, int):
+        return act
+    return ACT[act]
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _s(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _lib_call(name, *args):
+    fn = getattr(_lib.lib(), name)
+    _lib.check(fn(*args), name)
+
+
+def _gpu(t):
+    return t is not None and t.is_cuda
+
+
+# --------------------------------------------------------------- activations
+def act_fwd_ref(x, act):
+    act = act_code(act)
+    if act == 1:
+        return 1.7159 * torch.tanh(0.6666 * x)
+    if act == 2:
+        return torch.where(x > 15, x, torch.log1p(torch.exp(x.clamp(max=15))))
+    if act == 3:
+        return torch.clamp(x, min=0)
+    if act == 4:
+        return torch.sigmoid(x)
+    return x
+
+
+def act_bwd_ref(y, act):
+    act = act_code(act)
+    if act == 1:
+        return 0.6666 * 1.7159 - (0.6666 / 1.7159) * y * y
+    if act == 2:
+        return 1 - torch.exp(-y)
+    if act == 3:
+        return (y > 0).to(y.dtype)
+    if act == 4:
+        return y * (1 - y)
+    return torch.ones_like(y)
+
+
+def act_fwd(x, act, out=None):
+    act = act_code(act)
+    if _gpu(x):
+        out = torch.empty_like(x) if out is None else out
+        _lib_call("hvk_act_fwd", _p(x), DT[x.dtype], _p(out), DT[out.dtype],
+                  x.numel(), act, _s(x))
+        return out
+    r = act_fwd_ref(x.float(), act).to(x.dtype)
+    if out is None:
+        return r
+    out.copy_(r)
+    return out
+
+
+def act_bwd(dy, y, act, out=None):
+    """dx = dy * f'(y) (derivative expressed through the output y)."""
+    act = act_code(act)
+    if _gpu(dy):
+        out = torch.empty_like(dy) if out is None else out
+        _lib_call("hvk_act_bwd", _p(dy), DT[dy.dtype], _p(y), DT[y.dtype],
+                  _p(out), DT[out.dtype], dy.numel(), act, _s(dy))
+        return out
+    r = (dy.float() * act_bwd_ref(y.float(), act)).to(dy.dtype)
+    if out is None:
+        return r
+    out.copy_(r)
+    return out
+
+
+# --------------------------------------------------------------------- GEMM
+def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
+         alpha=1.0, beta=0.0, bias=None, bias_mode="col", act=0, aux=None,
+         aux_act=0, accumulate=False, splits=1):
+    """out[M][N] = act(alpha*op(a)@op(b) + beta*out + bias) * f'_aux(aux).
+
+    ``accumulate``: out (float32) += alpha*op(a)@op(b) (+bias) - split-K
+    partial sums are reduced with float atomics on the GPU.
+    """
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    Kb = b.shape[1] if trans_b else b.shape[0]
+    if K != Kb:
+        raise ValueError("gemm: inner dimensions differ (%d vs %d)" % (K, Kb))
+    act = act_code(act)
+    aux_act = act_code(aux_act)
+    bm = {"col": 1, "row": 2}[bias_mode]
+    dev = a.device
+    if out is None:
+        out_dtype = out_dtype or (torch.float32 if accumulate else a.dtype)
+        out = (torch.zeros if accumulate else torch.empty)(
+            M, N, dtype=out_dtype, device=dev)
+    if _gpu(a):
+        if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+            raise TypeError("GPU gemm operands must be bfloat16")
+        for t in (a, b, out):
+            if t.stride(-1) != 1:
+                raise ValueError("gemm operands must be row-major")
+        if accumulate and out.dtype != torch.float32:
+            raise TypeError("accumulate requires a float32 output")
+        atomic = 1 if accumulate else 0
+        if splits > 1 and not accumulate:
+            raise ValueError("split-K requires accumulate=True")
+        _lib_call("hvk_gemm", int(trans_a), int(trans_b), M, N, K, _p(a),
+                  a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0),
+                  int(out.dtype == torch.float32), atomic, float(alpha),
+                  float(beta), _p(bias), bm, act, _p(aux),
+                  0 if aux is None else aux.stride(0), aux_act, int(splits),
+                  _s(a))
+        return out
+    A = a.float().t() if trans_a else a.float()
+    B = b.float().t() if trans_b else b.float()
+    r = alpha * (A @ B)
+    if bias is not None:
+        r = r + (bias.float().view(1, -1) if bm == 1 else
+                 bias.float().view(-1, 1))
+    if accumulate:
+        out += r.to(out.dtype)
+        return out
+    if beta != 0.0:
+        r = r + beta * out.float()
+    r = act_fwd_ref(r, act)
+    if aux is not None:
+        r = r * act_bwd_ref(aux.float(), aux_act)
+    out.copy_(r.to(out.dtype))
+    return out
+
+
+def linear_fwd(x, w, bias=None, act=0, out=None):
+    """y[B][out] = act(x[B][in] @ w[out][in]^T + bias)."""
+    return gemm(x, w, trans_b=True, bias=bias, act=act, out=out)
+
+
+# --------------------------------------------------------------- convolution
+def conv_out_size(h, w, kh, kw, sliding, padding):
+    sx, sy = sliding
+    pl, pt, pr, pb = padding
+    return (h + pt + pb - kh) // sy + 1, (w + pl + pr - kw) // sx + 1
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).float()
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
+             groups=1, act=0, out=None):
+    """x [N,H,W,C], w [OC,KH,KW,C/g] -> y [N,OH,OW,OC]."""
+    N, H, W, C = x.shape
+    OC, KH, KW, Cg = w.shape
+    if Cg * groups != C or OC % groups:
+        raise ValueError("conv_fwd: bad grouping %s %s g=%d" %
+                         (tuple(x.shape), tuple(w.shape), groups))
+    sx, sy = sliding
+    pl, pt, pr, pb = padding
+    OH, OW = conv_out_size(H, W, KH, KW, sliding, padding)
+    act = act_code(act)
+    if out is None:
+        out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        _lib_call("hvk_conv_fwd", _p(x), _p(w), _p(bias), _p(out), N, H, W, C,
+                  OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, act, _s(x))
+        return out
+    xp = F.pad(_nchw(x), (pl, pr, pt, pb))
+    y = F.conv2d(xp, w.permute(0, 3, 1, 2).float(),
+                 None if bias is None else bias.float(), stride=(sy, sx),
+                 groups=groups)
+    y = act_fwd_ref(y, act)
+    out.copy_(_nhwc(y).to(out.dtype))
+    return out
+
+
+def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
+               groups=1, aux=None, aux_act=0, out=None):
+    """dx [N,H,W,C] = conv^T(dy, w) [* f'(aux)]."""
+    N, H, W, C = x_shape
+    _, OH, OW, OC = dy.shape
+    _, KH, KW, Cg = w.shape
+    sx, sy = sliding
+    pl, pt, pr, pb = padding
+    aux_act = act_code(aux_act)
+    if out is None:
+        out = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    if _gpu(dy):
+        _lib_call("hvk_conv_dgrad", _p(dy), _p(w), _p(out), N, H, W, C, OC, KH,
+                  KW, sy, sx, pt, pl, OH, OW, groups, _p(aux), aux_act, _s(dy))
+        return out
+    Hp, Wp = H + pt + pb, W + pl + pr
+    dxp = torch.nn.grad.conv2d_input((N, C, Hp, Wp),
+                                     w.permute(0, 3, 1, 2).float(),
+                                     _nchw(dy), stride=(sy, sx), groups=groups)
+    dx = dxp[:, :, pt:pt + H, pl:pl + W]
+    if aux is not None:
+        dx = dx * act_bwd_ref(_nchw(aux), aux_act)
+    out.copy_(_nhwc(dx).to(out.dtype))
+    return out
+
+
+def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
+               splits=None):
+    """dw (float32 [OC,KH,KW,C/g]) += sum over pixels of dy (x) im2col(x)."""
+    N, H, W, C = x.shape
+    _, OH, OW, OC = dy.shape
+    _, KH, KW, Cg = dw.shape
+    sx, sy = sliding
+    pl, pt, pr, pb = padding
+    if dw.dtype != torch.float32:
+        raise TypeError("conv_wgrad accumulates into float32")
+    if _gpu(x):
+        if splits is None:
+            splits = wgrad_splits(N * OH * OW, OC // groups,
+                                  KH * KW * Cg, groups)
+        _lib_call("hvk_conv_wgrad", _p(x), _p(dy), _p(dw), N, H, W, C, OC, KH,
+                  KW, sy, sx, pt, pl, OH, OW, groups, int(splits), _s(x))
+        return dw
+    xp = F.pad(_nchw(x), (pl, pr, pt, pb))
+    g = torch.nn.grad.conv2d_weight(xp, (OC, Cg, KH, KW), _nchw(dy),
+                                    stride=(sy, sx), groups=groups)
+    dw += g.permute(0, 2, 3, 1)
+    return dw
+
+
+def wgrad_splits(P, M, N, groups, target_blocks=2048):
+    tiles = ((M + 127) // 128) * ((N + 127) // 128) * groups
+    splits = max(1, min(target_blocks // max(tiles, 1), P // 512))
+    return splits
+
+
+# ------------------------------------------------------------- reductions
+def col_sum(x2d, out=None, scale=1.0, accumulate=False):
+    """out[c] (+)= scale * sum_r x[r][c]  (float32 out)."""
+    R, C = x2d.shape
+    if out is None:
+        out = torch.zeros(C, dtype=torch.float32, device=x2d.device)
+    elif not accumulate:
+        out.zero_()
+    if _gpu(x2d):
+        _lib_call("hvk_col_sum", _p(x2d), DT[x2d.dtype], R, C, _p(out),
+                  float(scale), _s(x2d))
+        return out
+    out += scale * x2d.float().sum(0)
+    return out
+
+
+def row_sum(x2d, out=None, scale=1.0):
+    R, C = x2d.shape
+    if out is None:
+        out = torch.empty(R, dtype=torch.float32, device=x2d.device)
+    if _gpu(x2d):
+        _lib_call("hvk_row_sum", _p(x2d), DT[x2d.dtype], R, C, _p(out),
+                  float(scale), _s(x2d))
+        return out
+    out.copy_(scale * x2d.float().sum(1))
+    return out
+
+
+# ----------------------------------------------------------------- pooling
+POOL = {"max": 0, "avg": 1, "maxabs": 2}
+
+
+def pool_out_size(h, w, ky, kx, sy, sx):
+    """Znicz pooling geometry: partial windows at the far edge are kept
+    (ceil), never a window that starts outside the input."""
+    return (h - ky + sy - 1) // sy + 1 if h > ky else 1, \
+        (w - kx + sx - 1) // sx + 1 if w > kx else 1
+
+
+def _pool_ref(x, ky, kx, sy, sx, mode, OH, OW):
+    N, H, W, C = x.shape
+    xf = x.float()
+    neg = float("-inf")
+    Hp, Wp = (OH - 1) * sy + ky, (OW - 1) * sx + kx
+    pad = torch.full((N, Hp, Wp, C), float("nan"))
+    pad[:, :H, :W, :] = xf
+    idx = torch.arange(N * H * W * C).view(N, H, W, C)
+    pidx = torch.full((N, Hp, Wp, C), -1, dtype=torch.long)
+    pidx[:, :H, :W, :] = idx
+    best = torch.full((N, OH, OW, C), neg)
+    bkey = torch.full((N, OH, OW, C), neg)
+    bidx = torch.full((N, OH, OW, C), -1, dtype=torch.long)
+    s = torch.zeros(N, OH, OW, C)
+    cnt = torch.zeros(N, OH, OW, C)
+    for dy in range(ky):
+        for dx in range(kx):
+            v = pad[:, dy:dy + (OH - 1) * sy + 1:sy, dx:dx + (OW - 1) * sx + 1:sx, :]
+            vi = pidx[:, dy:dy + (OH - 1) * sy + 1:sy, dx:dx + (OW - 1) * sx + 1:sx, :]
+            valid = ~torch.isnan(v)
+            if mode == 1:
+                s += torch.where(valid, v, torch.zeros_like(v))
+                cnt += valid.float()
+            else:
+                key = v.abs() if mode == 2 else v
+                better = valid & ((bidx < 0) | (key > bkey))
+                best = torch.where(better, v, best)
+                bkey = torch.where(better, key, bkey)
+                bidx = torch.where(better, vi, bidx)
+    if mode == 1:
+        return s / cnt.clamp(min=1), None
+    return best, bidx.to(torch.int32)
+
+
+def pool_fwd(x, ky, kx, sliding=None, mode="max", out=None, argmax=None):
+    """NHWC pooling; returns (y, argmax) - argmax is the flat input index of
+    the chosen element (None for avg)."""
+    sx, sy = sliding or (kx, ky)
+    N, H, W, C = x.shape
+    OH, OW = pool_out_size(H, W, ky, kx, sy, sx)
+    m = POOL[mode]
+    if out is None:
+        out = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
+    if m != 1 and argmax is None:
+        argmax = torch.empty(N, OH, OW, C, dtype=torch.int32, device=x.device)
+    if _gpu(x):
+        _lib_call("hvk_pool_fwd", _p(x), _p(out), _p(argmax), N, H, W, C, OH,
+                  OW, ky, kx, sy, sx, 0, 0, m, _s(x))
+        return out, argmax
+    y, idx = _pool_ref(x.cpu(), ky, kx, sy, sx, m, OH, OW)
+    out.copy_(y.to(out.dtype))
+    if idx is not None:
+        argmax.copy_(idx)
+    return out, argmax
+
+
+def pool_bwd(dy, argmax, x_shape, ky, kx, sliding=None, mode="max",
+             aux=None, aux_act=0, out=None):
+    sx, sy = sliding or (kx, ky)
+    N, H, W, C = x_shape
+    _, OH, OW, _ = dy.shape
+    m = POOL[mode]
+    aux_act = act_code(aux_act)
+    if out is None:
+        out = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    if _gpu(dy):
+        _lib_call("hvk_pool_bwd", _p(dy), _p(argmax), _p(out), N, H, W, C, OH,
+                  OW, ky, kx, sy, sx, 0, 0, m, _p(aux), aux_act, _s(dy))
+        return out
+    g = dy.float()
+    dx = torch.zeros(N * H * W * C)
+    if m == 1:
+        dx = dx.view(N, H, W, C)
+        cnt = torch.zeros(N, OH, OW, C)
+        for oh in range(OH):
+            h0, h1 = oh * sy, min(oh * sy + ky, H)
+            for ow in range(OW):
+                w0, w1 = ow * sx, min(ow * sx + kx, W)
+                c = (h1 - h0) * (w1 - w0)
+                dx[:, h0:h1, w0:w1, :] += (g[:, oh, ow, :] / c)[:, None, None, :]
+    else:
+        dx.index_add_(0, argmax.long().reshape(-1), g.reshape(-1))
+        dx = dx.view(N, H, W, C)
+    if aux is not None:
+        dx = dx * act_bwd_ref(aux.float(), aux_act)
+    out.copy_(dx.to(out.dtype))
+    return out
+
+
+# --------------------------------------------------------------------- LRN
+def _lrn_ref(x, n, alpha, beta, k):
+    x2 = x * x
+    half = n // 2
+    xp = F.pad(x2, (half, half))
+    s = sum(xp[..., i:i + x.shape[-1]] for i in range(2 * half + 1))
+    return x * torch.pow(k + alpha * s, -beta)
+
+
+def lrn_fwd(x, n=5, alpha=1e-4, beta=0.75, k=2.0, out=None):
+    """Across-channel LRN on NHWC: y = x (k + alpha sum x^2)^-beta."""
+    C = x.shape[-1]
+    P = x.numel() // C
+    if out is None:
+        out = torch.empty_like(x)
+    if _gpu(x):
+        _lib_call("hvk_lrn_fwd", _p(x), _p(out), P, C, n, float(alpha),
+                  float(beta), float(k), _s(x))
+        return out
+    out.copy_(_lrn_ref(x.float(), n, alpha, beta, k).to(out.dtype))
+    return out
+
+
+def lrn_bwd(x, dy, n=5, alpha=1e-4, beta=0.75, k=2.0, aux=None, aux_act=0,
+            out=None):
+    C = x.shape[-1]
+    P = x.numel() // C
+    aux_act = act_code(aux_act)
+    if out is None:
+        out = torch.empty_like(dy)
+    if _gpu(x):
+        _lib_call("hvk_lrn_bwd", _p(x), _p(dy), _p(out), P, C, n, float(alpha),
+                  float(beta), float(k), _p(aux), aux_act, _s(x))
+        return out
+    xf = x.float().detach().requires_grad_(True)
+    y = _lrn_ref(xf, n, alpha, beta, k)
+    y.backward(dy.float())
+    dx = xf.grad
+    if aux is not None:
+        dx = dx * act_bwd_ref(aux.float(), aux_act)
+    out.copy_(dx.to(out.dtype))
+    return out
+
+
+# --------------------------------------------------------------- evaluators
+def softmax_ce(logits, labels, *, scale=None, err=None, probs=None,
+               max_idx=None, metrics=None, confusion=None):
+    """Fused softmax + cross-entropy gradient + error counting.
+
+    err = (softmax(logits) - onehot(labels)) * scale (rows with label < 0 get
+    0); metrics (float32[3]) += [n_err, sum CE loss, n_valid]."""
+    B, C = logits.shape
+    if scale is None:
+        scale = 1.0 / B
+    if _gpu(logits):
+        _lib_call("hvk_softmax_ce", _p(logits), DT[logits.dtype], B, C,
+                  _p(labels), float(scale), _p(err),
+                  0 if err is None else DT[err.dtype], _p(probs), _p(max_idx),
+                  _p(metrics), _p(confusion), _s(logits))
+        return err
+    lf = logits.float()
+    p = torch.softmax(lf, 1)
+    lab = labels.long()
+    valid = lab >= 0
+    if probs is not None:
+        probs.copy_(p)
+    if max_idx is not None:
+        max_idx.copy_(lf.argmax(1).to(max_idx.dtype))
+    if err is not None:
+        oh = torch.zeros_like(p)
+        oh[valid, lab[valid]] = 1.0
+        e = (p - oh) * scale
+        e[~valid] = 0
+        err.copy_(e.to(err.dtype))
+    if metrics is not None and valid.any():
+        am = lf.argmax(1)
+        pl = p[valid, lab[valid]].clamp(min=1e-30)
+        metrics[0] += (am[valid] != lab[valid]).sum().float()
+        metrics[1] += -torch.log(pl).sum()
+        metrics[2] += valid.sum().float()
+        if confusion is not None:
+            for a, b in zip(am[valid].tolist(), lab[valid].tolist()):
+                confusion[a, b] += 1
+    return err
+
+
+def mse(y, target, *, scale=1.0, err=None, mse_out=None, metrics=None,
+        valid_rows=None):
+    B = y.shape[0]
+    D = y.numel() // B
+    valid_rows = B if valid_rows is None else valid_rows
+    if _gpu(y):
+        _lib_call("hvk_mse", _p(y), DT[y.dtype], _p(target), DT[target.dtype],
+                  B, D, float(scale), _p(err),
+                  0 if err is None else DT[err.dtype], _p(mse_out),
+                  _p(metrics), int(valid_rows), _s(y))
+        return err
+    d = y.float().reshape(B, D) - target.float().reshape(B, D)
+    d[valid_rows:] = 0
+    if err is not None:
+        err.copy_((d * scale).reshape(err.shape).to(err.dtype))
+    m = (d * d).mean(1)
+    if mse_out is not None:
+        mse_out.copy_(m)
+    if metrics is not None:
+        metrics[0] += m[:valid_rows].sum()
+        metrics[1] += m[:valid_rows].sqrt().sum()
+        metrics[2] += valid_rows
+    return err
+
+
+# --------------------------------------------------------------- optimizer
+_SEG_CACHE = {}
+
+
+def _segs_tensor(segs, device):
+    key = (tuple(segs), str(device))
+    t = _SEG_CACHE.get(key)
+    if t is None:
+        raw = b"".join(struct.pack("<qqffff", int(b), int(e), float(lr),
+                                   float(d), float(l1), float(m))
+                       for b, e, lr, d, l1, m in segs)
+        t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        if len(_SEG_CACHE) > 256:
+            _SEG_CACHE.clear()
+        _SEG_CACHE[key] = t
+    return t
+
+
+def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0):
+    """Fused multi-segment SGD (flat float32 buffers).
+
+    segs: [(begin, end, lr, weights_decay, l1_vs_l2, gradient_moment)]
+      g = grad*gscale + decay*((1-l1)*w + l1*sign(w));  v = moment*v - lr*g;
+      w += v;  w_lp = bfloat16(w)"""
+    n = w.numel()
+    if _gpu(w):
+        st = _segs_tensor(segs, w.device)
+        _lib_call("hvk_sgd", _p(w), _p(grad), _p(mom), _p(w_lp), _p(st),
+                  len(segs), n, float(gscale), _s(w))
+        return w
+    for b, e, lr, d, l1, m in segs:
+        ws = w[b:e]
+        g = grad[b:e] * gscale
+        if d:
+            g = g + d * ((1 - l1) * ws + l1 * torch.sign(ws))
+        v = -lr * g
+        if mom is not None:
+            v = v + m * mom[b:e]
+            mom[b:e] = v
+        ws += v
+    if w_lp is not None:
+        w_lp.copy_(w.to(w_lp.dtype))
+    return w
+
+
+# ---------------------------------------------------------------- dropout
+def _hash32(i, seed):
+    M = 0xFFFFFFFF
+    x = i ^ ((seed * 0x9E3779B9) & M)
+    x ^= x >> 16
+    x = (x * 0x7feb352d) & M
+    x ^= x >> 15
+    x = (x * 0x846ca68b) & M
+    x ^= x >> 16
+    return x
+
+
+def dropout_mask_ref(n, seed, p):
+    i = torch.arange(n, dtype=torch.int64)
+    h = _hash32(i, int(seed) & 0xFFFFFFFF)
+    thresh = min(0xFFFFFFFF, int(p * 4294967296.0))
+    return h >= thresh
+
+
+def dropout(x, p, seed, out=None):
+    """y = x * keep / (1-p) with a counter-based mask (same seed -> same mask:
+    the backward pass calls this on dy)."""
+    if out is None:
+        out = torch.empty_like(x)
+    if _gpu(x):
+        _lib_call("hvk_dropout", _p(x), DT[x.dtype], _p(out), DT[out.dtype],
+                  x.numel(), int(seed) & 0xFFFFFFFF, float(p), None, _s(x))
+        return out
+    keep = dropout_mask_ref(x.numel(), seed, p).view(x.shape)
+    scale = 1.0 / (1.0 - p) if p < 1 else 0.0
+    out.copy_((x.float() * keep * scale).to(out.dtype))
+    return out
+
+
+# --------------------------------------------------------------------- RNG
+def xorshift1024star(states, rounds, out=None):
+    """states: int64 [n,16] (raw uint64 bits, updated in place); returns int64
+    [rounds*16*n] laid out out[round*16*n + i*n + id]."""
+    n = states.shape[0]
+    if out is None:
+        out = torch.empty(rounds * 16 * n, dtype=torch.int64,
+                          device=states.device)
+    if _gpu(states):
+        _lib_call("hvk_xorshift1024star", _p(states), n, int(rounds), _p(out),
+                  _s(states))
+        return out
+    from veles_amd.prng.random_generator import xorshift1024star as ref
+    s = states.numpy().view("uint64")
+    r = ref(s, rounds)
+    out.copy_(torch.from_numpy(r.view("int64")))
+    return out
+
+
+def xorshift128plus(states, out=None):
+    n = states.shape[0]
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=states.device)
+    if _gpu(states):
+        _lib_call("hvk_xorshift128plus", _p(states), n, _p(out), _s(states))
+        return out
+    from veles_amd.prng.random_generator import xorshift128plus as ref
+    r = ref(states.numpy().view("uint64"), 1)
+    out.copy_(torch.from_numpy(r.view("int64")))
+    return out
+
+
+# ------------------------------------------------------------- data moving
+def join(inputs, out=None):
+    """Feature-wise concatenation of [B, n_i] inputs (InputJoiner)."""
+    B = inputs[0].shape[0]
+    lens = [t.numel() // B for t in inputs]
+    if out is None:
+        out = torch.empty(B, sum(lens), dtype=inputs[0].dtype,
+                          device=inputs[0].device)
+    if _gpu(out) and len(inputs) <= 16:
+        import ctypes
+        arr = (ctypes.c_void_p * len(inputs))(*[t.data_ptr() for t in inputs])
+        la = (ctypes.c_int * len(inputs))(*lens)
+        _lib_call("hvk_join", ctypes.cast(arr, ctypes.c_void_p),
+                  ctypes.cast(la, ctypes.c_void_p), len(inputs),
+                  DT[out.dtype], _p(out), B, _s(out))
+        return out
+    out.copy_(torch.cat([t.reshape(B, -1).to(out.dtype) for t in inputs], 1))
+    return out
+
+
+def cast(x, dtype, scale=1.0, out=None):
+    if out is None:
+        out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    if _gpu(x) and x.dtype in DT and out.dtype in DT:
+        _lib_call("hvk_cast", _p(x), DT[x.dtype], _p(out), DT[out.dtype],
+                  x.numel(), float(scale), _s(x))
+        return out
+    out.copy_((x.float() * scale).to(dtype))
+    return out
+
+
+def fill_minibatch(src, shuffled, start, count, dst, *, mean=None,
+                   rdisp=None, labels=None, labels_out=None, idx_out=None):
+    """Gather a minibatch: dst[i] = (src[shuffled[start+i]] - mean) * rdisp
+    for i < count, zeros after; labels/indices gathered (-1 padding)."""
+    max_mb = dst.shape[0]
+    sample = src.numel() // src.shape[0]
+    if _gpu(dst):
+        _lib_call("hvk_fill_minibatch", _p(src), DT[src.dtype], _p(shuffled),
+                  int(start), int(count), max_mb, sample, _p(mean), _p(rdisp),
+                  _p(dst), DT[dst.dtype], _p(labels), _p(labels_out),
+                  _p(idx_out), _s(dst))
+        return dst
+    idx = shuffled[start:start + count].long()
+    v = src.reshape(src.shape[0], -1)[idx].float()
+    if mean is not None:
+        v = v - mean.reshape(1, -1).float()
+    if rdisp is not None:
+        v = v * rdisp.reshape(1, -1).float()
+    d = dst.view(max_mb, -1)
+    d[:count] = v.to(dst.dtype)
+    d[count:] = 0
+    if labels_out is not None:
+        labels_out[:count] = labels[idx] if labels is not None else -1
+        labels_out[count:] = -1
+    if idx_out is not None:
+        idx_out[:count] = idx.to(idx_out.dtype)
+        idx_out[count:] = -1
+    return dst
+
+
+def mean_disp_normalize(x, mean, rdisp, out=None, out_dtype=None):
+    """out = (float(x) - mean) * rdisp, mean/rdisp broadcast per sample."""
+    if out is None:
+        out = torch.empty(x.shape, dtype=out_dtype or torch.float32,
+                          device=x.device)
+    sample = mean.numel()
+    if _gpu(x):
+        _lib_call("hvk_mean_disp_normalize", _p(x), DT[x.dtype], _p(mean),
+                  _p(rdisp), _p(out), DT[out.dtype], x.numel(), sample, _s(x))
+        return out
+    v = (x.float().reshape(-1, sample) - mean.reshape(1, -1).float()) * \
+        rdisp.reshape(1, -1).float()
+    out.copy_(v.reshape(out.shape).to(out.dtype))
+    return out

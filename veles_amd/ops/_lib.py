@@ -1,0 +1,96 @@
+"""ctypes binding of the in-tree HIP kernel library ``libhvk.so``.
+
+The kernels take raw device pointers and the current HIP stream, so they are
+stream-ordered with PyTorch's own work and capture into HIP graphs.  On a GPU
+box the library is REQUIRED: ``require_library()`` raises instead of silently
+falling back to PyTorch (the CPU path is only the numerics reference).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from veles_amd.error import KernelLibraryMissing
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HVK_LIBRARY", os.path.join(_HERE, "libhvk.so"))
+
+_lib = None
+_lock = threading.Lock()
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_longlong
+F = ctypes.c_float
+U = ctypes.c_uint
+
+_SIGS = {
+    "hvk_gemm": [I, I, I, I, I, P, I, P, I, P, I, I, I, F, F, P, I, I, P, I, I,
+                 I, P],
+    "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
+    "hvk_conv_dgrad": [P, P, P] + [I] * 14 + [P, I, P],
+    "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P],
+    "hvk_fill_minibatch": [P, I, P, I, I, I, L, P, P, P, I, P, P, P, P],
+    "hvk_mean_disp_normalize": [P, I, P, P, P, I, L, L, P],
+    "hvk_softmax_ce": [P, I, I, I, P, F, P, I, P, P, P, P, P],
+    "hvk_mse": [P, I, P, I, I, I, F, P, I, P, P, I, P],
+    "hvk_sgd": [P, P, P, P, P, I, L, F, P],
+    "hvk_col_sum": [P, I, I, I, P, F, P],
+    "hvk_row_sum": [P, I, I, I, P, F, P],
+    "hvk_act_fwd": [P, I, P, I, L, I, P],
+    "hvk_act_bwd": [P, I, P, I, P, I, L, I, P],
+    "hvk_dropout": [P, I, P, I, L, U, F, P, P],
+    "hvk_xorshift1024star": [P, I, I, P, P],
+    "hvk_xorshift128plus": [P, I, P, P],
+    "hvk_u64_to_uniform": [P, P, L, F, F, P],
+    "hvk_join": [P, P, I, I, P, I, P],
+    "hvk_cast": [P, I, P, I, L, F, P],
+    "hvk_pool_fwd": [P, P, P] + [I] * 13 + [P],
+    "hvk_pool_bwd": [P, P, P] + [I] * 13 + [P, I, P],
+    "hvk_lrn_fwd": [P, P, L, I, I, F, F, F, P],
+    "hvk_lrn_bwd": [P, P, P, L, I, I, F, F, F, P, I, P],
+}
+_OPTIONAL = {}
+
+
+def _load():
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            return None
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, sig in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                raise KernelLibraryMissing("%s lacks %s - rebuild with python "
+                                           "-m veles_amd.ops.build" %
+                                           (LIB_PATH, name))
+            fn.argtypes = sig
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def available():
+    return _load() is not None
+
+
+def require_library():
+    lib = _load()
+    if lib is None:
+        raise KernelLibraryMissing(
+            "HIP kernel library %s is missing; build it with `python -m "
+            "veles_amd.ops.build` (gfx950)" % LIB_PATH)
+    return lib
+
+
+def lib():
+    return require_library()
+
+
+def check(rc, name):
+    if rc != 0:
+        raise RuntimeError("%s failed with HIP error %d" % (name, rc))
