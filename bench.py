@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Headline benchmark: AlexNet-ImageNet training throughput (samples/s for the
+whole node), bf16, synthetic data, random-init weights, synchronous data
+parallelism over RCCL (one process per MI355X).
+
+    python bench.py --gpus N --steps K --warmup W [--batch B]
+
+For N > 1 launch under torch.distributed.run (one rank per GPU; the driver
+does this).  Every timed step is a full training step through the veles_amd
+StandardWorkflow: device minibatch gather + normalisation, forward, softmax
+evaluator, decision, backward, bucketed gradient all-reduce, fused SGD.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_METRIC = ("samples/sec (whole node) AlexNet-ImageNet training at "
+                   "1/2/4/8 MI355X")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=512,
+                    help="per-GPU minibatch (weak scaling)")
+    ap.add_argument("--model", default="alexnet")
+    ap.add_argument("--steps-per-epoch", type=int, default=16)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--profile-json", default=None)
+    args = ap.parse_args()
+
+    import torch
+    from veles_amd.utils.config import root
+    root.common.disable.snapshotting = True
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    from veles_amd.models.zoo import MODELS
+    from veles_amd.parallel.dp import DataParallel
+    import veles_amd.loader  # noqa: F401 (registers loaders)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and args.gpus > 1:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d; launch with "
+              "torch.distributed.run" % (args.gpus, world), file=sys.stderr)
+    backend = "cpu" if args.cpu or not torch.cuda.is_available() else "hip"
+    dp = DataParallel(backend="gloo" if backend == "cpu" else "nccl")
+    if backend == "hip":
+        torch.cuda.set_device(dp.local_rank % torch.cuda.device_count())
+    device = Device(backend=backend)
+    layers_fn, dataset = MODELS[args.model]
+    global_batch = args.batch * dp.world_size
+    n_train = global_batch * args.steps_per_epoch
+    launcher = DummyLauncher()
+    launcher.dp_ = dp
+    wf = StandardWorkflow(
+        launcher, loader_name="synthetic_images",
+        loader_config={"dataset": dataset, "class_lengths": (0, 0, n_train),
+                       "minibatch_size": global_batch,
+                       "normalization_type": "mean_disp",
+                       "generate_on_device": backend == "hip"},
+        layers=layers_fn(), decision_config={"max_epochs": None,
+                                             "fail_iterations": None})
+    wf.initialize(device=device)
+
+    def sync():
+        if backend == "hip":
+            torch.cuda.synchronize()
+
+    wf.run_steps(args.warmup)
+    sync()
+    dp.barrier()
+    sync()
+    t0 = time.perf_counter()
+    wf.run_steps(args.steps)
+    sync()
+    dp.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    if dp.world_size > 1:
+        if backend == "hip":
+            t = t.cuda()
+        dp.all_reduce_max(t)
+    dt = float(t.cpu()[0])
+    value = args.steps * global_batch / dt
+    if dp.rank == 0:
+        base = None
+        try:
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                   "BASELINE.json")) as f:
+                base = json.load(f).get("published", {}).get("value")
+        except Exception:
+            base = None
+        out = {"metric": BASELINE_METRIC, "value": round(value, 2),
+               "unit": "samples/s", "n_gpus": dp.world_size,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt / args.steps * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": (value / base) if base else None,
+               "dtype": "bf16" if backend == "hip" else "fp32",
+               "data": "synthetic (uint8 227x227x3 images resident in HBM, "
+                       "random-init weights)",
+               "config": {"model": args.model, "global_batch": global_batch,
+                          "per_gpu_batch": args.batch, "seq_len": None,
+                          "parallelism": "dp%d" % dp.world_size,
+                          "image": "227x227x3", "grad_allreduce":
+                          "bucketed RCCL, overlapped with backward"}}
+        print(json.dumps(out), flush=True)
+        if args.profile_json:
+            with open(args.profile_json, "w") as f:
+                stats = [(u.name, t_, n) for u, t_, n in
+                         wf.get_unit_run_time_stats()]
+                json.dump({"result": out, "unit_stats": stats}, f, indent=1)
+    dp.barrier()
+    dp.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -71,6 +71,35 @@ __global__ void fill_minibatch_kernel(const void* src, int src_dt,
   }
 }
 
+// Row kernel for arbitrary sample sizes: blockIdx.y = row, threads sweep
+// the row (coalesced byte loads, no 64-bit division).
+__global__ void fill_minibatch_rows_kernel(const void* src, int src_dt,
+                                           const int* shuffled, int start,
+                                           int count, long long sample_size,
+                                           const float* mean,
+                                           const float* rdisp, void* dst,
+                                           int dst_dt, const int* labels,
+                                           int* labels_out, int* idx_out) {
+  const int i = blockIdx.y;
+  const int s = i < count ? shuffled[start + i] : -1;
+  const long long sbase = (long long)s * sample_size;
+  const long long dbase = (long long)i * sample_size;
+  for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       j < sample_size; j += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (s >= 0) {
+      v = ld_any(src, sbase + j, src_dt);
+      if (mean) v -= mean[j];
+      if (rdisp) v *= rdisp[j];
+    }
+    st_any(dst, dbase + j, dst_dt, v);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (labels_out) labels_out[i] = (s >= 0 && labels) ? labels[s] : -1;
+    if (idx_out) idx_out[i] = s;
+  }
+}
+
 // Vectorised special case: uint8 source, bf16 destination, sample_size % 16
 // == 0.  16 bytes in, 32 bytes out per lane.
 __global__ void fill_minibatch_u8_bf16_kernel(const uint8_t* src,
@@ -216,6 +245,48 @@ struct SgdSeg {
   long long begin, end;
   float lr, decay, l1, moment;
 };
+__global__ void sgd4_kernel(float4* w, float4* grad, float4* mom,
+                            uint2* w_lp, const SgdSeg* segs, int nseg,
+                            long long total4, float gscale, int zero_grad) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       i < total4; i += (long long)gridDim.x * blockDim.x) {
+    long long e = i * 4;
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (segs[mid].begin <= e) lo = mid; else hi = mid - 1;
+    }
+    const SgdSeg sg = segs[lo];
+    float4 wv = w[i], gv = grad[i];
+    float4 mv = mom ? mom[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float* wp = (float*)&wv;
+    float* gp = (float*)&gv;
+    float* mp = (float*)&mv;
+    bool in = e >= sg.begin && e < sg.end;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float wi = wp[q];
+      float g = gp[q] * gscale;
+      if (sg.decay != 0.f)
+        g += sg.decay * ((1.f - sg.l1) * wi +
+                         sg.l1 * (wi > 0.f ? 1.f : (wi < 0.f ? -1.f : 0.f)));
+      float v = -sg.lr * g + sg.moment * mp[q];
+      if (!in) v = 0.f;
+      mp[q] = in ? v : mp[q];
+      wp[q] = wi + v;
+    }
+    w[i] = wv;
+    if (mom) mom[i] = mv;
+    if (zero_grad) grad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (w_lp) {
+      uint2 o;
+      o.x = f2bf(wp[0]) | ((uint32_t)f2bf(wp[1]) << 16);
+      o.y = f2bf(wp[2]) | ((uint32_t)f2bf(wp[3]) << 16);
+      w_lp[i] = o;
+    }
+  }
+}
+
 __global__ void sgd_kernel(float* w, const float* grad, float* mom,
                            uint16_t* w_lp, const SgdSeg* segs, int nseg,
                            long long total, float gscale) {
@@ -256,6 +327,46 @@ __global__ void col_sum_kernel(const void* in, int dt, int R, int C, float* out,
   float s = 0.f;
   for (int r = r0; r < r1; ++r) s += ld_any(in, (long long)r * C + c, dt);
   atomicAdd(&out[c], s * scale);
+}
+
+// bf16 column sums, 8 columns (16 B) per thread.  A block sweeps a slab of
+// rows; threads with the same chunk are reduced through LDS, then one
+// atomic per column per block.
+__global__ void col_sum_bf16x8_kernel(const uint16_t* in, int R, int C,
+                                      float* out, int rows_per_block,
+                                      float scale) {
+  const int CH = C >> 3;                 // chunks per row (<= 256)
+  const int rpi = blockDim.x / CH;       // rows per sweep
+  const int t = threadIdx.x;
+  const int ch = t % CH, rr = t / CH;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(R, r0 + rows_per_block);
+  if (rr < rpi) {
+    for (int r = r0 + rr; r < r1; r += rpi) {
+      uint4 v = *(const uint4*)(in + (long long)r * C + ch * 8);
+      const uint16_t* h = (const uint16_t*)&v;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += bf2f(h[q]);
+    }
+  }
+  __shared__ float red[256 * 8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[t * 8 + q] = (rr < rpi) ? acc[q] : 0.f;
+  __syncthreads();
+  if (t < CH) {
+    float s[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = 0.f;
+    for (int k = 0; k < rpi; ++k) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += red[(k * CH + t) * 8 + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) atomicAdd(&out[t * 8 + q], s[q] * scale);
+  }
 }
 
 // out[r] = sum_c in[r][c] * scale  (one wave per row)
@@ -425,6 +536,13 @@ HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                        dim3(256), 0, s, (const uint8_t*)src, shuffled, start,
                        count, max_mb, sample_size, mean, rdisp, (uint16_t*)dst,
                        labels, labels_out, idx_out);
+  } else if (max_mb <= 65535) {
+    long long gx = (sample_size + 1023) / 1024;
+    if (gx > 1024) gx = 1024;
+    hipLaunchKernelGGL(fill_minibatch_rows_kernel, dim3((int)gx, max_mb),
+                       dim3(256), 0, s, src, src_dt, shuffled, start, count,
+                       sample_size, mean, rdisp, dst, dst_dt, labels,
+                       labels_out, idx_out);
   } else {
     long long total = (long long)max_mb * sample_size;
     hipLaunchKernelGGL(fill_minibatch_kernel, dim3(grid_for(total)), dim3(256), 0,
@@ -463,6 +581,18 @@ HVK_API int hvk_mse(const void* y, int y_dt, const void* t, int t_dt, int B,
   return (int)hipGetLastError();
 }
 
+HVK_API int hvk_sgd4(float* w, float* grad, float* mom, void* w_lp,
+                     const void* segs, int nseg, long long total, float gscale,
+                     int zero_grad, hipStream_t s) {
+  if (total % 4 || ((uintptr_t)w & 15) || ((uintptr_t)grad & 15) ||
+      ((uintptr_t)mom & 15) || ((uintptr_t)w_lp & 7))
+    return -1;
+  hipLaunchKernelGGL(sgd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, s,
+                     (float4*)w, (float4*)grad, (float4*)mom, (uint2*)w_lp,
+                     (const SgdSeg*)segs, nseg, total / 4, gscale, zero_grad);
+  return (int)hipGetLastError();
+}
+
 HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
                     const void* segs, int nseg, long long total, float gscale,
                     hipStream_t s) {
@@ -474,6 +604,16 @@ HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
 
 HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
                         float scale, hipStream_t s) {
+  if (dt == DT_BF16 && C % 8 == 0 && C / 8 <= 256 &&
+      ((uintptr_t)in & 15) == 0) {
+    // ~2048 blocks over the rows
+    int rpb = (R + 2047) / 2048;
+    if (rpb < 64) rpb = 64;
+    int blocks = (R + rpb - 1) / rpb;
+    hipLaunchKernelGGL(col_sum_bf16x8_kernel, dim3(blocks), dim3(256), 0, s,
+                       (const uint16_t*)in, R, C, out, rpb, scale);
+    return (int)hipGetLastError();
+  }
   int rpb = 256;
   // aim for >= 1024 blocks in total
   int cb = (C + 255) / 256;

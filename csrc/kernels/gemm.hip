@@ -303,10 +303,13 @@ struct Epi {
 
 __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
-template <class LA, bool AK, class LB, bool BKM>
+template <class LA, bool AK, class LB, bool BKM, int BN_>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
             int tiles_n) {
+  constexpr int NB = BN_ / 32;          // B chunks per thread / MFMA n-tiles
+  constexpr int CPR = BN_ / 8;          // MN-major B: chunks per k-row
+  constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
   __shared__ __attribute__((aligned(16))) uint16_t smem[4 * TILE];
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
@@ -320,7 +323,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   if (kbeg >= kend) return;
   la.group(gi);
   lb.group(gi);
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BM, n0 = tn * BN_;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
@@ -334,19 +337,22 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
   if constexpr (BKM) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cb[i] = lb.row_ctx(n0 + (t >> 3) + 32 * i);
+    for (int i = 0; i < NB; ++i) cb[i] = lb.row_ctx(n0 + (t >> 3) + 32 * i);
   } else {
-    cb[0] = lb.col_ctx(n0 + (t & 15) * 8);
+    cb[0] = lb.col_ctx(n0 + (t % CPR) * 8);
   }
 
-  uint4 ra[4], rb[4];
+  uint4 ra[4], rb[NB];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if constexpr (AK) ra[i] = la.load(ca[i], k0 + (t & 7) * 8);
       else ra[i] = la.load(ca[0], k0 + (t >> 4) + 16 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       if constexpr (BKM) rb[i] = lb.load(cb[i], k0 + (t & 7) * 8);
-      else rb[i] = lb.load(cb[0], k0 + (t >> 4) + 16 * i);
+      else rb[i] = lb.load(cb[0], k0 + t / CPR + RPS * i);
     }
   };
   auto sstore = [&](uint16_t* sA, uint16_t* sB) {
@@ -359,21 +365,24 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         int k = (t >> 4) + 16 * i, c = t & 15;
         *(uint4*)(sA + k * 128 + (((c >> 1) ^ hk(k)) << 4) + ((c & 1) << 3)) = ra[i];
       }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
       if constexpr (BKM) {
         int row = (t >> 3) + 32 * i, c = t & 7;
         *(uint4*)(sB + row * 64 + ((c ^ (row & 7)) << 3)) = rb[i];
       } else {
-        int k = (t >> 4) + 16 * i, c = t & 15;
+        int k = t / CPR + RPS * i, c = t % CPR;
         *(uint4*)(sB + k * 128 + (((c >> 1) ^ hk(k)) << 4) + ((c & 1) << 3)) = rb[i];
       }
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][NB];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
   const int trq = fr >> 2, trp = fr & 3;
@@ -407,18 +416,21 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     const uint16_t* sB = smem + (2 + cur) * TILE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfv[4];
+      bf16x8 af[4], bfv[NB];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (AK) af[i] = frag_k(sA, wm * 64 + i * 16, ks);
         else af[i] = frag_mn(sA, wm * 64 + i * 16, ks);
-        if constexpr (BKM) bfv[i] = frag_k(sB, wn * 64 + i * 16, ks);
-        else bfv[i] = frag_mn(sB, wn * 64 + i * 16, ks);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        if constexpr (BKM) bfv[i] = frag_k(sB, wn * (BN_ / 2) + i * 16, ks);
+        else bfv[i] = frag_mn(sB, wn * (BN_ / 2) + i * 16, ks);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
                                                               acc[i][j], 0, 0, 0);
     }
@@ -430,25 +442,38 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NB; ++j) {
       int mb = m0 + wm * 64 + i * 16 + fq * 4;
-      int n = n0 + wn * 64 + j * 16 + fr;
+      int n = n0 + wn * (BN_ / 2) + j * 16 + fr;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) epi.store(gi, mb + rr, n, acc[i][j][rr]);
     }
 }
 
+// Tile width: 64 when it pads N less than 128 does (N = 48, 96->?, 192).
+inline bool use_bn64(int N) {
+  int w128 = (N + 127) / 128 * 128 - N;
+  int w64 = (N + 63) / 64 * 64 - N;
+  return w64 < w128;
+}
+
 template <class LA, bool AK, class LB, bool BKM>
 hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                   int K, int splits, int groups, hipStream_t s) {
-  int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const bool n64 = use_bn64(N);
+  const int bn = n64 ? 64 : 128;
+  int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
   if (splits < 1) splits = 1;
   int k_split = (K + splits - 1) / splits;
   k_split = (k_split + BK - 1) / BK * BK;
   splits = (K + k_split - 1) / k_split;
   dim3 grid(tiles_m * tiles_n, splits, groups);
-  hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM>), grid, dim3(NTHR), 0, s,
-                     la, lb, epi, M, N, K, k_split, tiles_n);
+  if (n64)
+    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64>), grid, dim3(NTHR), 0,
+                       s, la, lb, epi, M, N, K, k_split, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128>), grid, dim3(NTHR), 0,
+                       s, la, lb, epi, M, N, K, k_split, tiles_n);
   return hipGetLastError();
 }
 
@@ -479,7 +504,56 @@ Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
   return e;
 }
 
+// Explicit im2col for convolutions whose channel count is not a multiple of
+// 8 (AlexNet conv1, C = 3): col[m][k] with k = (kh*KW + kw)*C + c padded to
+// Kp (multiple of 8) with zeros, so the GEMM reads 16-B vectors.  The same
+// matrix feeds the forward GEMM and the weight-gradient GEMM.
+__global__ void im2col_kernel(const uint16_t* x, uint16_t* col, ConvGeom g,
+                              int M, int K, int Kp) {
+  const int KC = Kp >> 3;  // 8-element chunks per row
+  const long long total = (long long)M * KC;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       e < total; e += (long long)gridDim.x * blockDim.x) {
+    uint32_t m = (uint32_t)(e / KC);
+    int kc = (int)(e - (long long)m * KC);
+    uint32_t n, rem, oh, ow;
+    fdivmod(m, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    int ih0 = oh * g.sy - g.pt, iw0 = ow * g.sx - g.pl;
+    const uint16_t* xb = x + (long long)n * g.H * g.W * g.C;
+    uint16_t o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int k = kc * 8 + j;
+      o[j] = 0;
+      if (k < K) {
+        uint32_t t, ch, kh, kw;
+        fdivmod(k, g.fCg, t, ch);
+        fdivmod(t, g.fKW, kh, kw);
+        int ih = ih0 + (int)kh, iw = iw0 + (int)kw;
+        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+          o[j] = xb[(ih * g.W + iw) * g.C + ch];
+      }
+    }
+    *(uint4*)(col + (long long)m * Kp + kc * 8) = *(uint4*)o;
+  }
+}
+
 }  // namespace
+
+// col[M][Kp] = im2col(X) for a single-group conv (Kp = round_up(KH*KW*C, 8))
+HVK_API int hvk_im2col(const void* X, void* col, int N, int H, int W, int C,
+                       int KH, int KW, int sy, int sx, int pt, int pl, int OH,
+                       int OW, int Kp, hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, C, KH, KW, sy, sx, pt, pl, OH, OW, 1);
+  int M = N * OH * OW, K = KH * KW * C;
+  long long total = (long long)M * (Kp / 8);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(im2col_kernel, dim3((int)blocks), dim3(256), 0, s,
+                     (const uint16_t*)X, (uint16_t*)col, g, M, K, Kp);
+  return (int)hipGetLastError();
+}
 
 // C[M][N] = alpha*op(A)*op(B) + beta*C (+bias, act, aux-derivative mask)
 // transA=0: A is [M][K] (lda); transA=1: A is [K][M].

@@ -14,7 +14,7 @@ using namespace hvk;
 namespace {
 inline int grid_for(long long n, int per_block = 256) {
   long long g = (n + per_block - 1) / per_block;
-  if (g > 4096) g = 4096;
+  if (g > 16384) g = 16384;
   return g < 1 ? 1 : (int)g;
 }
 
@@ -27,15 +27,15 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
                                 int ky, int kx, int sy, int sx, int pt, int pl,
                                 int mode) {
   const int CV = C / VEC;
-  long long total = (long long)N * OH * OW * CV;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    int cv = (int)(e % CV);
-    long long pix = e / CV;
-    int ow = (int)(pix % OW);
-    long long t = pix / OW;
-    int oh = (int)(t % OH);
-    int n = (int)(t / OH);
+  const int total = N * OH * OW * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    int pix = e / CV;
+    int cv = e - pix * CV;
+    int t = pix / OW;
+    int ow = pix - t * OW;
+    int n = t / OH;
+    int oh = t - n * OH;
     int h0 = oh * sy - pt, w0 = ow * sx - pl;
     int h1 = min(h0 + ky, H), w1 = min(w0 + kx, W);
     h0 = max(h0, 0);
@@ -46,7 +46,7 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
     for (int q = 0; q < VEC; ++q) { best[q] = -INFINITY; sum[q] = 0.f; bidx[q] = -1; }
     for (int h = h0; h < h1; ++h)
       for (int w = w0; w < w1; ++w) {
-        long long off = (((long long)n * H + h) * W + w) * C + cv * VEC;
+        int off = ((n * H + h) * W + w) * C + cv * VEC;
         uint16_t v[VEC];
         if (VEC == 8) *(uint4*)v = *(const uint4*)(x + off);
         else v[0] = x[off];
@@ -58,7 +58,7 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
           } else {
             float key = mode == POOL_MAXABS ? fabsf(f) : f;
             float bk = mode == POOL_MAXABS ? fabsf(best[q]) : best[q];
-            if (bidx[q] < 0 || key > bk) { best[q] = f; bidx[q] = (int)(off + q); }
+            if (bidx[q] < 0 || key > bk) { best[q] = f; bidx[q] = off + q; }
           }
         }
       }
@@ -67,7 +67,7 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
 #pragma unroll
     for (int q = 0; q < VEC; ++q)
       o[q] = f2bf(mode == POOL_AVG ? sum[q] / (float)max(cnt, 1) : best[q]);
-    long long yo = pix * C + cv * VEC;
+    int yo = pix * C + cv * VEC;
     if (VEC == 8) *(uint4*)(y + yo) = *(uint4*)o;
     else y[yo] = o[0];
     if (argmax && mode != POOL_AVG) {
@@ -85,16 +85,16 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
                                 int pt, int pl, int mode, const uint16_t* aux,
                                 int aux_act) {
   const int CV = C / VEC;
-  long long total = (long long)N * H * W * CV;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    int cv = (int)(e % CV);
-    long long pix = e / CV;
-    int w = (int)(pix % W);
-    long long t = pix / W;
-    int h = (int)(t % H);
-    int n = (int)(t / H);
-    long long xoff = pix * C + cv * VEC;
+  const int total = N * H * W * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    int pix = e / CV;
+    int cv = e - pix * CV;
+    int t = pix / W;
+    int w = pix - t * W;
+    int n = t / H;
+    int h = t - n * H;
+    int xoff = pix * C + cv * VEC;
     // windows oh with oh*sy - pt <= h < oh*sy - pt + ky
     int hp = h + pt, wp = w + pl;
     int oh0 = hp - ky + 1 <= 0 ? 0 : (hp - ky + sy) / sy;
@@ -106,7 +106,7 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
     for (int q = 0; q < VEC; ++q) acc[q] = 0.f;
     for (int oh = oh0; oh <= oh1; ++oh)
       for (int ow = ow0; ow <= ow1; ++ow) {
-        long long yo = (((long long)n * OH + oh) * OW + ow) * C + cv * VEC;
+        int yo = ((n * OH + oh) * OW + ow) * C + cv * VEC;
         uint16_t g[VEC];
         if (VEC == 8) *(uint4*)g = *(const uint4*)(dy + yo);
         else g[0] = dy[yo];
@@ -119,7 +119,7 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
         } else {
 #pragma unroll
           for (int q = 0; q < VEC; ++q)
-            if (argmax[yo + q] == (int)(xoff + q)) acc[q] += bf2f(g[q]);
+            if (argmax[yo + q] == xoff + q) acc[q] += bf2f(g[q]);
         }
       }
     uint16_t o[VEC];
@@ -178,8 +178,10 @@ __global__ void lrn_bwd_kernel(const uint16_t* x, const uint16_t* dy,
     __builtin_amdgcn_wave_barrier();
     // t_c = dy_c * x_c * s_c^(-beta-1); keep s_c^-beta * dy_c in registers
     float keep[LRN_MAXC / 64];
-    int idx = 0;
-    for (int c = lane; c < C; c += 64, ++idx) {
+#pragma unroll
+    for (int idx = 0; idx < LRN_MAXC / 64; ++idx) {
+      int c = lane + idx * 64;
+      if (c >= C) break;
       float s = 0.f;
       int c0 = max(0, c - half), c1 = min(C - 1, c + half);
       for (int j = c0; j <= c1; ++j) s += xs[j] * xs[j];
@@ -190,8 +192,10 @@ __global__ void lrn_bwd_kernel(const uint16_t* x, const uint16_t* dy,
       keep[idx] = g * sb;
     }
     __builtin_amdgcn_wave_barrier();
-    idx = 0;
-    for (int c = lane; c < C; c += 64, ++idx) {
+#pragma unroll
+    for (int idx = 0; idx < LRN_MAXC / 64; ++idx) {
+      int c = lane + idx * 64;
+      if (c >= C) break;
       float acc = 0.f;
       int c0 = max(0, c - half), c1 = min(C - 1, c + half);
       for (int j = c0; j <= c1; ++j) acc += ts[j];
@@ -200,6 +204,99 @@ __global__ void lrn_bwd_kernel(const uint16_t* x, const uint16_t* dy,
       dx[p * C + c] = f2bf(v);
     }
     __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Vectorised LRN (C % 8 == 0, n/2 <= 4): a thread owns 8 channels of one
+// pixel and reads the neighbouring 8-channel chunks for the window halo;
+// all arrays are compile-time indexed (registers, no scratch).
+__device__ __forceinline__ void load8(const uint16_t* p, float* d) {
+  uint4 v = *(const uint4*)p;
+  const uint16_t* h = (const uint16_t*)&v;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) d[q] = bf2f(h[q]);
+}
+__device__ __forceinline__ void load24(const uint16_t* row, int c0, int C,
+                                       float* d) {
+#pragma unroll
+  for (int q = 0; q < 24; ++q) d[q] = 0.f;
+  if (c0 >= 8) load8(row + c0 - 8, d);
+  load8(row + c0, d + 8);
+  if (c0 + 8 < C) load8(row + c0 + 8, d + 16);
+}
+__global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
+                                   int C, int half, float alpha, float beta,
+                                   float k) {
+  const int CV = C >> 3;
+  const int total = P * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    int p = e / CV;
+    int c0 = (e - p * CV) << 3;
+    const uint16_t* row = x + (long long)p * C;
+    float v[24];
+    load24(row, c0, C, v);
+    uint16_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = -4; d <= 4; ++d) {
+        float t = v[8 + q + d];
+        s += (d >= -half && d <= half) ? t * t : 0.f;
+      }
+      s = k + alpha * s;
+      o[q] = f2bf(v[8 + q] * exp2f(-beta * __log2f(s)));
+    }
+    *(uint4*)(y + (long long)p * C + c0) = *(uint4*)o;
+  }
+}
+__global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
+                                   uint16_t* dx, int P, int C, int half,
+                                   float alpha, float beta, float k,
+                                   const uint16_t* aux, int aux_act) {
+  const int CV = C >> 3;
+  const int total = P * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    int p = e / CV;
+    int c0 = (e - p * CV) << 3;
+    long long base = (long long)p * C;
+    float xv[24], gv[24];
+    load24(x + base, c0, C, xv);
+    load24(dy + base, c0, C, gv);
+    // t_j = dy_j x_j s_j^(-beta-1) for j in [c0-4, c0+12) (16 values)
+    float tj[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = -4; d <= 4; ++d) {
+        int idx = 4 + j + d;
+        float t = (idx >= 0 && idx < 24) ? xv[idx] : 0.f;
+        s += (d >= -half && d <= half) ? t * t : 0.f;
+      }
+      s = k + alpha * s;
+      float sb = exp2f(-beta * __log2f(s));
+      tj[j] = gv[4 + j] * xv[4 + j] * sb / s;
+      // keep s^-beta of the owned channels in gv's free slots? recompute
+      // below instead (cheap)
+      if (j >= 4 && j < 12) xv[(j - 4) + 0] = sb;  // xv[0..7] unused now
+    }
+    uint16_t o[8];
+    float a[8];
+    if (aux) load8(aux + base + c0, a);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = -4; d <= 4; ++d)
+        acc += (d >= -half && d <= half) ? tj[4 + q + d] : 0.f;
+      float v = gv[8 + q] * xv[q] - 2.f * alpha * beta * xv[8 + q] * acc;
+      if (aux) v *= act_bwd(a[q], aux_act);
+      o[q] = f2bf(v);
+    }
+    *(uint4*)(dx + base + c0) = *(uint4*)o;
   }
 }
 }  // namespace
@@ -244,6 +341,14 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
 
 HVK_API int hvk_lrn_fwd(const void* x, void* y, long long P, int C, int n,
                         float alpha, float beta, float k, hipStream_t s) {
+  if (C % 8 == 0 && n / 2 <= 4 && P * C < (1ll << 31) &&
+      ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    long long total = P * (C / 8);
+    hipLaunchKernelGGL(lrn_fwd_vec_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       s, (const uint16_t*)x, (uint16_t*)y, (int)P, C, n / 2,
+                       alpha, beta, k);
+    return (int)hipGetLastError();
+  }
   if (C > 1024) return -1;
   hipLaunchKernelGGL(lrn_fwd_kernel, dim3(grid_for(P, 4)), dim3(256), 0, s,
                      (const uint16_t*)x, (uint16_t*)y, P, C, n, alpha, beta, k);
@@ -253,6 +358,16 @@ HVK_API int hvk_lrn_fwd(const void* x, void* y, long long P, int C, int n,
 HVK_API int hvk_lrn_bwd(const void* x, const void* dy, void* dx, long long P,
                         int C, int n, float alpha, float beta, float k,
                         const void* aux, int aux_act, hipStream_t s) {
+  if (C % 8 == 0 && n / 2 <= 4 && P * C < (1ll << 31) &&
+      ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 &&
+      ((uintptr_t)dx & 15) == 0 && ((uintptr_t)aux & 15) == 0) {
+    long long total = P * (C / 8);
+    hipLaunchKernelGGL(lrn_bwd_vec_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       s, (const uint16_t*)x, (const uint16_t*)dy,
+                       (uint16_t*)dx, (int)P, C, n / 2, alpha, beta, k,
+                       (const uint16_t*)aux, aux_act);
+    return (int)hipGetLastError();
+  }
   if (C > 1024) return -1;
   hipLaunchKernelGGL(lrn_bwd_kernel, dim3(grid_for(P, 4)), dim3(256), 0, s,
                      (const uint16_t*)x, (const uint16_t*)dy, (uint16_t*)dx, P,

@@ -240,3 +240,42 @@ def test_join_and_cast():
     close(ops.join([a.to(DEV), b.to(DEV)]), ops.join([a, b]), 0)
     x = torch.randn(1000)
     close(ops.cast(x.to(DEV), BF), ops.cast(x, BF), 0)
+
+
+def test_conv_im2col_path_fwd_and_wgrad():
+    N, H, W, C, OC, k, s = 2, 35, 35, 3, 96, 11, 4
+    x = rnd(N, H, W, C)
+    w = rnd(OC, k, k, C, seed=1, scale=0.1)
+    b = torch.randn(OC)
+    ws = {}
+    ref = ops.conv_fwd(x, w, b, (s, s), (0, 0, 0, 0), 1, 3)
+    got = ops.conv_fwd(x.to(DEV), w.to(DEV), b.to(DEV), (s, s), (0, 0, 0, 0),
+                       1, 3, col_out=ws)
+    close(got, ref, 1e-2)
+    assert "col" in ws
+    OH, OW = ops.conv_out_size(H, W, k, k, (s, s), (0, 0, 0, 0))
+    dy = rnd(N, OH, OW, OC, seed=2)
+    dref = torch.zeros(OC, k, k, C)
+    ops.conv_wgrad(x, dy, dref, (s, s), (0, 0, 0, 0), 1)
+    dgot = torch.zeros(OC, k, k, C, device=DEV)
+    ops.conv_wgrad(x.to(DEV), dy.to(DEV), dgot, (s, s), (0, 0, 0, 0), 1,
+                   col=ws["col"])
+    close(dgot, dref, 1e-2)
+
+
+@pytest.mark.parametrize("C", [96, 256, 8])
+def test_col_sum_vectorised(C):
+    x = rnd(3001, C)
+    close(ops.col_sum(x.to(DEV)), ops.col_sum(x), 1e-4)
+
+
+def test_fill_minibatch_odd_sample():
+    src = torch.randint(0, 256, (20, 227 * 3), dtype=torch.uint8)
+    sh = torch.randperm(20).to(torch.int32)
+    mean, rd = torch.rand(681) * 100, torch.rand(681) * 0.01
+    d = torch.empty(8, 681, dtype=BF)
+    ops.fill_minibatch(src, sh, 2, 6, d, mean=mean, rdisp=rd)
+    dg = torch.empty(8, 681, dtype=BF, device=DEV)
+    ops.fill_minibatch(src.to(DEV), sh.to(DEV), 2, 6, dg, mean=mean.to(DEV),
+                       rdisp=rd.to(DEV))
+    close(dg, d, 1e-2)

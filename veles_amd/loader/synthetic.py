@@ -37,7 +37,7 @@ class SyntheticImageLoader(FullBatchLoader):
         super().__init__(workflow, **kwargs)
         ds = kwargs.get("dataset", "mnist")
         shape, ncls = SHAPES.get(ds, ((28, 28, 1), 10))
-        self.sample_shape_ = tuple(kwargs.get("sample_shape", shape))
+        self._sample_shape = tuple(kwargs.get("sample_shape", shape))
         self.n_classes = int(kwargs.get("n_classes", ncls))
         self.requested_lengths = list(kwargs.get(
             "class_lengths", (1000, 1000, 6000)))
@@ -47,13 +47,13 @@ class SyntheticImageLoader(FullBatchLoader):
 
     @property
     def sample_shape(self):
-        return self.sample_shape_
+        return self._sample_shape
 
     def _want_device(self):
         dev = self.device
         if self.generate_on_device == "auto":
             total = sum(self.requested_lengths) * int(numpy.prod(
-                self.sample_shape_))
+                self._sample_shape))
             return dev is not None and getattr(dev, "is_gpu", False) and \
                 total > (64 << 20)
         return bool(self.generate_on_device) and dev is not None and \
@@ -64,7 +64,7 @@ class SyntheticImageLoader(FullBatchLoader):
         self.class_lengths = [int(x) for x in self.requested_lengths]
         self._apply_validation_ratio()
         n = sum(self.class_lengths)
-        feat = int(numpy.prod(self.sample_shape_))
+        feat = int(numpy.prod(self._sample_shape))
         rs = numpy.random.RandomState(self.seed)
         labels = rs.randint(0, self.n_classes, n).astype(numpy.int32)
         protos = rs.randint(32, 224, (self.n_classes, feat)).astype(
@@ -74,7 +74,7 @@ class SyntheticImageLoader(FullBatchLoader):
             dev = self.device.torch_device
             g = torch.Generator(device=dev)
             g.manual_seed(self.seed)
-            data = torch.empty((n,) + self.sample_shape_, dtype=torch.uint8,
+            data = torch.empty((n,) + self._sample_shape, dtype=torch.uint8,
                                device=dev)
             tp = torch.from_numpy(protos).to(dev)
             tl = torch.from_numpy(labels).to(dev).long()
@@ -96,13 +96,12 @@ class SyntheticImageLoader(FullBatchLoader):
                     (j - i, feat)).astype(numpy.float32) * self.noise
                 numpy.clip(v, 0, 255, out=v)
                 out[i:j] = v.astype(numpy.uint8)
-            self.original_data.reset(out.reshape((n,) + self.sample_shape_))
+            self.original_data.reset(out.reshape((n,) + self._sample_shape))
         self.labels_mapping = {i: i for i in range(self.n_classes)}
         self.reversed_labels_mapping = list(range(self.n_classes))
 
     def analyze_dataset(self):
-        if self.original_data.mem is not None and \
-                self.original_data.devmem is not None and \
+        if self.original_data.devmem is not None and \
                 self.original_data.devmem.is_cuda and \
                 self.normalization_type != "none":
             # device-generated set: analyse a host copy of a TRAIN sample
@@ -114,7 +113,7 @@ class SyntheticImageLoader(FullBatchLoader):
                 numpy.float32)
             self.normalizer.analyze(sub)
             aff = self.normalizer.affine()
-            feat = int(numpy.prod(self.sample_shape_))
+            feat = int(numpy.prod(self._sample_shape))
             if aff is None:
                 raise ValueError("device-resident synthetic data needs an "
                                  "affine normalizer")
@@ -133,7 +132,7 @@ class SyntheticMSELoader(FullBatchLoaderMSE):
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
-        self.sample_shape_ = tuple(kwargs.get("sample_shape", (28, 28, 1)))
+        self._sample_shape = tuple(kwargs.get("sample_shape", (28, 28, 1)))
         self.target_shape = kwargs.get("target_shape")
         self.requested_lengths = list(kwargs.get("class_lengths",
                                                  (200, 200, 1000)))
@@ -141,12 +140,12 @@ class SyntheticMSELoader(FullBatchLoaderMSE):
 
     @property
     def sample_shape(self):
-        return self.sample_shape_
+        return self._sample_shape
 
     def load_data(self):
         self.class_lengths = [int(x) for x in self.requested_lengths]
         n = sum(self.class_lengths)
-        feat = int(numpy.prod(self.sample_shape_))
+        feat = int(numpy.prod(self._sample_shape))
         rs = numpy.random.RandomState(self.seed)
         x = rs.uniform(-1, 1, (n, feat)).astype(numpy.float32)
         if self.target_shape:
@@ -155,7 +154,7 @@ class SyntheticMSELoader(FullBatchLoaderMSE):
                 numpy.sqrt(feat)
             t = numpy.tanh(x @ m).reshape((n,) + tuple(self.target_shape))
         else:
-            t = x.copy().reshape((n,) + self.sample_shape_)
-        self.original_data.reset(x.reshape((n,) + self.sample_shape_))
+            t = x.copy().reshape((n,) + self._sample_shape)
+        self.original_data.reset(x.reshape((n,) + self._sample_shape))
         self.original_targets.reset(t)
         self.original_labels = []

@@ -95,6 +95,11 @@ class Array(object):
 
     # -- pickling -----------------------------------------------------------
     def __getstate__(self):
+        if self.shallow_pickle and self._devmem is not None:
+            return {"shallow_pickle": True, "device_dtype": None,
+                    "shape": tuple(self._devmem.shape),
+                    "dtype": numpy.dtype(to_numpy_dtype(
+                        self._devmem.dtype)).str}
         self.map_read()
         st = {"shallow_pickle": self.shallow_pickle,
               "device_dtype": None if self._device_dtype is None
@@ -137,9 +142,10 @@ class Array(object):
             self._devmem = tensor
             if tensor is not None and tensor.device.type == "cuda":
                 self._state = 0
-                if self._mem is None or self._mem.shape != tuple(tensor.shape):
-                    self._mem = numpy.zeros(tuple(tensor.shape),
-                                            to_numpy_dtype(tensor.dtype))
+                # host mirror allocated lazily by the first map_*()
+                if self._mem is not None and \
+                        self._mem.shape != tuple(tensor.shape):
+                    self._mem = None
             elif tensor is not None:
                 self._mem = tensor.numpy() if tensor.dtype in _NP_OK() \
                     else tensor.float().numpy()
@@ -154,10 +160,13 @@ class Array(object):
         return self._devmem is not None and self._devmem.device.type == "cuda"
 
     def __bool__(self):
+        if self._devmem is not None:
+            return self._devmem.numel() > 0
         return self._mem is not None and self._mem.size > 0
 
     def __len__(self):
-        return 0 if self._mem is None else len(self._mem)
+        sh = self.shape
+        return 0 if not sh else sh[0]
 
     @property
     def shape(self):
@@ -167,19 +176,30 @@ class Array(object):
 
     @property
     def dtype(self):
+        if self._mem is None and self._devmem is not None:
+            return numpy.dtype(to_numpy_dtype(self._devmem.dtype))
         return None if self._mem is None else self._mem.dtype
 
     @property
     def size(self):
+        if self._devmem is not None:
+            return self._devmem.numel()
         return 0 if self._mem is None else self._mem.size
 
     @property
     def nbytes(self):
+        if self._mem is None and self._devmem is not None:
+            return self._devmem.numel() * self._devmem.element_size()
         return 0 if self._mem is None else self._mem.nbytes
 
     @property
     def sample_size(self):
         return self.size // self.shape[0] if self.size else 0
+
+    def _ensure_host(self):
+        if self._mem is None and self._devmem is not None:
+            self._mem = numpy.zeros(tuple(self._devmem.shape),
+                                    to_numpy_dtype(self._devmem.dtype))
 
     @property
     def plain(self):
@@ -259,12 +279,14 @@ class Array(object):
 
     def map_read(self):
         with self._lock:
+            self._ensure_host()
             if self._state == 0 and self.on_gpu:
                 self._d2h()
                 self._state = 1
 
     def map_write(self):
         with self._lock:
+            self._ensure_host()
             if self._state == 0 and self.on_gpu:
                 self._d2h()
             if self.on_gpu:
@@ -272,6 +294,7 @@ class Array(object):
 
     def map_invalidate(self):
         with self._lock:
+            self._ensure_host()
             if self._state == 0 and self.on_gpu:
                 import torch
                 torch.cuda.current_stream(self._devmem.device).synchronize()

@@ -1,0 +1,116 @@
+"""Convolutional layers (Znicz ``conv*`` types; docs/OPS.md §Conv).
+
+NHWC input [B, H, W, C]; weights [n_kernels][ky][kx][C/grouping];
+``padding`` = (left, top, right, bottom), ``sliding`` = (x, y).  Forward is
+one implicit-GEMM MFMA kernel (``hvk_conv_fwd``: im2col gathered on the fly
+from NHWC, bias + activation in the epilogue, groups on grid z).
+"""
+from __future__ import annotations
+
+from veles_amd.models.nn_units import Forward
+from veles_amd import ops
+
+__all__ = ["Conv", "ConvTanh", "ConvRELU", "ConvStrictRELU", "ConvSigmoid",
+           "norm_padding", "norm_sliding"]
+
+
+def norm_padding(p):
+    if p is None:
+        return (0, 0, 0, 0)
+    if isinstance(p, int):
+        return (p, p, p, p)
+    p = tuple(p)
+    if len(p) == 2:
+        return (p[0], p[1], p[0], p[1])
+    return p
+
+
+def norm_sliding(s):
+    if s is None:
+        return (1, 1)
+    if isinstance(s, int):
+        return (s, s)
+    return tuple(s)
+
+
+class Conv(Forward):
+    __id__ = "bd4f8f3d-0a43-4a8e-b4d5-5b1b9d3a1c10"
+    MAPPING = "conv"
+    ACTIVATION = 0
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.n_kernels = int(kwargs["n_kernels"])
+        self.kx = int(kwargs["kx"])
+        self.ky = int(kwargs["ky"])
+        self.padding = norm_padding(kwargs.get("padding"))
+        self.sliding = norm_sliding(kwargs.get("sliding"))
+        self.grouping = int(kwargs.get("grouping", 1))
+        self.unsafe_padding = kwargs.get("unsafe_padding", False)
+
+    def initialize(self, device=None, **kwargs):
+        super().initialize(device=device, **kwargs)
+        shape = self.input.shape
+        if len(shape) == 3:
+            shape = tuple(shape) + (1,)
+        self.in_shape_ = shape
+        C = shape[3]
+        if C % self.grouping or self.n_kernels % self.grouping:
+            raise ValueError("%s: channels %d / kernels %d not divisible by "
+                             "grouping %d" % (self, C, self.n_kernels,
+                                              self.grouping))
+        cg = C // self.grouping
+        self.register_params((self.n_kernels, self.ky, self.kx, cg),
+                             self.ky * self.kx * cg)
+        OH, OW = self.output_hw(shape[1], shape[2])
+        self.alloc_output((shape[0], OH, OW, self.n_kernels))
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.col_ = None
+
+    def output_hw(self, H, W):
+        return ops.conv_out_size(H, W, self.ky, self.kx, self.sliding,
+                                 self.padding)
+
+    def run(self):
+        x = self.input.devmem
+        if x.dim() == 3:
+            x = x.unsqueeze(-1)
+        B, H, W, C = x.shape
+        OH, OW = self.output_hw(H, W)
+        y = self.alloc_output((B, OH, OW, self.n_kernels))
+        if x.dtype != self.weights_lp.dtype:
+            x = x.to(self.weights_lp.dtype)
+        ws = {}
+        ops.conv_fwd(x, self.weights_lp, self.bias_master, self.sliding,
+                     self.padding, self.grouping, self.activation, out=y,
+                     col_out=ws)
+        self.col_ = ws.get("col")
+
+    def package_export(self):
+        d = super().package_export()
+        d.update({"kx": self.kx, "ky": self.ky, "n_kernels": self.n_kernels,
+                  "padding": list(self.padding),
+                  "sliding": list(self.sliding), "grouping": self.grouping})
+        return d
+
+
+class ConvTanh(Conv):
+    MAPPING = "conv_tanh"
+    ACTIVATION = 1
+
+
+class ConvRELU(Conv):
+    MAPPING = "conv_relu"
+    ACTIVATION = 2
+
+
+class ConvStrictRELU(Conv):
+    MAPPING = "conv_str"
+    ACTIVATION = 3
+
+
+class ConvSigmoid(Conv):
+    MAPPING = "conv_sigmoid"
+    ACTIVATION = 4

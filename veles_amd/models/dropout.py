@@ -1,0 +1,82 @@
+"""Dropout (Znicz ``dropout``): inverted dropout with a counter-based mask
+(``hvk_dropout``).  The forward unit draws a fresh 32-bit seed per minibatch;
+the backward unit re-applies the same mask to err_output from that seed -
+no mask tensor is stored.  Identity when the workflow is testing or for
+non-TRAIN minibatches (``forward_mode``)."""
+from __future__ import annotations
+
+from veles_amd.accelerated_units import AcceleratedUnit
+from veles_amd.memory import Array
+from veles_amd.models.nn_units import GradientDescentBase
+from veles_amd.prng import random_generator
+from veles_amd import ops
+
+__all__ = ["DropoutForward", "DropoutBackward"]
+
+
+class DropoutForward(AcceleratedUnit):
+    MAPPING = "dropout"
+
+    def __init__(self, workflow, **kwargs):
+        kwargs.setdefault("view_group", "WORKER")
+        super().__init__(workflow, **kwargs)
+        self.dropout_ratio = float(kwargs.get("dropout_ratio", 0.5))
+        self.rand = kwargs.get("rand", random_generator.get())
+        self.output = Array(shallow_pickle=True)
+        self.seed = 0
+        self.forward_mode = False
+        self.demand("input")
+
+    @property
+    def activation(self):
+        return 0
+
+    def initialize(self, device=None, **kwargs):
+        super().initialize(device=device, **kwargs)
+        import torch
+        x = self.input.devmem
+        self.output.devmem = torch.zeros(
+            tuple(self.input.shape), dtype=x.dtype if x is not None else
+            self.compute_dtype, device=self.torch_device)
+
+    def run(self):
+        import torch
+        x = self.input.devmem
+        train = not self.forward_mode and not bool(
+            getattr(self.workflow, "testing", False))
+        mc = getattr(self, "minibatch_class", None)
+        if mc is not None and mc != 2:
+            train = False
+        if not train or self.dropout_ratio <= 0:
+            self.output.devmem = x
+            self.active_ = False
+            return
+        self.active_ = True
+        self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
+        y = self.output.devmem
+        if y is None or y is x or y.shape != x.shape or y.dtype != x.dtype:
+            self.output.devmem = y = torch.empty_like(x)
+        ops.dropout(x, self.dropout_ratio, self.seed, out=y)
+
+
+class DropoutBackward(GradientDescentBase):
+    MAPPING = "dropout"
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.demand("forward_unit")
+
+    def run(self):
+        fwd = self.forward_unit
+        err = self.err_output.devmem
+        if not getattr(fwd, "active_", True):
+            out = err
+        else:
+            ei = self.alloc_err_input(tuple(err.shape))
+            out = ops.dropout(err, fwd.dropout_ratio, fwd.seed, out=ei)
+        aux, aux_act = self.aux_tensor()
+        if aux is not None:
+            ei = self.alloc_err_input(tuple(err.shape))
+            ops.act_bwd(out, aux, aux_act, out=ei)
+        else:
+            self.err_input.devmem = out

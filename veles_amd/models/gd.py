@@ -1,0 +1,71 @@
+"""Backward units of the fully connected layers (Znicz ``gd.py`` family).
+
+grad_W[out][in] += err^T . x        (MFMA GEMM, TN layout, f32 accumulate)
+grad_b[out]     += colsum(err)      (hvk_col_sum)
+err_input       =  err . W  [* f'(below.output)]   (GEMM, NN layout, fused
+                                                    derivative epilogue)
+where err = err_output * f'(output) unless the unit above already fused it.
+"""
+from __future__ import annotations
+
+from veles_amd.models.nn_units import GradientDescentBase
+from veles_amd import ops
+
+__all__ = ["GradientDescent", "GDTanh", "GDRELU", "GDStrictRELU",
+           "GDSigmoid", "GDSoftmax"]
+
+
+class GradientDescent(GradientDescentBase):
+    MAPPING = "all2all"
+
+    def initialize(self, device=None, **kwargs):
+        super().initialize(device=device, **kwargs)
+        fwd = self.forward
+        if fwd is None:
+            raise AttributeError("%s: forward_unit is not set" % self)
+        self.attach_params(fwd)
+
+    def run(self):
+        fwd = self.forward
+        fwd.ensure_params()
+        err = self.err_output_effective()
+        B = err.shape[0]
+        e2 = err.reshape(B, -1)
+        x = self.input.devmem.reshape(B, -1)
+        if x.dtype != e2.dtype:
+            x = x.to(e2.dtype)
+        pw, pb = fwd._pw_, fwd._pb_
+        if not fwd.weights_transposed:
+            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=True)
+        else:
+            ops.gemm(x, e2, trans_a=True, out=pw.grad, accumulate=True)
+        if pb is not None:
+            ops.col_sum(e2, out=pb.grad, accumulate=True)
+        if self.need_err_input:
+            ei = self.alloc_err_input(self.input.devmem.shape)
+            aux, aux_act = self.aux_tensor()
+            ops.gemm(e2, fwd.weights_lp, trans_b=fwd.weights_transposed,
+                     out=ei.view(B, -1),
+                     aux=None if aux is None else aux.reshape(B, -1),
+                     aux_act=aux_act)
+        self.report_gradients()
+
+
+class GDTanh(GradientDescent):
+    MAPPING = "all2all_tanh"
+
+
+class GDRELU(GradientDescent):
+    MAPPING = "all2all_relu"
+
+
+class GDStrictRELU(GradientDescent):
+    MAPPING = "all2all_str"
+
+
+class GDSigmoid(GradientDescent):
+    MAPPING = "all2all_sigmoid"
+
+
+class GDSoftmax(GradientDescent):
+    MAPPING = "softmax"

@@ -1,0 +1,247 @@
+"""Flat parameter / gradient / momentum storage shared by all layers of a
+workflow on one device.
+
+Why flat (MI355X-first):
+* ONE fused multi-segment SGD kernel updates every layer per step
+  (``hvk_sgd``: reads grad, master, momentum; writes master, momentum and the
+  bf16 compute copy) instead of a launch per tensor;
+* gradient buckets for the data-parallel all-reduce are contiguous slices of
+  the flat fp32 gradient buffer: no pack/unpack copies before RCCL;
+* parameters are laid out in REVERSE registration (= reverse forward) order,
+  so backward fills the buffer front to back and bucket k can be reduced over
+  xGMI while the layers below it are still computing their gradients.
+
+Master weights are float32; the compute copy is the device compute dtype
+(bf16 on the MI355X, the master itself on the CPU).
+"""
+from __future__ import annotations
+
+import numpy
+
+__all__ = ["ParameterStore", "Param"]
+
+
+def _cover(segs, total):
+    """Extend segments so they tile [0, total) (gaps get lr = 0)."""
+    out = []
+    pos = 0
+    for b, e, lr, d, l1, m in sorted(segs):
+        if b > pos:
+            out.append((pos, b, 0.0, 0.0, 0.0, 0.0))
+        out.append((b, e, lr, d, l1, m))
+        pos = e
+    if pos < total:
+        out.append((pos, total, 0.0, 0.0, 0.0, 0.0))
+    return out
+
+
+class Param(object):
+    __slots__ = ("owner", "name", "shape", "host", "offset", "size", "master",
+                 "lp", "grad", "mom", "gd", "is_bias", "bucket", "host_mom")
+
+    def __init__(self, owner, name, host):
+        self.owner = owner
+        self.name = name
+        self.host = numpy.ascontiguousarray(host, dtype=numpy.float32)
+        self.shape = self.host.shape
+        self.size = self.host.size
+        self.offset = None
+        self.master = self.lp = self.grad = self.mom = None
+        self.gd = None
+        self.is_bias = name == "bias"
+        self.bucket = None
+        self.host_mom = None
+
+
+class ParameterStore(object):
+    def __init__(self, device, dp=None):
+        self.device = device
+        self.dp = dp
+        self.params = []
+        self.finalized = False
+        self._ready = set()
+        self._works = []
+        self._launched = set()
+        self.buckets = []
+        self._segs = None
+        self._seg_key = None
+        self.steps = 0
+        self.accumulate = 1
+        self._accum_count = 0
+
+    # -- registration -------------------------------------------------------
+    def register(self, owner, name, host):
+        if self.finalized:
+            # late registration (e.g. re-initialize): rebuild
+            self.finalized = False
+        p = Param(owner, name, host)
+        self.params = [q for q in self.params
+                       if not (q.owner is owner and q.name == name)]
+        self.params.append(p)
+        return p
+
+    def find(self, owner, name):
+        for p in self.params:
+            if p.owner is owner and p.name == name:
+                return p
+        return None
+
+    def attach_gd(self, param, gd):
+        param.gd = gd
+
+    # -- layout -------------------------------------------------------------
+    def finalize(self):
+        if self.finalized:
+            return
+        import torch
+        dev = self.device
+        tdev = dev.torch_device if dev is not None else torch.device("cpu")
+        gpu = dev is not None and getattr(dev, "is_gpu", False)
+        order = list(reversed(self.params))
+        off = 0
+        for p in order:
+            # keep every parameter 64-element (256 B) aligned for 16-B loads
+            off = (off + 63) // 64 * 64
+            p.offset = off
+            off += p.size
+        total = max(off, 1)
+        self.total = total
+        self.master = torch.zeros(total, dtype=torch.float32, device=tdev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=tdev)
+        self.mom = torch.zeros(total, dtype=torch.float32, device=tdev)
+        lp_dtype = dev.compute_dtype if gpu else torch.float32
+        self.lp = torch.zeros(total, dtype=lp_dtype, device=tdev) \
+            if lp_dtype != torch.float32 else None
+        for p in order:
+            sl = slice(p.offset, p.offset + p.size)
+            self.master[sl].copy_(torch.from_numpy(p.host.reshape(-1)))
+            p.master = self.master[sl].view(p.shape)
+            p.grad = self.grad[sl].view(p.shape)
+            p.mom = self.mom[sl].view(p.shape)
+            p.lp = (self.lp[sl].view(p.shape) if self.lp is not None
+                    else p.master)
+            if p.host_mom is not None and p.host_mom.size == p.size:
+                self.mom[sl].copy_(torch.from_numpy(numpy.ascontiguousarray(
+                    p.host_mom, numpy.float32).reshape(-1)))
+        if self.dp is not None and self.dp.world_size > 1:
+            self.dp.broadcast_(self.master)
+        if self.lp is not None:
+            self.lp.copy_(self.master)
+        self._build_buckets(order)
+        self.finalized = True
+        for p in order:
+            if hasattr(p.owner, "on_params_finalized"):
+                p.owner.on_params_finalized()
+
+    def _build_buckets(self, order):
+        from veles_amd.utils.config import root, get
+        mb = get(root.common.engine.dp.bucket_mb, 32)
+        cap = int(mb * (1 << 20) / 4)
+        self.buckets = []
+        cur = []
+        size = 0
+        for p in order:
+            cur.append(p)
+            size += p.size
+            if size >= cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        for i, b in enumerate(self.buckets):
+            for p in b:
+                p.bucket = i
+
+    def bucket_view(self, i):
+        b = self.buckets[i]
+        lo = b[0].offset
+        hi = b[-1].offset + b[-1].size
+        return self.grad[lo:hi]
+
+    # -- step ---------------------------------------------------------------
+    def grads_ready(self, params):
+        """Called by a GD unit once its gradients are enqueued."""
+        for p in params:
+            self._ready.add(id(p))
+        if self.dp is None or self.dp.world_size <= 1:
+            return
+        if self._accum_count + 1 < self.accumulate:
+            return
+        for i, b in enumerate(self.buckets):
+            if i in self._launched:
+                continue
+            if all(id(p) in self._ready for p in b):
+                self._launched.add(i)
+                self._works.append(self.dp.all_reduce_async(
+                    self.bucket_view(i)))
+
+    def all_ready(self):
+        return len(self._ready) >= len([p for p in self.params
+                                        if p.gd is not None])
+
+    def segments(self):
+        segs = []
+        for p in sorted(self.params, key=lambda q: q.offset):
+            gd = p.gd
+            if gd is None:
+                continue
+            lr, decay, l1, moment = gd.hyper(p.is_bias)
+            segs.append((p.offset, p.offset + p.size, lr, decay, l1, moment))
+        return segs
+
+    def _cached_segments(self):
+        key = tuple((id(p.gd), p.gd.hyper(p.is_bias)) for p in self.params
+                    if p.gd is not None)
+        if key != self._seg_key:
+            self._seg_key = key
+            self._segs = self.segments()
+            # cover alignment gaps so every float4 group has a segment
+            self._segs = _cover(self._segs, self.total)
+        return self._segs
+
+    def apply(self, gscale=1.0):
+        """Wait for the gradient all-reduces, then one fused SGD update."""
+        from veles_amd import ops
+        self._accum_count += 1
+        if self._accum_count < self.accumulate:
+            self._ready.clear()
+            return False
+        if self.dp is not None and self.dp.world_size > 1:
+            # buckets not launched yet (e.g. params without GD) go now
+            for i in range(len(self.buckets)):
+                if i not in self._launched:
+                    self._works.append(self.dp.all_reduce_async(
+                        self.bucket_view(i)))
+            for w in self._works:
+                w.wait()
+        segs = self._cached_segments()
+        if segs:
+            # the fused kernel also zeroes the gradient buffer
+            ops.sgd_update(self.master, self.grad, self.mom, segs,
+                           w_lp=self.lp, gscale=gscale / self.accumulate,
+                           zero_grad=True)
+        else:
+            self.grad.zero_()
+        self._works = []
+        self._launched = set()
+        self._ready.clear()
+        self._accum_count = 0
+        self.steps += 1
+        return True
+
+    def sync_host(self):
+        """Copy master weights back into each Param.host (for snapshots)."""
+        for p in self.params:
+            if p.master is not None:
+                p.host = p.master.detach().float().cpu().numpy().copy()
+
+    def state_dict(self):
+        return {"master": self.master.detach().cpu(),
+                "mom": self.mom.detach().cpu(), "steps": self.steps}
+
+    def load_state_dict(self, st):
+        self.master.copy_(st["master"])
+        self.mom.copy_(st["mom"])
+        if self.lp is not None:
+            self.lp.copy_(self.master)
+        self.steps = st.get("steps", 0)

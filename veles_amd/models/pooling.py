@@ -1,0 +1,248 @@
+"""Pooling layers and their backward units (Znicz ``pooling`` /
+``gd_pooling``; docs/OPS.md §Pooling).
+
+NHWC, window ``kx`` x ``ky``, ``sliding`` (x, y) (defaults to the window);
+windows start inside the input and the last one may be partial (ceil).
+max / avg / maxabs run as ``hvk_pool_fwd`` (8 channels per lane) with the
+argmax offset kept for the backward GATHER (``hvk_pool_bwd``, deterministic,
+no atomics).  Stochastic variants draw the window element with probability
+proportional to its (absolute) value during training and use the weighted
+average at test time; they are composed from device tensor ops.
+"""
+from __future__ import annotations
+
+import torch
+
+from veles_amd.accelerated_units import AcceleratedUnit
+from veles_amd.memory import Array
+from veles_amd.models.nn_units import GradientDescentBase
+from veles_amd.prng import random_generator
+from veles_amd import ops
+
+__all__ = ["Pooling", "MaxPooling", "AvgPooling", "MaxAbsPooling",
+           "StochasticPooling", "StochasticAbsPooling",
+           "StochasticPoolingDepooling", "StochasticAbsPoolingDepooling",
+           "GDPooling", "GDMaxPooling", "GDAvgPooling", "GDMaxAbsPooling",
+           "Depooling"]
+
+
+class Pooling(AcceleratedUnit):
+    hide_from_registry = True
+    MODE = "max"
+
+    def __init__(self, workflow, **kwargs):
+        kwargs.setdefault("view_group", "WORKER")
+        super().__init__(workflow, **kwargs)
+        self.kx = int(kwargs.get("kx", 2))
+        self.ky = int(kwargs.get("ky", 2))
+        s = kwargs.get("sliding", (self.kx, self.ky))
+        self.sliding = (s, s) if isinstance(s, int) else tuple(s)
+        self.output = Array(shallow_pickle=True)
+        self.input_offset = Array(shallow_pickle=True)
+        self.demand("input")
+
+    @property
+    def activation(self):
+        return 0
+
+    def _in(self):
+        x = self.input.devmem
+        return x.unsqueeze(-1) if x.dim() == 3 else x
+
+    def initialize(self, device=None, **kwargs):
+        super().initialize(device=device, **kwargs)
+        shape = tuple(self.input.shape)
+        if len(shape) == 3:
+            shape = shape + (1,)
+        B, H, W, C = shape
+        OH, OW = ops.pool_out_size(H, W, self.ky, self.kx, self.sliding[1],
+                                   self.sliding[0])
+        dt = self.input.devmem.dtype if self.input.devmem is not None \
+            else self.compute_dtype
+        self.output.devmem = torch.zeros(B, OH, OW, C, dtype=dt,
+                                         device=self.torch_device)
+        self.input_offset.devmem = torch.zeros(B, OH, OW, C,
+                                               dtype=torch.int32,
+                                               device=self.torch_device)
+
+    def run(self):
+        x = self._in()
+        B, H, W, C = x.shape
+        OH, OW = ops.pool_out_size(H, W, self.ky, self.kx, self.sliding[1],
+                                   self.sliding[0])
+        y = self.output.devmem
+        if y is None or tuple(y.shape) != (B, OH, OW, C) or y.dtype != x.dtype \
+                or y.device != x.device:
+            self.output.devmem = y = torch.zeros(B, OH, OW, C, dtype=x.dtype,
+                                                 device=x.device)
+            if self.MODE != "avg":
+                self.input_offset.devmem = torch.zeros(
+                    B, OH, OW, C, dtype=torch.int32, device=x.device)
+        ops.pool_fwd(x, self.ky, self.kx, self.sliding, self.MODE, out=y,
+                     argmax=self.input_offset.devmem
+                     if self.MODE != "avg" else None)
+
+
+class MaxPooling(Pooling):
+    MAPPING = "max_pooling"
+    MODE = "max"
+
+
+class AvgPooling(Pooling):
+    MAPPING = "avg_pooling"
+    MODE = "avg"
+
+
+class MaxAbsPooling(Pooling):
+    MAPPING = "maxabs_pooling"
+    MODE = "maxabs"
+
+
+class StochasticPooling(Pooling):
+    """Training: sample a window element with p ~ max(x, 0) (or |x|);
+    testing: probability-weighted average.  ``input_offset`` records the
+    sampled element for the max-style backward."""
+    MAPPING = "stochastic_pooling"
+    MODE = "max"
+    USE_ABS = False
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.rand = kwargs.get("rand", random_generator.get())
+        self.uniform_seed = 0
+
+    def run(self):
+        x = self._in()
+        B, H, W, C = x.shape
+        kx, ky = self.kx, self.ky
+        sx, sy = self.sliding
+        OH, OW = ops.pool_out_size(H, W, ky, kx, sy, sx)
+        Hp, Wp = (OH - 1) * sy + ky, (OW - 1) * sx + kx
+        xf = x.float()
+        pad = torch.zeros(B, Hp, Wp, C, device=x.device)
+        pad[:, :H, :W] = xf
+        valid = torch.zeros(B, Hp, Wp, C, device=x.device, dtype=torch.bool)
+        valid[:, :H, :W] = True
+        idx = torch.full((B, Hp, Wp, C), -1, dtype=torch.long, device=x.device)
+        idx[:, :H, :W] = torch.arange(B * H * W * C, device=x.device).view(
+            B, H, W, C)
+        vals, ids, oks = [], [], []
+        for dy in range(ky):
+            for dx in range(kx):
+                sl = (slice(None), slice(dy, dy + (OH - 1) * sy + 1, sy),
+                      slice(dx, dx + (OW - 1) * sx + 1, sx))
+                vals.append(pad[sl])
+                ids.append(idx[sl])
+                oks.append(valid[sl])
+        v = torch.stack(vals, -1)
+        i = torch.stack(ids, -1)
+        ok = torch.stack(oks, -1)
+        w = (v.abs() if self.USE_ABS else v.clamp(min=0)) * ok
+        tot = w.sum(-1, keepdim=True)
+        prob = torch.where(tot > 0, w / tot.clamp(min=1e-30),
+                           ok.float() / ok.float().sum(-1, keepdim=True))
+        testing = bool(getattr(self.workflow, "testing", False))
+        if testing:
+            y = (prob * v).sum(-1)
+            choice = prob.argmax(-1, keepdim=True)
+        else:
+            g = torch.Generator(device=x.device)
+            g.manual_seed(int(self.rand.randint(0, 2 ** 31 - 1)))
+            u = torch.rand(prob.shape[:-1] + (1,), generator=g,
+                           device=x.device)
+            choice = (prob.cumsum(-1) < u).sum(-1, keepdim=True).clamp(
+                max=prob.shape[-1] - 1)
+            y = v.gather(-1, choice).squeeze(-1)
+        self.output.devmem = y.to(x.dtype)
+        self.input_offset.devmem = i.gather(-1, choice).squeeze(-1).to(
+            torch.int32)
+
+
+class StochasticAbsPooling(StochasticPooling):
+    MAPPING = "stochastic_abs_pooling"
+    USE_ABS = True
+
+
+class StochasticPoolingDepooling(StochasticPooling):
+    """Pool then scatter back to the input geometry (output has the input
+    shape, zeros except at the sampled positions)."""
+    MAPPING = "stochastic_pool_depool"
+
+    def run(self):
+        super().run()
+        x = self._in()
+        out = torch.zeros(x.numel(), dtype=x.dtype, device=x.device)
+        out.index_put_((self.input_offset.devmem.reshape(-1).long(),),
+                       self.output.devmem.reshape(-1), accumulate=False)
+        self.output.devmem = out.view(x.shape)
+
+
+class StochasticAbsPoolingDepooling(StochasticPoolingDepooling):
+    MAPPING = "stochastic_abs_pool_depool"
+    USE_ABS = True
+
+
+class Depooling(AcceleratedUnit):
+    """Inverse of a max pooling: scatter ``input`` to the positions recorded
+    in ``get_output_shape_from.input_offset`` (Znicz depooling)."""
+    MAPPING = "depooling"
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.output = Array(shallow_pickle=True)
+        self.demand("input", "input_offset", "output_shape_source")
+
+    def run(self):
+        x = self.input.devmem
+        src = self.output_shape_source.devmem
+        out = torch.zeros(src.numel(), dtype=x.dtype, device=x.device)
+        out.index_put_((self.input_offset.devmem.reshape(-1).long(),),
+                       x.reshape(-1), accumulate=True)
+        self.output.devmem = out.view(src.shape)
+
+
+class GDPooling(GradientDescentBase):
+    hide_from_registry = True
+    MODE = "max"
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.kx = int(kwargs.get("kx", 2))
+        self.ky = int(kwargs.get("ky", 2))
+        s = kwargs.get("sliding", (self.kx, self.ky))
+        self.sliding = (s, s) if isinstance(s, int) else tuple(s)
+        self.demand("input_offset")
+
+    def run(self):
+        err = self.err_output.devmem
+        x = self.input.devmem
+        shape = tuple(x.shape) if x.dim() == 4 else tuple(x.shape) + (1,)
+        ei = self.alloc_err_input(shape)
+        aux, aux_act = self.aux_tensor()
+        if aux is not None and aux.dim() == 3:
+            aux = aux.unsqueeze(-1)
+        ops.pool_bwd(err, self.input_offset.devmem
+                     if self.MODE != "avg" else None, shape, self.ky, self.kx,
+                     self.sliding, self.MODE, aux=aux, aux_act=aux_act, out=ei)
+        if x.dim() == 3:
+            self.err_input.devmem = ei.squeeze(-1)
+
+
+class GDMaxPooling(GDPooling):
+    MAPPING = "max_pooling"
+    MODE = "max"
+
+
+class GDAvgPooling(GDPooling):
+    MAPPING = "avg_pooling"
+    MODE = "avg"
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.undemand("input_offset")
+        self.input_offset = None
+
+
+class GDMaxAbsPooling(GDPooling):
+    MAPPING = "maxabs_pooling"
+    MODE = "maxabs"

@@ -94,7 +94,7 @@ class Bool(object):
     def __ilshift__(self, value):
         if self._op is not None:
             raise RuntimeError("Derived expressions cannot be assigned to.")
-        if isinstance(value, Bool):
+        if isinstance(value, Bool) or type(value).__module__ == "numpy":
             value = bool(value)
         self._check(value)
         self._value = value

@@ -194,9 +194,52 @@ def _nhwc(x):
     return x.permute(0, 2, 3, 1)
 
 
+_WS = {}
+
+
+def _workspace(key, shape, dtype, device):
+    t = _WS.get(key)
+    if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or \
+            t.device != device:
+        t = torch.empty(shape, dtype=dtype, device=device)
+        _WS[key] = t
+    return t
+
+
+def needs_im2col(C, groups):
+    """Small-channel convs (C/groups % 8 != 0, e.g. RGB input) run as an
+    explicit bf16 im2col + dense MFMA GEMM instead of per-element gathers."""
+    return groups == 1 and C % 8 != 0
+
+
+def im2col(x, KH, KW, sliding, padding, out=None):
+    N, H, W, C = x.shape
+    sx, sy = sliding
+    pl, pt, pr, pb = padding
+    OH, OW = conv_out_size(H, W, KH, KW, sliding, padding)
+    K = KH * KW * C
+    Kp = (K + 7) // 8 * 8
+    M = N * OH * OW
+    if out is None:
+        out = torch.empty(M, Kp, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        _lib_call("hvk_im2col", _p(x), _p(out), N, H, W, C, KH, KW, sy, sx,
+                  pt, pl, OH, OW, Kp, _s(x))
+        return out
+    xp = F.pad(_nchw(x), (pl, pr, pt, pb))
+    cols = F.unfold(xp, (KH, KW), stride=(sy, sx))  # [N, C*KH*KW, L]
+    cols = cols.view(N, C, KH, KW, -1).permute(0, 4, 2, 3, 1).reshape(M, K)
+    out.zero_()
+    out[:, :K] = cols.to(out.dtype)
+    return out
+
+
 def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
-             groups=1, act=0, out=None):
-    """x [N,H,W,C], w [OC,KH,KW,C/g] -> y [N,OH,OW,OC]."""
+             groups=1, act=0, out=None, col_out=None):
+    """x [N,H,W,C], w [OC,KH,KW,C/g] -> y [N,OH,OW,OC].
+
+    ``col_out``: a dict that receives the im2col matrix when the explicit
+    path is used (the weight-gradient GEMM reuses it)."""
     N, H, W, C = x.shape
     OC, KH, KW, Cg = w.shape
     if Cg * groups != C or OC % groups:
@@ -209,6 +252,23 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
     if out is None:
         out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
     if _gpu(x):
+        if needs_im2col(C, groups):
+            K = KH * KW * C
+            Kp = (K + 7) // 8 * 8
+            col = im2col(x, KH, KW, sliding, padding, out=_workspace(
+                ("col", id(w)), (N * OH * OW, Kp), x.dtype, x.device))
+            wp = w.reshape(OC, K)
+            if Kp != K:
+                wpad = _workspace(("wpad", id(w)), (OC, Kp), w.dtype, w.device)
+                wpad[:, K:].zero_()
+                wpad[:, :K].copy_(wp)
+                wp = wpad
+            gemm(col, wp, trans_b=True, bias=bias, act=act,
+                 out=out.view(N * OH * OW, OC))
+            if col_out is not None:
+                col_out["col"] = col
+                col_out["K"] = K
+            return out
         _lib_call("hvk_conv_fwd", _p(x), _p(w), _p(bias), _p(out), N, H, W, C,
                   OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, act, _s(x))
         return out
@@ -248,8 +308,9 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
 
 
 def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
-               splits=None):
-    """dw (float32 [OC,KH,KW,C/g]) += sum over pixels of dy (x) im2col(x)."""
+               splits=None, col=None):
+    """dw (float32 [OC,KH,KW,C/g]) += sum over pixels of dy (x) im2col(x).
+    ``col``: the forward's explicit im2col matrix (small-channel convs)."""
     N, H, W, C = x.shape
     _, OH, OW, OC = dy.shape
     _, KH, KW, Cg = dw.shape
@@ -258,6 +319,13 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     if dw.dtype != torch.float32:
         raise TypeError("conv_wgrad accumulates into float32")
     if _gpu(x):
+        if col is not None:
+            K = KH * KW * Cg
+            M = N * OH * OW
+            sp = splits or wgrad_splits(M, OC, K, 1)
+            gemm(dy.reshape(M, OC), col[:, :K], trans_a=True,
+                 out=dw.view(OC, K), accumulate=True, splits=sp)
+            return dw
         if splits is None:
             splits = wgrad_splits(N * OH * OW, OC // groups,
                                   KH * KW * Cg, groups)
@@ -467,7 +535,8 @@ def softmax_ce(logits, labels, *, scale=None, err=None, probs=None,
         return err
     lf = logits.float()
     p = torch.softmax(lf, 1)
-    lab = labels.long()
+    lab = labels.long() if labels is not None else torch.full(
+        (B,), -1, dtype=torch.long)
     valid = lab >= 0
     if probs is not None:
         probs.copy_(p)
@@ -534,7 +603,7 @@ def _segs_tensor(segs, device):
     return t
 
 
-def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0):
+def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False):
     """Fused multi-segment SGD (flat float32 buffers).
 
     segs: [(begin, end, lr, weights_decay, l1_vs_l2, gradient_moment)]
@@ -543,8 +612,15 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0):
     n = w.numel()
     if _gpu(w):
         st = _segs_tensor(segs, w.device)
+        fn = getattr(_lib.lib(), "hvk_sgd4")
+        if mom is not None and fn(_p(w), _p(grad), _p(mom), _p(w_lp),
+                                  _p(st), len(segs), n, float(gscale),
+                                  int(zero_grad), _s(w)) == 0:
+            return w
         _lib_call("hvk_sgd", _p(w), _p(grad), _p(mom), _p(w_lp), _p(st),
                   len(segs), n, float(gscale), _s(w))
+        if zero_grad:
+            grad.zero_()
         return w
     for b, e, lr, d, l1, m in segs:
         ws = w[b:e]
@@ -558,6 +634,8 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0):
         ws += v
     if w_lp is not None:
         w_lp.copy_(w.to(w_lp.dtype))
+    if zero_grad:
+        grad.zero_()
     return w
 
 

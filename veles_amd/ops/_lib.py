@@ -31,11 +31,13 @@ _SIGS = {
     "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
     "hvk_conv_dgrad": [P, P, P] + [I] * 14 + [P, I, P],
     "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P],
+    "hvk_im2col": [P, P] + [I] * 13 + [P],
     "hvk_fill_minibatch": [P, I, P, I, I, I, L, P, P, P, I, P, P, P, P],
     "hvk_mean_disp_normalize": [P, I, P, P, P, I, L, L, P],
     "hvk_softmax_ce": [P, I, I, I, P, F, P, I, P, P, P, P, P],
     "hvk_mse": [P, I, P, I, I, I, F, P, I, P, P, I, P],
     "hvk_sgd": [P, P, P, P, P, I, L, F, P],
+    "hvk_sgd4": [P, P, P, P, P, I, L, F, I, P],
     "hvk_col_sum": [P, I, I, I, P, F, P],
     "hvk_row_sum": [P, I, I, I, P, F, P],
     "hvk_act_fwd": [P, I, P, I, L, I, P],

@@ -1,0 +1,248 @@
+"""Workflow snapshots and exact resume.
+
+Reference: veles/snapshotter.py:82-535 (``SnapshotterBase`` rate-limited by
+``interval`` runs and ``time_interval`` seconds; ``SnapshotterToFile`` naming
+``{prefix}_{suffix}.{protocol}.pickle[.ext]`` + ``{prefix}_current...`` symlink,
+codecs none/snappy/gz/bz2/xz; ``SnapshotterToDB`` (ODBC); ``import_``).
+
+Kept: file naming, codecs (snappy is not available on this image and maps to
+gz with a warning), the symlink, the size warning with the top-5 units, the
+final snapshot on ``stop()``.  The DB sink is SQLite (stdlib) with the same
+(prefix, suffix, timestamp, blob) shape.  Data-parallel: only rank 0 writes,
+after a barrier, at a point where every replica holds identical weights.
+Device tensors are pulled to the host by the units' ``__getstate__``; the
+HIP RNG / torch generator states are captured via RandomGenerator.state.
+"""
+from __future__ import annotations
+
+import bz2
+import gzip
+import io
+import lzma
+import logging
+import os
+import pickle
+import sqlite3
+import time
+
+from veles_amd.mutable import Bool
+from veles_amd.units import Unit
+from veles_amd.utils.config import root, get
+
+__all__ = ["SnapshotterBase", "SnapshotterToFile", "SnapshotterToDB",
+           "SnapshotterRegistry"]
+
+PROTOCOL = pickle.HIGHEST_PROTOCOL
+
+
+class SnapshotterRegistry(type(Unit)):
+    snapshotters = {}
+
+    def __init__(cls, name, bases, clsdict):
+        super().__init__(name, bases, clsdict)
+        m = clsdict.get("MAPPING")
+        if m:
+            SnapshotterRegistry.snapshotters[m] = cls
+
+
+def _rank():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank()
+    except Exception:
+        pass
+    return int(os.environ.get("RANK", "0"))
+
+
+class SnapshotterBase(Unit, metaclass=SnapshotterRegistry):
+    hide_from_registry = True
+    SIZE_WARNING_THRESHOLD = 200 * 1000 * 1000
+
+    def __init__(self, workflow, **kwargs):
+        kwargs.setdefault("view_group", "SERVICE")
+        super().__init__(workflow, **kwargs)
+        self.prefix = kwargs.get("prefix", "")
+        self._destination = ""
+        self.compression = kwargs.get("compression", "gz")
+        self.compression_level = kwargs.get("compression_level", 6)
+        self.interval = kwargs.get("interval", 1)
+        self.time_interval = kwargs.get("time_interval", 15)
+        self.time = 0
+        self._skipped_counter = 0
+        self.skip = Bool(False)
+        self.warn_about_size = kwargs.get("warn_about_size", True)
+        self.demand("suffix")
+
+    @property
+    def destination(self):
+        return self._destination
+
+    def initialize(self, **kwargs):
+        self.time = time.time()
+
+    def run(self):
+        if get(root.common.disable.snapshotting, False) is True:
+            return
+        self._skipped_counter += 1
+        if self._skipped_counter < self.interval or self.skip:
+            return
+        self._skipped_counter = 0
+        if time.time() - self.time < self.time_interval:
+            return
+        self.export_if_rank0()
+        self.time = time.time()
+        return True
+
+    def stop(self):
+        if self._skipped_counter > 0 and not self.skip and \
+                get(root.common.disable.snapshotting, False) is not True:
+            self._skipped_counter = 0
+            self.export_if_rank0()
+
+    def export_if_rank0(self):
+        from veles_amd.parallel import find_dp
+        dp = find_dp(self)
+        if dp is not None and dp.world_size > 1:
+            dp.barrier()
+        if _rank() == 0:
+            self.export()
+
+    def export(self):
+        raise NotImplementedError
+
+    def check_snapshot_size(self, size):
+        if size > self.SIZE_WARNING_THRESHOLD and self.warn_about_size:
+            sizes = []
+            for u in self.workflow:
+                try:
+                    sizes.append((len(pickle.dumps(u, PROTOCOL)), u.name))
+                except Exception:
+                    pass
+            sizes.sort(reverse=True)
+            self.warning("Snapshot size %.1f MB; biggest units: %s",
+                         size / 1e6, ", ".join("%s %.1f MB" % (n, s / 1e6)
+                                               for s, n in sizes[:5]))
+
+    def get_metric_values(self):
+        return {"Snapshot": self.destination}
+
+    @staticmethod
+    def import_(file_name):
+        return SnapshotterToFile.import_(file_name)
+
+
+class SnapshotterToFile(SnapshotterBase):
+    MAPPING = "file"
+
+    WRITE_CODECS = {
+        None: lambda n, l: open(n, "wb"),
+        "": lambda n, l: open(n, "wb"),
+        "gz": lambda n, l: gzip.GzipFile(n, "wb", compresslevel=l),
+        "bz2": lambda n, l: bz2.BZ2File(n, "wb", compresslevel=l),
+        "xz": lambda n, l: lzma.LZMAFile(n, "wb", preset=l),
+    }
+    READ_CODECS = {
+        "pickle": lambda n: open(n, "rb"),
+        "gz": lambda n: gzip.GzipFile(n, "rb"),
+        "bz2": lambda n: bz2.BZ2File(n, "rb"),
+        "xz": lambda n: lzma.LZMAFile(n, "rb"),
+    }
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.directory = kwargs.get("directory",
+                                    get(root.common.dirs.snapshots, "."))
+        if self.compression == "snappy":
+            self.warning("snappy is unavailable; using gz")
+            self.compression = "gz"
+
+    def export(self):
+        os.makedirs(self.directory, exist_ok=True)
+        ext = ("." + self.compression) if self.compression else ""
+        rel = "%s_%s.%d.pickle%s" % (self.prefix, self.suffix, PROTOCOL, ext)
+        self._destination = os.path.abspath(os.path.join(self.directory, rel))
+        self.info("Snapshotting to %s", self._destination)
+        tmp = self._destination + ".tmp"
+        with self.WRITE_CODECS[self.compression](
+                tmp, self.compression_level) as f:
+            pickle.dump(self.workflow, f, protocol=PROTOCOL)
+        os.replace(tmp, self._destination)
+        self.check_snapshot_size(os.path.getsize(self._destination))
+        link = os.path.join(self.directory, "%s_current.%d.pickle%s" % (
+            self.prefix, PROTOCOL, ext))
+        try:
+            os.remove(link)
+        except OSError:
+            pass
+        try:
+            os.symlink(rel, link)
+        except OSError:
+            pass
+        return self._destination
+
+    @staticmethod
+    def import_(file_name):
+        """Load a snapshot written by this framework (own file: pickle)."""
+        file_name = file_name.strip()
+        if not os.path.exists(file_name):
+            raise FileNotFoundError(file_name)
+        ext = os.path.splitext(file_name)[1][1:]
+        if ext == "snappy":
+            raise ValueError("snappy snapshots are not supported")
+        codec = SnapshotterToFile.READ_CODECS.get(
+            ext, SnapshotterToFile.READ_CODECS["pickle"])
+        logging.getLogger("Snapshotter").info("Reading %s", file_name)
+        with codec(file_name) as f:
+            return pickle.load(f)
+
+
+class SnapshotterToDB(SnapshotterBase):
+    """Snapshots into an SQLite table (id, prefix, suffix, timestamp,
+    codec, data) - the reference's ODBC sink shape."""
+    MAPPING = "db"
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.database = kwargs.get("database", os.path.join(
+            get(root.common.dirs.snapshots, "."), "snapshots.sqlite"))
+        self.table = kwargs.get("table", "veles")
+
+    def _conn(self):
+        d = os.path.dirname(os.path.abspath(self.database))
+        os.makedirs(d, exist_ok=True)
+        c = sqlite3.connect(self.database)
+        c.execute("CREATE TABLE IF NOT EXISTS %s (id INTEGER PRIMARY KEY, "
+                  "prefix TEXT, suffix TEXT, timestamp REAL, codec TEXT, "
+                  "data BLOB)" % self.table)
+        return c
+
+    def export(self):
+        bio = io.BytesIO()
+        with gzip.GzipFile(fileobj=bio, mode="wb",
+                           compresslevel=self.compression_level) as f:
+            pickle.dump(self.workflow, f, protocol=PROTOCOL)
+        c = self._conn()
+        with c:
+            cur = c.execute("INSERT INTO %s (prefix, suffix, timestamp, codec,"
+                            " data) VALUES (?, ?, ?, ?, ?)" % self.table,
+                            (self.prefix, str(self.suffix), time.time(), "gz",
+                             bio.getvalue()))
+            rid = cur.lastrowid
+        c.close()
+        self._destination = "sqlite://%s/%s/%d" % (self.database, self.table,
+                                                   rid)
+        return self._destination
+
+    @staticmethod
+    def import_from(database, table="veles", row_id=None):
+        c = sqlite3.connect(database)
+        if row_id is None:
+            row = c.execute("SELECT data FROM %s ORDER BY id DESC LIMIT 1" %
+                            table).fetchone()
+        else:
+            row = c.execute("SELECT data FROM %s WHERE id=?" % table,
+                            (row_id,)).fetchone()
+        c.close()
+        with gzip.GzipFile(fileobj=io.BytesIO(row[0])) as f:
+            return pickle.load(f)

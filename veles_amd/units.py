@@ -531,8 +531,8 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
             for dst in targets:
                 self.debug("%s -> %s @%s", self, dst,
                            threading.current_thread().name)
-        if len(targets) > 1 and root.common.engine.get(
-                "parallel_fanout", False) is True:
+        if len(targets) > 1 and get(root.common.engine.parallel_fanout,
+                                    False) is True:
             for dst in targets:
                 self.thread_pool.callInThread(_run_in_pool, dst, self)
             return
