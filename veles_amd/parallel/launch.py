@@ -1,0 +1,113 @@
+"""Local multi-process launcher: one data-parallel rank per GPU.
+
+Replaces the reference's SSH/YARN node spawning and master/slave roles
+(veles/launcher.py:617-660, 808-842; server.py ``--respawn`` 637-655).  Each
+rank is a child process with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT set (the torch.distributed.run contract, 127.0.0.1 rendezvous).
+Failure handling: if any rank dies, the whole group is terminated (a
+collective would otherwise hang until its timeout) and, with ``respawn > 0``,
+restarted from the newest ``*_current`` snapshot - the elastic-restart path
+of SURVEY §5.3.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+from veles_amd.backends import parse_device_spec
+
+__all__ = ["spawn_ranks", "free_port", "latest_snapshot"]
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def latest_snapshot(directory):
+    cands = glob.glob(os.path.join(directory, "*_current.*.pickle*"))
+    cands = [c for c in cands if os.path.exists(os.path.realpath(c))]
+    if not cands:
+        return None
+    return max(cands, key=lambda c: os.path.getmtime(os.path.realpath(c)))
+
+
+def _launch(devices, cmd, port, env_extra=None):
+    procs = []
+    n = len(devices)
+    for rank, dev in enumerate(devices):
+        env = dict(os.environ)
+        env.update({"RANK": str(rank), "LOCAL_RANK": str(rank),
+                    "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port),
+                    "VELES_AMD_DEVICE": str(dev)})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if env_extra:
+            env.update(env_extra)
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    return procs
+
+
+def _kill_all(procs):
+    for p in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except OSError:
+                pass
+    deadline = time.time() + 10
+    for p in procs:
+        try:
+            p.wait(max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except OSError:
+                pass
+
+
+def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5):
+    """Run ``cmd`` once per device in ``spec`` ("0-7", "0,1", "4").
+    Returns the group's exit code (0 when every rank succeeded)."""
+    devices = parse_device_spec(spec) if isinstance(spec, str) else list(spec)
+    attempt = 0
+    cmd = list(cmd)
+    while True:
+        procs = _launch(devices, cmd, free_port())
+        failed = None
+        try:
+            while True:
+                codes = [p.poll() for p in procs]
+                bad = [c for c in codes if c not in (None, 0)]
+                if bad:
+                    failed = bad[0]
+                    break
+                if all(c == 0 for c in codes):
+                    return 0
+                time.sleep(poll)
+        except KeyboardInterrupt:
+            _kill_all(procs)
+            return 130
+        _kill_all(procs)
+        if attempt >= respawn:
+            return failed
+        attempt += 1
+        from veles_amd.utils.config import root, get
+        snap = latest_snapshot(snapshot_dir or get(root.common.dirs.snapshots,
+                                                   "."))
+        if snap is not None:
+            cmd = [c for c in cmd]
+            if "-w" in cmd:
+                i = cmd.index("-w")
+                del cmd[i:i + 2]
+            cmd = cmd[:3] + ["-w", snap] + cmd[3:]
+        print("[launch] rank failed with %s; respawn %d/%d from %s" %
+              (failed, attempt, respawn, snap), file=sys.stderr)
