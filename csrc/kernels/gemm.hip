@@ -71,16 +71,21 @@ struct DenseMN {
   const uint16_t* p;
   long long gstride;
   int cols, K, ld, vec;
+  int ones_col;  // >= 0: column of ones appended at index cols (bias grad)
   struct Ctx { int c; };
   __device__ void group(int g) { p += (long long)g * gstride; }
   __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
   __device__ uint4 load(const Ctx& cx, int k) const {
-    if (k >= K || cx.c >= cols) return zero4();
+    if (k >= K) return zero4();
     const uint16_t* row = p + (long long)k * ld;
     if (vec && cx.c + 8 <= cols) return *(const uint4*)(row + cx.c);
+    if (cx.c >= cols && (ones_col < 0 || cx.c > ones_col)) return zero4();
     uint16_t e[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) e[j] = (cx.c + j < cols) ? row[cx.c + j] : 0;
+    for (int j = 0; j < 8; ++j) {
+      int c = cx.c + j;
+      e[j] = c < cols ? row[c] : (c == ones_col ? (uint16_t)0x3F80 : 0);
+    }
     return pack8(e);
   }
 };
@@ -220,11 +225,12 @@ struct ConvWgradB {
   ConvGeom g;
   int K /* pixels */, KK, vec;
   int coff;
+  int ones;  // append a ones column at index KK (bias gradient)
   struct Ctx { int kh, kw, ch, ok; };
   __device__ void group(int gi) { coff = gi * g.Cg; }
   __device__ Ctx col_ctx(int kk) const {
     Ctx c;
-    c.ok = kk < KK;
+    c.ok = kk < KK ? 1 : ((ones && kk == KK) ? 2 : 0);
     uint32_t t, ch, kh, kw;
     fdivmod(c.ok ? kk : 0, g.fCg, t, ch);
     fdivmod(t, g.fKW, kh, kw);
@@ -233,6 +239,7 @@ struct ConvWgradB {
   }
   __device__ uint4 load(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return zero4();
+    if (cx.ok == 2) return make_uint4(0x3F80u, 0, 0, 0);
     uint32_t n, rem, oh, ow;
     fdivmod(p, g.fOHOW, n, rem);
     fdivmod(rem, g.fOW, oh, ow);
@@ -252,6 +259,7 @@ struct ConvWgradB {
       // element j is column kk+j: recompute its tap
       int kk = (cx.kh * g.KW + cx.kw) * g.Cg + cx.ch + j;
       e[j] = 0;
+      if (ones && kk == KK) e[j] = 0x3F80;
       if (kk < KK) {
         uint32_t t, ch, kh, kw;
         fdivmod(kk, g.fCg, t, ch);
@@ -259,6 +267,124 @@ struct ConvWgradB {
         int ih = ih0 + (int)kh, iw = iw0 + (int)kw;
         if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
           e[j] = x[base + (ih * g.W + iw) * g.C + ch];
+      }
+    }
+    return pack8(e);
+  }
+};
+
+
+// Small-channel convs (C % 8 != 0, groups == 1, e.g. AlexNet conv1 with
+// C = 3): K is re-laid out as (kh, j) with j < RUNP, where j < RUN = KW*C
+// indexes the CONTIGUOUS (kw, c) run of one input row and RUNP pads it to
+// a multiple of 8 (weights zero there).  A chunk of 8 k's is then 8
+// consecutive input elements: one (2-byte aligned) 16-B load; gfx950 runs
+// in unaligned-access mode, hipcc emits global_load_dwordx4 for it.
+__device__ __forceinline__ uint4 ld16u(const uint16_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+
+struct RunGeom {
+  int RUN, RUNP;
+  FastDiv fRUNP, fC;
+  long long total;  // elements of x (tail guard)
+};
+
+struct ConvFwdRunA {
+  const uint16_t* x;
+  ConvGeom g;
+  RunGeom r;
+  int M, K;  // K = KH * RUNP
+  struct Ctx { long long base; int ih0, iw0, ok, full; };
+  __device__ void group(int) {}
+  __device__ Ctx row_ctx(int m) const {
+    Ctx c;
+    c.ok = m < M;
+    uint32_t mm = c.ok ? m : 0, n, rem, oh, ow;
+    fdivmod(mm, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    c.base = (long long)n * g.H * g.W * g.C;
+    c.ih0 = oh * g.sy - g.pt;
+    c.iw0 = ow * g.sx - g.pl;
+    c.full = c.iw0 >= 0 && c.iw0 + g.KW <= g.W;
+    return c;
+  }
+  __device__ uint4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
+    uint32_t kh, j;
+    fdivmod(k, r.fRUNP, kh, j);
+    int ih = c.ih0 + (int)kh;
+    if ((unsigned)ih >= (unsigned)g.H) return zero4();
+    long long a = c.base + ((long long)ih * g.W + c.iw0) * g.C + j;
+    if (c.full && a + 8 <= r.total) return ld16u(x + a);
+    uint16_t e[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int jj = (int)j + q;
+      e[q] = 0;
+      if (jj < r.RUN) {
+        uint32_t kw, ch;
+        fdivmod(jj, r.fC, kw, ch);
+        int iw = c.iw0 + (int)kw;
+        if ((unsigned)iw < (unsigned)g.W)
+          e[q] = x[c.base + ((long long)ih * g.W + iw) * g.C + ch];
+      }
+    }
+    return pack8(e);
+  }
+};
+
+// wgrad B for small-channel convs: MN-major, rows = pixels, cols = (kh, j)
+struct ConvWgradRunB {
+  const uint16_t* x;
+  ConvGeom g;
+  RunGeom r;
+  int K /* pixels */, KK /* KH*RUNP */, ones;
+  struct Ctx { int kh, j, ok; };
+  __device__ void group(int) {}
+  __device__ Ctx col_ctx(int kk) const {
+    Ctx c;
+    c.ok = kk < KK ? 1 : ((ones && kk == KK) ? 2 : 0);
+    uint32_t kh, j;
+    fdivmod(kk < KK ? kk : 0, r.fRUNP, kh, j);
+    c.kh = kh;
+    c.j = j;
+    return c;
+  }
+  __device__ uint4 load(const Ctx& cx, int p) const {
+    if (!cx.ok || p >= K) return zero4();
+    if (cx.ok == 2) return make_uint4(0x3F80u, 0, 0, 0);
+    uint32_t n, rem, oh, ow;
+    fdivmod(p, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    int ih = oh * g.sy - g.pt + cx.kh;
+    if ((unsigned)ih >= (unsigned)g.H) return zero4();
+    int iw0 = ow * g.sx - g.pl;
+    long long base = (long long)n * g.H * g.W * g.C;
+    long long a = base + ((long long)ih * g.W + iw0) * g.C + cx.j;
+    if (iw0 >= 0 && iw0 + g.KW <= g.W && a + 8 <= r.total) {
+      uint4 v = ld16u(x + a);
+      if (cx.j + 8 > r.RUN) {  // zero the pad tail of the run
+        uint16_t* h = (uint16_t*)&v;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (cx.j + q >= r.RUN) h[q] = 0;
+      }
+      return v;
+    }
+    uint16_t e[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int jj = cx.j + q;
+      e[q] = 0;
+      if (jj < r.RUN) {
+        uint32_t kw, ch;
+        fdivmod(jj, r.fC, kw, ch);
+        int iw = iw0 + (int)kw;
+        if ((unsigned)iw < (unsigned)g.W)
+          e[q] = x[base + ((long long)ih * g.W + iw) * g.C + ch];
       }
     }
     return pack8(e);
@@ -279,8 +405,20 @@ struct Epi {
   int ld_aux, aux_act;
   int grow, gcol;  // per-group row / column offsets
   float* preact;   // optional f32 copy of the pre-activation (unused = null)
+  int ones_col;    // column routed to bias_grad[m] (fused bias gradient)
+  float* bias_grad;
+  int run_in, run_out;  // column remap n = kh*run_in + j -> kh*run_out + j
   __device__ void store(int gi, int m, int n, float v) const {
     if (m >= M || n >= N) return;
+    if (n == ones_col) {
+      atomicAdd(bias_grad + m + gi * grow, v * alpha);
+      return;
+    }
+    if (run_in) {
+      int kh = n / run_in, j = n - kh * run_in;
+      if (j >= run_out) return;
+      n = kh * run_out + j;
+    }
     int gm = m + gi * grow, gn = n + gi * gcol;
     long long idx = (long long)gm * ldc + gn;
     v *= alpha;
@@ -299,6 +437,49 @@ struct Epi {
     if (out_f32) ((float*)c)[idx] = v;
     else ((uint16_t*)c)[idx] = f2bf(v);
   }
+  // 8 consecutive columns of one row: 16-B vector stores when possible
+  __device__ void store8(int gi, int m, int n, const float* v) const {
+    if (m >= M || n >= N) return;
+    int gm = m + gi * grow, gn = n + gi * gcol;
+    long long idx = (long long)gm * ldc + gn;
+    const bool vecok = !atomic && !run_in && ones_col < 0 && n + 8 <= N &&
+                       beta == 0.f && bias_mode != 2 && (ldc & 7) == 0 &&
+                       (((uintptr_t)c) & 15) == 0 && (gn & 7) == 0 &&
+                       (!aux || (ld_aux & 7) == 0);
+    if (!vecok) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) store(gi, m, n + q, v[q]);
+      return;
+    }
+    float o[8];
+    float a[8];
+    if (aux) {
+      uint4 av = *(const uint4*)(aux + (long long)gm * ld_aux + gn);
+      const uint16_t* ah = (const uint16_t*)&av;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = act_bwd(bf2f(ah[q]), aux_act);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float t = v[q] * alpha;
+      if (bias_mode == 1) t += bias[gn + q];
+      if (act) t = act_fwd(t, act);
+      if (aux) t *= a[q];
+      o[q] = t;
+    }
+    if (out_f32) {
+      float4* d = (float4*)((float*)c + idx);
+      d[0] = make_float4(o[0], o[1], o[2], o[3]);
+      d[1] = make_float4(o[4], o[5], o[6], o[7]);
+    } else {
+      uint4 w;
+      w.x = f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+      w.y = f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      w.z = f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+      w.w = f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+      *(uint4*)((uint16_t*)c + idx) = w;
+    }
+  }
 };
 
 __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -310,7 +491,11 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   constexpr int NB = BN_ / 32;          // B chunks per thread / MFMA n-tiles
   constexpr int CPR = BN_ / 8;          // MN-major B: chunks per k-row
   constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
-  __shared__ __attribute__((aligned(16))) uint16_t smem[4 * TILE];
+  // operand double buffers (64 KiB); reused as the f32 C tile (with a
+  // 4-float row pad) by the epilogue
+  constexpr int SMEM_BYTES = (4 * TILE * 2 > 128 * (BN_ + 4) * 4)
+                                 ? 4 * TILE * 2 : 128 * (BN_ + 4) * 4;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES / 2];
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   // bijective XCD remap (cdna_hip_programming.md T1)
@@ -439,15 +624,43 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     cur ^= 1;
   }
 
+  if (epi.atomic) {
+    // split-K partial sums: f32 atomics straight from the accumulators
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        int mb = m0 + wm * 64 + i * 16 + fq * 4;
+        int n = n0 + wn * (BN_ / 2) + j * 16 + fr;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) epi.store(gi, mb + rr, n, acc[i][j][rr]);
+      }
+    return;
+  }
+  // stage the f32 tile through LDS, then row-contiguous 16-B stores
+  constexpr int LDC = BN_ + 4;
+  float* sC = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      int mb = m0 + wm * 64 + i * 16 + fq * 4;
-      int n = n0 + wn * (BN_ / 2) + j * 16 + fr;
+      int rb = wm * 64 + i * 16 + fq * 4;
+      int cc = wn * (BN_ / 2) + j * 16 + fr;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) epi.store(gi, mb + rr, n, acc[i][j][rr]);
+      for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + cc] = acc[i][j][rr];
     }
+  __syncthreads();
+  constexpr int CH = BN_ / 8;
+  for (int q = t; q < BM * CH; q += NTHR) {
+    int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
+    if (m0 + row >= M) continue;
+    const float4* src = (const float4*)(sC + row * LDC + c8);
+    float v[8];
+    float4 lo = src[0], hi = src[1];
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    epi.store8(gi, m0 + row, n0 + c8, v);
+  }
 }
 
 // Tile width: 64 when it pads N less than 128 does (N = 48, 96->?, 192).
@@ -501,6 +714,7 @@ Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
   e.bias_mode = bias ? bias_mode : 0; e.act = act;
   e.aux = (const uint16_t*)aux; e.ld_aux = ld_aux; e.aux_act = aux_act;
   e.grow = 0; e.gcol = 0; e.preact = nullptr;
+  e.ones_col = -1; e.bias_grad = nullptr; e.run_in = 0; e.run_out = 0;
   return e;
 }
 
@@ -558,13 +772,23 @@ HVK_API int hvk_im2col(const void* X, void* col, int N, int H, int W, int C,
 // C[M][N] = alpha*op(A)*op(B) + beta*C (+bias, act, aux-derivative mask)
 // transA=0: A is [M][K] (lda); transA=1: A is [K][M].
 // transB=0: B is [K][N] (ldb); transB=1: B is [N][K].
+// bias_grad (optional, requires transB == 0 and atomic): a ones column is
+// appended to B so bias_grad[m] += sum_k A[m][k] comes out of the same GEMM.
 HVK_API int hvk_gemm(int transA, int transB, int M, int N, int K,
                      const void* A, int lda, const void* B, int ldb, void* C,
                      int ldc, int out_f32, int atomic, float alpha, float beta,
                      const float* bias, int bias_mode, int act, const void* aux,
-                     int ld_aux, int aux_act, int splits, hipStream_t s) {
-  Epi e = make_epi(C, ldc, M, N, out_f32, atomic, alpha, beta, bias,
+                     int ld_aux, int aux_act, int splits, float* bias_grad,
+                     hipStream_t s) {
+  if (bias_grad && (transB || !atomic)) return -2;
+  const int Nk = bias_grad ? N + 1 : N;
+  Epi e = make_epi(C, ldc, M, Nk, out_f32, atomic, alpha, beta, bias,
                    bias_mode, act, aux, ld_aux, aux_act);
+  if (bias_grad) {
+    e.ones_col = N;
+    e.bias_grad = bias_grad;
+  }
+  const int oc = bias_grad ? N : -1;
   const uint16_t* a = (const uint16_t*)A;
   const uint16_t* b = (const uint16_t*)B;
   int va = al16(a) && (lda % 8 == 0), vb = al16(b) && (ldb % 8 == 0);
@@ -575,14 +799,14 @@ HVK_API int hvk_gemm(int transA, int transB, int M, int N, int K,
     err = launch<DenseK, true, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
   } else if (!transA && !transB) {
     DenseK la{a, 0, M, K, lda, va};
-    DenseMN lb{b, 0, N, K, ldb, vb};
-    err = launch<DenseK, true, DenseMN, false>(la, lb, e, M, N, K, splits, 1, s);
+    DenseMN lb{b, 0, N, K, ldb, vb, oc};
+    err = launch<DenseK, true, DenseMN, false>(la, lb, e, M, Nk, K, splits, 1, s);
   } else if (transA && !transB) {
-    DenseMN la{a, 0, M, K, lda, va};
-    DenseMN lb{b, 0, N, K, ldb, vb};
-    err = launch<DenseMN, false, DenseMN, false>(la, lb, e, M, N, K, splits, 1, s);
+    DenseMN la{a, 0, M, K, lda, va, -1};
+    DenseMN lb{b, 0, N, K, ldb, vb, oc};
+    err = launch<DenseMN, false, DenseMN, false>(la, lb, e, M, Nk, K, splits, 1, s);
   } else {
-    DenseMN la{a, 0, M, K, lda, va};
+    DenseMN la{a, 0, M, K, lda, va, -1};
     DenseK lb{b, 0, N, K, ldb, vb};
     err = launch<DenseMN, false, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
   }
@@ -627,15 +851,71 @@ HVK_API int hvk_conv_dgrad(const void* dY, const void* Wt, void* dX, int N,
 HVK_API int hvk_conv_wgrad(const void* X, const void* dY, float* dW, int N,
                            int H, int W, int C, int OC, int KH, int KW, int sy,
                            int sx, int pt, int pl, int OH, int OW, int groups,
-                           int splits, hipStream_t s) {
+                           int splits, float* dbias, hipStream_t s) {
   ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
   int P = N * OH * OW, KK = KH * KW * g.Cg;
   DenseMN la{(const uint16_t*)dY, (long long)g.OCg, g.OCg, P, OC,
-             (OC % 8 == 0 && g.OCg % 8 == 0 && al16(dY)) ? 1 : 0};
+             (OC % 8 == 0 && g.OCg % 8 == 0 && al16(dY)) ? 1 : 0, -1};
   ConvWgradB lb{(const uint16_t*)X, g, P, KK,
-                (g.Cg % 8 == 0 && C % 8 == 0 && al16(X)) ? 1 : 0, 0};
-  Epi e = make_epi(dW, KK, g.OCg, KK, 1, 1, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0);
+                (g.Cg % 8 == 0 && C % 8 == 0 && al16(X)) ? 1 : 0, 0,
+                dbias ? 1 : 0};
+  const int Nk = dbias ? KK + 1 : KK;
+  Epi e = make_epi(dW, KK, g.OCg, Nk, 1, 1, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0);
   e.grow = g.OCg;
-  return (int)launch<DenseMN, false, ConvWgradB, false>(la, lb, e, g.OCg, KK, P,
+  if (dbias) {
+    e.ones_col = KK;
+    e.bias_grad = dbias;
+  }
+  return (int)launch<DenseMN, false, ConvWgradB, false>(la, lb, e, g.OCg, Nk, P,
                                                         splits, groups, s);
+}
+
+static RunGeom make_run(const ConvGeom& g) {
+  RunGeom r;
+  r.RUN = g.KW * g.C;
+  r.RUNP = (r.RUN + 7) / 8 * 8;
+  r.fRUNP = make_fastdiv(r.RUNP);
+  r.fC = make_fastdiv(g.C);
+  r.total = (long long)g.N * g.H * g.W * g.C;
+  return r;
+}
+
+// Small-channel forward: Wp is [OC][KH][RUNP] (zero padded runs)
+HVK_API int hvk_conv_fwd_run(const void* X, const void* Wp, const float* bias,
+                             void* Y, int N, int H, int W, int C, int OC,
+                             int KH, int KW, int sy, int sx, int pt, int pl,
+                             int OH, int OW, int act, hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, 1);
+  RunGeom r = make_run(g);
+  int M = N * OH * OW, K = KH * r.RUNP;
+  ConvFwdRunA la{(const uint16_t*)X, g, r, M, K};
+  DenseK lb{(const uint16_t*)Wp, 0, OC, K, K, al16(Wp) ? 1 : 0};
+  Epi e = make_epi(Y, OC, M, OC, 0, 0, 1.f, 0.f, bias, 1, act, nullptr, 0, 0);
+  return (int)launch<ConvFwdRunA, true, DenseK, true>(la, lb, e, M, OC, K, 1, 1,
+                                                      s);
+}
+
+// Small-channel weight gradient into dW [OC][KH][KW][C] (+ fused bias grad)
+HVK_API int hvk_conv_wgrad_run(const void* X, const void* dY, float* dW,
+                               float* dbias, int N, int H, int W, int C,
+                               int OC, int KH, int KW, int sy, int sx, int pt,
+                               int pl, int OH, int OW, int splits,
+                               hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, 1);
+  RunGeom r = make_run(g);
+  int P = N * OH * OW, KKp = KH * r.RUNP;
+  DenseMN la{(const uint16_t*)dY, 0, OC, P, OC,
+             (OC % 8 == 0 && al16(dY)) ? 1 : 0, -1};
+  ConvWgradRunB lb{(const uint16_t*)X, g, r, P, KKp, dbias ? 1 : 0};
+  const int Nk = dbias ? KKp + 1 : KKp;
+  Epi e = make_epi(dW, KH * r.RUN, OC, Nk, 1, 1, 1.f, 0.f, nullptr, 0, 0,
+                   nullptr, 0, 0);
+  e.run_in = r.RUNP;
+  e.run_out = r.RUN;
+  if (dbias) {
+    e.ones_col = KKp;
+    e.bias_grad = dbias;
+  }
+  return (int)launch<DenseMN, false, ConvWgradRunB, false>(la, lb, e, OC, Nk, P,
+                                                           splits, 1, s);
 }

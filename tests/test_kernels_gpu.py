@@ -73,6 +73,21 @@ def test_gemm_splitk_accumulate():
     close(out, ref, 2e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(96, 363, 5000), (100, 784, 100),
+                                   (256, 128, 64)])
+def test_gemm_fused_bias_grad(M, N, K):
+    a, b = rnd(K, M), rnd(K, N, seed=6)
+    ref = torch.zeros(M, N)
+    rbg = torch.zeros(M)
+    ops.gemm(a, b, trans_a=True, out=ref, accumulate=True, bias_grad=rbg)
+    out = torch.zeros(M, N, device=DEV)
+    bg = torch.zeros(M, device=DEV)
+    ops.gemm(a.to(DEV), b.to(DEV), trans_a=True, out=out, accumulate=True,
+             splits=4, bias_grad=bg)
+    close(out, ref, 2e-3)
+    close(bg, rbg, 2e-3)
+
+
 def test_gemm_nan_tail_guard():
     M, N, K = 33, 65, 64
     a, b = rnd(M, K), rnd(N, K, seed=5)
@@ -126,10 +141,13 @@ def test_conv_wgrad(cfg):
     OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
     dy = rnd(N, OH, OW, OC, seed=2)
     ref = torch.zeros(OC, KH, KW, C // g)
-    ops.conv_wgrad(x, dy, ref, sl, pad, g)
+    rb = torch.zeros(OC)
+    ops.conv_wgrad(x, dy, ref, sl, pad, g, dbias=rb)
     got = torch.zeros(OC, KH, KW, C // g, device=DEV)
-    ops.conv_wgrad(x.to(DEV), dy.to(DEV), got, sl, pad, g)
+    gb = torch.zeros(OC, device=DEV)
+    ops.conv_wgrad(x.to(DEV), dy.to(DEV), got, sl, pad, g, dbias=gb)
     close(got, ref, 1e-2)
+    close(gb, rb, 1e-2)
 
 
 @pytest.mark.parametrize("mode", ["max", "avg", "maxabs"])
@@ -247,12 +265,12 @@ def test_conv_im2col_path_fwd_and_wgrad():
     x = rnd(N, H, W, C)
     w = rnd(OC, k, k, C, seed=1, scale=0.1)
     b = torch.randn(OC)
-    ws = {}
     ref = ops.conv_fwd(x, w, b, (s, s), (0, 0, 0, 0), 1, 3)
     got = ops.conv_fwd(x.to(DEV), w.to(DEV), b.to(DEV), (s, s), (0, 0, 0, 0),
-                       1, 3, col_out=ws)
+                       1, 3)
     close(got, ref, 1e-2)
-    assert "col" in ws
+    ws = {"col": ops.im2col(x.to(DEV), k, k, (s, s), (0, 0, 0, 0))}
+    close(ws["col"], ops.im2col(x, k, k, (s, s), (0, 0, 0, 0)), 0)
     OH, OW = ops.conv_out_size(H, W, k, k, (s, s), (0, 0, 0, 0))
     dy = rnd(N, OH, OW, OC, seed=2)
     dref = torch.zeros(OC, k, k, C)

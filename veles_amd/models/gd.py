@@ -35,12 +35,15 @@ class GradientDescent(GradientDescentBase):
         if x.dtype != e2.dtype:
             x = x.to(e2.dtype)
         pw, pb = fwd._pw_, fwd._pb_
+        bg = None if pb is None else pb.grad
         if not fwd.weights_transposed:
-            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=True)
+            # grad_W and grad_b (ones column) from one GEMM
+            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=True,
+                     bias_grad=bg)
         else:
             ops.gemm(x, e2, trans_a=True, out=pw.grad, accumulate=True)
-        if pb is not None:
-            ops.col_sum(e2, out=pb.grad, accumulate=True)
+            if bg is not None:
+                ops.col_sum(e2, out=bg, accumulate=True)
         if self.need_err_input:
             ei = self.alloc_err_input(self.input.devmem.shape)
             aux, aux_act = self.aux_tensor()

@@ -33,11 +33,10 @@ class GradientDescentConv(GradientDescentBase):
         if x.dtype != err.dtype:
             x = x.to(err.dtype)
         pw, pb = fwd._pw_, fwd._pb_
+        # weight AND bias gradients from one implicit-GEMM launch
         ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,
-                       fwd.grouping, col=getattr(fwd, "col_", None))
-        if pb is not None:
-            ops.col_sum(err.reshape(-1, err.shape[-1]), out=pb.grad,
-                        accumulate=True)
+                       fwd.grouping, col=getattr(fwd, "col_", None),
+                       dbias=None if pb is None else pb.grad)
         if self.need_err_input:
             ei = self.alloc_err_input(tuple(x.shape))
             aux, aux_act = self.aux_tensor()

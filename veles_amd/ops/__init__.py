@@ -118,11 +118,13 @@ def act_bwd(dy, y, act, out=None):
 # --------------------------------------------------------------------- GEMM
 def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
          alpha=1.0, beta=0.0, bias=None, bias_mode="col", act=0, aux=None,
-         aux_act=0, accumulate=False, splits=1):
+         aux_act=0, accumulate=False, splits=1, bias_grad=None):
     """out[M][N] = act(alpha*op(a)@op(b) + beta*out + bias) * f'_aux(aux).
 
     ``accumulate``: out (float32) += alpha*op(a)@op(b) (+bias) - split-K
     partial sums are reduced with float atomics on the GPU.
+    ``bias_grad`` (float32 [M], accumulate only): += alpha * row sums of
+    op(a), computed by the same kernel (a ones column appended to op(b)).
     """
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
@@ -149,12 +151,14 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         atomic = 1 if accumulate else 0
         if splits > 1 and not accumulate:
             raise ValueError("split-K requires accumulate=True")
+        if bias_grad is not None and (trans_b or not accumulate):
+            raise ValueError("bias_grad needs accumulate=True, trans_b=False")
         _lib_call("hvk_gemm", int(trans_a), int(trans_b), M, N, K, _p(a),
                   a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0),
                   int(out.dtype == torch.float32), atomic, float(alpha),
                   float(beta), _p(bias), bm, act, _p(aux),
                   0 if aux is None else aux.stride(0), aux_act, int(splits),
-                  _s(a))
+                  _p(bias_grad), _s(a))
         return out
     A = a.float().t() if trans_a else a.float()
     B = b.float().t() if trans_b else b.float()
@@ -164,6 +168,8 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
                  bias.float().view(-1, 1))
     if accumulate:
         out += r.to(out.dtype)
+        if bias_grad is not None:
+            bias_grad += alpha * A.sum(1)
         return out
     if beta != 0.0:
         r = r + beta * out.float()
@@ -253,21 +259,17 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
         out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
     if _gpu(x):
         if needs_im2col(C, groups):
-            K = KH * KW * C
-            Kp = (K + 7) // 8 * 8
-            col = im2col(x, KH, KW, sliding, padding, out=_workspace(
-                ("col", id(w)), (N * OH * OW, Kp), x.dtype, x.device))
-            wp = w.reshape(OC, K)
-            if Kp != K:
-                wpad = _workspace(("wpad", id(w)), (OC, Kp), w.dtype, w.device)
-                wpad[:, K:].zero_()
-                wpad[:, :K].copy_(wp)
-                wp = wpad
-            gemm(col, wp, trans_b=True, bias=bias, act=act,
-                 out=out.view(N * OH * OW, OC))
-            if col_out is not None:
-                col_out["col"] = col
-                col_out["K"] = K
+            # packed (kw, c) runs: no im2col pass (csrc/kernels/gemm.hip)
+            run = KW * C
+            runp = (run + 7) // 8 * 8
+            wp = _workspace(("wrun", id(w)), (OC, KH, runp), w.dtype,
+                            w.device)
+            if runp != run:
+                wp[:, :, run:].zero_()
+            wp[:, :, :run].copy_(w.reshape(OC, KH, run))
+            _lib_call("hvk_conv_fwd_run", _p(x), _p(wp), _p(bias), _p(out),
+                      N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, act,
+                      _s(x))
             return out
         _lib_call("hvk_conv_fwd", _p(x), _p(w), _p(bias), _p(out), N, H, W, C,
                   OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, act, _s(x))
@@ -308,9 +310,10 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
 
 
 def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
-               splits=None, col=None):
-    """dw (float32 [OC,KH,KW,C/g]) += sum over pixels of dy (x) im2col(x).
-    ``col``: the forward's explicit im2col matrix (small-channel convs)."""
+               splits=None, col=None, dbias=None):
+    """dw (float32 [OC,KH,KW,C/g]) += sum over pixels of dy (x) im2col(x);
+    ``dbias`` (float32 [OC]) += sum over pixels of dy, fused into the same
+    GEMM.  ``col``: an explicit im2col matrix to use instead (optional)."""
     N, H, W, C = x.shape
     _, OH, OW, OC = dy.shape
     _, KH, KW, Cg = dw.shape
@@ -324,18 +327,29 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             M = N * OH * OW
             sp = splits or wgrad_splits(M, OC, K, 1)
             gemm(dy.reshape(M, OC), col[:, :K], trans_a=True,
-                 out=dw.view(OC, K), accumulate=True, splits=sp)
+                 out=dw.view(OC, K), accumulate=True, splits=sp,
+                 bias_grad=dbias)
+            return dw
+        if needs_im2col(C, groups):
+            runp = (KW * C + 7) // 8 * 8
+            sp = splits or wgrad_splits(N * OH * OW, OC, KH * runp + 1, 1)
+            _lib_call("hvk_conv_wgrad_run", _p(x), _p(dy), _p(dw), _p(dbias),
+                      N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW,
+                      int(sp), _s(x))
             return dw
         if splits is None:
             splits = wgrad_splits(N * OH * OW, OC // groups,
-                                  KH * KW * Cg, groups)
+                                  KH * KW * Cg + 1, groups)
         _lib_call("hvk_conv_wgrad", _p(x), _p(dy), _p(dw), N, H, W, C, OC, KH,
-                  KW, sy, sx, pt, pl, OH, OW, groups, int(splits), _s(x))
+                  KW, sy, sx, pt, pl, OH, OW, groups, int(splits), _p(dbias),
+                  _s(x))
         return dw
     xp = F.pad(_nchw(x), (pl, pr, pt, pb))
     g = torch.nn.grad.conv2d_weight(xp, (OC, Cg, KH, KW), _nchw(dy),
                                     stride=(sy, sx), groups=groups)
     dw += g.permute(0, 2, 3, 1)
+    if dbias is not None:
+        dbias += dy.float().reshape(-1, OC).sum(0)
     return dw
 
 

@@ -27,10 +27,12 @@ U = ctypes.c_uint
 
 _SIGS = {
     "hvk_gemm": [I, I, I, I, I, P, I, P, I, P, I, I, I, F, F, P, I, I, P, I, I,
-                 I, P],
+                 I, P, P],
     "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
     "hvk_conv_dgrad": [P, P, P] + [I] * 14 + [P, I, P],
-    "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P],
+    "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P, P],
+    "hvk_conv_fwd_run": [P, P, P, P] + [I] * 14 + [P],
+    "hvk_conv_wgrad_run": [P, P, P, P] + [I] * 14 + [P],
     "hvk_im2col": [P, P] + [I] * 13 + [P],
     "hvk_fill_minibatch": [P, I, P, I, I, I, L, P, P, P, I, P, P, P, P],
     "hvk_mean_disp_normalize": [P, I, P, P, P, I, L, L, P],
