@@ -35,6 +35,9 @@ class ActivationForward(AcceleratedUnit):
     def activation(self):
         return 0  # derivative handled by the paired backward unit
 
+    def package_export(self):
+        return {"act": self.ACT}
+
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
         import torch

@@ -31,6 +31,10 @@ class DropoutForward(AcceleratedUnit):
     def activation(self):
         return 0
 
+    def package_export(self):
+        # inference: dropout is the identity
+        return {}
+
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
         import torch

@@ -33,6 +33,10 @@ class LRNormalizerForward(AcceleratedUnit, _LRNParams):
     def activation(self):
         return 0
 
+    def package_export(self):
+        return {"alpha": self.alpha, "beta": self.beta, "k": self.k,
+                "n": self.n}
+
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
         import torch

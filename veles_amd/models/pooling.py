@@ -49,6 +49,9 @@ class Pooling(AcceleratedUnit):
         x = self.input.devmem
         return x.unsqueeze(-1) if x.dim() == 3 else x
 
+    def package_export(self):
+        return {"kx": self.kx, "ky": self.ky, "sliding": list(self.sliding)}
+
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
         shape = tuple(self.input.shape)
