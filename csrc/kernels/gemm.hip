@@ -33,6 +33,12 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 __device__ __forceinline__ uint4 zero4() { return make_uint4(0, 0, 0, 0); }
 
+// Source pages for LDS-DMA loads: out-of-bounds lanes read zeros, the fused
+// bias-gradient column reads (1, 0, ..., 0).
+__device__ __attribute__((aligned(16))) const uint16_t g_zero8[8] = {0};
+__device__ __attribute__((aligned(16))) const uint16_t g_ones8[8] = {
+    0x3F80, 0, 0, 0, 0, 0, 0, 0};
+
 __device__ __forceinline__ uint4 pack8(const uint16_t* e) {
   uint4 v;
   v.x = e[0] | ((uint32_t)e[1] << 16);
@@ -56,6 +62,11 @@ struct DenseK {
     c.row = p + (long long)(c.ok ? r : 0) * ld;
     return c;
   }
+  static constexpr bool kGlds = true;
+  __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
+  __device__ const uint16_t* src(const Ctx& c, int k) const {
+    return (c.ok && k < K) ? c.row + k : g_zero8;
+  }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec && k + 8 <= K) return *(const uint4*)(c.row + k);
@@ -75,6 +86,15 @@ struct DenseMN {
   struct Ctx { int c; };
   __device__ void group(int g) { p += (long long)g * gstride; }
   __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
+  static constexpr bool kGlds = true;
+  __device__ bool dma_ok() const {
+    return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
+  }
+  __device__ const uint16_t* src(const Ctx& cx, int k) const {
+    if (k >= K) return g_zero8;
+    if (cx.c < cols) return p + (long long)k * ld + cx.c;
+    return cx.c == ones_col ? g_ones8 : g_zero8;
+  }
   __device__ uint4 load(const Ctx& cx, int k) const {
     if (k >= K) return zero4();
     const uint16_t* row = p + (long long)k * ld;
@@ -125,6 +145,18 @@ struct ConvFwdA {
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return 0;
     return x[c.base + (ih * g.W + iw) * g.C + ch];
   }
+  static constexpr bool kGlds = true;
+  __device__ bool dma_ok() const { return vec; }
+  __device__ const uint16_t* src(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return g_zero8;
+    uint32_t t, ch, kh, kw;
+    fdivmod(k, g.fCg, t, ch);
+    fdivmod(t, g.fKW, kh, kw);
+    int ih = c.ih0 + (int)kh, iw = c.iw0 + (int)kw;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
+      return g_zero8;
+    return x + c.base + (ih * g.W + iw) * g.C + ch;
+  }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec) {  // Cg % 8 == 0: the 8 elements are 8 channels of one tap
@@ -173,6 +205,14 @@ struct ConvDgradA {
       return -1;
     return c.base + (oh * g.OW + ow) * g.OC;
   }
+  static constexpr bool kGlds = true;
+  __device__ bool dma_ok() const { return vec; }
+  __device__ const uint16_t* src(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return g_zero8;
+    uint32_t oc;
+    int off = tap(c, k, oc);
+    return off < 0 ? g_zero8 : dy + off + oc;
+  }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec) {
@@ -204,6 +244,16 @@ struct ConvDgradB {
   struct Ctx { int c; };
   __device__ void group(int gi) { ocoff = gi * g.OCg; }
   __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
+  static constexpr bool kGlds = true;
+  __device__ bool dma_ok() const { return vec && (g.Cg & 7) == 0; }
+  __device__ const uint16_t* src(const Ctx& cx, int k) const {
+    if (k >= K || cx.c >= g.Cg) return g_zero8;
+    uint32_t t, oc, kh, kw;
+    fdivmod(k, g.fOCg, t, oc);
+    fdivmod(t, g.fKW, kh, kw);
+    return w + (((long long)(ocoff + oc) * g.KH + kh) * g.KW + kw) * g.Cg +
+           cx.c;
+  }
   __device__ uint4 load(const Ctx& cx, int k) const {
     if (k >= K || cx.c >= g.Cg) return zero4();
     uint32_t t, oc, kh, kw;
@@ -236,6 +286,20 @@ struct ConvWgradB {
     fdivmod(t, g.fKW, kh, kw);
     c.kh = kh; c.kw = kw; c.ch = ch;
     return c;
+  }
+  static constexpr bool kGlds = true;
+  __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
+  __device__ const uint16_t* src(const Ctx& cx, int p) const {
+    if (!cx.ok || p >= K) return g_zero8;
+    if (cx.ok == 2) return g_ones8;
+    uint32_t n, rem, oh, ow;
+    fdivmod(p, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    int ih = oh * g.sy - g.pt + cx.kh, iw = ow * g.sx - g.pl + cx.kw;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
+      return g_zero8;
+    return x + (long long)n * g.H * g.W * g.C + coff + (ih * g.W + iw) * g.C +
+           cx.ch;
   }
   __device__ uint4 load(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return zero4();
@@ -293,6 +357,8 @@ struct RunGeom {
 };
 
 struct ConvFwdRunA {
+  static constexpr bool kGlds = false;
+  __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
   RunGeom r;
@@ -338,6 +404,8 @@ struct ConvFwdRunA {
 
 // wgrad B for small-channel convs: MN-major, rows = pixels, cols = (kh, j)
 struct ConvWgradRunB {
+  static constexpr bool kGlds = false;
+  __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
   RunGeom r;
@@ -512,6 +580,134 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
+  const int fr = lane & 15, fq = lane >> 4;
+  const int trq = fr >> 2, trp = fr & 3;
+  f32x4 acc[4][NB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto frag_k = [&](const uint16_t* s, int rowbase, int ks) -> bf16x8 {
+    int row = rowbase + fr;
+    int c = ks * 4 + fq;
+    return *(const bf16x8*)(s + row * 64 + ((c ^ (row & 7)) << 3));
+  };
+  auto frag_mn = [&](const uint16_t* s, int colbase, int ks) -> bf16x8 {
+    int k = ks * 32 + fq * 8 + trq;
+    int b = colbase >> 4;  // 32-B block of this 16-col tile
+    const uint16_t* p0 = s + k * 128 + ((b ^ hk(k)) << 4) + trp * 4;
+    const uint16_t* p1 = s + (k + 4) * 128 + ((b ^ hk(k + 4)) << 4) + trp * 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto compute = [&](const uint16_t* sA, const uint16_t* sB) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfv[NB];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (AK) af[i] = frag_k(sA, wm * 64 + i * 16, ks);
+        else af[i] = frag_mn(sA, wm * 64 + i * 16, ks);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        if constexpr (BKM) bfv[i] = frag_k(sB, wn * (BN_ / 2) + i * 16, ks);
+        else bfv[i] = frag_mn(sB, wn * (BN_ / 2) + i * 16, ks);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
+                                                              acc[i][j], 0, 0, 0);
+    }
+  };
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  bool done = false;
+  constexpr bool GL = LA::kGlds && LB::kGlds && (BKM || BN_ == 128);
+  if constexpr (GL) {
+    if (la.dma_ok() && lb.dma_ok()) {
+      // ---- LDS-DMA pipeline (global_load_lds_dwordx4): the next tile's
+      // loads stay in flight across the barrier; one counted vmcnt per tile.
+      constexpr int NIA = 4;               // DMA instructions / wave (A)
+      constexpr int NIB = BKM ? BN_ / 32 : 4;
+      const int w = __builtin_amdgcn_readfirstlane(wid);
+      typename LA::Ctx da[NIA];
+      typename LB::Ctx db[NIB];
+      int ka[NIA], kb[NIB];
+#pragma unroll
+      for (int i = 0; i < NIA; ++i) {
+        const int I = w * NIA + i;
+        if constexpr (AK) {
+          int row = 8 * I + (lane >> 3);
+          int c = (lane & 7) ^ ((lane >> 3) & 7);
+          da[i] = la.row_ctx(m0 + row);
+          ka[i] = 8 * c;
+        } else {
+          int hkv = ((lane >> 4) & 3) | (((I >> 1) & 1) << 2);
+          int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
+          da[i] = la.col_ctx(m0 + 8 * c);
+          ka[i] = 4 * I + (lane >> 4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NIB; ++i) {
+        const int I = w * NIB + i;
+        if constexpr (BKM) {
+          int row = 8 * I + (lane >> 3);
+          int c = (lane & 7) ^ ((lane >> 3) & 7);
+          db[i] = lb.row_ctx(n0 + row);
+          kb[i] = 8 * c;
+        } else {
+          int hkv = ((lane >> 4) & 3) | (((I >> 1) & 1) << 2);
+          int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
+          db[i] = lb.col_ctx(n0 + 8 * c);
+          kb[i] = 4 * I + (lane >> 4);
+        }
+      }
+      auto issue = [&](int k0, uint16_t* sA, uint16_t* sB) {
+#pragma unroll
+        for (int i = 0; i < NIA; ++i)
+          __builtin_amdgcn_global_load_lds(
+              (const void*)la.src(da[i], k0 + ka[i]),
+              (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
+              16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NIB; ++i)
+          __builtin_amdgcn_global_load_lds(
+              (const void*)lb.src(db[i], k0 + kb[i]),
+              (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 512),
+              16, 0, 0);
+      };
+      issue(kbeg, smem, smem + 2 * TILE);
+      for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) {
+          issue(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * TILE,
+                smem + (2 + (cur ^ 1)) * TILE);
+          if constexpr (NIA + NIB == 8)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        compute(smem + cur * TILE, smem + (2 + cur) * TILE);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      done = true;
+    }
+  }
+  if (!done) {
   typename LA::Ctx ca[4];
   typename LB::Ctx cb[4];
   if constexpr (AK) {
@@ -563,33 +759,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     }
   };
 
-  f32x4 acc[4][NB];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  const int trq = fr >> 2, trp = fr & 3;
-
-  auto frag_k = [&](const uint16_t* s, int rowbase, int ks) -> bf16x8 {
-    int row = rowbase + fr;
-    int c = ks * 4 + fq;
-    return *(const bf16x8*)(s + row * 64 + ((c ^ (row & 7)) << 3));
-  };
-  auto frag_mn = [&](const uint16_t* s, int colbase, int ks) -> bf16x8 {
-    int k = ks * 32 + fq * 8 + trq;
-    int b = colbase >> 4;  // 32-B block of this 16-col tile
-    const uint16_t* p0 = s + k * 128 + ((b ^ hk(k)) << 4) + trp * 4;
-    const uint16_t* p1 = s + (k + 4) * 128 + ((b ^ hk(k + 4)) << 4) + trp * 4;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, v);
-  };
-
-  int nk = (kend - kbeg + BK - 1) / BK;
   gload(kbeg);
   sstore(smem, smem + 2 * TILE);
   __syncthreads();
@@ -597,32 +766,12 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) gload(kbeg + (kt + 1) * BK);
-    const uint16_t* sA = smem + cur * TILE;
-    const uint16_t* sB = smem + (2 + cur) * TILE;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfv[NB];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (AK) af[i] = frag_k(sA, wm * 64 + i * 16, ks);
-        else af[i] = frag_mn(sA, wm * 64 + i * 16, ks);
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        if constexpr (BKM) bfv[i] = frag_k(sB, wn * (BN_ / 2) + i * 16, ks);
-        else bfv[i] = frag_mn(sB, wn * (BN_ / 2) + i * 16, ks);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
-                                                              acc[i][j], 0, 0, 0);
-    }
+    compute(smem + cur * TILE, smem + (2 + cur) * TILE);
     if (more) sstore(smem + (cur ^ 1) * TILE, smem + (2 + (cur ^ 1)) * TILE);
     __syncthreads();
     cur ^= 1;
   }
+  }  // register-staged path
 
   if (epi.atomic) {
     // split-K partial sums: f32 atomics straight from the accumulators
