@@ -523,6 +523,117 @@ __global__ void f32_to_bf16x4_kernel(const float4* in, uint2* out, long long n4)
 }
 }  // namespace
 
+
+// Space-to-depth for strided small-channel convs (AlexNet conv1: 227x227x3,
+// 11x11 stride 4 -> 57x57x48 image, 3x3 stride 1 kernel): y[n][Y][X][(dy*s +
+// dx)*C + c] = x[n][s*Y+dy-pt][s*X+dx-pl][c] (0 outside).  The result has
+// C2 = s*s*C % 8 == 0 channels, so the conv runs on the aligned LDS-DMA
+// implicit-GEMM path instead of per-element run gathers.
+__global__ void space_to_depth_kernel(const uint16_t* __restrict__ x,
+                                      uint4* __restrict__ y, int H, int W,
+                                      int C, int s, int pt, int pl, int H2,
+                                      int W2, int C2, long long chunks) {
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       q < chunks; q += (long long)gridDim.x * blockDim.x) {
+    long long e0 = q * 8;
+    long long pix = e0 / C2;
+    int c2 = (int)(e0 - pix * C2);
+    int X = (int)(pix % W2);
+    long long t = pix / W2;
+    int Y = (int)(t % H2);
+    long long n = t / H2;
+    uint16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      int cc = c2 + j;
+      int dy = cc / (s * C), r = cc - dy * s * C;
+      int dx = r / C, c = r - dx * C;
+      int iy = s * Y + dy - pt, ix = s * X + dx - pl;
+      v[j] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
+                 ? x[((n * H + iy) * W + ix) * C + c]
+                 : (uint16_t)0;
+    }
+    uint4 o;
+    o.x = v[0] | ((uint32_t)v[1] << 16);
+    o.y = v[2] | ((uint32_t)v[3] << 16);
+    o.z = v[4] | ((uint32_t)v[5] << 16);
+    o.w = v[6] | ((uint32_t)v[7] << 16);
+    y[q] = o;
+  }
+}
+
+
+// Adaptive solvers over the same flat buffers (Znicz GD "solvers":
+// docs/source/manualrst_veles_workflow_parameters.rst:543-578), one mode per
+// segment:
+//   0 momentum  v = m*v - lr*g ; w += v                         (s1 = v)
+//   1 adagrad   s1 += g^2 ; w -= lr*g/(sqrt(s1)+eps)
+//   2 adadelta  s1 = r*s1+(1-r)g^2 ; d = g*sqrt(s2+eps)/sqrt(s1+eps) ;
+//               s2 = r*s2+(1-r)d^2 ; w -= lr*d
+//   3 rprop     (iRprop-) s1 = step, s2 = previous gradient:
+//               same sign -> step*1.2 (<= 50), flip -> step*0.5 (>= 1e-6),
+//               g = 0 ; w -= sign(g)*step ; s2 = g
+struct SolverSeg {
+  long long begin, end;
+  float lr, decay, l1, moment;
+  int mode;
+  float eps, rho, pad;
+};
+__global__ void solver_kernel(float* w, float* grad, float* s1, float* s2,
+                              uint16_t* w_lp, const SolverSeg* segs, int nseg,
+                              long long total, float gscale, int zero_grad) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       i < total; i += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (segs[mid].begin <= i) lo = mid; else hi = mid - 1;
+    }
+    const SolverSeg sg = segs[lo];
+    float wi = w[i];
+    if (i < sg.end) {
+      float g = grad[i] * gscale;
+      if (sg.decay != 0.f)
+        g += sg.decay * ((1.f - sg.l1) * wi +
+                         sg.l1 * (wi > 0.f ? 1.f : (wi < 0.f ? -1.f : 0.f)));
+      switch (sg.mode) {
+        case 1: {
+          float a = s1[i] + g * g;
+          s1[i] = a;
+          wi -= sg.lr * g / (sqrtf(a) + sg.eps);
+          break;
+        }
+        case 2: {
+          float a = sg.rho * s1[i] + (1.f - sg.rho) * g * g;
+          float d = g * sqrtf(s2[i] + sg.eps) / sqrtf(a + sg.eps);
+          s1[i] = a;
+          s2[i] = sg.rho * s2[i] + (1.f - sg.rho) * d * d;
+          wi -= sg.lr * d;
+          break;
+        }
+        case 3: {
+          float step = s1[i] > 0.f ? s1[i] : sg.lr;
+          float pg = s2[i];
+          if (pg * g > 0.f) step = fminf(step * 1.2f, 50.f);
+          else if (pg * g < 0.f) { step = fmaxf(step * 0.5f, 1e-6f); g = 0.f; }
+          wi -= (g > 0.f ? step : (g < 0.f ? -step : 0.f));
+          s1[i] = step;
+          s2[i] = g;
+          break;
+        }
+        default: {
+          float v = sg.moment * s1[i] - sg.lr * g;
+          s1[i] = v;
+          wi += v;
+        }
+      }
+      w[i] = wi;
+    }
+    if (zero_grad) grad[i] = 0.f;
+    if (w_lp) w_lp[i] = f2bf(wi);
+  }
+}
+
 HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                                int start, int count, int max_mb,
                                long long sample_size, const float* mean,
@@ -590,6 +701,16 @@ HVK_API int hvk_sgd4(float* w, float* grad, float* mom, void* w_lp,
   hipLaunchKernelGGL(sgd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, s,
                      (float4*)w, (float4*)grad, (float4*)mom, (uint2*)w_lp,
                      (const SgdSeg*)segs, nseg, total / 4, gscale, zero_grad);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_solver(float* w, float* grad, float* s1, float* s2,
+                       void* w_lp, const void* segs, int nseg,
+                       long long total, float gscale, int zero_grad,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(solver_kernel, dim3(grid_for(total)), dim3(256), 0, s, w,
+                     grad, s1, s2, (uint16_t*)w_lp, (const SolverSeg*)segs,
+                     nseg, total, gscale, zero_grad);
   return (int)hipGetLastError();
 }
 
@@ -698,6 +819,18 @@ HVK_API int hvk_join(const void* const* ins, const int* lens, int nin, int dt,
   long long total = (long long)B * off;
   hipLaunchKernelGGL(join_kernel, dim3(grid_for(total)), dim3(256), 0, s, a, nin,
                      dt, out, B, off);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
+                               int C, int s, int pt, int pl, int H2, int W2,
+                               hipStream_t st) {
+  int C2 = s * s * C;
+  if (C2 % 8 || ((uintptr_t)y & 15)) return -1;
+  long long chunks = (long long)N * H2 * W2 * C2 / 8;
+  hipLaunchKernelGGL(space_to_depth_kernel, dim3(grid_for(chunks)), dim3(256),
+                     0, st, (const uint16_t*)x, (uint4*)y, H, W, C, s, pt, pl,
+                     H2, W2, C2, chunks);
   return (int)hipGetLastError();
 }
 

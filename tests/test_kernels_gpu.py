@@ -106,6 +106,10 @@ CONVS = [
     (3, 9, 11, 8, 16, 3, 2, (2, 1), (1, 0, 0, 1), 1),
     (1, 7, 7, 5, 6, 3, 3, (1, 1), (1, 1, 1, 1), 1),
     (2, 14, 14, 64, 64, 3, 3, (1, 1), (1, 1, 1, 1), 4),
+    # space-to-depth path (C*s*s % 8 == 0) with padding, and the run path
+    (2, 40, 37, 3, 64, 8, 8, (4, 4), (2, 1, 2, 1), 1),
+    (2, 20, 20, 2, 16, 5, 5, (2, 2), (2, 2, 2, 2), 1),
+    (2, 31, 29, 3, 32, 7, 7, (2, 2), (3, 3, 3, 3), 1),
 ]
 
 
@@ -269,8 +273,12 @@ def test_conv_im2col_path_fwd_and_wgrad():
     got = ops.conv_fwd(x.to(DEV), w.to(DEV), b.to(DEV), (s, s), (0, 0, 0, 0),
                        1, 3)
     close(got, ref, 1e-2)
-    ws = {"col": ops.im2col(x.to(DEV), k, k, (s, s), (0, 0, 0, 0))}
-    close(ws["col"], ops.im2col(x, k, k, (s, s), (0, 0, 0, 0)), 0)
+    close(ops.im2col(x.to(DEV), k, k, (s, s), (0, 0, 0, 0)),
+          ops.im2col(x, k, k, (s, s), (0, 0, 0, 0)), 0)
+    ws = {}
+    ops.conv_fwd(x.to(DEV), w.to(DEV), b.to(DEV), (s, s), (0, 0, 0, 0), 1, 3,
+                 col_out=ws)
+    assert isinstance(ws["col"], ops.S2DImage)  # reused by the wgrad
     OH, OW = ops.conv_out_size(H, W, k, k, (s, s), (0, 0, 0, 0))
     dy = rnd(N, OH, OW, OC, seed=2)
     dref = torch.zeros(OC, k, k, C)

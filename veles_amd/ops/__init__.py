@@ -203,11 +203,12 @@ def _nhwc(x):
 _WS = {}
 
 
-def _workspace(key, shape, dtype, device):
+def _workspace(key, shape, dtype, device, zero=False):
     t = _WS.get(key)
     if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or \
             t.device != device:
-        t = torch.empty(shape, dtype=dtype, device=device)
+        t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype,
+                                                   device=device)
         _WS[key] = t
     return t
 
@@ -216,6 +217,53 @@ def needs_im2col(C, groups):
     """Small-channel convs (C/groups % 8 != 0, e.g. RGB input) run as an
     explicit bf16 im2col + dense MFMA GEMM instead of per-element gathers."""
     return groups == 1 and C % 8 != 0
+
+
+class S2DImage(object):
+    """The space-to-depth image of a strided small-channel conv input,
+    kept by the forward pass for the weight-gradient GEMM."""
+    __slots__ = ("x", "s")
+
+    def __init__(self, x, s):
+        self.x = x
+        self.s = s
+
+
+def s2d_factor(C, groups, sliding, KH, KW):
+    """Stride s when a conv is better run as space-to-depth (C -> s*s*C
+    channels, stride 1, ceil(K/s) taps): small C, equal strides, s*s*C a
+    multiple of 8 (the aligned LDS-DMA loaders), kernel at least s wide."""
+    sx, sy = sliding
+    if groups != 1 or C % 8 == 0 or sx != sy or sx < 2:
+        return 0
+    if (sx * sx * C) % 8 or KH < sx or KW < sx:
+        return 0
+    return sx
+
+
+def _s2d_geometry(H, W, KH, KW, s, padding):
+    OH, OW = conv_out_size(H, W, KH, KW, (s, s), padding)
+    KH2, KW2 = -(-KH // s), -(-KW // s)
+    return OH, OW, KH2, KW2, OH - 1 + KH2, OW - 1 + KW2
+
+
+def space_to_depth(x, s, KH, KW, padding):
+    N, H, W, C = x.shape
+    _, _, KH2, KW2, H2, W2 = _s2d_geometry(H, W, KH, KW, s, padding)
+    y = torch.empty(N, H2, W2, s * s * C, dtype=x.dtype, device=x.device)
+    _lib_call("hvk_space_to_depth", _p(x), _p(y), N, H, W, C, s, padding[1],
+              padding[0], H2, W2, _s(x))
+    return y
+
+
+def _s2d_weights(w, s):
+    OC, KH, KW, C = w.shape
+    KH2, KW2 = -(-KH // s), -(-KW // s)
+    wp = _workspace(("s2dw", id(w)), (OC, KH2 * s, KW2 * s, C), w.dtype,
+                    w.device, zero=True)
+    wp[:, :KH, :KW].copy_(w)   # taps past KH/KW stay zero
+    return wp.view(OC, KH2, s, KW2, s, C).permute(0, 1, 3, 2, 4, 5) \
+        .reshape(OC, KH2, KW2, s * s * C)
 
 
 def im2col(x, KH, KW, sliding, padding, out=None):
@@ -258,6 +306,19 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
     if out is None:
         out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
     if _gpu(x):
+        s2 = s2d_factor(C, groups, sliding, KH, KW)
+        if s2:
+            # strided RGB conv as a stride-1 conv on the space-to-depth image
+            _, _, KH2, KW2, H2, W2 = _s2d_geometry(H, W, KH, KW, s2, padding)
+            x2 = space_to_depth(x, s2, KH, KW, padding)
+            w2 = _s2d_weights(w, s2)
+            C2 = s2 * s2 * C
+            _lib_call("hvk_conv_fwd", _p(x2), _p(w2), _p(bias), _p(out), N,
+                      H2, W2, C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, act,
+                      _s(x))
+            if col_out is not None:
+                col_out["col"] = S2DImage(x2, s2)
+            return out
         if needs_im2col(C, groups):
             # packed (kw, c) runs: no im2col pass (csrc/kernels/gemm.hip)
             run = KW * C
@@ -322,6 +383,26 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     if dw.dtype != torch.float32:
         raise TypeError("conv_wgrad accumulates into float32")
     if _gpu(x):
+        s2 = s2d_factor(C, groups, sliding, KH, KW)
+        if s2:
+            x2 = col.x if isinstance(col, S2DImage) else \
+                space_to_depth(x, s2, KH, KW, padding)
+            H2, W2, C2 = x2.shape[1], x2.shape[2], x2.shape[3]
+            KH2, KW2 = -(-KH // s2), -(-KW // s2)
+            dw2 = _workspace(("s2dg", dw.data_ptr()), (OC, KH2, KW2, C2),
+                             torch.float32, dw.device)
+            dw2.zero_()
+            sp = splits or wgrad_splits(N * OH * OW, OC, KH2 * KW2 * C2 + 1,
+                                        1)
+            _lib_call("hvk_conv_wgrad", _p(x2), _p(dy), _p(dw2), N, H2, W2,
+                      C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, int(sp),
+                      _p(dbias), _s(x))
+            full = dw2.view(OC, KH2, KW2, s2, s2, C).permute(
+                0, 1, 3, 2, 4, 5).reshape(OC, KH2 * s2, KW2 * s2, C)
+            dw += full[:, :KH, :KW]
+            return dw
+        if isinstance(col, S2DImage):
+            col = None
         if col is not None:
             K = KH * KW * Cg
             M = N * OH * OW
@@ -646,6 +727,66 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False):
             v = v + m * mom[b:e]
             mom[b:e] = v
         ws += v
+    if w_lp is not None:
+        w_lp.copy_(w.to(w_lp.dtype))
+    if zero_grad:
+        grad.zero_()
+    return w
+
+
+SOLVERS = {"momentum": 0, "adagrad": 1, "adadelta": 2, "rprop": 3}
+
+
+def solver_update(w, grad, s1, s2, segs, w_lp=None, gscale=1.0,
+                  zero_grad=False):
+    """Fused multi-segment update with a solver per segment.
+
+    segs: [(begin, end, lr, decay, l1_vs_l2, moment, mode, eps, rho)], modes
+    in :data:`SOLVERS` (csrc/kernels/elementwise.hip ``solver_kernel``)."""
+    n = w.numel()
+    if _gpu(w):
+        key = ("solver", tuple(segs), str(w.device))
+        st = _SEG_CACHE.get(key)
+        if st is None:
+            raw = b"".join(struct.pack(
+                "<qqffffifff", int(b), int(e), float(lr), float(d), float(l1),
+                float(m), int(mode), float(eps), float(rho), 0.0)
+                for b, e, lr, d, l1, m, mode, eps, rho in segs)
+            st = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(
+                w.device)
+            _SEG_CACHE[key] = st
+        _lib_call("hvk_solver", _p(w), _p(grad), _p(s1), _p(s2), _p(w_lp),
+                  _p(st), len(segs), n, float(gscale), int(zero_grad), _s(w))
+        return w
+    for b, e, lr, d, l1, m, mode, eps, rho in segs:
+        ws = w[b:e]
+        g = grad[b:e] * gscale
+        if d:
+            g = g + d * ((1 - l1) * ws + l1 * torch.sign(ws))
+        a = s1[b:e]
+        if mode == 1:
+            a += g * g
+            ws -= lr * g / (a.sqrt() + eps)
+        elif mode == 2:
+            c = s2[b:e]
+            a.mul_(rho).add_((1 - rho) * g * g)
+            dd = g * (c + eps).sqrt() / (a + eps).sqrt()
+            c.mul_(rho).add_((1 - rho) * dd * dd)
+            ws -= lr * dd
+        elif mode == 3:
+            prev = s2[b:e]
+            step = torch.where(a > 0, a, torch.full_like(a, lr))
+            same = prev * g > 0
+            flip = prev * g < 0
+            step = torch.where(same, (step * 1.2).clamp(max=50.0), step)
+            step = torch.where(flip, (step * 0.5).clamp(min=1e-6), step)
+            g = torch.where(flip, torch.zeros_like(g), g)
+            ws -= torch.sign(g) * step
+            a.copy_(step)
+            prev.copy_(g)
+        else:
+            a.mul_(m).sub_(lr * g)
+            ws += a
     if w_lp is not None:
         w_lp.copy_(w.to(w_lp.dtype))
     if zero_grad:

@@ -50,6 +50,8 @@ _SIGS = {
     "hvk_u64_to_uniform": [P, P, L, F, F, P],
     "hvk_join": [P, P, I, I, P, I, P],
     "hvk_cast": [P, I, P, I, L, F, P],
+    "hvk_solver": [P, P, P, P, P, P, I, L, F, I, P],
+    "hvk_space_to_depth": [P, P] + [I] * 9 + [P],
     "hvk_pool_fwd": [P, P, P] + [I] * 13 + [P],
     "hvk_pool_bwd": [P, P, P] + [I] * 13 + [P, I, P],
     "hvk_lrn_fwd": [P, P, L, I, I, F, F, F, P],
