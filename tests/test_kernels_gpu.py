@@ -305,3 +305,24 @@ def test_fill_minibatch_odd_sample():
     ops.fill_minibatch(src.to(DEV), sh.to(DEV), 2, 6, dg, mean=mean.to(DEV),
                        rdisp=rd.to(DEV))
     close(dg, d, 1e-2)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_solver_kernel(mode):
+    n = 4096 + 13
+    w0 = torch.randn(n)
+    segs = [(0, 2000, 0.1, 1e-3, 0.2, 0.9, mode, 1e-6, 0.95),
+            (2000, n, 0.05, 0.0, 0.0, 0.5, mode, 1e-6, 0.9)]
+    wc, s1c, s2c = w0.clone(), torch.zeros(n), torch.zeros(n)
+    wg, s1g, s2g = w0.to(DEV), torch.zeros(n, device=DEV), \
+        torch.zeros(n, device=DEV)
+    lp = torch.zeros(n, dtype=BF, device=DEV)
+    for it in range(3):
+        g = torch.randn(n, generator=torch.Generator().manual_seed(it))
+        ops.solver_update(wc, g.clone(), s1c, s2c, segs)
+        gg = g.to(DEV)
+        ops.solver_update(wg, gg, s1g, s2g, segs, w_lp=lp, zero_grad=True)
+        assert float(gg.abs().max()) == 0.0
+    close(wg, wc, 1e-5)
+    close(s1g, s1c, 1e-5)
+    close(lp.float(), wc, 1e-2)

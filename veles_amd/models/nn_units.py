@@ -201,6 +201,24 @@ class GradientDescentBase(AcceleratedUnit):
         self.gradient_moment_bias = kwargs.get("gradient_moment_bias",
                                                self.gradient_moment)
         self.accumulate_gradient = kwargs.get("accumulate_gradient", False)
+        # adaptive solvers (one of momentum / adagrad / adadelta per unit)
+        solvers = kwargs.get("solvers", ("momentum",))
+        if isinstance(solvers, str):
+            solvers = (solvers,)
+        self.solvers = set(solvers)
+        unknown = self.solvers - set(ops.SOLVERS) - {"fast"}
+        if unknown:
+            raise ValueError("Unknown solvers %s" % sorted(unknown))
+        self.adagrad_epsilon = kwargs.get("adagrad_epsilon", 1e-8)
+        self.adadelta_momentum = kwargs.get("adadelta_momentum", 0.9)
+        self.adadelta_epsilon = kwargs.get("adadelta_epsilon", 1e-8)
+        self.adadelta_adom = kwargs.get("adadelta_adom", 0.3)
+        self.fast_learning_rate = kwargs.get("fast_learning_rate", 0.02)
+        self.factor_ortho = kwargs.get("factor_ortho", 0)
+        self.variant_gradient = kwargs.get("variant_gradient", True)
+        self.variant_moment_gradient = kwargs.get(
+            "variant_moment_gradient", True)
+        self.last_minibatch = kwargs.get("last_minibatch", False)
         self.need_err_input = kwargs.get("need_err_input", True)
         self.apply_gradient = kwargs.get("apply_gradient", True)
         self.err_input = Array(shallow_pickle=True)
@@ -224,6 +242,20 @@ class GradientDescentBase(AcceleratedUnit):
                     self.l1_vs_l2_bias, self.gradient_moment_bias)
         return (self.learning_rate, self.weights_decay, self.l1_vs_l2,
                 self.gradient_moment)
+
+    SOLVER = None  # a subclass may force one (RPropAll2All: "rprop")
+
+    def solver(self):
+        """(mode, eps, rho) of this unit's update rule (ops.SOLVERS)."""
+        names = getattr(self, "solvers", ("momentum",))
+        if self.SOLVER is not None:
+            return ops.SOLVERS[self.SOLVER], 0.0, 0.0
+        if "adadelta" in names:
+            return (ops.SOLVERS["adadelta"], self.adadelta_epsilon,
+                    self.adadelta_momentum)
+        if "adagrad" in names:
+            return ops.SOLVERS["adagrad"], self.adagrad_epsilon, 0.0
+        return 0, 0.0, 0.0
 
     @property
     def forward(self):

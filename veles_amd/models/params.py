@@ -64,10 +64,13 @@ class ParameterStore(object):
         self._launched = set()
         self.buckets = []
         self._segs = None
+        self._solver_segs = None
         self._seg_key = None
         self.steps = 0
         self.accumulate = 1
         self._accum_count = 0
+        # callables run after every applied update (e.g. ZeroFiller masks)
+        self.post_update_hooks = []
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -109,6 +112,7 @@ class ParameterStore(object):
         self.master = torch.zeros(total, dtype=torch.float32, device=tdev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=tdev)
         self.mom = torch.zeros(total, dtype=torch.float32, device=tdev)
+        self.mom2 = None  # second solver state (adadelta / rprop), lazily
         lp_dtype = dev.compute_dtype if gpu else torch.float32
         self.lp = torch.zeros(total, dtype=lp_dtype, device=tdev) \
             if lp_dtype != torch.float32 else None
@@ -189,14 +193,25 @@ class ParameterStore(object):
             segs.append((p.offset, p.offset + p.size, lr, decay, l1, moment))
         return segs
 
+    def _solver_of(self, p):
+        fn = getattr(p.gd, "solver", None)
+        return fn() if fn is not None else (0, 0.0, 0.0)
+
     def _cached_segments(self):
-        key = tuple((id(p.gd), p.gd.hyper(p.is_bias)) for p in self.params
-                    if p.gd is not None)
+        key = tuple((id(p.gd), p.gd.hyper(p.is_bias), self._solver_of(p))
+                    for p in self.params if p.gd is not None)
         if key != self._seg_key:
             self._seg_key = key
             self._segs = self.segments()
             # cover alignment gaps so every float4 group has a segment
             self._segs = _cover(self._segs, self.total)
+            solv = {p.offset: self._solver_of(p) for p in self.params
+                    if p.gd is not None}
+            self._solver_segs = None
+            if any(m for m, _, _ in solv.values()):
+                self._solver_segs = [
+                    seg + solv.get(seg[0], (0, 0.0, 0.0))
+                    for seg in self._segs]
         return self._segs
 
     def apply(self, gscale=1.0):
@@ -215,7 +230,14 @@ class ParameterStore(object):
             for w in self._works:
                 w.wait()
         segs = self._cached_segments()
-        if segs:
+        if segs and self._solver_segs is not None:
+            import torch
+            if self.mom2 is None:
+                self.mom2 = torch.zeros_like(self.mom)
+            ops.solver_update(self.master, self.grad, self.mom, self.mom2,
+                              self._solver_segs, w_lp=self.lp,
+                              gscale=gscale / self.accumulate, zero_grad=True)
+        elif segs:
             # the fused kernel also zeroes the gradient buffer
             ops.sgd_update(self.master, self.grad, self.mom, segs,
                            w_lp=self.lp, gscale=gscale / self.accumulate,
@@ -227,6 +249,8 @@ class ParameterStore(object):
         self._ready.clear()
         self._accum_count = 0
         self.steps += 1
+        for hook in self.post_update_hooks:
+            hook()
         return True
 
     def sync_host(self):
@@ -236,12 +260,19 @@ class ParameterStore(object):
                 p.host = p.master.detach().float().cpu().numpy().copy()
 
     def state_dict(self):
-        return {"master": self.master.detach().cpu(),
-                "mom": self.mom.detach().cpu(), "steps": self.steps}
+        st = {"master": self.master.detach().cpu(),
+              "mom": self.mom.detach().cpu(), "steps": self.steps}
+        if self.mom2 is not None:
+            st["mom2"] = self.mom2.detach().cpu()
+        return st
 
     def load_state_dict(self, st):
         self.master.copy_(st["master"])
         self.mom.copy_(st["mom"])
+        if "mom2" in st:
+            import torch
+            self.mom2 = torch.zeros_like(self.mom)
+            self.mom2.copy_(st["mom2"])
         if self.lp is not None:
             self.lp.copy_(self.master)
         self.steps = st.get("steps", 0)

@@ -195,6 +195,13 @@ class Depooling(AcceleratedUnit):
         self.output = Array(shallow_pickle=True)
         self.demand("input", "input_offset", "output_shape_source")
 
+    def initialize(self, device=None, **kwargs):
+        super().initialize(device=device, **kwargs)
+        src = self.output_shape_source
+        x = self.input.devmem
+        self.output.devmem = torch.zeros(tuple(src.shape), dtype=x.dtype,
+                                         device=x.device)
+
     def run(self):
         x = self.input.devmem
         src = self.output_shape_source.devmem
@@ -202,6 +209,35 @@ class Depooling(AcceleratedUnit):
         out.index_put_((self.input_offset.devmem.reshape(-1).long(),),
                        x.reshape(-1), accumulate=True)
         self.output.devmem = out.view(src.shape)
+
+
+class GDDepooling(GradientDescentBase):
+    """Backward of Depooling: gather err_output at the recorded offsets."""
+    MAPPING = "depooling"
+
+    def run(self):
+        if not self.need_err_input:
+            return
+        fwd = self.forward
+        off = fwd.input_offset.devmem.reshape(-1).long()
+        err = self.err_output.devmem.reshape(-1)
+        self.err_input.devmem = err[off].view(self.input.devmem.shape)
+
+
+class GDPoolDepool(GradientDescentBase):
+    """Backward of the stochastic pool-depool units: the output keeps the
+    input geometry, so err passes through at the sampled positions only."""
+    MAPPING = "stochastic_pool_depool"
+
+    def run(self):
+        if not self.need_err_input:
+            return
+        fwd = self.forward
+        err = self.err_output.devmem
+        off = fwd.input_offset.devmem.reshape(-1).long()
+        ei = torch.zeros(err.numel(), dtype=err.dtype, device=err.device)
+        ei[off] = err.reshape(-1)[off]
+        self.err_input.devmem = ei.view(err.shape)
 
 
 class GDPooling(GradientDescentBase):

@@ -41,8 +41,16 @@ from veles_amd.models.lr_adjust import LearningRateAdjust
 from veles_amd.models.normalization_units import (
     LRNormalizerBackward, LRNormalizerForward)
 from veles_amd.models.pooling import (
-    AvgPooling, GDAvgPooling, GDMaxAbsPooling, GDMaxPooling, MaxAbsPooling,
-    MaxPooling, StochasticAbsPooling, StochasticPooling)
+    AvgPooling, Depooling, GDAvgPooling, GDDepooling, GDMaxAbsPooling,
+    GDMaxPooling, GDPoolDepool, MaxAbsPooling, MaxPooling,
+    StochasticAbsPooling, StochasticAbsPoolingDepooling, StochasticPooling,
+    StochasticPoolingDepooling)
+from veles_amd.models.channel_splitting import (
+    ChannelMerger, ChannelSplitter, GDChannelMerger, GDChannelSplitter)
+from veles_amd.models.cutter import Cutter, GDCutter
+from veles_amd.models.deconv import Deconv, GDDeconv
+from veles_amd.models.rprop_all2all import RPropAll2All
+from veles_amd.models.weights_zerofilling import GDZeroFiller, ZeroFiller
 from veles_amd.plumbing import Repeater
 from veles_amd.snapshotter import SnapshotterRegistry, SnapshotterToFile
 from veles_amd.utils.config import Config, fix_contents
@@ -67,6 +75,16 @@ LAYER_TYPES = {
     "maxabs_pooling": (MaxAbsPooling, GDMaxAbsPooling),
     "stochastic_pooling": (StochasticPooling, GDMaxPooling),
     "stochastic_abs_pooling": (StochasticAbsPooling, GDMaxAbsPooling),
+    "stochastic_pool_depool": (StochasticPoolingDepooling, GDPoolDepool),
+    "stochastic_abs_pool_depool": (StochasticAbsPoolingDepooling,
+                                   GDPoolDepool),
+    "depooling": (Depooling, GDDepooling),
+    "deconv": (Deconv, GDDeconv),
+    "cutter": (Cutter, GDCutter),
+    "channel_splitter": (ChannelSplitter, GDChannelSplitter),
+    "channel_merger": (ChannelMerger, GDChannelMerger),
+    "zero_filter": (ZeroFiller, GDZeroFiller),
+    "rprop_all2all": (All2All, RPropAll2All),
     "norm": (LRNormalizerForward, LRNormalizerBackward),
     "dropout": (DropoutForward, DropoutBackward),
     "activation_tanh": (act_units.ForwardTanh, act_units.BackwardTanh),
@@ -203,6 +221,7 @@ class StandardWorkflow(AcceleratedWorkflow):
 
     def link_forwards(self, init_attrs, *parents):
         prev = None
+        pools, convs, weighted = [], [], None
         for i, layer in enumerate(self.layers):
             typ = layer["type"]
             fcls, _ = LAYER_TYPES[typ]
@@ -218,6 +237,29 @@ class StandardWorkflow(AcceleratedWorkflow):
                 unit.link_attrs(prev, ("input", "output"))
             if isinstance(unit, DropoutForward):
                 unit.link_attrs(self.loader, "minibatch_class")
+            # encoder/decoder pairing (auto-encoders): depooling inverts the
+            # latest pooling, deconv the latest conv (LIFO)
+            if isinstance(unit, Depooling):
+                if not pools:
+                    raise ValueError("depooling without a pooling before it")
+                pool = pools.pop()
+                unit.link_attrs(pool, "input_offset")
+                unit.output_shape_source = pool.input
+            elif isinstance(unit, (MaxPooling, MaxAbsPooling,
+                                   StochasticPooling)) and \
+                    not isinstance(unit, StochasticPoolingDepooling):
+                pools.append(unit)
+            if isinstance(unit, Deconv):
+                if unit.output_shape_source is None and \
+                        unit.n_channels is None and convs:
+                    unit.output_shape_source = convs.pop()
+            elif isinstance(unit, Conv):
+                convs.append(unit)
+            if isinstance(unit, ZeroFiller) and unit.weights_unit is None:
+                unit.weights_unit = weighted
+            if getattr(unit, "has_weights", False) and \
+                    hasattr(unit, "register_params"):
+                weighted = unit
             self.forwards.append(unit)
             prev = unit
             del allowed
