@@ -90,6 +90,8 @@ class Main(object):
             wf = SnapshotterToFile.import_(args.snapshot)
             wf.workflow = self.launcher
             self.launcher.add_ref(wf)
+            if args.test and hasattr(wf, "switch_to_testing"):
+                wf.switch_to_testing()
             restored = True
         else:
             if args.test:
@@ -124,7 +126,7 @@ class Main(object):
         from veles_amd import __version__
         from veles_amd.cmdline import make_parser
         from veles_amd.utils.config import root
-        args = make_parser().parse_args(self.argv)
+        args = make_parser().parse_intermixed_args(self.argv)
         self.args = args
         if args.version:
             print("veles_amd", __version__)
@@ -146,6 +148,7 @@ class Main(object):
         if args.force_cpu:
             root.common.engine.force_cpu = tuple(args.force_cpu.split(","))
         root.common.engine.sync_run = args.sync_run
+        root.common.loader.train_ratio = args.train_ratio
         module = self._import_workflow(args.workflow)
         cfg = args.config
         if cfg == "-":

@@ -7,3 +7,13 @@ from veles_amd.loader.fullbatch import (  # noqa: F401
     FullBatchLoader, FullBatchLoaderMSE)
 from veles_amd.loader.synthetic import (  # noqa: F401
     SyntheticImageLoader, SyntheticMSELoader)
+from veles_amd.loader.image import (  # noqa: F401
+    FullBatchFileImageLoader, FullBatchAutoLabelFileImageLoader,
+    FileListImageLoader, FullBatchImageLoaderMSE)
+from veles_amd.loader.pickles import PicklesImageFullBatchLoader  # noqa
+from veles_amd.loader.ensemble import EnsembleLoader  # noqa: F401
+from veles_amd.loader.loader_hdf5 import FullBatchHDF5Loader  # noqa: F401
+from veles_amd.loader.interactive import (  # noqa: F401
+    InteractiveLoader, RestfulLoader)
+from veles_amd.loader.saver import (  # noqa: F401
+    MinibatchesSaver, MinibatchesLoader)

@@ -119,7 +119,9 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
             "normalization_parameters", {})
         self.normalizer = make_normalizer(self.normalization_type,
                                           **self.normalization_parameters)
-        self.train_ratio = float(kwargs.get("train_ratio", 1.0))
+        from veles_amd.utils.config import root, get
+        self.train_ratio = float(kwargs.get(
+            "train_ratio", get(root.common.loader.train_ratio, 1.0)))
         # data parallel sharding (set by the launcher / process group)
         self.rank = int(kwargs.get("rank", 0))
         self.world_size = int(kwargs.get("world_size", 1))
@@ -207,6 +209,8 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
                                  "create_minibatch_data()")
         if self.class_lengths[TRAIN] > 0 and not self.restored_from_snapshot:
             self.analyze_dataset()
+        elif self.normalizer is not None and self.normalizer.is_initialized:
+            self.apply_derived_normalization()
         if not self.restored_from_snapshot or self.testing:
             self.shuffled_indices.reset()
             self.shuffle()
@@ -218,6 +222,10 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
 
     def on_initialized(self, **kwargs):
         """Hook: allocate device buffers after the host state is ready."""
+
+    def apply_derived_normalization(self):
+        """Hook: a loader without TRAIN data that shares an analysed
+        normalizer (``derive_from``) prepares to apply it."""
 
     def run(self):
         self.pending_minibatches_.pop(None, None)

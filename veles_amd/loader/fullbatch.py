@@ -123,6 +123,18 @@ class FullBatchLoader(Loader, IFullBatchLoader):
             self.original_data.reset(d)
             self._affine = None
 
+    def apply_derived_normalization(self):
+        aff = self.normalizer.affine()
+        if aff is None:
+            d = self.original_data.mem.astype(numpy.float32)
+            self.normalizer.normalize(d)
+            self.original_data.reset(d)
+            self._affine = None
+            return
+        feat = int(numpy.prod(self.sample_shape))
+        self._affine = tuple(numpy.broadcast_to(
+            numpy.asarray(a, numpy.float32), (feat,)).copy() for a in aff)
+
     def normalize_minibatch(self):
         pass  # folded into the gather
 

@@ -66,9 +66,11 @@ class SyntheticImageLoader(FullBatchLoader):
         n = sum(self.class_lengths)
         feat = int(numpy.prod(self._sample_shape))
         rs = numpy.random.RandomState(self.seed)
-        labels = rs.randint(0, self.n_classes, n).astype(numpy.int32)
+        # prototypes first: the same seed gives the same classes whatever
+        # the set sizes (a test-only loader matches the training one)
         protos = rs.randint(32, 224, (self.n_classes, feat)).astype(
             numpy.float32)
+        labels = rs.randint(0, self.n_classes, n).astype(numpy.int32)
         self.original_labels = labels
         if self._want_device():
             dev = self.device.torch_device

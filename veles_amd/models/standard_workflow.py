@@ -189,9 +189,47 @@ class StandardWorkflow(AcceleratedWorkflow):
                 last_gd = self.link_lr_adjuster(last_gd)
             self.link_loop(last_gd)
         else:
+            last = self.link_output_collector(last)
             self.link_loop(last)
         self.link_end_point(last)
 
+    def link_output_collector(self, *parents):
+        from veles_amd.models.result_collector import OutputCollector
+        self.output_collector = OutputCollector(self)
+        self.output_collector.link_from(*parents)
+        self.output_collector.link_attrs(self.forwards[-1], "output")
+        self.output_collector.link_attrs(
+            self.loader, "minibatch_class", "minibatch_size",
+            "minibatch_indices")
+        self.output_collector.labels_source = self.loader
+        return self.output_collector
+
+    def switch_to_testing(self):
+        """Turn a trained (e.g. snapshot-restored) workflow into a test run
+        (``--test -w snapshot``): serve the TEST class once, no backward, no
+        snapshots, collect ``Output`` / ``Labels`` into the results."""
+        from veles_amd.mutable import Bool
+        self.testing = True
+        self.loader.testing = True
+        for gd in self.gds:
+            gd.gate_block = Bool(True)
+        if self.lr_adjuster is not None:
+            self.lr_adjuster.gate_block = Bool(True)
+        if self.snapshotter is not None:
+            self.snapshotter.gate_block = Bool(True)
+        if getattr(self, "output_collector", None) is None:
+            self.link_output_collector(self.decision)
+            self.repeater.unlink_from(self.gds[0] if self.gds else
+                                      self.decision)
+            self.repeater.link_from(self.output_collector)
+            # finish only after the last test minibatch was collected
+            for u in list(self.end_point.links_from):
+                self.end_point.unlink_from(u)
+            self.end_point.link_from(self.output_collector)
+        d = self.decision
+        d.max_epochs = d.epoch_number + 1
+        d.fail_iterations = None
+        d.complete <<= False
     def link_repeater(self, *parents):
         self.repeater = Repeater(self)
         self.repeater.link_from(*parents)

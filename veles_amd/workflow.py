@@ -187,6 +187,11 @@ class Workflow(Container):
             self.device = getattr(self.workflow, "device", None)
         kwargs["device"] = self.device
         pending = list(self.units_in_dependency_order)
+        # a re-initialized workflow runs again (FireStarter semantics)
+        self._finished_ = False
+        for u in pending:
+            if u is not self:
+                u.stopped = False
         if self._restored_from_snapshot:
             for u in pending:
                 if not getattr(u, "_remembers_gates", True):
