@@ -153,6 +153,11 @@ class SnapshotterToFile(SnapshotterBase):
         super().__init__(workflow, **kwargs)
         self.directory = kwargs.get("directory",
                                     get(root.common.dirs.snapshots, "."))
+        # ensemble members / GA children share a config: keep their
+        # snapshots apart
+        idx = get(root.common.ensemble.model_index, None)
+        if idx is not None:
+            self.prefix = "%s_model%d" % (self.prefix, int(idx))
         if self.compression == "snappy":
             self.warning("snappy is unavailable; using gz")
             self.compression = "gz"
@@ -163,7 +168,7 @@ class SnapshotterToFile(SnapshotterBase):
         rel = "%s_%s.%d.pickle%s" % (self.prefix, self.suffix, PROTOCOL, ext)
         self._destination = os.path.abspath(os.path.join(self.directory, rel))
         self.info("Snapshotting to %s", self._destination)
-        tmp = self._destination + ".tmp"
+        tmp = "%s.%d.tmp" % (self._destination, os.getpid())
         with self.WRITE_CODECS[self.compression](
                 tmp, self.compression_level) as f:
             pickle.dump(self.workflow, f, protocol=PROTOCOL)
@@ -171,12 +176,10 @@ class SnapshotterToFile(SnapshotterBase):
         self.check_snapshot_size(os.path.getsize(self._destination))
         link = os.path.join(self.directory, "%s_current.%d.pickle%s" % (
             self.prefix, PROTOCOL, ext))
+        tmp_link = "%s.%d.tmp" % (link, os.getpid())
         try:
-            os.remove(link)
-        except OSError:
-            pass
-        try:
-            os.symlink(rel, link)
+            os.symlink(rel, tmp_link)
+            os.replace(tmp_link, link)  # atomic for concurrent writers
         except OSError:
             pass
         return self._destination
