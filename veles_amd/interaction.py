@@ -1,0 +1,76 @@
+"""Interactive shell into a running workflow (reference
+veles/interaction.py:49-95 IPython embed on a keypress, and the manhole
+UNIX-socket REPL).
+
+``Shell`` is a unit; when it runs and ``root.common.interactive`` is set, or
+when the process receives SIGUSR2 (``install_signal``), it opens a Python
+console (``code.interact``) with ``workflow`` / ``root`` / the unit in
+scope.  With ``socket_path`` the console is served on a UNIX socket
+instead (one client at a time), so a detached training run can be
+inspected with ``nc -U``.
+"""
+from __future__ import annotations
+
+import code
+import os
+import signal
+import socket
+import threading
+
+from veles_amd.units import Unit
+from veles_amd.utils.config import get, root
+
+__all__ = ["Shell"]
+
+
+class Shell(Unit):
+    MAPPING = "shell"
+
+    def __init__(self, workflow, **kwargs):
+        kwargs.setdefault("view_group", "SERVICE")
+        super().__init__(workflow, **kwargs)
+        self.socket_path = kwargs.get("socket_path")
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.requested_ = False
+
+    def namespace(self):
+        return {"workflow": self.workflow, "root": root, "shell": self,
+                "units": {u.name: u for u in self.workflow}}
+
+    def install_signal(self):
+        def handler(signum, frame):
+            self.requested_ = True
+        signal.signal(signal.SIGUSR2, handler)
+
+    def run(self):
+        if not (self.requested_ or get(root.common.interactive, False)):
+            return
+        self.requested_ = False
+        if self.socket_path:
+            threading.Thread(target=self.serve_socket, daemon=True).start()
+        else:
+            code.interact(banner="veles_amd shell (Ctrl-D to resume)",
+                          local=self.namespace())
+
+    def serve_socket(self):
+        path = self.socket_path
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+        srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        srv.bind(path)
+        srv.listen(1)
+        conn, _ = srv.accept()
+        f = conn.makefile("rw")
+        console = code.InteractiveConsole(self.namespace())
+        f.write(">>> ")
+        f.flush()
+        for line in f:
+            more = console.push(line.rstrip("\n"))
+            f.write("... " if more else ">>> ")
+            f.flush()
+        conn.close()
+        srv.close()

@@ -53,6 +53,17 @@ class StartPoint(UttermostPoint):
         super().__init__(workflow, **kwargs)
 
 
+class _Deferred(object):
+    """A scheduler entry that calls ``fn`` when its turn comes."""
+    __slots__ = ("fn",)
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def _check_gate_and_run(self, src):
+        self.fn()
+
+
 class EndPoint(UttermostPoint):
     """Ends the pipeline; notifies the workflow that it finished."""
     hide_from_registry = True
@@ -62,7 +73,15 @@ class EndPoint(UttermostPoint):
         super().__init__(workflow, **kwargs)
 
     def run(self):
-        self.workflow.on_workflow_finished()
+        from veles_amd.units import _Scheduler
+        sched = _Scheduler.current()
+        if sched is None:
+            self.workflow.on_workflow_finished()
+            return
+        # let the units already notified in this wave (siblings of the end
+        # point, e.g. plotters of the final epoch) run before finishing
+        sched.pending.append((_Deferred(self.workflow.on_workflow_finished),
+                              self))
 
     def generate_data_for_master(self):
         return True

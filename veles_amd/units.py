@@ -20,13 +20,14 @@ firing rules SURVEY Appendix B items 1-3):
 Execution model (MI355X-first, differs from the reference): the reference
 calls a single successor inline and fans out through Twisted worker threads.
 Here notifications are processed by a per-thread *trampoline* (an explicit
-work stack) so a training loop of any length never grows the Python stack,
+work queue, FIFO) so a training loop of any length never grows the Python stack,
 and all units of a rank run on one host thread that enqueues HIP work on one
 compute stream (stream order = data-dependency order, no host sync needed).
 ``root.common.engine.parallel_fanout = True`` restores thread-pool fan-out.
 """
 from __future__ import annotations
 
+import collections
 import threading
 import time
 import uuid
@@ -84,7 +85,11 @@ class _Scheduler(object):
         return stack[-1] if stack else None
 
     def __init__(self):
-        self.pending = []
+        # FIFO: the siblings of a fan-out all run before any of their
+        # successors (the single-thread equivalent of the reference running
+        # fan-out successors concurrently, units.py:500-505); a LIFO would
+        # starve a side branch (e.g. a plotter) behind the training loop
+        self.pending = collections.deque()
 
     def __enter__(self):
         stack = getattr(self._tls, "stack", None)
@@ -100,7 +105,7 @@ class _Scheduler(object):
     def drain(self):
         pending = self.pending
         while pending:
-            dst, src = pending.pop()
+            dst, src = pending.popleft()
             dst._check_gate_and_run(src)
 
 
@@ -539,11 +544,11 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
         sched = _Scheduler.current()
         if sched is None:
             with _Scheduler() as sched:
-                for dst in reversed(targets):
+                for dst in targets:
                     sched.pending.append((dst, self))
                 sched.drain()
         else:
-            for dst in reversed(targets):
+            for dst in targets:
                 sched.pending.append((dst, self))
 
     def _check_gate_and_run(self, src):
