@@ -99,19 +99,22 @@ def main():
                 base = json.load(f).get("published", {}).get("value")
         except Exception:
             base = None
-        out = {"metric": BASELINE_METRIC, "value": round(value, 2),
+        shape = "x".join(str(v) for v in wf.loader.sample_shape)
+        metric = BASELINE_METRIC if args.model == "alexnet" else \
+            "samples/sec (whole node) %s training" % args.model
+        out = {"metric": metric, "value": round(value, 2),
                "unit": "samples/s", "n_gpus": dp.world_size,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(dt / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak",
                "vs_baseline": (value / base) if base else None,
                "dtype": "bf16" if backend == "hip" else "fp32",
-               "data": "synthetic (uint8 227x227x3 images resident in HBM, "
-                       "random-init weights)",
+               "data": "synthetic (uint8 %s images resident in HBM, "
+                       "random-init weights)" % shape,
                "config": {"model": args.model, "global_batch": global_batch,
                           "per_gpu_batch": args.batch, "seq_len": None,
                           "parallelism": "dp%d" % dp.world_size,
-                          "image": "227x227x3", "grad_allreduce":
+                          "image": shape, "grad_allreduce":
                           "bucketed RCCL, overlapped with backward"}}
         print(json.dumps(out), flush=True)
         if args.profile_json:

@@ -56,7 +56,7 @@ struct DenseK {
   int rows, K, ld, vec;
   struct Ctx { const uint16_t* row; int ok; };
   __device__ void group(int g) { p += (long long)g * gstride; }
-  __device__ Ctx row_ctx(int r) const {
+  __device__ __forceinline__ Ctx row_ctx(int r) const {
     Ctx c;
     c.ok = r < rows;
     c.row = p + (long long)(c.ok ? r : 0) * ld;
@@ -64,10 +64,10 @@ struct DenseK {
   }
   static constexpr bool kGlds = true;
   __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
-  __device__ const uint16_t* src(const Ctx& c, int k) const {
+  __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     return (c.ok && k < K) ? c.row + k : g_zero8;
   }
-  __device__ uint4 load(const Ctx& c, int k) const {
+  __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec && k + 8 <= K) return *(const uint4*)(c.row + k);
     uint16_t e[8];
@@ -85,17 +85,17 @@ struct DenseMN {
   int ones_col;  // >= 0: column of ones appended at index cols (bias grad)
   struct Ctx { int c; };
   __device__ void group(int g) { p += (long long)g * gstride; }
-  __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
+  __device__ __forceinline__ Ctx col_ctx(int c) const { return Ctx{c}; }
   static constexpr bool kGlds = true;
   __device__ bool dma_ok() const {
     return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
   }
-  __device__ const uint16_t* src(const Ctx& cx, int k) const {
+  __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int k) const {
     if (k >= K) return g_zero8;
     if (cx.c < cols) return p + (long long)k * ld + cx.c;
     return cx.c == ones_col ? g_ones8 : g_zero8;
   }
-  __device__ uint4 load(const Ctx& cx, int k) const {
+  __device__ __forceinline__ uint4 load(const Ctx& cx, int k) const {
     if (k >= K) return zero4();
     const uint16_t* row = p + (long long)k * ld;
     if (vec && cx.c + 8 <= cols) return *(const uint4*)(row + cx.c);
@@ -114,7 +114,7 @@ struct ConvGeom {
   int N, H, W, C, Cg;       // input NHWC, C total, Cg per group
   int OH, OW, OC, OCg;      // output
   int KH, KW, sy, sx, pt, pl;
-  FastDiv fOW, fOHOW, fW, fHW, fCg, fOCg, fKW;
+  FastDiv fOW, fOHOW, fW, fHW, fCg, fOCg, fKW, fSy, fSx;
 };
 
 // conv forward A: rows = output pixels (n,oh,ow), k = (kh,kw,c)
@@ -125,7 +125,7 @@ struct ConvFwdA {
   int coff;
   struct Ctx { int base, ih0, iw0, ok; };
   __device__ void group(int gi) { coff = gi * g.Cg; }
-  __device__ Ctx row_ctx(int m) const {
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
     c.ok = m < M;
     uint32_t mm = c.ok ? m : 0, n, rem, oh, ow;
@@ -147,7 +147,7 @@ struct ConvFwdA {
   }
   static constexpr bool kGlds = true;
   __device__ bool dma_ok() const { return vec; }
-  __device__ const uint16_t* src(const Ctx& c, int k) const {
+  __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t t, ch, kh, kw;
     fdivmod(k, g.fCg, t, ch);
@@ -157,7 +157,7 @@ struct ConvFwdA {
       return g_zero8;
     return x + c.base + (ih * g.W + iw) * g.C + ch;
   }
-  __device__ uint4 load(const Ctx& c, int k) const {
+  __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec) {  // Cg % 8 == 0: the 8 elements are 8 channels of one tap
       uint32_t t, ch, kh, kw;
@@ -183,7 +183,7 @@ struct ConvDgradA {
   int coff;
   struct Ctx { int base, hp, wp, ok; };
   __device__ void group(int gi) { coff = gi * g.OCg; }
-  __device__ Ctx row_ctx(int m) const {
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
     c.ok = m < M;
     uint32_t mm = c.ok ? m : 0, n, rem, h, w;
@@ -200,20 +200,24 @@ struct ConvDgradA {
     fdivmod(t, g.fKW, kh, kw);
     int ohs = c.hp - (int)kh, ows = c.wp - (int)kw;
     if (ohs < 0 || ows < 0) return -1;
-    int oh = ohs / g.sy, ow = ows / g.sx;
+    if (g.sy == 1 && g.sx == 1) {  // stride 1: no divisions (uniform branch)
+      if (ohs >= g.OH || ows >= g.OW) return -1;
+      return c.base + (ohs * g.OW + ows) * g.OC;
+    }
+    int oh = (int)fdiv((uint32_t)ohs, g.fSy), ow = (int)fdiv((uint32_t)ows, g.fSx);
     if (oh * g.sy != ohs || ow * g.sx != ows || oh >= g.OH || ow >= g.OW)
       return -1;
     return c.base + (oh * g.OW + ow) * g.OC;
   }
   static constexpr bool kGlds = true;
   __device__ bool dma_ok() const { return vec; }
-  __device__ const uint16_t* src(const Ctx& c, int k) const {
+  __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t oc;
     int off = tap(c, k, oc);
     return off < 0 ? g_zero8 : dy + off + oc;
   }
-  __device__ uint4 load(const Ctx& c, int k) const {
+  __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec) {
       uint32_t oc;
@@ -221,6 +225,18 @@ struct ConvDgradA {
       if (off < 0) return zero4();
       return *(const uint4*)(dy + off + oc);
     }
+    return zero4();  // OC % 8 != 0 uses ConvDgradAS
+  }
+};
+
+// scalar-gather variant for OC % 8 != 0 (a separate instantiation: its
+// 8-tap loop pushes the loader struct into scratch, which must not happen
+// to the common vectorised kernels)
+struct ConvDgradAS : ConvDgradA {
+  static constexpr bool kGlds = false;
+  __device__ bool dma_ok() const { return false; }
+  __device__ uint4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
     uint16_t e[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -235,40 +251,6 @@ struct ConvDgradA {
   }
 };
 
-// conv dgrad B: MN-major, rows k = (kh,kw,oc) gathered from W[oc][kh][kw][c]
-struct ConvDgradB {
-  const uint16_t* w;
-  ConvGeom g;
-  int K, vec;
-  int ocoff;
-  struct Ctx { int c; };
-  __device__ void group(int gi) { ocoff = gi * g.OCg; }
-  __device__ Ctx col_ctx(int c) const { return Ctx{c}; }
-  static constexpr bool kGlds = true;
-  __device__ bool dma_ok() const { return vec && (g.Cg & 7) == 0; }
-  __device__ const uint16_t* src(const Ctx& cx, int k) const {
-    if (k >= K || cx.c >= g.Cg) return g_zero8;
-    uint32_t t, oc, kh, kw;
-    fdivmod(k, g.fOCg, t, oc);
-    fdivmod(t, g.fKW, kh, kw);
-    return w + (((long long)(ocoff + oc) * g.KH + kh) * g.KW + kw) * g.Cg +
-           cx.c;
-  }
-  __device__ uint4 load(const Ctx& cx, int k) const {
-    if (k >= K || cx.c >= g.Cg) return zero4();
-    uint32_t t, oc, kh, kw;
-    fdivmod(k, g.fOCg, t, oc);
-    fdivmod(t, g.fKW, kh, kw);
-    const uint16_t* row =
-        w + (((long long)(ocoff + oc) * g.KH + kh) * g.KW + kw) * g.Cg;
-    if (vec && cx.c + 8 <= g.Cg) return *(const uint4*)(row + cx.c);
-    uint16_t e[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) e[j] = (cx.c + j < g.Cg) ? row[cx.c + j] : 0;
-    return pack8(e);
-  }
-};
-
 // conv wgrad B: MN-major, rows = output pixel p, cols kk = (kh,kw,c)
 struct ConvWgradB {
   const uint16_t* x;
@@ -278,7 +260,7 @@ struct ConvWgradB {
   int ones;  // append a ones column at index KK (bias gradient)
   struct Ctx { int kh, kw, ch, ok; };
   __device__ void group(int gi) { coff = gi * g.Cg; }
-  __device__ Ctx col_ctx(int kk) const {
+  __device__ __forceinline__ Ctx col_ctx(int kk) const {
     Ctx c;
     c.ok = kk < KK ? 1 : ((ones && kk == KK) ? 2 : 0);
     uint32_t t, ch, kh, kw;
@@ -289,7 +271,7 @@ struct ConvWgradB {
   }
   static constexpr bool kGlds = true;
   __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
-  __device__ const uint16_t* src(const Ctx& cx, int p) const {
+  __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return g_zero8;
     if (cx.ok == 2) return g_ones8;
     uint32_t n, rem, oh, ow;
@@ -301,7 +283,7 @@ struct ConvWgradB {
     return x + (long long)n * g.H * g.W * g.C + coff + (ih * g.W + iw) * g.C +
            cx.ch;
   }
-  __device__ uint4 load(const Ctx& cx, int p) const {
+  __device__ __forceinline__ uint4 load(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return zero4();
     if (cx.ok == 2) return make_uint4(0x3F80u, 0, 0, 0);
     uint32_t n, rem, oh, ow;
@@ -365,7 +347,7 @@ struct ConvFwdRunA {
   int M, K;  // K = KH * RUNP
   struct Ctx { long long base; int ih0, iw0, ok, full; };
   __device__ void group(int) {}
-  __device__ Ctx row_ctx(int m) const {
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
     c.ok = m < M;
     uint32_t mm = c.ok ? m : 0, n, rem, oh, ow;
@@ -377,7 +359,7 @@ struct ConvFwdRunA {
     c.full = c.iw0 >= 0 && c.iw0 + g.KW <= g.W;
     return c;
   }
-  __device__ uint4 load(const Ctx& c, int k) const {
+  __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     uint32_t kh, j;
     fdivmod(k, r.fRUNP, kh, j);
@@ -412,7 +394,7 @@ struct ConvWgradRunB {
   int K /* pixels */, KK /* KH*RUNP */, ones;
   struct Ctx { int kh, j, ok; };
   __device__ void group(int) {}
-  __device__ Ctx col_ctx(int kk) const {
+  __device__ __forceinline__ Ctx col_ctx(int kk) const {
     Ctx c;
     c.ok = kk < KK ? 1 : ((ones && kk == KK) ? 2 : 0);
     uint32_t kh, j;
@@ -421,7 +403,7 @@ struct ConvWgradRunB {
     c.j = j;
     return c;
   }
-  __device__ uint4 load(const Ctx& cx, int p) const {
+  __device__ __forceinline__ uint4 load(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return zero4();
     if (cx.ok == 2) return make_uint4(0x3F80u, 0, 0, 0);
     uint32_t n, rem, oh, ow;
@@ -555,7 +537,7 @@ __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2
 template <class LA, bool AK, class LB, bool BKM, int BN_>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
-            int tiles_n) {
+            int tiles_n, int tiles, int splits) {
   constexpr int NB = BN_ / 32;          // B chunks per thread / MFMA n-tiles
   constexpr int CPR = BN_ / 8;          // MN-major B: chunks per k-row
   constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
@@ -564,14 +546,19 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   constexpr int SMEM_BYTES = (4 * TILE * 2 > 128 * (BN_ + 4) * 4)
                                  ? 4 * TILE * 2 : 128 * (BN_ + 4) * 4;
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES / 2];
+  // 1-D grid over (group, split, tile), tile fastest.  Bijective XCD remap
+  // (cdna_hip_programming.md T1): each XCD gets a contiguous wgid range, so
+  // the tiles of one K split (which share the A rows / B columns of that
+  // split) and neighbouring output tiles share one L2.
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
-  // bijective XCD remap (cdna_hip_programming.md T1)
   int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = wgid / tiles_n, tn = wgid - (wgid / tiles_n) * tiles_n;
-  const int gi = blockIdx.z;
-  const int kbeg = blockIdx.y * k_split;
+  const int tile = wgid % tiles;
+  const int gs = wgid / tiles;
+  const int gi = gs / splits;
+  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  const int kbeg = (gs - gi * splits) * k_split;
   const int kend = min(K, kbeg + k_split);
   if (kbeg >= kend) return;
   la.group(gi);
@@ -629,7 +616,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   bool done = false;
-  constexpr bool GL = LA::kGlds && LB::kGlds && (BKM || BN_ == 128);
+  constexpr bool GL = LA::kGlds && LB::kGlds;
   if constexpr (GL) {
     if (la.dma_ok() && lb.dma_ok()) {
       // ---- LDS-DMA pipeline (global_load_lds_dwordx4): the next tile's
@@ -640,6 +627,9 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       typename LA::Ctx da[NIA];
       typename LB::Ctx db[NIB];
       int ka[NIA], kb[NIB];
+      // MN-major B at BN = 64: the DMA image keeps the 256-B rows of the
+      // 128-wide layout; the chunks of columns >= 64 read the zero page
+      bool bz[NIB];
 #pragma unroll
       for (int i = 0; i < NIA; ++i) {
         const int I = w * NIA + i;
@@ -666,9 +656,11 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         } else {
           int hkv = ((lane >> 4) & 3) | (((I >> 1) & 1) << 2);
           int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
-          db[i] = lb.col_ctx(n0 + 8 * c);
+          bz[i] = BN_ < 128 && 8 * c >= BN_;
+          db[i] = lb.col_ctx(n0 + (bz[i] ? 0 : 8 * c));
           kb[i] = 4 * I + (lane >> 4);
         }
+        if constexpr (BKM) bz[i] = false;
       }
       auto issue = [&](int k0, uint16_t* sA, uint16_t* sB) {
 #pragma unroll
@@ -680,7 +672,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 #pragma unroll
         for (int i = 0; i < NIB; ++i)
           __builtin_amdgcn_global_load_lds(
-              (const void*)lb.src(db[i], k0 + kb[i]),
+              (const void*)(bz[i] ? g_zero8 : lb.src(db[i], k0 + kb[i])),
               (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 512),
               16, 0, 0);
       };
@@ -812,11 +804,13 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
 }
 
-// Tile width: 64 when it pads N less than 128 does (N = 48, 96->?, 192).
+// Tile width: 64 only when the 128-wide tile would waste more than 1/8 of
+// its columns (N = 48, 96, 192, 432); wide N keeps 128 so the A operand is
+// re-read by half as many column tiles (weight-gradient GEMMs, N = taps*C).
 inline bool use_bn64(int N) {
   int w128 = (N + 127) / 128 * 128 - N;
   int w64 = (N + 63) / 64 * 64 - N;
-  return w64 < w128;
+  return w64 < w128 && w128 * 8 > N;
 }
 
 template <class LA, bool AK, class LB, bool BKM>
@@ -829,13 +823,16 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   int k_split = (K + splits - 1) / splits;
   k_split = (k_split + BK - 1) / BK * BK;
   splits = (K + k_split - 1) / k_split;
-  dim3 grid(tiles_m * tiles_n, splits, groups);
+  const int tiles = tiles_m * tiles_n;
+  dim3 grid((unsigned)((long long)tiles * splits * groups));
   if (n64)
     hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64>), grid, dim3(NTHR), 0,
-                       s, la, lb, epi, M, N, K, k_split, tiles_n);
+                       s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
+                       splits);
   else
     hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128>), grid, dim3(NTHR), 0,
-                       s, la, lb, epi, M, N, K, k_split, tiles_n);
+                       s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
+                       splits);
   return hipGetLastError();
 }
 
@@ -849,6 +846,8 @@ ConvGeom make_geom(int N, int H, int W, int C, int OC, int KH, int KW, int sy,
   g.fW = make_fastdiv(W); g.fHW = make_fastdiv(H * W);
   g.fCg = make_fastdiv(g.Cg); g.fOCg = make_fastdiv(g.OCg);
   g.fKW = make_fastdiv(KW);
+  g.fSy = make_fastdiv(sy);
+  g.fSx = make_fastdiv(sx);
   return g;
 }
 
@@ -979,21 +978,32 @@ HVK_API int hvk_conv_fwd(const void* X, const void* Wt, const float* bias,
                                                    groups, s);
 }
 
-// dX = conv_transpose(dY, W); optional multiply by act_bwd(aux) (the
-// derivative of the previous layer's activation, aux = its output).
-HVK_API int hvk_conv_dgrad(const void* dY, const void* Wt, void* dX, int N,
-                           int H, int W, int C, int OC, int KH, int KW, int sy,
-                           int sx, int pt, int pl, int OH, int OW, int groups,
-                           const void* aux, int aux_act, hipStream_t s) {
+
+// dgrad with the weights pre-permuted to Wt[g][kh][kw][oc][c] (c fastest):
+// the B operand (rows k = (kh, kw, oc)) is then a dense MN-major matrix
+// [K][Cg] per group -- full 128-B lines through the LDS-DMA path instead of
+// one 16-B piece per weight row.
+HVK_API int hvk_conv_dgrad_t(const void* dY, const void* Wt, void* dX, int N,
+                             int H, int W, int C, int OC, int KH, int KW,
+                             int sy, int sx, int pt, int pl, int OH, int OW,
+                             int groups, const void* aux, int aux_act,
+                             hipStream_t s) {
   ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
   int M = N * H * W, K = KH * KW * g.OCg;
-  ConvDgradA la{(const uint16_t*)dY, g, M, K,
-                (g.OCg % 8 == 0 && OC % 8 == 0 && al16(dY)) ? 1 : 0, 0};
-  ConvDgradB lb{(const uint16_t*)Wt, g, K, (g.Cg % 8 == 0 && al16(Wt)) ? 1 : 0, 0};
+  const int vec = (g.OCg % 8 == 0 && OC % 8 == 0 && al16(dY)) ? 1 : 0;
+  ConvDgradA la{(const uint16_t*)dY, g, M, K, vec, 0};
+  DenseMN lb{(const uint16_t*)Wt, (long long)K * g.Cg, g.Cg, K, g.Cg,
+             (g.Cg % 8 == 0 && al16(Wt)) ? 1 : 0, -1};
   Epi e = make_epi(dX, C, M, g.Cg, 0, 0, 1.f, 0.f, nullptr, 0, 0, aux, C, aux_act);
   e.gcol = g.Cg;
-  return (int)launch<ConvDgradA, true, ConvDgradB, false>(la, lb, e, M, g.Cg, K,
-                                                          1, groups, s);
+  if (!vec) {
+    ConvDgradAS ls;
+    static_cast<ConvDgradA&>(ls) = la;
+    return (int)launch<ConvDgradAS, true, DenseMN, false>(ls, lb, e, M, g.Cg,
+                                                          K, 1, groups, s);
+  }
+  return (int)launch<ConvDgradA, true, DenseMN, false>(la, lb, e, M, g.Cg, K,
+                                                       1, groups, s);
 }
 
 // dW[oc][kh][kw][c] (+)= sum_p dY[p][oc] * im2col(X)[p][kk]  (f32, atomics)

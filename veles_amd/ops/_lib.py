@@ -29,7 +29,7 @@ _SIGS = {
     "hvk_gemm": [I, I, I, I, I, P, I, P, I, P, I, I, I, F, F, P, I, I, P, I, I,
                  I, P, P],
     "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
-    "hvk_conv_dgrad": [P, P, P] + [I] * 14 + [P, I, P],
+    "hvk_conv_dgrad_t": [P, P, P] + [I] * 14 + [P, I, P],
     "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P, P],
     "hvk_conv_fwd_run": [P, P, P, P] + [I] * 14 + [P],
     "hvk_conv_wgrad_run": [P, P, P, P] + [I] * 14 + [P],
