@@ -530,35 +530,37 @@ __global__ void f32_to_bf16x4_kernel(const float4* in, uint2* out, long long n4)
 // C2 = s*s*C % 8 == 0 channels, so the conv runs on the aligned LDS-DMA
 // implicit-GEMM path instead of per-element run gathers.
 __global__ void space_to_depth_kernel(const uint16_t* __restrict__ x,
-                                      uint4* __restrict__ y, int H, int W,
+                                      uint16_t* __restrict__ y, int H, int W,
                                       int C, int s, int pt, int pl, int H2,
-                                      int W2, int C2, long long chunks) {
+                                      int W2, FastDiv fS, FastDiv fW2,
+                                      FastDiv fH2, long long runs) {
+  // one thread = one (output pixel, dy) run: the s*C contiguous input
+  // elements x[n][s*Y+dy-pt][s*X-pl .. +s)[0..C) land contiguously at
+  // channel offset dy*s*C of the output pixel
+  const int RUN = s * C;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-       q < chunks; q += (long long)gridDim.x * blockDim.x) {
-    long long e0 = q * 8;
-    long long pix = e0 / C2;
-    int c2 = (int)(e0 - pix * C2);
-    int X = (int)(pix % W2);
-    long long t = pix / W2;
-    int Y = (int)(t % H2);
-    long long n = t / H2;
-    uint16_t v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int cc = c2 + j;
-      int dy = cc / (s * C), r = cc - dy * s * C;
-      int dx = r / C, c = r - dx * C;
-      int iy = s * Y + dy - pt, ix = s * X + dx - pl;
-      v[j] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
-                 ? x[((n * H + iy) * W + ix) * C + c]
-                 : (uint16_t)0;
+       q < runs; q += (long long)gridDim.x * blockDim.x) {
+    uint32_t pix, dy, X, t, Y, n;
+    fdivmod((uint32_t)q, fS, pix, dy);
+    fdivmod(pix, fW2, t, X);
+    fdivmod(t, fH2, n, Y);
+    uint16_t* out = y + (long long)pix * s * RUN + dy * RUN;
+    int iy = s * (int)Y + (int)dy - pt, ix0 = s * (int)X - pl;
+    if (iy < 0 || iy >= H) {
+      for (int e = 0; e < RUN; ++e) out[e] = 0;
+      continue;
     }
-    uint4 o;
-    o.x = v[0] | ((uint32_t)v[1] << 16);
-    o.y = v[2] | ((uint32_t)v[3] << 16);
-    o.z = v[4] | ((uint32_t)v[5] << 16);
-    o.w = v[6] | ((uint32_t)v[7] << 16);
-    y[q] = o;
+    const uint16_t* in = x + ((long long)n * H + iy) * W * C;
+    if (ix0 >= 0 && ix0 + s <= W) {
+      const uint16_t* src = in + (long long)ix0 * C;
+      for (int e = 0; e < RUN; ++e) out[e] = src[e];
+    } else {
+      for (int e = 0; e < RUN; ++e) {
+        int ix = ix0 + e / C;
+        out[e] = (ix >= 0 && ix < W) ? in[(long long)ix * C + e % C]
+                                     : (uint16_t)0;
+      }
+    }
   }
 }
 
@@ -634,6 +636,61 @@ __global__ void solver_kernel(float* w, float* grad, float* s1, float* s2,
   }
 }
 
+
+// uint8 -> bf16 rows of any length (e.g. 227*227*3): 8 elements per lane,
+// unaligned 8-B loads / 16-B stores (gfx950 unaligned access), per-feature
+// mean / rdisp as float4 pairs; the row tail is scalar.
+__global__ void fill_rows_u8_bf16_kernel(const uint8_t* __restrict__ src,
+                                         const int* shuffled, int start,
+                                         int count, long long sample_size,
+                                         const float* __restrict__ mean,
+                                         const float* __restrict__ rdisp,
+                                         uint16_t* __restrict__ dst,
+                                         const int* labels, int* labels_out,
+                                         int* idx_out) {
+  const int i = blockIdx.y;
+  const int sidx = i < count ? shuffled[start + i] : -1;
+  const uint8_t* in = src + (long long)(sidx < 0 ? 0 : sidx) * sample_size;
+  uint16_t* out = dst + (long long)i * sample_size;
+  const long long nv = sample_size / 8;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       v < nv; v += (long long)gridDim.x * blockDim.x) {
+    const long long j = v * 8;
+    uint16_t o[8];
+    if (sidx >= 0) {
+      uint8_t b[8];
+      __builtin_memcpy(b, in + j, 8);
+      float4 m0 = make_float4(0.f, 0.f, 0.f, 0.f), m1 = m0;
+      float4 r0 = make_float4(1.f, 1.f, 1.f, 1.f), r1 = r0;
+      if (mean) { m0 = ((const float4*)(mean + j))[0]; m1 = ((const float4*)(mean + j))[1]; }
+      if (rdisp) { r0 = ((const float4*)(rdisp + j))[0]; r1 = ((const float4*)(rdisp + j))[1]; }
+      const float mm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+      const float rr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = f2bf(((float)b[q] - mm[q]) * rr[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = 0;
+    }
+    __builtin_memcpy(out + j, o, 16);
+  }
+  if (blockIdx.x == 0) {
+    for (long long j = nv * 8 + threadIdx.x; j < sample_size; j += blockDim.x) {
+      float x = 0.f;
+      if (sidx >= 0) {
+        x = (float)in[j];
+        if (mean) x -= mean[j];
+        if (rdisp) x *= rdisp[j];
+      }
+      out[j] = f2bf(x);
+    }
+    if (threadIdx.x == 0) {
+      if (labels_out) labels_out[i] = (sidx >= 0 && labels) ? labels[sidx] : -1;
+      if (idx_out) idx_out[i] = sidx;
+    }
+  }
+}
+
 HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                                int start, int count, int max_mb,
                                long long sample_size, const float* mean,
@@ -647,6 +704,16 @@ HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                        dim3(256), 0, s, (const uint8_t*)src, shuffled, start,
                        count, max_mb, sample_size, mean, rdisp, (uint16_t*)dst,
                        labels, labels_out, idx_out);
+  } else if (src_dt == DT_U8 && dst_dt == DT_BF16 && max_mb <= 65535 &&
+             (!mean || ((uintptr_t)mean & 15) == 0) &&
+             (!rdisp || ((uintptr_t)rdisp & 15) == 0)) {
+    long long gx = (sample_size / 8 + 255) / 256;
+    if (gx > 1024) gx = 1024;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(fill_rows_u8_bf16_kernel, dim3((int)gx, max_mb),
+                       dim3(256), 0, s, (const uint8_t*)src, shuffled, start,
+                       count, sample_size, mean, rdisp, (uint16_t*)dst, labels,
+                       labels_out, idx_out);
   } else if (max_mb <= 65535) {
     long long gx = (sample_size + 1023) / 1024;
     if (gx > 1024) gx = 1024;
@@ -826,11 +893,13 @@ HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
                                int C, int s, int pt, int pl, int H2, int W2,
                                hipStream_t st) {
   int C2 = s * s * C;
-  if (C2 % 8 || ((uintptr_t)y & 15)) return -1;
-  long long chunks = (long long)N * H2 * W2 * C2 / 8;
-  hipLaunchKernelGGL(space_to_depth_kernel, dim3(grid_for(chunks)), dim3(256),
-                     0, st, (const uint16_t*)x, (uint4*)y, H, W, C, s, pt, pl,
-                     H2, W2, C2, chunks);
+  if (C2 % 8) return -1;
+  long long runs = (long long)N * H2 * W2 * s;
+  if (runs >= (1ll << 32)) return -1;
+  hipLaunchKernelGGL(space_to_depth_kernel, dim3(grid_for(runs)), dim3(256), 0,
+                     st, (const uint16_t*)x, (uint16_t*)y, H, W, C, s, pt, pl,
+                     H2, W2, make_fastdiv(s), make_fastdiv(W2),
+                     make_fastdiv(H2), runs);
   return (int)hipGetLastError();
 }
 

@@ -543,8 +543,13 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
   // operand double buffers (64 KiB); reused as the f32 C tile (with a
   // 4-float row pad) by the epilogue
-  constexpr int SMEM_BYTES = (4 * TILE * 2 > 128 * (BN_ + 4) * 4)
-                                 ? 4 * TILE * 2 : 128 * (BN_ + 4) * 4;
+  // A stages (BM x BK) then B stages (BN x BK K-major, or the 128-wide
+  // MN-major image); a 64-wide K-major B halves its stage, so such kernels
+  // fit 3 blocks per CU (48 KiB) instead of 2
+  constexpr int SA = BM * BK;
+  constexpr int SB = (BKM ? BN_ : 128) * BK;
+  constexpr int SMEM_BYTES = (2 * (SA + SB) * 2 > 128 * (BN_ + 4) * 4)
+                                 ? 2 * (SA + SB) * 2 : 128 * (BN_ + 4) * 4;
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES / 2];
   // 1-D grid over (group, split, tile), tile fastest.  Bijective XCD remap
   // (cdna_hip_programming.md T1): each XCD gets a contiguous wgid range, so
@@ -676,12 +681,12 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
               (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 512),
               16, 0, 0);
       };
-      issue(kbeg, smem, smem + 2 * TILE);
+      issue(kbeg, smem, smem + 2 * SA);
       for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nk) {
-          issue(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * TILE,
-                smem + (2 + (cur ^ 1)) * TILE);
+          issue(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * SA,
+                smem + 2 * SA + (cur ^ 1) * SB);
           if constexpr (NIA + NIB == 8)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else
@@ -691,7 +696,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        compute(smem + cur * TILE, smem + (2 + cur) * TILE);
+        compute(smem + cur * SA, smem + 2 * SA + cur * SB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -752,14 +757,14 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   };
 
   gload(kbeg);
-  sstore(smem, smem + 2 * TILE);
+  sstore(smem, smem + 2 * SA);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) gload(kbeg + (kt + 1) * BK);
-    compute(smem + cur * TILE, smem + (2 + cur) * TILE);
-    if (more) sstore(smem + (cur ^ 1) * TILE, smem + (2 + (cur ^ 1)) * TILE);
+    compute(smem + cur * SA, smem + 2 * SA + cur * SB);
+    if (more) sstore(smem + (cur ^ 1) * SA, smem + 2 * SA + (cur ^ 1) * SB);
     __syncthreads();
     cur ^= 1;
   }

@@ -25,17 +25,17 @@ template <int VEC>
 __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
                                 int N, int H, int W, int C, int OH, int OW,
                                 int ky, int kx, int sy, int sx, int pt, int pl,
-                                int mode) {
+                                int mode, FastDiv fCV, FastDiv fOW,
+                                FastDiv fOH) {
   const int CV = C / VEC;
   const int total = N * OH * OW * CV;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
-    int pix = e / CV;
-    int cv = e - pix * CV;
-    int t = pix / OW;
-    int ow = pix - t * OW;
-    int n = t / OH;
-    int oh = t - n * OH;
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
+    const int cv = cvu, ow = owu, n = nu, oh = ohu;
     int h0 = oh * sy - pt, w0 = ow * sx - pl;
     int h1 = min(h0 + ky, H), w1 = min(w0 + kx, W);
     h0 = max(h0, 0);
@@ -83,24 +83,24 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
                                 uint16_t* dx, int N, int H, int W, int C,
                                 int OH, int OW, int ky, int kx, int sy, int sx,
                                 int pt, int pl, int mode, const uint16_t* aux,
-                                int aux_act) {
+                                int aux_act, FastDiv fCV, FastDiv fW,
+                                FastDiv fH, FastDiv fSy, FastDiv fSx) {
   const int CV = C / VEC;
   const int total = N * H * W * CV;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
-    int pix = e / CV;
-    int cv = e - pix * CV;
-    int t = pix / W;
-    int w = pix - t * W;
-    int n = t / H;
-    int h = t - n * H;
+    uint32_t pix, cvu, t, wu, nu, hu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fW, t, wu);
+    fdivmod(t, fH, nu, hu);
+    const int cv = cvu, w = wu, n = nu, h = hu;
     int xoff = pix * C + cv * VEC;
     // windows oh with oh*sy - pt <= h < oh*sy - pt + ky
     int hp = h + pt, wp = w + pl;
-    int oh0 = hp - ky + 1 <= 0 ? 0 : (hp - ky + sy) / sy;
-    int oh1 = min(OH - 1, hp / sy);
-    int ow0 = wp - kx + 1 <= 0 ? 0 : (wp - kx + sx) / sx;
-    int ow1 = min(OW - 1, wp / sx);
+    int oh0 = hp - ky + 1 <= 0 ? 0 : (int)fdiv(hp - ky + sy, fSy);
+    int oh1 = min(OH - 1, (int)fdiv(hp, fSy));
+    int ow0 = wp - kx + 1 <= 0 ? 0 : (int)fdiv(wp - kx + sx, fSx);
+    int ow1 = min(OW - 1, (int)fdiv(wp, fSx));
     float acc[VEC];
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[q] = 0.f;
@@ -226,12 +226,12 @@ __device__ __forceinline__ void load24(const uint16_t* row, int c0, int C,
 }
 __global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
                                    int C, int half, float alpha, float beta,
-                                   float k) {
+                                   float k, FastDiv fCV) {
   const int CV = C >> 3;
   const int total = P * CV;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
-    int p = e / CV;
+    int p = (int)fdiv((uint32_t)e, fCV);
     int c0 = (e - p * CV) << 3;
     const uint16_t* row = x + (long long)p * C;
     float v[24];
@@ -254,12 +254,13 @@ __global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
 __global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
                                    uint16_t* dx, int P, int C, int half,
                                    float alpha, float beta, float k,
-                                   const uint16_t* aux, int aux_act) {
+                                   const uint16_t* aux, int aux_act,
+                                   FastDiv fCV) {
   const int CV = C >> 3;
   const int total = P * CV;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
-    int p = e / CV;
+    int p = (int)fdiv((uint32_t)e, fCV);
     int c0 = (e - p * CV) << 3;
     long long base = (long long)p * C;
     float xv[24], gv[24];
@@ -277,8 +278,10 @@ __global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
         s += (d >= -half && d <= half) ? t * t : 0.f;
       }
       s = k + alpha * s;
-      float sb = exp2f(-beta * __log2f(s));
-      tj[j] = gv[4 + j] * xv[4 + j] * sb / s;
+      const float ls = __log2f(s);
+      float sb = exp2f(-beta * ls);
+      // s^(-beta-1) as a second exp instead of a division
+      tj[j] = gv[4 + j] * xv[4 + j] * exp2f((-beta - 1.f) * ls);
       // keep s^-beta of the owned channels in gv's free slots? recompute
       // below instead (cheap)
       if (j >= 4 && j < 12) xv[(j - 4) + 0] = sb;  // xv[0..7] unused now
@@ -308,12 +311,14 @@ HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
     long long total = (long long)N * OH * OW * (C / 8);
     hipLaunchKernelGGL(pool_fwd_kernel<8>, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C, OH,
-                       OW, ky, kx, sy, sx, pt, pl, mode);
+                       OW, ky, kx, sy, sx, pt, pl, mode, make_fastdiv(C / 8),
+                       make_fastdiv(OW), make_fastdiv(OH));
   } else {
     long long total = (long long)N * OH * OW * C;
     hipLaunchKernelGGL(pool_fwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C, OH,
-                       OW, ky, kx, sy, sx, pt, pl, mode);
+                       OW, ky, kx, sy, sx, pt, pl, mode, make_fastdiv(C),
+                       make_fastdiv(OW), make_fastdiv(OH));
   }
   return (int)hipGetLastError();
 }
@@ -328,13 +333,15 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
     hipLaunchKernelGGL(pool_bwd_kernel<8>, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W, C, OH,
                        OW, ky, kx, sy, sx, pt, pl, mode, (const uint16_t*)aux,
-                       aux_act);
+                       aux_act, make_fastdiv(C / 8), make_fastdiv(W),
+                       make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
   } else {
     long long total = (long long)N * H * W * C;
     hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W, C, OH,
                        OW, ky, kx, sy, sx, pt, pl, mode, (const uint16_t*)aux,
-                       aux_act);
+                       aux_act, make_fastdiv(C), make_fastdiv(W),
+                       make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
   }
   return (int)hipGetLastError();
 }
@@ -346,7 +353,7 @@ HVK_API int hvk_lrn_fwd(const void* x, void* y, long long P, int C, int n,
     long long total = P * (C / 8);
     hipLaunchKernelGGL(lrn_fwd_vec_kernel, dim3(grid_for(total)), dim3(256), 0,
                        s, (const uint16_t*)x, (uint16_t*)y, (int)P, C, n / 2,
-                       alpha, beta, k);
+                       alpha, beta, k, make_fastdiv(C / 8));
     return (int)hipGetLastError();
   }
   if (C > 1024) return -1;
@@ -365,7 +372,7 @@ HVK_API int hvk_lrn_bwd(const void* x, const void* dy, void* dx, long long P,
     hipLaunchKernelGGL(lrn_bwd_vec_kernel, dim3(grid_for(total)), dim3(256), 0,
                        s, (const uint16_t*)x, (const uint16_t*)dy,
                        (uint16_t*)dx, (int)P, C, n / 2, alpha, beta, k,
-                       (const uint16_t*)aux, aux_act);
+                       (const uint16_t*)aux, aux_act, make_fastdiv(C / 8));
     return (int)hipGetLastError();
   }
   if (C > 1024) return -1;
