@@ -540,10 +540,12 @@ __global__ void space_to_depth_kernel(const uint16_t* __restrict__ x,
   const int RUN = s * C;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
        q < runs; q += (long long)gridDim.x * blockDim.x) {
-    uint32_t pix, dy, X, t, Y, n;
-    fdivmod((uint32_t)q, fS, pix, dy);
-    fdivmod(pix, fW2, t, X);
+    // X fastest: a wave reads consecutive runs of one input row
+    uint32_t r, dy, X, t, Y, n, pix;
+    fdivmod((uint32_t)q, fW2, r, X);
+    fdivmod(r, fS, t, dy);
     fdivmod(t, fH2, n, Y);
+    pix = (n * H2 + Y) * W2 + X;
     uint16_t* out = y + (long long)pix * s * RUN + dy * RUN;
     int iy = s * (int)Y + (int)dy - pt, ix0 = s * (int)X - pl;
     if (iy < 0 || iy >= H) {

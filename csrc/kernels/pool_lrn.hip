@@ -77,6 +77,79 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
   }
 }
 
+
+// 3x3 windows, 8 channels per lane: all nine 16-B loads issued up front
+// (clamped addresses + validity masks), argmax stored as two int4s.
+__global__ void pool_fwd3_kernel(const uint16_t* __restrict__ x,
+                                 uint16_t* __restrict__ y,
+                                 int* __restrict__ argmax, int N, int H,
+                                 int W, int C, int OH, int OW, int sy, int sx,
+                                 int pt, int pl, int mode, FastDiv fCV,
+                                 FastDiv fOW, FastDiv fOH) {
+  const int CV = C >> 3;
+  const int total = N * OH * OW * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
+    const int h0 = (int)ohu * sy - pt, w0 = (int)owu * sx - pl;
+    const long long img = (long long)nu * H * W * C + cvu * 8;
+    uint4 v[9];
+    int off[9];
+    bool ok[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int h = h0 + i / 3, w = w0 + i % 3;
+      ok[i] = h >= 0 && h < H && w >= 0 && w < W;
+      const int hc = min(max(h, 0), H - 1), wc = min(max(w, 0), W - 1);
+      off[i] = (hc * W + wc) * C;
+      v[i] = *(const uint4*)(x + img + off[i]);
+    }
+    float best[8], sum[8];
+    int bi[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { best[q] = -INFINITY; sum[q] = 0.f; bi[q] = -1; }
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      if (!ok[i]) continue;
+      ++cnt;
+      const uint16_t* hv = (const uint16_t*)&v[i];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float f = bf2f(hv[q]);
+        if (mode == POOL_AVG) {
+          sum[q] += f;
+        } else {
+          const float key = mode == POOL_MAXABS ? fabsf(f) : f;
+          const float bk = mode == POOL_MAXABS ? fabsf(best[q]) : best[q];
+          if (bi[q] < 0 || key > bk) { best[q] = f; bi[q] = i; }
+        }
+      }
+    }
+    uint16_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      o[q] = f2bf(mode == POOL_AVG ? sum[q] / (float)max(cnt, 1) : best[q]);
+    const long long yo = (long long)pix * C + cvu * 8;
+    *(uint4*)(y + yo) = *(const uint4*)o;
+    if (argmax && mode != POOL_AVG) {
+      int a[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        int o2 = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) o2 = bi[q] == i ? off[i] : o2;
+        a[q] = bi[q] < 0 ? -1 : (int)(img + o2) + q;
+      }
+      *(int4*)(argmax + yo) = make_int4(a[0], a[1], a[2], a[3]);
+      *(int4*)(argmax + yo + 4) = make_int4(a[4], a[5], a[6], a[7]);
+    }
+  }
+}
+
 // gather backward: dx[n][h][w][c] = sum over windows covering (h,w)
 template <int VEC>
 __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
@@ -307,7 +380,15 @@ __global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
 HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
                          int W, int C, int OH, int OW, int ky, int kx, int sy,
                          int sx, int pt, int pl, int mode, hipStream_t s) {
-  if (C % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+  if (C % 8 == 0 && ky == 3 && kx == 3 && ((uintptr_t)x & 15) == 0 &&
+      ((uintptr_t)y & 15) == 0 && ((uintptr_t)argmax & 15) == 0 &&
+      (long long)N * H * W * C < (1ll << 31)) {
+    long long total = (long long)N * OH * OW * (C / 8);
+    hipLaunchKernelGGL(pool_fwd3_kernel, dim3(grid_for(total)), dim3(256), 0,
+                       s, (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W,
+                       C, OH, OW, sy, sx, pt, pl, mode, make_fastdiv(C / 8),
+                       make_fastdiv(OW), make_fastdiv(OH));
+  } else if (C % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
     long long total = (long long)N * OH * OW * (C / 8);
     hipLaunchKernelGGL(pool_fwd_kernel<8>, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C, OH,

@@ -156,6 +156,7 @@ def test_conv_wgrad(cfg):
 
 @pytest.mark.parametrize("mode", ["max", "avg", "maxabs"])
 @pytest.mark.parametrize("shape,k,s", [((2, 55, 55, 96), 3, 2),
+                                       ((2, 56, 54, 16), 3, 2),
                                        ((2, 13, 13, 5), 3, 2),
                                        ((1, 8, 8, 16), 2, 2)])
 def test_pool(mode, shape, k, s):
@@ -163,6 +164,8 @@ def test_pool(mode, shape, k, s):
     y, am = ops.pool_fwd(x, k, k, (s, s), mode)
     yg, amg = ops.pool_fwd(x.to(DEV), k, k, (s, s), mode)
     close(yg, y, 1e-6)
+    if mode != "avg":
+        assert torch.equal(amg.cpu().long(), am.long())
     dy = rnd(*y.shape, seed=7)
     aux = rnd(*shape, seed=8)
     dx = ops.pool_bwd(dy, am, shape, k, k, (s, s), mode, aux=aux, aux_act=3)

@@ -356,11 +356,11 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
     if out is None:
         out = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
     if _gpu(dy):
-        # weights permuted to [g][kh][kw][oc][c]: a dense B operand
+        # weights permuted to [g][c][kh][kw][oc]: a dense K-major B operand
         OCg, Cg = OC // groups, C // groups
-        wt = _workspace(("dgrad_wt", id(w)), (groups, KH, KW, OCg, Cg),
+        wt = _workspace(("dgrad_wt", id(w)), (groups, Cg, KH, KW, OCg),
                         w.dtype, w.device)
-        wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 2, 3, 1, 4))
+        wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1))
         _lib_call("hvk_conv_dgrad_t", _p(dy), _p(wt), _p(out), N, H, W, C,
                   OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, _p(aux),
                   aux_act, _s(dy))
