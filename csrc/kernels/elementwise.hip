@@ -693,6 +693,52 @@ __global__ void fill_rows_u8_bf16_kernel(const uint8_t* __restrict__ src,
   }
 }
 
+
+// Specialised space-to-depth (compile-time S, C; S*S*C % 8 == 0): a thread
+// builds one output pixel (S*S*C elements) in registers from S unaligned
+// 8-B-chunked row runs and writes it with 16-B stores; a wave reads S
+// contiguous 64-run spans and writes one contiguous span.
+template <int S, int C>
+__global__ void space_to_depth_px_kernel(const uint16_t* __restrict__ x,
+                                         uint16_t* __restrict__ y, int H,
+                                         int W, int pt, int pl, int H2,
+                                         int W2, FastDiv fW2, FastDiv fH2,
+                                         long long pixels) {
+  constexpr int RUN = S * C, PIX = S * RUN;
+  static_assert(RUN % 4 == 0 && PIX % 8 == 0, "vector shape");
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       q < pixels; q += (long long)gridDim.x * blockDim.x) {
+    uint32_t t, X, n, Y;
+    fdivmod((uint32_t)q, fW2, t, X);
+    fdivmod(t, fH2, n, Y);
+    uint16_t v[PIX];
+    const int ix0 = S * (int)X - pl;
+    const bool xin = ix0 >= 0 && ix0 + S <= W;
+#pragma unroll
+    for (int dy = 0; dy < S; ++dy) {
+      const int iy = S * (int)Y + dy - pt;
+      const bool yin = iy >= 0 && iy < H;
+      const uint16_t* row = x + ((long long)n * H + (yin ? iy : 0)) * W * C;
+      if (yin && xin) {
+#pragma unroll
+        for (int e = 0; e < RUN; e += 4)
+          __builtin_memcpy(&v[dy * RUN + e], row + (long long)ix0 * C + e, 8);
+      } else {
+#pragma unroll
+        for (int e = 0; e < RUN; ++e) {
+          const int ix = ix0 + e / C;
+          v[dy * RUN + e] = (yin && ix >= 0 && ix < W)
+                                ? row[(long long)ix * C + e % C]
+                                : (uint16_t)0;
+        }
+      }
+    }
+    uint4* out = (uint4*)(y + q * PIX);
+#pragma unroll
+    for (int j = 0; j < PIX / 8; ++j) out[j] = ((const uint4*)v)[j];
+  }
+}
+
 HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                                int start, int count, int max_mb,
                                long long sample_size, const float* mean,
@@ -898,6 +944,14 @@ HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
   if (C2 % 8) return -1;
   long long runs = (long long)N * H2 * W2 * s;
   if (runs >= (1ll << 32)) return -1;
+  if (s == 4 && C == 3 && ((uintptr_t)y & 15) == 0) {
+    long long pixels = (long long)N * H2 * W2;
+    hipLaunchKernelGGL((space_to_depth_px_kernel<4, 3>), dim3(grid_for(pixels)),
+                       dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y, H,
+                       W, pt, pl, H2, W2, make_fastdiv(W2), make_fastdiv(H2),
+                       pixels);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(space_to_depth_kernel, dim3(grid_for(runs)), dim3(256), 0,
                      st, (const uint16_t*)x, (uint16_t*)y, H, W, C, s, pt, pl,
                      H2, W2, make_fastdiv(s), make_fastdiv(W2),

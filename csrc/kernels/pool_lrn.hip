@@ -80,12 +80,14 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
 
 // 3x3 windows, 8 channels per lane: all nine 16-B loads issued up front
 // (clamped addresses + validity masks), argmax stored as two int4s.
+template <int MODE>
 __global__ void pool_fwd3_kernel(const uint16_t* __restrict__ x,
                                  uint16_t* __restrict__ y,
                                  int* __restrict__ argmax, int N, int H,
                                  int W, int C, int OH, int OW, int sy, int sx,
-                                 int pt, int pl, int mode, FastDiv fCV,
+                                 int pt, int pl, FastDiv fCV,
                                  FastDiv fOW, FastDiv fOH) {
+  constexpr int mode = MODE;
   const int CV = C >> 3;
   const int total = N * OH * OW * CV;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -151,11 +153,11 @@ __global__ void pool_fwd3_kernel(const uint16_t* __restrict__ x,
 }
 
 // gather backward: dx[n][h][w][c] = sum over windows covering (h,w)
-template <int VEC>
+template <int VEC, int MODE>
 __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
                                 uint16_t* dx, int N, int H, int W, int C,
                                 int OH, int OW, int ky, int kx, int sy, int sx,
-                                int pt, int pl, int mode, const uint16_t* aux,
+                                int pt, int pl, int, const uint16_t* aux,
                                 int aux_act, FastDiv fCV, FastDiv fW,
                                 FastDiv fH, FastDiv fSy, FastDiv fSx) {
   const int CV = C / VEC;
@@ -183,7 +185,7 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
         uint16_t g[VEC];
         if (VEC == 8) *(uint4*)g = *(const uint4*)(dy + yo);
         else g[0] = dy[yo];
-        if (mode == POOL_AVG) {
+        if (MODE == POOL_AVG) {
           int hh0 = max(oh * sy - pt, 0), hh1 = min(oh * sy - pt + ky, H);
           int ww0 = max(ow * sx - pl, 0), ww1 = min(ow * sx - pl + kx, W);
           float inv = 1.f / (float)max((hh1 - hh0) * (ww1 - ww0), 1);
@@ -297,8 +299,9 @@ __device__ __forceinline__ void load24(const uint16_t* row, int c0, int C,
   load8(row + c0, d + 8);
   if (c0 + 8 < C) load8(row + c0 + 8, d + 16);
 }
+template <int half>
 __global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
-                                   int C, int half, float alpha, float beta,
+                                   int C, float alpha, float beta,
                                    float k, FastDiv fCV) {
   const int CV = C >> 3;
   const int total = P * CV;
@@ -324,8 +327,9 @@ __global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
     *(uint4*)(y + (long long)p * C + c0) = *(uint4*)o;
   }
 }
+template <int half>
 __global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
-                                   uint16_t* dx, int P, int C, int half,
+                                   uint16_t* dx, int P, int C,
                                    float alpha, float beta, float k,
                                    const uint16_t* aux, int aux_act,
                                    FastDiv fCV) {
@@ -384,9 +388,12 @@ HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
       ((uintptr_t)y & 15) == 0 && ((uintptr_t)argmax & 15) == 0 &&
       (long long)N * H * W * C < (1ll << 31)) {
     long long total = (long long)N * OH * OW * (C / 8);
-    hipLaunchKernelGGL(pool_fwd3_kernel, dim3(grid_for(total)), dim3(256), 0,
-                       s, (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W,
-                       C, OH, OW, sy, sx, pt, pl, mode, make_fastdiv(C / 8),
+    auto k = mode == POOL_AVG ? pool_fwd3_kernel<POOL_AVG>
+             : mode == POOL_MAXABS ? pool_fwd3_kernel<POOL_MAXABS>
+                                   : pool_fwd3_kernel<POOL_MAX>;
+    hipLaunchKernelGGL(k, dim3(grid_for(total)), dim3(256), 0, s,
+                       (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C,
+                       OH, OW, sy, sx, pt, pl, make_fastdiv(C / 8),
                        make_fastdiv(OW), make_fastdiv(OH));
   } else if (C % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
     long long total = (long long)N * OH * OW * (C / 8);
@@ -411,14 +418,18 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
   if (C % 8 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
       ((uintptr_t)aux & 15) == 0) {
     long long total = (long long)N * H * W * (C / 8);
-    hipLaunchKernelGGL(pool_bwd_kernel<8>, dim3(grid_for(total)), dim3(256), 0, s,
+    auto k8 = mode == POOL_AVG ? pool_bwd_kernel<8, POOL_AVG>
+                               : pool_bwd_kernel<8, POOL_MAX>;
+    hipLaunchKernelGGL(k8, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W, C, OH,
                        OW, ky, kx, sy, sx, pt, pl, mode, (const uint16_t*)aux,
                        aux_act, make_fastdiv(C / 8), make_fastdiv(W),
                        make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
   } else {
     long long total = (long long)N * H * W * C;
-    hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s,
+    auto k1 = mode == POOL_AVG ? pool_bwd_kernel<1, POOL_AVG>
+                               : pool_bwd_kernel<1, POOL_MAX>;
+    hipLaunchKernelGGL(k1, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W, C, OH,
                        OW, ky, kx, sy, sx, pt, pl, mode, (const uint16_t*)aux,
                        aux_act, make_fastdiv(C), make_fastdiv(W),
@@ -432,8 +443,11 @@ HVK_API int hvk_lrn_fwd(const void* x, void* y, long long P, int C, int n,
   if (C % 8 == 0 && n / 2 <= 4 && P * C < (1ll << 31) &&
       ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
     long long total = P * (C / 8);
-    hipLaunchKernelGGL(lrn_fwd_vec_kernel, dim3(grid_for(total)), dim3(256), 0,
-                       s, (const uint16_t*)x, (uint16_t*)y, (int)P, C, n / 2,
+    const int h = n / 2;
+    auto kf = h == 0 ? lrn_fwd_vec_kernel<0> : h == 1 ? lrn_fwd_vec_kernel<1> : h == 2 ? lrn_fwd_vec_kernel<2>
+            : h == 3 ? lrn_fwd_vec_kernel<3> : lrn_fwd_vec_kernel<4>;
+    hipLaunchKernelGGL(kf, dim3(grid_for(total)), dim3(256), 0,
+                       s, (const uint16_t*)x, (uint16_t*)y, (int)P, C,
                        alpha, beta, k, make_fastdiv(C / 8));
     return (int)hipGetLastError();
   }
@@ -450,9 +464,12 @@ HVK_API int hvk_lrn_bwd(const void* x, const void* dy, void* dx, long long P,
       ((uintptr_t)x & 15) == 0 && ((uintptr_t)dy & 15) == 0 &&
       ((uintptr_t)dx & 15) == 0 && ((uintptr_t)aux & 15) == 0) {
     long long total = P * (C / 8);
-    hipLaunchKernelGGL(lrn_bwd_vec_kernel, dim3(grid_for(total)), dim3(256), 0,
+    const int h = n / 2;
+    auto kb = h == 0 ? lrn_bwd_vec_kernel<0> : h == 1 ? lrn_bwd_vec_kernel<1> : h == 2 ? lrn_bwd_vec_kernel<2>
+            : h == 3 ? lrn_bwd_vec_kernel<3> : lrn_bwd_vec_kernel<4>;
+    hipLaunchKernelGGL(kb, dim3(grid_for(total)), dim3(256), 0,
                        s, (const uint16_t*)x, (const uint16_t*)dy,
-                       (uint16_t*)dx, (int)P, C, n / 2, alpha, beta, k,
+                       (uint16_t*)dx, (int)P, C, alpha, beta, k,
                        (const uint16_t*)aux, aux_act, make_fastdiv(C / 8));
     return (int)hipGetLastError();
   }
