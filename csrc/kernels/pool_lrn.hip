@@ -212,6 +212,88 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
   }
 }
 
+
+// 3x3 windows with stride >= 2: an input pixel lies in at most 2x2 windows;
+// their dy / argmax loads are issued together (clamped addresses + masks).
+template <int MODE>
+__global__ void pool_bwd3_kernel(const uint16_t* __restrict__ dy,
+                                 const int* __restrict__ argmax,
+                                 uint16_t* __restrict__ dx, int N, int H,
+                                 int W, int C, int OH, int OW, int sy, int sx,
+                                 int pt, int pl, const uint16_t* aux,
+                                 int aux_act, FastDiv fCV, FastDiv fW,
+                                 FastDiv fH, FastDiv fSy, FastDiv fSx) {
+  const int CV = C >> 3;
+  const int total = N * H * W * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, wu, nu, hu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fW, t, wu);
+    fdivmod(t, fH, nu, hu);
+    const int xoff = (int)pix * C + (int)cvu * 8;
+    const int hp = (int)hu + pt, wp = (int)wu + pl;
+    // last window starting at or before hp; the one before it may also cover
+    const int oh1 = min(OH - 1, (int)fdiv(hp, fSy));
+    const int ow1 = min(OW - 1, (int)fdiv(wp, fSx));
+    int yo[4];
+    bool ok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oh = oh1 - (i >> 1), ow = ow1 - (i & 1);
+      ok[i] = oh >= 0 && ow >= 0 && hp - oh * sy < 3 && wp - ow * sx < 3 &&
+              hp >= oh * sy && wp >= ow * sx;
+      const int ohc = max(oh, 0), owc = max(ow, 0);
+      yo[i] = (((int)nu * OH + ohc) * OW + owc) * C + (int)cvu * 8;
+    }
+    uint4 g[4];
+    int4 a0[4], a1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      g[i] = *(const uint4*)(dy + yo[i]);
+      if (MODE != POOL_AVG) {
+        a0[i] = *(const int4*)(argmax + yo[i]);
+        a1[i] = *(const int4*)(argmax + yo[i] + 4);
+      }
+    }
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (!ok[i]) continue;
+      const uint16_t* gv = (const uint16_t*)&g[i];
+      if (MODE == POOL_AVG) {
+        const int oh = oh1 - (i >> 1), ow = ow1 - (i & 1);
+        const int hh0 = max(oh * sy - pt, 0), hh1 = min(oh * sy - pt + 3, H);
+        const int ww0 = max(ow * sx - pl, 0), ww1 = min(ow * sx - pl + 3, W);
+        const float inv = 1.f / (float)max((hh1 - hh0) * (ww1 - ww0), 1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += bf2f(gv[q]) * inv;
+      } else {
+        const int am[8] = {a0[i].x, a0[i].y, a0[i].z, a0[i].w,
+                           a1[i].x, a1[i].y, a1[i].z, a1[i].w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          acc[q] += am[q] == xoff + q ? bf2f(gv[q]) : 0.f;
+      }
+    }
+    if (aux) {
+      float a[8];
+      const uint4 av = *(const uint4*)(aux + xoff);
+      const uint16_t* ah = (const uint16_t*)&av;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = bf2f(ah[q]);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] *= act_bwd(a[q], aux_act);
+    }
+    uint16_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(acc[q]);
+    *(uint4*)(dx + xoff) = *(const uint4*)o;
+  }
+}
+
 // LRN across channels: s_c = k + alpha * sum_{|c'-c|<=n/2} x_c'^2 ;
 // y_c = x_c * s_c^-beta.  One wave per pixel; channels staged in LDS.
 constexpr int LRN_MAXC = 1024;
@@ -418,6 +500,18 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
   if (C % 8 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
       ((uintptr_t)aux & 15) == 0) {
     long long total = (long long)N * H * W * (C / 8);
+    if (ky == 3 && kx == 3 && sy >= 2 && sx >= 2 &&
+        ((uintptr_t)argmax & 15) == 0 &&
+        (long long)N * H * W * C < (1ll << 31)) {
+      auto k3 = mode == POOL_AVG ? pool_bwd3_kernel<POOL_AVG>
+                                 : pool_bwd3_kernel<POOL_MAX>;
+      hipLaunchKernelGGL(k3, dim3(grid_for(total)), dim3(256), 0, s,
+                         (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W,
+                         C, OH, OW, sy, sx, pt, pl, (const uint16_t*)aux,
+                         aux_act, make_fastdiv(C / 8), make_fastdiv(W),
+                         make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
+      return (int)hipGetLastError();
+    }
     auto k8 = mode == POOL_AVG ? pool_bwd_kernel<8, POOL_AVG>
                                : pool_bwd_kernel<8, POOL_MAX>;
     hipLaunchKernelGGL(k8, dim3(grid_for(total)), dim3(256), 0, s,
