@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--batch", type=int, default=512,
                     help="per-GPU minibatch (weak scaling)")
     ap.add_argument("--model", default="alexnet")
+    ap.add_argument("--precision", default="bfloat16",
+                    choices=("bfloat16", "float8"),
+                    help="float8: e4m3/e5m2 MFMA for conv and FC forward + "
+                         "backward-data (BASELINE config 5, VGG-16)")
     ap.add_argument("--steps-per-epoch", type=int, default=16)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--profile-json", default=None)
@@ -39,6 +43,7 @@ def main():
     import torch
     from veles_amd.utils.config import root
     root.common.disable.snapshotting = True
+    root.common.engine.precision_type = args.precision
     from veles_amd.backends import Device
     from veles_amd.dummy import DummyLauncher
     from veles_amd.models import StandardWorkflow
@@ -108,7 +113,8 @@ def main():
                "ms_per_step": round(dt / args.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak",
                "vs_baseline": (value / base) if base else None,
-               "dtype": "bf16" if backend == "hip" else "fp32",
+               "dtype": ("fp8" if args.precision == "float8" else "bf16")
+               if backend == "hip" else "fp32",
                "data": "synthetic (uint8 %s images resident in HBM, "
                        "random-init weights)" % shape,
                "config": {"model": args.model, "global_batch": global_batch,

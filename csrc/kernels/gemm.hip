@@ -20,7 +20,7 @@
 //            b ^ h(k), h(k) = (k&3) | ((k>>3)&1)<<2 -> ds_read_b64_tr_b16
 //            transposed fragment reads conflict-free
 // Grid x is remapped so that consecutive output tiles share one XCD's L2.
-#include "hvk_common.h"
+#include "conv_geom.h"
 
 using namespace hvk;
 
@@ -110,12 +110,6 @@ struct DenseMN {
   }
 };
 
-struct ConvGeom {
-  int N, H, W, C, Cg;       // input NHWC, C total, Cg per group
-  int OH, OW, OC, OCg;      // output
-  int KH, KW, sy, sx, pt, pl;
-  FastDiv fOW, fOHOW, fW, fHW, fCg, fOCg, fKW, fSy, fSx;
-};
 
 // conv forward A: rows = output pixels (n,oh,ow), k = (kh,kw,c)
 struct ConvFwdA {
@@ -555,10 +549,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   // (cdna_hip_programming.md T1): each XCD gets a contiguous wgid range, so
   // the tiles of one K split (which share the A rows / B columns of that
   // split) and neighbouring output tiles share one L2.
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wgid % tiles;
   const int gs = wgid / tiles;
   const int gi = gs / splits;
@@ -841,22 +832,6 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   return hipGetLastError();
 }
 
-ConvGeom make_geom(int N, int H, int W, int C, int OC, int KH, int KW, int sy,
-                   int sx, int pt, int pl, int OH, int OW, int groups) {
-  ConvGeom g;
-  g.N = N; g.H = H; g.W = W; g.C = C; g.Cg = C / groups;
-  g.OH = OH; g.OW = OW; g.OC = OC; g.OCg = OC / groups;
-  g.KH = KH; g.KW = KW; g.sy = sy; g.sx = sx; g.pt = pt; g.pl = pl;
-  g.fOW = make_fastdiv(OW); g.fOHOW = make_fastdiv(OH * OW);
-  g.fW = make_fastdiv(W); g.fHW = make_fastdiv(H * W);
-  g.fCg = make_fastdiv(g.Cg); g.fOCg = make_fastdiv(g.OCg);
-  g.fKW = make_fastdiv(KW);
-  g.fSy = make_fastdiv(sy);
-  g.fSx = make_fastdiv(sx);
-  return g;
-}
-
-inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
              float alpha, float beta, const float* bias, int bias_mode,

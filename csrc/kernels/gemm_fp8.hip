@@ -1,0 +1,576 @@
+// gemm_fp8.hip - FP8 (OCP e4m3 / e5m2) MFMA GEMM and implicit-GEMM
+// convolution (forward and backward-data) for gfx950, plus the per-tensor
+// delayed-scaling quantizers that feed them.
+//
+// Matrix core: v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales
+// (E8M0 127 = 2^0).  Per MI355X_MICROARCH.md (Matrix cores) this form runs at
+// twice the bf16 rate per clock; the non-scaled 16x16x32 fp8 form would only
+// match bf16.  Per-tensor scales are applied once, in the epilogue.
+//
+// Tile: 128 x {128,64} x 128 (k in BYTES = fp8 elements), 4 waves (2x2), each
+// wave 64 x BN/2 = 4 x BN/32 MFMA tiles; one MFMA consumes the whole 128-deep
+// K tile.  A K-major LDS row is 128 B - byte-for-byte the layout of the bf16
+// kernel's 64-wide K tile (gemm.hip) - so the same 16-B chunk XOR swizzle
+// (chunk c at c ^ (row & 7)) keeps the LDS-DMA image lane-linear.  Operands
+// move by global_load_lds_dwordx4 with the next tile in flight across the
+// (raw) barrier, one counted vmcnt per tile.
+//
+// Operand lane map: lane l feeds row (l & 15) with the 32 bytes
+// k = 32*(l >> 4) ... +31 of both A and B.  The k order inside an MFMA is a
+// permutation shared by A and B, so the sum over k is the same whatever
+// order the hardware assigns (tests/test_fp8.py checks it against fp32).
+//
+// Only K-major operands exist here (fp8 has no transposed LDS read that the
+// bf16 MN-major path relies on), which covers conv forward (A = im2col(X),
+// B = W[OC][K]), conv dgrad (A = gather(dY), B = W permuted to [C][K]) and
+// the fully-connected forward / dgrad (W^T is materialised once per step).
+// Weight gradients stay on the bf16 kernels (docs/OPS.md §FP8).
+#include "conv_geom.h"
+
+using namespace hvk;
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+namespace {
+
+constexpr int BM = 128, BK = 128, NTHR = 256;
+
+__device__ __attribute__((aligned(16))) const uint8_t g_zero16[16] = {0};
+
+// ------------------------------------------------------------------ scales
+// A scaler state is float st[hist + 1]: amax history, then the running amax
+// of the current step.  scale = fmax_eff / max(history) (1 when empty); the
+// quantizer multiplies by it and the GEMM epilogue divides by sA * sB.
+__device__ __forceinline__ float fp8_scale(const float* st, int hist,
+                                           float fmax_eff) {
+  float m = 0.f;
+  for (int i = 0; i < hist; ++i) m = fmaxf(m, st[i]);
+  return m > 0.f ? fmax_eff / m : 1.f;
+}
+
+// ----------------------------------------------------------------- loaders
+struct Dense8 {
+  const uint8_t* p;
+  long long gstride;
+  int rows, K, ld;
+  struct Ctx { const uint8_t* row; int ok; };
+  __device__ void group(int g) { p += (long long)g * gstride; }
+  __device__ __forceinline__ Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < rows;
+    c.row = p + (long long)(c.ok ? r : 0) * ld;
+    return c;
+  }
+  __device__ __forceinline__ const uint8_t* src(const Ctx& c, int k) const {
+    return (c.ok && k < K) ? c.row + k : g_zero16;
+  }
+};
+
+// conv forward A: rows = output pixels (n, oh, ow), k = (kh, kw, c); a
+// 16-byte chunk is 16 channels of one tap (Cg % 16 == 0)
+struct ConvFwdA8 {
+  const uint8_t* x;
+  ConvGeom g;
+  int M, K, coff;
+  struct Ctx { int base, ih0, iw0, ok; };
+  __device__ void group(int gi) { coff = gi * g.Cg; }
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
+    Ctx c;
+    c.ok = m < M;
+    uint32_t mm = c.ok ? m : 0, n, rem, oh, ow;
+    fdivmod(mm, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    c.base = n * g.H * g.W * g.C + coff;
+    c.ih0 = oh * g.sy - g.pt;
+    c.iw0 = ow * g.sx - g.pl;
+    return c;
+  }
+  __device__ __forceinline__ const uint8_t* src(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return g_zero16;
+    uint32_t t, ch, kh, kw;
+    fdivmod(k, g.fCg, t, ch);
+    fdivmod(t, g.fKW, kh, kw);
+    int ih = c.ih0 + (int)kh, iw = c.iw0 + (int)kw;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
+      return g_zero16;
+    return x + c.base + (ih * g.W + iw) * g.C + ch;
+  }
+};
+
+// conv dgrad A: rows = input pixels (n, h, w), k = (kh, kw, oc) over dY
+struct ConvDgradA8 {
+  const uint8_t* dy;
+  ConvGeom g;
+  int M, K, coff;
+  struct Ctx { int base, hp, wp, ok; };
+  __device__ void group(int gi) { coff = gi * g.OCg; }
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
+    Ctx c;
+    c.ok = m < M;
+    uint32_t mm = c.ok ? m : 0, n, rem, h, w;
+    fdivmod(mm, g.fHW, n, rem);
+    fdivmod(rem, g.fW, h, w);
+    c.base = n * g.OH * g.OW * g.OC + coff;
+    c.hp = h + g.pt;
+    c.wp = w + g.pl;
+    return c;
+  }
+  __device__ __forceinline__ const uint8_t* src(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return g_zero16;
+    uint32_t t, oc, kh, kw;
+    fdivmod(k, g.fOCg, t, oc);
+    fdivmod(t, g.fKW, kh, kw);
+    int ohs = c.hp - (int)kh, ows = c.wp - (int)kw;
+    if (ohs < 0 || ows < 0) return g_zero16;
+    int oh = ohs, ow = ows;
+    if (g.sy != 1 || g.sx != 1) {
+      oh = (int)fdiv((uint32_t)ohs, g.fSy);
+      ow = (int)fdiv((uint32_t)ows, g.fSx);
+      if (oh * g.sy != ohs || ow * g.sx != ows) return g_zero16;
+    }
+    if (oh >= g.OH || ow >= g.OW) return g_zero16;
+    return dy + c.base + (oh * g.OW + ow) * g.OC + oc;
+  }
+};
+
+// ---------------------------------------------------------------- epilogue
+struct Epi8 {
+  uint16_t* c;           // bf16 output
+  int ldc, M, N;
+  int grow_unused, gcol;  // per-group column offset
+  const float* bias;     // per column (f32) or null
+  int act;
+  const uint16_t* aux;   // multiply by act_bwd(aux, aux_act)
+  int ld_aux, aux_act;
+  const float* sa;       // scaler states of A and B
+  const float* sb;
+  int hist;
+  float fa, fb;          // effective fp8 maxima of A and B
+};
+
+__device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
+                                       int m, int n, const float* v) {
+  if (m >= e.M || n >= e.N) return;
+  const int gn = n + gi * e.gcol;
+  const long long idx = (long long)m * e.ldc + gn;
+  const bool vec = n + 8 <= e.N && (e.ldc & 7) == 0 && (gn & 7) == 0 &&
+                   (!e.aux || (e.ld_aux & 7) == 0);
+  float a[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a[q] = 1.f;
+  if (e.aux) {
+    if (vec) {
+      uint4 av = *(const uint4*)(e.aux + (long long)m * e.ld_aux + gn);
+      const uint16_t* ah = (const uint16_t*)&av;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = act_bwd(bf2f(ah[q]), e.aux_act);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (n + q < e.N)
+          a[q] = act_bwd(bf2f(e.aux[(long long)m * e.ld_aux + gn + q]),
+                         e.aux_act);
+    }
+  }
+  float o[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float t = v[q] * alpha;
+    if (e.bias && n + q < e.N) t += e.bias[gn + q];
+    if (e.act) t = act_fwd(t, e.act);
+    o[q] = t * a[q];
+  }
+  if (vec) {
+    uint4 w;
+    w.x = f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+    w.y = f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+    w.z = f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+    w.w = f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+    *(uint4*)(e.c + idx) = w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (n + q < e.N) e.c[idx + q] = f2bf(o[q]);
+  }
+}
+
+// ------------------------------------------------------------------ kernel
+template <class LA, class LB, int BN_, int FA, int FB>
+__global__ void __launch_bounds__(NTHR, 2)
+gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
+                int tiles) {
+  constexpr int NB = BN_ / 32;            // MFMA n-tiles per wave
+  constexpr int SA = BM * BK;             // bytes per A stage
+  constexpr int SB = BN_ * BK;            // bytes per B stage
+  constexpr int OPER = 2 * (SA + SB);
+  constexpr int LDC = BN_ + 4;            // f32 C tile row pitch
+  constexpr int CT = BM * LDC * 4;
+  constexpr int SMEM = OPER > CT ? OPER : CT;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  const int gi = wgid / tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  la.group(gi);
+  lb.group(gi);
+  const int m0 = tm * BM, n0 = tn * BN_;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[4][NB];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // 32 bytes of row (rowbase + fr): chunks 2fq and 2fq+1 at their swizzled
+  // slots (c ^ (row & 7)) of the 128-B row
+  auto frag = [&](const uint8_t* s, int rowbase) -> i32x8 {
+    const int row = rowbase + fr;
+    const int sw = row & 7;
+    const uint8_t* base = s + row * BK;
+    uint4 lo = *(const uint4*)(base + (((2 * fq) ^ sw) << 4));
+    uint4 hi = *(const uint4*)(base + (((2 * fq + 1) ^ sw) << 4));
+    i32x8 v;
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    return v;
+  };
+  auto compute = [&](const uint8_t* sA, const uint8_t* sB) {
+    i32x8 af[4], bfv[NB];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(sA, wm * 64 + i * 16);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) bfv[j] = frag(sB, wn * (BN_ / 2) + j * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            af[i], bfv[j], acc[i][j], FA, FB, 0, 127, 0, 127);
+  };
+
+  // LDS-DMA issue map: instruction I of a stage covers rows 8I..8I+7; lane
+  // -> row 8I + (lane >> 3), LDS slot (lane & 7) holds chunk slot ^ (row & 7)
+  constexpr int NIA = SA / (NTHR * 16);   // 4
+  constexpr int NIB = SB / (NTHR * 16);   // 4 (BN 128) or 2 (BN 64)
+  const int w = __builtin_amdgcn_readfirstlane(wid);
+  typename LA::Ctx da[NIA];
+  typename LB::Ctx db[NIB];
+  int ka[NIA], kb[NIB];
+#pragma unroll
+  for (int i = 0; i < NIA; ++i) {
+    const int I = w * NIA + i;
+    const int row = 8 * I + (lane >> 3);
+    da[i] = la.row_ctx(m0 + row);
+    ka[i] = 16 * ((lane & 7) ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < NIB; ++i) {
+    const int I = w * NIB + i;
+    const int row = 8 * I + (lane >> 3);
+    db[i] = lb.row_ctx(n0 + row);
+    kb[i] = 16 * ((lane & 7) ^ (row & 7));
+  }
+  auto issue = [&](int k0, uint8_t* sA, uint8_t* sB) {
+#pragma unroll
+    for (int i = 0; i < NIA; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)la.src(da[i], k0 + ka[i]),
+          (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 1024),
+          16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NIB; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)lb.src(db[i], k0 + kb[i]),
+          (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 1024),
+          16, 0, 0);
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  issue(0, smem, smem + 2 * SA);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue((kt + 1) * BK, smem + (cur ^ 1) * SA, smem + 2 * SA + (cur ^ 1) * SB);
+      if constexpr (NIA + NIB == 8)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    compute(smem + cur * SA, smem + 2 * SA + cur * SB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // per-tensor dequantisation: 1 / (sA * sB)
+  const float alpha = 1.f / (fp8_scale(epi.sa, epi.hist, epi.fa) *
+                             fp8_scale(epi.sb, epi.hist, epi.fb));
+  float* sC = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int rb = wm * 64 + i * 16 + fq * 4;
+      const int cc = wn * (BN_ / 2) + j * 16 + fr;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + cc] = acc[i][j][rr];
+    }
+  __syncthreads();
+  constexpr int CH = BN_ / 8;
+  for (int q = t; q < BM * CH; q += NTHR) {
+    const int row = q / CH, c8 = (q - row * CH) * 8;
+    if (m0 + row >= M) continue;
+    const float4* src = (const float4*)(sC + row * LDC + c8);
+    float v[8];
+    float4 lo = src[0], hi = src[1];
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    store8(epi, alpha, gi, m0 + row, n0 + c8, v);
+  }
+}
+
+inline bool use_bn64(int N) {
+  int w128 = (N + 127) / 128 * 128 - N;
+  int w64 = (N + 63) / 64 * 64 - N;
+  return w64 < w128 && w128 * 8 > N;
+}
+
+template <class LA, class LB, int FA, int FB>
+hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
+                   int K, int groups, hipStream_t s) {
+  const bool n64 = use_bn64(N);
+  const int bn = n64 ? 64 : 128;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
+  const int tiles = tiles_m * tiles_n;
+  dim3 grid((unsigned)((long long)tiles * groups));
+  if (n64)
+    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB>), grid, dim3(NTHR),
+                       0, s, la, lb, e, M, N, K, tiles_n, tiles);
+  else
+    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB>), grid,
+                       dim3(NTHR), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
+  return hipGetLastError();
+}
+
+// fmt: 0 = e4m3 (fp8), 1 = e5m2 (bf8) -> the f8f6f4 cbsz/blgp codes.  B is
+// always a weight (e4m3); A is an activation (e4m3) or a gradient (e5m2).
+template <class LA, class LB>
+hipError_t dispatch8(int fa, int fb, const LA& la, const LB& lb,
+                     const Epi8& e, int M, int N, int K, int groups,
+                     hipStream_t s) {
+  if (fb != 0) return hipErrorInvalidValue;
+  if (fa == 0) return launch8<LA, LB, 0, 0>(la, lb, e, M, N, K, groups, s);
+  return launch8<LA, LB, 1, 0>(la, lb, e, M, N, K, groups, s);
+}
+
+Epi8 make_epi8(void* c, int ldc, int M, int N, const float* bias, int act,
+               const void* aux, int ld_aux, int aux_act, const float* sa,
+               const float* sb, int hist, float fa, float fb) {
+  Epi8 e;
+  e.c = (uint16_t*)c; e.ldc = ldc; e.M = M; e.N = N;
+  e.grow_unused = 0; e.gcol = 0; e.bias = bias; e.act = act;
+  e.aux = (const uint16_t*)aux; e.ld_aux = ld_aux; e.aux_act = aux_act;
+  e.sa = sa; e.sb = sb; e.hist = hist; e.fa = fa; e.fb = fb;
+  return e;
+}
+
+// -------------------------------------------------------------- quantizers
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c,
+                                              float d, int fmt) {
+  int v;
+  if (fmt == 0) {
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  } else {
+    v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
+  }
+  return (uint32_t)v;
+}
+
+__device__ __forceinline__ float sat(float v, float lim) {
+  return fminf(fmaxf(v, -lim), lim);
+}
+
+// 16 elements per thread: bf16 (two 16-B loads) or f32 (four) -> 16 B fp8.
+// amax of |x| (unscaled) goes to st[hist] with an integer atomicMax on the
+// float bits (non-negative floats order like their bit patterns).
+__global__ void fp8_quant_kernel(const void* x, int x_f32, long long n,
+                                 uint8_t* out, int fmt, float* st, int hist,
+                                 float fmax_eff, float lim, int record) {
+  const float scale = fp8_scale(st, hist, fmax_eff);
+  float amax = 0.f;
+  const long long nv = n / 16;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v[16];
+    if (x_f32) {
+      const float4* p = (const float4*)x + i * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float4 f = p[j];
+        v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
+      }
+    } else {
+      const uint4* p = (const uint4*)x + i * 2;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint4 u = p[j];
+        const uint16_t* h = (const uint16_t*)&u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[8 * j + q] = bf2f(h[q]);
+      }
+    }
+    uint4 o;
+    uint32_t* ow = (uint32_t*)&o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) amax = fmaxf(amax, fabsf(v[4 * j + q]));
+      ow[j] = pack4_fp8(sat(v[4 * j] * scale, lim), sat(v[4 * j + 1] * scale, lim),
+                        sat(v[4 * j + 2] * scale, lim),
+                        sat(v[4 * j + 3] * scale, lim), fmt);
+    }
+    ((uint4*)out)[i] = o;
+  }
+  // scalar tail (n % 16)
+  const long long tail0 = nv * 16;
+  if (blockIdx.x == 0 && threadIdx.x < n - tail0) {
+    const long long e = tail0 + threadIdx.x;
+    float v = x_f32 ? ((const float*)x)[e] : bf2f(((const uint16_t*)x)[e]);
+    amax = fmaxf(amax, fabsf(v));
+    out[e] = (uint8_t)(pack4_fp8(sat(v * scale, lim), 0.f, 0.f, 0.f, fmt) & 0xFF);
+  }
+  if (!record) return;
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0 && amax > 0.f)
+    atomicMax((unsigned int*)(st + hist), __float_as_uint(amax));
+}
+
+__global__ void fp8_amax_kernel(const void* x, int x_f32, long long n,
+                                float* st, int hist) {
+  float amax = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v = x_f32 ? ((const float*)x)[i] : bf2f(((const uint16_t*)x)[i]);
+    amax = fmaxf(amax, fabsf(v));
+  }
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0 && amax > 0.f)
+    atomicMax((unsigned int*)(st + hist), __float_as_uint(amax));
+}
+
+// history[idx] = current amax (or every slot when fill), current = 0; one
+// thread per scaler of a [count][hist + 1] state block
+__global__ void fp8_roll_kernel(float* states, int count, int hist, int idx,
+                                int fill) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= count) return;
+  float* st = states + (long long)s * (hist + 1);
+  const float cur = st[hist];
+  if (fill) {
+    for (int i = 0; i < hist; ++i) st[i] = cur;
+  } else if (cur > 0.f) {
+    st[idx] = cur;
+  }
+  st[hist] = 0.f;
+}
+
+inline int grid_for(long long work, int per_block) {
+  long long b = (work + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > 8192) b = 8192;
+  return (int)b;
+}
+
+}  // namespace
+
+// out (fp8, n bytes) = sat(x * scale(st)); st[hist] = max(st[hist], amax|x|)
+HVK_API int hvk_fp8_quant(const void* x, int x_f32, long long n, void* out,
+                          int fmt, float* st, int hist, float fmax_eff,
+                          int record, hipStream_t s) {
+  if (((uintptr_t)x & 15) || ((uintptr_t)out & 15)) return -3;
+  const float lim = fmt == 0 ? 448.f : 57344.f;
+  hipLaunchKernelGGL(fp8_quant_kernel, dim3(grid_for(n / 16 + 1, 256)),
+                     dim3(256), 0, s, x, x_f32, n, (uint8_t*)out, fmt, st,
+                     hist, fmax_eff, lim, record);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_fp8_amax(const void* x, int x_f32, long long n, float* st,
+                         int hist, hipStream_t s) {
+  hipLaunchKernelGGL(fp8_amax_kernel, dim3(grid_for(n, 1024)), dim3(256), 0,
+                     s, x, x_f32, n, st, hist);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_fp8_roll(float* states, int count, int hist, int idx,
+                         int fill, hipStream_t s) {
+  if (count <= 0) return 0;
+  hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
+                     states, count, hist, idx, fill);
+  return (int)hipGetLastError();
+}
+
+// C[M][N] (bf16) = act(A[M][K] . B[N][K]^T / (sA sB) + bias) * f'(aux)
+HVK_API int hvk_gemm_fp8(int M, int N, int K, const void* A, int lda, int fa,
+                         const void* B, int ldb, int fb, void* C, int ldc,
+                         const float* bias, int act, const void* aux,
+                         int ld_aux, int aux_act, const float* sa,
+                         const float* sb, int hist, float fmax_a, float fmax_b,
+                         hipStream_t s) {
+  if ((K & 15) || (lda & 15) || (ldb & 15) || !al16(A) || !al16(B)) return -3;
+  Dense8 la{(const uint8_t*)A, 0, M, K, lda};
+  Dense8 lb{(const uint8_t*)B, 0, N, K, ldb};
+  Epi8 e = make_epi8(C, ldc, M, N, bias, act, aux, ld_aux, aux_act, sa, sb,
+                     hist, fmax_a, fmax_b);
+  return (int)dispatch8(fa, fb, la, lb, e, M, N, K, 1, s);
+}
+
+// Y[n][oh][ow][oc] (bf16) = act(conv(X8, W8) / (sX sW) + bias)
+// X8 NHWC fp8, W8 [OC][KH][KW][C/g] fp8; C/g, C and K multiples of 16
+HVK_API int hvk_conv_fwd_fp8(const void* X, const void* Wt, const float* bias,
+                             void* Y, int N, int H, int W, int C, int OC,
+                             int KH, int KW, int sy, int sx, int pt, int pl,
+                             int OH, int OW, int groups, int act, int fx,
+                             int fw, const float* sxs, const float* sws,
+                             int hist, float fmax_x, float fmax_w,
+                             hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
+  const int M = N * OH * OW, K = KH * KW * g.Cg;
+  if ((g.Cg & 15) || (C & 15) || !al16(X) || !al16(Wt)) return -3;
+  ConvFwdA8 la{(const uint8_t*)X, g, M, K, 0};
+  Dense8 lb{(const uint8_t*)Wt, (long long)g.OCg * K, g.OCg, K, K};
+  Epi8 e = make_epi8(Y, OC, M, g.OCg, bias, act, nullptr, 0, 0, sxs, sws,
+                     hist, fmax_x, fmax_w);
+  e.gcol = g.OCg;
+  return (int)dispatch8(fx, fw, la, lb, e, M, g.OCg, K, groups, s);
+}
+
+// dX (bf16) = conv^T(dY8, Wt8) / (sdY sW) [* f'(aux)]; Wt8 is the weight
+// permuted to [g][c][kh][kw][oc] (dense K-major per group)
+HVK_API int hvk_conv_dgrad_fp8(const void* dY, const void* Wt, void* dX,
+                               int N, int H, int W, int C, int OC, int KH,
+                               int KW, int sy, int sx, int pt, int pl, int OH,
+                               int OW, int groups, const void* aux,
+                               int aux_act, int fdy, int fw, const float* sds,
+                               const float* sws, int hist, float fmax_dy,
+                               float fmax_w, hipStream_t s) {
+  ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
+  const int M = N * H * W, K = KH * KW * g.OCg;
+  if ((g.OCg & 15) || (OC & 15) || !al16(dY) || !al16(Wt)) return -3;
+  ConvDgradA8 la{(const uint8_t*)dY, g, M, K, 0};
+  Dense8 lb{(const uint8_t*)Wt, (long long)K * g.Cg, g.Cg, K, K};
+  Epi8 e = make_epi8(dX, C, M, g.Cg, nullptr, 0, aux, C, aux_act, sds, sws,
+                     hist, fmax_dy, fmax_w);
+  e.gcol = g.Cg;
+  return (int)dispatch8(fdy, fw, la, lb, e, M, g.Cg, K, groups, s);
+}

@@ -1,0 +1,212 @@
+"""FP8 path (veles_amd/ops/fp8.py, csrc/kernels/gemm_fp8.hip): delayed
+scaling semantics and a float8 training run on the CPU reference; on the
+MI355X every fp8 kernel against the CPU reference fed with the SAME
+quantized operands (so only accumulation order differs), plus quantizer
+bit-exactness against PyTorch's float8 casts."""
+import pytest
+import torch
+
+from veles_amd import ops
+from veles_amd.ops import fp8
+from veles_amd.utils.config import root
+
+DEV = "cuda"
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed + sum(shape))
+    return torch.randn(*shape, generator=g) * scale
+
+
+def close(got, ref, tol):
+    got, ref = got.float().cpu(), ref.float().cpu()
+    err = (got - ref).abs().max().item()
+    mag = ref.abs().max().item() + 1e-6
+    assert err <= tol * mag, "max err %g vs scale %g (tol %g)" % (err, mag, tol)
+
+
+# ------------------------------------------------------------------ CPU
+def test_scaler_prime_record_roll_cpu():
+    s = fp8.Scaler("cpu", fp8.E4M3)
+    x = rnd(64, 32, scale=3.0)
+    q = fp8.quantize(x, s)
+    assert q.dtype == torch.float8_e4m3fn
+    amax = x.abs().max().item()
+    # primed from the tensor itself: amax maps to the format maximum
+    assert abs(s.scale() - 448.0 / amax) < 1e-3 * s.scale()
+    close(fp8.dequantize(q, s), x, 0.07)
+    # the quantizer records this step's amax; roll moves it into history
+    y = x * 4
+    fp8.quantize(y, s)
+    assert abs(s.state[fp8.HIST].item() - 4 * amax) < 1e-4 * amax
+    s.registry.roll()
+    assert s.state[fp8.HIST].item() == 0
+    assert abs(s.scale() - 448.0 / (4 * amax)) < 1e-3 * s.scale()
+
+
+def test_quantize_saturates_cpu():
+    s = fp8.Scaler("cpu", fp8.E5M2)
+    s.prime(torch.ones(4))           # scale = 57344
+    q = fp8.quantize(torch.tensor([10.0, -10.0, 0.5]), s, record=False)
+    assert torch.isfinite(q.float()).all()
+    assert q.float()[0].item() == 57344.0 and q.float()[1].item() == -57344.0
+
+
+def test_fp8_gemm_close_to_fp32_cpu():
+    a, b = rnd(96, 256), rnd(80, 256, seed=1)
+    sa, sb = fp8.Scaler("cpu"), fp8.Scaler("cpu")
+    got = fp8.gemm(fp8.quantize(a, sa), sa, fp8.quantize(b, sb), sb)
+    close(got, a @ b.t(), 0.06)
+
+
+def test_float8_workflow_trains_cpu():
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    import veles_amd.loader  # noqa: F401
+    g = {"learning_rate": 0.05, "gradient_moment": 0.9}
+    layers = [
+        {"type": "conv_str", "->": {"n_kernels": 16, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(g)},
+        {"type": "conv_str", "->": {"n_kernels": 32, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(g)},
+        {"type": "max_pooling", "->": {"kx": 2, "ky": 2, "sliding": 2}},
+        {"type": "all2all_str", "->": {"output_sample_shape": 64},
+         "<-": dict(g)},
+        {"type": "softmax", "->": {"output_sample_shape": 10}, "<-": dict(g)}]
+    old = root.common.engine.precision_type
+    root.common.engine.precision_type = "float8"
+    try:
+        torch.manual_seed(0)
+        wf = StandardWorkflow(
+            DummyLauncher(), loader_name="synthetic_images",
+            loader_config={"dataset": "mnist", "class_lengths": (0, 100, 400),
+                           "minibatch_size": 50, "normalization_type":
+                           "mean_disp", "seed": 7, "noise": 110.0},
+            layers=layers, decision_config={"max_epochs": 3,
+                                            "fail_iterations": 100})
+        wf.initialize(device=Device(backend="cpu"))
+        f = wf.forwards
+        assert not f[0].fp8_          # C = 1: bf16 / fp32 path
+        assert f[1].fp8_ and f[3].fp8_ and not f[4].fp8_
+        step0 = f[1].fp8_sx_.registry.step
+        wf.run()
+        h = wf.decision.history
+        assert h[-1]["validation_loss"] < h[0]["validation_loss"]
+        assert f[1].fp8_sx_.registry.step - step0 == wf.param_store_.steps
+    finally:
+        root.common.engine.precision_type = old
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [fp8.E4M3, fp8.E5M2])
+def test_quantize_matches_torch_cast(fmt):
+    x = rnd(4099, scale=2.0)          # odd length: vector body + tail
+    s_cpu, s_gpu = fp8.Scaler("cpu", fmt), fp8.Scaler(DEV, fmt)
+    q_cpu = fp8.quantize(x, s_cpu)
+    q_gpu = fp8.quantize(x.to(DEV).to(torch.bfloat16).float(), s_gpu)
+    xb = x.to(torch.bfloat16).float()
+    q_ref = fp8.quantize(xb, fp8.Scaler("cpu", fmt))
+    torch.cuda.synchronize()
+    assert abs(s_gpu.scale() - s_cpu.scale()) < 1e-2 * s_cpu.scale()
+    diff = (q_gpu.cpu().view(torch.uint8) != q_ref.view(torch.uint8))
+    assert diff.sum().item() == 0, "%d of %d codes differ" % (
+        diff.sum().item(), x.numel())
+    assert q_cpu.shape == q_gpu.shape
+    # amax recorded on the device
+    assert abs(s_gpu.state[fp8.HIST].item() - xb.abs().max().item()) < 1e-6
+
+
+def _pair(x, fmt=fp8.E4M3):
+    """Quantize on the GPU; return (gpu q, gpu scaler, cpu copy, cpu scaler
+    with the same state) so the reference sees identical operands."""
+    s = fp8.Scaler(DEV, fmt)
+    q = fp8.quantize(x.to(DEV).to(torch.bfloat16), s)
+    torch.cuda.synchronize()
+    sc = fp8.Scaler("cpu", fmt)
+    sc.state.copy_(s.state.cpu())
+    sc.primed = True
+    return q, s, q.cpu(), sc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (300, 200, 512),
+                                   (1000, 96, 784 + 16), (7, 9, 32)])
+def test_gemm_fp8(M, N, K):
+    a8, sa, a8c, sac = _pair(rnd(M, K))
+    b8, sb, b8c, sbc = _pair(rnd(N, K, seed=1, scale=0.1))
+    bias = torch.randn(N)
+    aux = rnd(M, N, seed=3).to(torch.bfloat16)
+    for act, auxt in ((0, None), (3, None), (0, aux)):
+        ref = fp8.gemm(a8c, sac, b8c, sbc, bias=bias, act=act,
+                       aux=auxt, aux_act=3)
+        got = fp8.gemm(a8, sa, b8, sb, bias=bias.to(DEV), act=act,
+                       aux=None if auxt is None else auxt.to(DEV), aux_act=3)
+        torch.cuda.synchronize()
+        close(got, ref, 1e-2)
+
+
+@pytest.mark.gpu
+def test_gemm_fp8_e5m2_a_operand():
+    a8, sa, a8c, sac = _pair(rnd(256, 256, scale=1e-3), fp8.E5M2)
+    b8, sb, b8c, sbc = _pair(rnd(192, 256, seed=2))
+    got = fp8.gemm(a8, sa, b8, sb)
+    ref = fp8.gemm(a8c, sac, b8c, sbc)
+    close(got, ref, 1e-2)
+
+
+CONVS8 = [
+    # N, H, W, C, OC, KH, KW, sliding(x,y), padding(l,t,r,b), groups
+    (2, 14, 14, 64, 64, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (2, 13, 13, 32, 48, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (2, 27, 27, 96, 256, 5, 5, (1, 1), (2, 2, 2, 2), 2),
+    (3, 11, 9, 16, 32, 3, 3, (2, 2), (1, 1, 0, 0), 1),
+    (2, 8, 8, 128, 160, 1, 1, (1, 1), (0, 0, 0, 0), 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", CONVS8)
+def test_conv_fwd_fp8(cfg):
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    x8, sx, x8c, sxc = _pair(rnd(N, H, W, C))
+    w8, sw, w8c, swc = _pair(rnd(OC, KH, KW, C // g, seed=1, scale=0.1))
+    b = torch.randn(OC)
+    for act in (0, 3):
+        ref = fp8.conv_fwd(x8c, sxc, w8c, swc, b, sl, pad, g, act)
+        got = fp8.conv_fwd(x8, sx, w8, sw, b.to(DEV), sl, pad, g, act)
+        torch.cuda.synchronize()
+        close(got, ref, 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", CONVS8)
+def test_conv_dgrad_fp8(cfg):
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
+    d8, sd, d8c, sdc = _pair(rnd(N, OH, OW, OC, seed=2, scale=1e-2),
+                             fp8.E5M2)
+    w8, sw, w8c, swc = _pair(rnd(OC, KH, KW, C // g, seed=1, scale=0.1))
+    aux = rnd(N, H, W, C, seed=3).to(torch.bfloat16)
+    ref = fp8.conv_dgrad(d8c, sdc, w8c, swc, (N, H, W, C), sl, pad, g,
+                         aux=aux, aux_act=3)
+    got = fp8.conv_dgrad(d8, sd, w8, sw, (N, H, W, C), sl, pad, g,
+                         aux=aux.to(DEV), aux_act=3)
+    torch.cuda.synchronize()
+    close(got, ref, 1e-2)
+
+
+@pytest.mark.gpu
+def test_fp8_roll_kernel():
+    r = fp8.registry(DEV)
+    s = fp8.Scaler(DEV)
+    s.prime(torch.full((64,), 2.0, device=DEV))
+    fp8.quantize(torch.full((64,), 8.0, device=DEV), s)
+    step = r.step
+    r.roll()
+    torch.cuda.synchronize()
+    st = s.state.cpu()
+    assert st[fp8.HIST].item() == 0
+    assert st[step % fp8.HIST].item() == 8.0
+    assert abs(s.scale() - 448.0 / 8.0) < 1e-4

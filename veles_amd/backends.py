@@ -151,6 +151,9 @@ class CpuDevice(Device):
         import torch
         self.torch_device = torch.device("cpu")
         self.compute_dtype = torch.float32
+        # precision_type "float8" on the CPU simulates the fp8 GEMM inputs
+        # (quantize / dequantize) around the float32 reference ops
+        self.fp8 = get(root.common.engine.precision_type, "") == "float8"
         self.index = None
         self.device_info = {"name": "cpu", "cores": os.cpu_count()}
 

@@ -2,7 +2,8 @@
 
 y[B][out] = act(x[B][in] . W[out][in]^T + b) - one MFMA GEMM with the bias and
 activation fused in the epilogue (``hvk_gemm`` NT layout, both operands
-K-contiguous).  Activations: linear, tanh (1.7159 tanh(0.6666x)), relu
+K-contiguous; under precision_type "float8" the e4m3 fp8 MFMA kernel,
+veles_amd/ops/fp8.py).  Activations: linear, tanh (1.7159 tanh(0.6666x)), relu
 (softplus log(1+e^x)), strict relu max(0,x), sigmoid; softmax is the linear
 layer followed by the fused softmax kernel.
 
@@ -17,6 +18,7 @@ import numpy
 from veles_amd.memory import Array
 from veles_amd.models.nn_units import Forward
 from veles_amd import ops
+from veles_amd.ops import fp8
 
 __all__ = ["All2All", "All2AllTanh", "All2AllRELU", "All2AllStrictRELU",
            "All2AllSigmoid", "All2AllSoftmax", "ResizableAll2All"]
@@ -26,6 +28,7 @@ class All2All(Forward):
     __id__ = "58a5eadf-ae1e-498f-bf35-7d93939c4c86"
     MAPPING = "all2all"
     ACTIVATION = 0
+    FP8 = True  # fp8 forward / dgrad under precision_type "float8"
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
@@ -47,6 +50,18 @@ class All2All(Forward):
             else (n_in, self.neurons_number)
         self.register_params(shape, n_in)
         self.allocate_outputs(self.input.shape[0])
+        self.fp8_ = bool(getattr(self.device, "fp8", False)) and \
+            self.FP8 and not self.weights_transposed and \
+            n_in % 16 == 0 and self.neurons_number % 16 == 0
+        if self.fp8_ and self.fp8_sx_ is None:
+            self.fp8_sx_ = fp8.Scaler(self.torch_device, fp8.E4M3)
+            self.fp8_sw_ = fp8.Scaler(self.torch_device, fp8.E4M3)
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.fp8_ = False
+        self.fp8_sx_ = self.fp8_sw_ = None
+        self.x8_ = self.w8_ = None
 
     def allocate_outputs(self, B):
         self.alloc_output((B,) + self.output_sample_shape)
@@ -55,6 +70,13 @@ class All2All(Forward):
         x = self.input.devmem
         B = x.shape[0]
         x2 = x.reshape(B, -1)
+        if self.fp8_:
+            self.x8_ = fp8.quantize(x2, self.fp8_sx_, out=self.x8_)
+            self.w8_ = fp8.quantize(self.weights_lp, self.fp8_sw_,
+                                    out=self.w8_)
+            fp8.gemm(self.x8_, self.fp8_sx_, self.w8_, self.fp8_sw_,
+                     bias=self.bias_master, act=act, out=out2d)
+            return
         if x2.dtype != self.weights_lp.dtype:
             x2 = x2.to(self.weights_lp.dtype)
         ops.gemm(x2, self.weights_lp, trans_b=not self.weights_transposed,
@@ -102,6 +124,7 @@ class All2AllSoftmax(All2All):
     __id__ = "420219fc-3e1a-45b1-87f8-aaa0c1540de4"
     MAPPING = "softmax"
     ACTIVATION = 0
+    FP8 = False  # float32 logits feed the loss: kept on the bf16 kernel
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)

@@ -3,12 +3,16 @@
 NHWC input [B, H, W, C]; weights [n_kernels][ky][kx][C/grouping];
 ``padding`` = (left, top, right, bottom), ``sliding`` = (x, y).  Forward is
 one implicit-GEMM MFMA kernel (``hvk_conv_fwd``: im2col gathered on the fly
-from NHWC, bias + activation in the epilogue, groups on grid z).
+from NHWC, bias + activation in the epilogue, groups on grid z).  With
+``precision_type = "float8"`` and 16-aligned channel counts the input and
+weights are quantized to e4m3 and the conv runs on the fp8 MFMA kernel
+(``hvk_conv_fwd_fp8``, veles_amd/ops/fp8.py).
 """
 from __future__ import annotations
 
 from veles_amd.models.nn_units import Forward
 from veles_amd import ops
+from veles_amd.ops import fp8
 
 __all__ = ["Conv", "ConvTanh", "ConvRELU", "ConvStrictRELU", "ConvSigmoid",
            "norm_padding", "norm_sliding"]
@@ -64,10 +68,18 @@ class Conv(Forward):
                              self.ky * self.kx * cg)
         OH, OW = self.output_hw(shape[1], shape[2])
         self.alloc_output((shape[0], OH, OW, self.n_kernels))
+        self.fp8_ = bool(getattr(self.device, "fp8", False)) and \
+            fp8.fp8_conv_ok(C, self.n_kernels, self.grouping)
+        if self.fp8_ and self.fp8_sx_ is None:
+            self.fp8_sx_ = fp8.Scaler(self.torch_device, fp8.E4M3)
+            self.fp8_sw_ = fp8.Scaler(self.torch_device, fp8.E4M3)
 
     def init_unpickled(self):
         super().init_unpickled()
         self.col_ = None
+        self.fp8_ = False
+        self.fp8_sx_ = self.fp8_sw_ = None
+        self.x8_ = self.w8_ = None
 
     def output_hw(self, H, W):
         return ops.conv_out_size(H, W, self.ky, self.kx, self.sliding,
@@ -80,6 +92,15 @@ class Conv(Forward):
         B, H, W, C = x.shape
         OH, OW = self.output_hw(H, W)
         y = self.alloc_output((B, OH, OW, self.n_kernels))
+        if self.fp8_:
+            # e4m3 input and weights, delayed per-tensor scaling (ops/fp8.py)
+            self.x8_ = fp8.quantize(x, self.fp8_sx_, out=self.x8_)
+            self.w8_ = fp8.quantize(self.weights_lp, self.fp8_sw_,
+                                    out=self.w8_)
+            fp8.conv_fwd(self.x8_, self.fp8_sx_, self.w8_, self.fp8_sw_,
+                         self.bias_master, self.sliding, self.padding,
+                         self.grouping, self.activation, out=y)
+            return
         if x.dtype != self.weights_lp.dtype:
             x = x.to(self.weights_lp.dtype)
         ws = {}

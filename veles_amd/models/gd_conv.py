@@ -3,11 +3,14 @@
 grad_W += wgrad(x, err)   implicit-GEMM MFMA, split over pixels, f32 atomics
 grad_b += colsum(err)
 err_input = dgrad(err, W) [* f'(below.output)]  implicit transposed-conv GEMM
+            (fp8: e5m2 err x e4m3 W on the fp8 MFMA kernel when the forward
+            layer runs in fp8; the weight gradient stays bf16)
 """
 from __future__ import annotations
 
 from veles_amd.models.nn_units import GradientDescentBase
 from veles_amd import ops
+from veles_amd.ops import fp8
 
 __all__ = ["GradientDescentConv", "GDTanhConv", "GDRELUConv",
            "GDStrictRELUConv", "GDSigmoidConv"]
@@ -21,6 +24,11 @@ class GradientDescentConv(GradientDescentBase):
         if self.forward is None:
             raise AttributeError("%s: forward_unit is not set" % self)
         self.attach_params(self.forward)
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.fp8_sdy_ = None
+        self.dy8_ = None
 
     def run(self):
         fwd = self.forward
@@ -42,9 +50,21 @@ class GradientDescentConv(GradientDescentBase):
             aux, aux_act = self.aux_tensor()
             if aux is not None and aux.dim() == 3:
                 aux = aux.unsqueeze(-1)
-            ops.conv_dgrad(err, fwd.weights_lp, tuple(x.shape), fwd.sliding,
-                           fwd.padding, fwd.grouping, aux=aux,
-                           aux_act=aux_act, out=ei)
+            if getattr(fwd, "fp8_", False):
+                # e5m2 gradient x e4m3 weights on the fp8 MFMA kernel
+                if self.fp8_sdy_ is None:
+                    self.fp8_sdy_ = fp8.Scaler(self.torch_device, fp8.E5M2)
+                self.dy8_ = fp8.quantize(err, self.fp8_sdy_, out=self.dy8_)
+                wt8 = fp8.permute_for_dgrad(fwd.w8_, fwd.grouping) \
+                    if err.is_cuda else None
+                fp8.conv_dgrad(self.dy8_, self.fp8_sdy_, fwd.w8_,
+                               fwd.fp8_sw_, tuple(x.shape), fwd.sliding,
+                               fwd.padding, fwd.grouping, aux=aux,
+                               aux_act=aux_act, out=ei, wt8=wt8)
+            else:
+                ops.conv_dgrad(err, fwd.weights_lp, tuple(x.shape),
+                               fwd.sliding, fwd.padding, fwd.grouping,
+                               aux=aux, aux_act=aux_act, out=ei)
             if squeeze:
                 self.err_input.devmem = ei.squeeze(-1)
         self.report_gradients()

@@ -249,6 +249,10 @@ class ParameterStore(object):
         self._ready.clear()
         self._accum_count = 0
         self.steps += 1
+        if self.device is not None and getattr(self.device, "fp8", False):
+            # fp8 delayed scaling: this step's amaxes enter the history
+            from veles_amd.ops import fp8
+            fp8.registry(self.device.torch_device).roll()
         for hook in self.post_update_hooks:
             hook()
         return True

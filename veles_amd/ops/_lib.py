@@ -56,6 +56,15 @@ _SIGS = {
     "hvk_pool_bwd": [P, P, P] + [I] * 13 + [P, I, P],
     "hvk_lrn_fwd": [P, P, L, I, I, F, F, F, P],
     "hvk_lrn_bwd": [P, P, P, L, I, I, F, F, F, P, I, P],
+    # fp8 (csrc/kernels/gemm_fp8.hip)
+    "hvk_fp8_quant": [P, I, L, P, I, P, I, F, I, P],
+    "hvk_fp8_amax": [P, I, L, P, I, P],
+    "hvk_fp8_roll": [P, I, I, I, I, P],
+    "hvk_gemm_fp8": [I, I, I, P, I, I, P, I, I, P, I, P, I, P, I, I, P, P, I,
+                     F, F, P],
+    "hvk_conv_fwd_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F, P],
+    "hvk_conv_dgrad_fp8": [P, P, P] + [I] * 14 + [P, I, I, I, P, P, I, F, F,
+                                                  P],
 }
 _OPTIONAL = {}
 

@@ -1,0 +1,258 @@
+"""FP8 compute path (OCP e4m3 activations / weights, e5m2 gradients) with
+per-tensor delayed scaling (BASELINE config 5).
+
+GPU: ``csrc/kernels/gemm_fp8.hip`` - quantizers that record the tensor's amax
+on the device, and MFMA kernels on ``v_mfma_scale_f32_16x16x128_f8f6f4``
+(2x the bf16 rate) for the conv forward / backward-data and the
+fully-connected forward / backward-data GEMMs.  Weight gradients stay bf16
+(docs/OPS.md §FP8).  CPU: the same quantization in PyTorch (``float8_e4m3fn``
+/ ``float8_e5m2`` casts) followed by the float32 reference op, so CPU tests
+pin the GPU numerics up to accumulation order.
+
+Scaling recipe (per tensor, no host synchronisation):
+
+* every ``Scaler`` owns a row ``[history(HIST), current_amax]`` of a
+  device-resident state block;
+* ``scale = fmax / 2**margin / max(history)`` (1 while the history is empty)
+  is recomputed inside every kernel that needs it from that row, so the
+  quantizer and the GEMM that consumes its output always agree;
+* quantizers ``atomicMax`` the unscaled amax into ``current``; once per step
+  ``roll()`` moves ``current`` into the history ring (one tiny kernel for all
+  scalers of the device);
+* the first use of a scaler primes its history from the tensor itself
+  (one amax pass), so step 0 is "current scaling".
+"""
+from __future__ import annotations
+
+import torch
+
+from veles_amd.ops import _lib
+
+__all__ = ["E4M3", "E5M2", "Scaler", "registry", "quantize", "gemm",
+           "conv_fwd", "conv_dgrad", "permute_for_dgrad", "transpose",
+           "dequantize", "HIST"]
+
+E4M3, E5M2 = 0, 1
+HIST = 16
+FMAX = {E4M3: 448.0, E5M2: 57344.0}
+TORCH_DT = {E4M3: torch.float8_e4m3fn, E5M2: torch.float8_e5m2}
+_CHUNK = 256
+
+
+def _s(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _call(name, *args):
+    _lib.check(getattr(_lib.lib(), name)(*args), name)
+
+
+class _Registry(object):
+    """All scaler states of one device, in fixed [CHUNK][HIST + 1] blocks."""
+
+    def __init__(self, device):
+        self.device = device
+        self.blocks = []
+        self.used = 0
+        self.step = 0
+
+    def allocate(self):
+        i = self.used
+        if i // _CHUNK >= len(self.blocks):
+            self.blocks.append(torch.zeros(_CHUNK, HIST + 1,
+                                           dtype=torch.float32,
+                                           device=self.device))
+        self.used += 1
+        return self.blocks[i // _CHUNK][i % _CHUNK]
+
+    def roll(self):
+        """End of step: current amax -> history slot; current = 0."""
+        idx = self.step % HIST
+        for bi, blk in enumerate(self.blocks):
+            count = min(_CHUNK, self.used - bi * _CHUNK)
+            if count <= 0:
+                break
+            if blk.is_cuda:
+                _call("hvk_fp8_roll", blk.data_ptr(), count, HIST, idx, 0,
+                      _s(blk))
+            else:
+                cur = blk[:count, HIST]
+                keep = cur > 0
+                blk[:count, idx] = torch.where(keep, cur, blk[:count, idx])
+                blk[:count, HIST] = 0
+        self.step += 1
+
+
+_REGISTRIES = {}
+
+
+def registry(device):
+    device = torch.device(device)
+    key = (device.type, device.index)
+    r = _REGISTRIES.get(key)
+    if r is None:
+        r = _REGISTRIES[key] = _Registry(device)
+    return r
+
+
+class Scaler(object):
+    """Per-tensor delayed scaling state (one row of the device registry)."""
+
+    def __init__(self, device, fmt=E4M3, margin=0):
+        self.fmt = fmt
+        self.margin = margin
+        self.registry = registry(device)
+        self.state = self.registry.allocate()
+        self.primed = False
+
+    @property
+    def fmax_eff(self):
+        return FMAX[self.fmt] / (2.0 ** self.margin)
+
+    def scale(self):
+        """Current scale (host read: tests / diagnostics only)."""
+        m = float(self.state[:HIST].max())
+        return self.fmax_eff / m if m > 0 else 1.0
+
+    def _scale_t(self):
+        m = self.state[:HIST].max()
+        return torch.where(m > 0, self.fmax_eff / m, torch.ones_like(m))
+
+    def prime(self, x):
+        if self.primed:
+            return
+        self.primed = True
+        st = self.state
+        if x.is_cuda:
+            xf = x if x.dtype in (torch.float32, torch.bfloat16) else x.float()
+            xf = xf.contiguous()
+            _call("hvk_fp8_amax", xf.data_ptr(),
+                  int(xf.dtype == torch.float32), xf.numel(), st.data_ptr(),
+                  HIST, _s(xf))
+            _call("hvk_fp8_roll", st.data_ptr(), 1, HIST, 0, 1, _s(xf))
+        else:
+            st[:HIST] = x.float().abs().max()
+            st[HIST] = 0
+
+
+def quantize(x, scaler, out=None, record=True):
+    """fp8 copy of ``x`` (bf16 / f32) at the scaler's current scale; records
+    amax|x| for the next roll.  Returns a ``float8_e4m3fn``/``e5m2`` tensor."""
+    scaler.prime(x)
+    dt = TORCH_DT[scaler.fmt]
+    if out is None or out.shape != x.shape or out.dtype != dt or \
+            out.device != x.device:
+        out = torch.empty(x.shape, dtype=dt, device=x.device)
+    if x.is_cuda:
+        if x.dtype not in (torch.float32, torch.bfloat16):
+            x = x.float()
+        x = x.contiguous()
+        _call("hvk_fp8_quant", x.data_ptr(), int(x.dtype == torch.float32),
+              x.numel(), out.data_ptr(), scaler.fmt, scaler.state.data_ptr(),
+              HIST, float(scaler.fmax_eff), int(bool(record)), _s(x))
+        return out
+    xf = x.float()
+    lim = FMAX[scaler.fmt]
+    q = (xf * scaler._scale_t()).clamp(-lim, lim).to(dt)
+    out.copy_(q)
+    if record:
+        st = scaler.state
+        st[HIST] = torch.maximum(st[HIST], xf.abs().max())
+    return out
+
+
+def dequantize(q, scaler):
+    return q.float() / scaler._scale_t()
+
+
+def _u8(t):
+    return t.view(torch.uint8)
+
+
+def transpose(w8):
+    """[R][C] fp8 -> contiguous [C][R] (the FC dgrad B operand)."""
+    return _u8(w8).t().contiguous().view(w8.dtype)
+
+
+def permute_for_dgrad(w8, groups):
+    """[OC][KH][KW][Cg] -> [g][Cg][KH][KW][OCg] (dense K-major dgrad B)."""
+    OC, KH, KW, Cg = w8.shape
+    OCg = OC // groups
+    u = _u8(w8).view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1)
+    return u.contiguous().view(w8.dtype)
+
+
+def gemm(a8, sa, b8, sb, bias=None, act=0, aux=None, aux_act=0, out=None):
+    """out[M][N] (bf16 on GPU) = act(deq(a8) @ deq(b8)^T + bias) * f'(aux)."""
+    from veles_amd import ops
+    M, K = a8.shape
+    N = b8.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16 if a8.is_cuda else
+                          torch.float32, device=a8.device)
+    if a8.is_cuda:
+        _call("hvk_gemm_fp8", M, N, K, a8.data_ptr(), a8.stride(0), sa.fmt,
+              b8.data_ptr(), b8.stride(0), sb.fmt, out.data_ptr(),
+              out.stride(0), ops._p(bias), ops.act_code(act), ops._p(aux),
+              0 if aux is None else aux.stride(0), ops.act_code(aux_act),
+              sa.state.data_ptr(), sb.state.data_ptr(), HIST,
+              float(sa.fmax_eff), float(sb.fmax_eff), _s(a8))
+        return out
+    return ops.gemm(dequantize(a8, sa), dequantize(b8, sb), trans_b=True,
+                    bias=bias, act=act, aux=aux, aux_act=aux_act, out=out)
+
+
+def fp8_conv_ok(C, OC, groups):
+    """Channel counts the fp8 implicit-GEMM loaders take (16-B chunks)."""
+    return C % 16 == 0 and (C // groups) % 16 == 0 and OC % 16 == 0 and \
+        (OC // groups) % 16 == 0
+
+
+def conv_fwd(x8, sx, w8, sw, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
+             groups=1, act=0, out=None):
+    from veles_amd import ops
+    N, H, W, C = x8.shape
+    OC, KH, KW, Cg = w8.shape
+    sxx, syy = sliding
+    pl, pt, pr, pb = padding
+    OH, OW = ops.conv_out_size(H, W, KH, KW, sliding, padding)
+    if out is None:
+        out = torch.empty(N, OH, OW, OC, dtype=torch.bfloat16 if x8.is_cuda
+                          else torch.float32, device=x8.device)
+    if x8.is_cuda:
+        _call("hvk_conv_fwd_fp8", x8.data_ptr(), w8.data_ptr(), ops._p(bias),
+              out.data_ptr(), N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH,
+              OW, groups, ops.act_code(act), sx.fmt, sw.fmt,
+              sx.state.data_ptr(), sw.state.data_ptr(), HIST,
+              float(sx.fmax_eff), float(sw.fmax_eff), _s(x8))
+        return out
+    return ops.conv_fwd(dequantize(x8, sx), dequantize(w8, sw), bias, sliding,
+                        padding, groups, act, out=out)
+
+
+def conv_dgrad(dy8, sdy, w8, sw, x_shape, sliding=(1, 1),
+               padding=(0, 0, 0, 0), groups=1, aux=None, aux_act=0, out=None,
+               wt8=None):
+    """dx = conv^T(deq(dy8), deq(w8)) [* f'(aux)]; ``wt8`` is the
+    ``permute_for_dgrad`` image of w8 (computed here when not given)."""
+    from veles_amd import ops
+    N, H, W, C = x_shape
+    _, OH, OW, OC = dy8.shape
+    _, KH, KW, Cg = w8.shape
+    sxx, syy = sliding
+    pl, pt, pr, pb = padding
+    if out is None:
+        out = torch.empty(N, H, W, C, dtype=torch.bfloat16 if dy8.is_cuda
+                          else torch.float32, device=dy8.device)
+    if dy8.is_cuda:
+        if wt8 is None:
+            wt8 = permute_for_dgrad(w8, groups)
+        _call("hvk_conv_dgrad_fp8", dy8.data_ptr(), wt8.data_ptr(),
+              out.data_ptr(), N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH,
+              OW, groups, ops._p(aux), ops.act_code(aux_act), sdy.fmt,
+              sw.fmt, sdy.state.data_ptr(), sw.state.data_ptr(), HIST,
+              float(sdy.fmax_eff), float(sw.fmax_eff), _s(dy8))
+        return out
+    return ops.conv_dgrad(dequantize(dy8, sdy), dequantize(w8, sw), x_shape,
+                          sliding, padding, groups, aux=aux, aux_act=aux_act,
+                          out=out)
