@@ -1,0 +1,18 @@
+"""MNIST LeNet-style convnet (BASELINE config 2): Caffe LeNet conv 20x5x5 -> pool -> conv 50x5x5 -> pool -> 500 -> 10.
+
+``python -m veles_amd samples/mnist_conv.py -`` (1 GPU), ``... --gpus 0-7``
+(8 ranks, one per MI355X).  Synthetic data of the dataset's shape and
+random-init weights: the reference sample workflows lived in the absent
+Znicz submodule."""
+from veles_amd.models import StandardWorkflow
+from veles_amd.utils.config import root, fix_contents
+import veles_amd.loader  # noqa: F401
+
+
+def run(load, main):
+    cfg = fix_contents(root.mnist_conv)
+    load(StandardWorkflow, loader_name=cfg["loader_name"],
+         loader_config=cfg["loader"], layers=cfg["layers"],
+         decision_config=cfg["decision"],
+         snapshotter_config=cfg.get("snapshotter"))
+    main()
