@@ -23,8 +23,9 @@
 // Only K-major operands exist here (fp8 has no transposed LDS read that the
 // bf16 MN-major path relies on), which covers conv forward (A = im2col(X),
 // B = W[OC][K]), conv dgrad (A = gather(dY), B = W permuted to [C][K]) and
-// the fully-connected forward / dgrad (W^T is materialised once per step).
-// Weight gradients stay on the bf16 kernels (docs/OPS.md §FP8).
+// the fully-connected forward.  Weight gradients and the fully-connected
+// dgrad (whose fp8 B operand would be W^T) stay on the bf16 kernels
+// (docs/OPS.md §FP8).
 #include "conv_geom.h"
 
 using namespace hvk;
@@ -400,52 +401,62 @@ __device__ __forceinline__ float sat(float v, float lim) {
   return fminf(fmaxf(v, -lim), lim);
 }
 
-// 16 elements per thread: bf16 (two 16-B loads) or f32 (four) -> 16 B fp8.
-// amax of |x| (unscaled) goes to st[hist] with an integer atomicMax on the
-// float bits (non-negative floats order like their bit patterns).
-__global__ void fp8_quant_kernel(const void* x, int x_f32, long long n,
-                                 uint8_t* out, int fmt, float* st, int hist,
-                                 float fmax_eff, float lim, int record) {
+// Units of 8 elements (one 16-B bf16 load or two float4 loads -> one 8-B
+// fp8 store), lanes on consecutive units so every load is fully coalesced;
+// each thread keeps UNR units in flight per iteration.  amax of |x|
+// (unscaled) goes to st[hist] with an integer atomicMax on the float bits
+// (non-negative floats order like their bit patterns).
+template <bool F32>
+__device__ __forceinline__ void load8(const void* x, long long u, float* v) {
+  if constexpr (F32) {
+    const float4* p = (const float4*)x + u * 2;
+    float4 a = p[0], b = p[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    uint4 w = ((const uint4*)x)[u];
+    const uint16_t* h = (const uint16_t*)&w;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = bf2f(h[q]);
+  }
+}
+
+template <bool F32>
+__global__ void fp8_quant_kernel(const void* x, long long n, uint8_t* out,
+                                 int fmt, float* st, int hist, float fmax_eff,
+                                 float lim, int record) {
+  constexpr int UNR = 4;
   const float scale = fp8_scale(st, hist, fmax_eff);
   float amax = 0.f;
-  const long long nv = n / 16;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nv;
-       i += (long long)gridDim.x * blockDim.x) {
-    float v[16];
-    if (x_f32) {
-      const float4* p = (const float4*)x + i * 4;
+  const long long nu = n / 8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long u0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       u0 < nu; u0 += stride * UNR) {
+    float v[UNR][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float4 f = p[j];
-        v[4 * j] = f.x; v[4 * j + 1] = f.y; v[4 * j + 2] = f.z; v[4 * j + 3] = f.w;
-      }
-    } else {
-      const uint4* p = (const uint4*)x + i * 2;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        uint4 u = p[j];
-        const uint16_t* h = (const uint16_t*)&u;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[8 * j + q] = bf2f(h[q]);
-      }
+    for (int k = 0; k < UNR; ++k) {
+      const long long u = u0 + k * stride;
+      if (u < nu) load8<F32>(x, u, v[k]);
     }
-    uint4 o;
-    uint32_t* ow = (uint32_t*)&o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int k = 0; k < UNR; ++k) {
+      const long long u = u0 + k * stride;
+      if (u >= nu) break;
+      uint2 o;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) amax = fmaxf(amax, fabsf(v[4 * j + q]));
-      ow[j] = pack4_fp8(sat(v[4 * j] * scale, lim), sat(v[4 * j + 1] * scale, lim),
-                        sat(v[4 * j + 2] * scale, lim),
-                        sat(v[4 * j + 3] * scale, lim), fmt);
+      for (int q = 0; q < 8; ++q) amax = fmaxf(amax, fabsf(v[k][q]));
+      o.x = pack4_fp8(sat(v[k][0] * scale, lim), sat(v[k][1] * scale, lim),
+                      sat(v[k][2] * scale, lim), sat(v[k][3] * scale, lim), fmt);
+      o.y = pack4_fp8(sat(v[k][4] * scale, lim), sat(v[k][5] * scale, lim),
+                      sat(v[k][6] * scale, lim), sat(v[k][7] * scale, lim), fmt);
+      ((uint2*)out)[u] = o;
     }
-    ((uint4*)out)[i] = o;
   }
-  // scalar tail (n % 16)
-  const long long tail0 = nv * 16;
+  // scalar tail (n % 8)
+  const long long tail0 = nu * 8;
   if (blockIdx.x == 0 && threadIdx.x < n - tail0) {
     const long long e = tail0 + threadIdx.x;
-    float v = x_f32 ? ((const float*)x)[e] : bf2f(((const uint16_t*)x)[e]);
+    float v = F32 ? ((const float*)x)[e] : bf2f(((const uint16_t*)x)[e]);
     amax = fmaxf(amax, fabsf(v));
     out[e] = (uint8_t)(pack4_fp8(sat(v * scale, lim), 0.f, 0.f, 0.f, fmt) & 0xFF);
   }
@@ -455,13 +466,22 @@ __global__ void fp8_quant_kernel(const void* x, int x_f32, long long n,
     atomicMax((unsigned int*)(st + hist), __float_as_uint(amax));
 }
 
-__global__ void fp8_amax_kernel(const void* x, int x_f32, long long n,
-                                float* st, int hist) {
+template <bool F32>
+__global__ void fp8_amax_kernel(const void* x, long long n, float* st,
+                                int hist) {
   float amax = 0.f;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    float v = x_f32 ? ((const float*)x)[i] : bf2f(((const uint16_t*)x)[i]);
-    amax = fmaxf(amax, fabsf(v));
+  const long long nu = n / 8;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nu;
+       u += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    load8<F32>(x, u, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) amax = fmaxf(amax, fabsf(v[q]));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - nu * 8) {
+    const long long e = nu * 8 + threadIdx.x;
+    amax = fmaxf(amax, fabsf(F32 ? ((const float*)x)[e]
+                                 : bf2f(((const uint16_t*)x)[e])));
   }
   amax = wave_max(amax);
   if ((threadIdx.x & 63) == 0 && amax > 0.f)
@@ -499,16 +519,26 @@ HVK_API int hvk_fp8_quant(const void* x, int x_f32, long long n, void* out,
                           int record, hipStream_t s) {
   if (((uintptr_t)x & 15) || ((uintptr_t)out & 15)) return -3;
   const float lim = fmt == 0 ? 448.f : 57344.f;
-  hipLaunchKernelGGL(fp8_quant_kernel, dim3(grid_for(n / 16 + 1, 256)),
-                     dim3(256), 0, s, x, x_f32, n, (uint8_t*)out, fmt, st,
-                     hist, fmax_eff, lim, record);
+  const dim3 grid(grid_for(n / 32 + 1, 256));
+  if (x_f32)
+    hipLaunchKernelGGL(fp8_quant_kernel<true>, grid, dim3(256), 0, s, x, n,
+                       (uint8_t*)out, fmt, st, hist, fmax_eff, lim, record);
+  else
+    hipLaunchKernelGGL(fp8_quant_kernel<false>, grid, dim3(256), 0, s, x, n,
+                       (uint8_t*)out, fmt, st, hist, fmax_eff, lim, record);
   return (int)hipGetLastError();
 }
 
 HVK_API int hvk_fp8_amax(const void* x, int x_f32, long long n, float* st,
                          int hist, hipStream_t s) {
-  hipLaunchKernelGGL(fp8_amax_kernel, dim3(grid_for(n, 1024)), dim3(256), 0,
-                     s, x, x_f32, n, st, hist);
+  if (((uintptr_t)x & 15)) return -3;
+  const dim3 grid(grid_for(n / 8 + 1, 256));
+  if (x_f32)
+    hipLaunchKernelGGL(fp8_amax_kernel<true>, grid, dim3(256), 0, s, x, n, st,
+                       hist);
+  else
+    hipLaunchKernelGGL(fp8_amax_kernel<false>, grid, dim3(256), 0, s, x, n,
+                       st, hist);
   return (int)hipGetLastError();
 }
 

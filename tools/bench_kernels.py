@@ -5,6 +5,7 @@ Writes gpurun_out/bench_kernels.json.  Random operands (cdna_hip_programming
 §5.4 rule 25), interleaved timing in one process (rule 24).
 """
 import json
+import os
 import sys
 import time
 
@@ -17,6 +18,8 @@ import veles_amd.ops as ops  # noqa: E402
 dev = "cuda"
 BF = torch.bfloat16
 res = {}
+BIG = int(os.environ.get("HVK_BIG_TILE", "1"))
+ops.set_gemm_big_tile(BIG)
 
 
 def timeit(fn, n=20, w=3):
@@ -78,6 +81,7 @@ def conv_case(name, N, H, W, C, OC, k, s, p, g):
 
 gemm_case("gemm_4096", 4096, 4096, 4096)
 gemm_case("gemm_8192", 8192, 8192, 8192)
+gemm_case("gemm_8192_nn", 8192, 8192, 8192, tb=False)
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 gemm_case("fc6_fwd", B, 4096, 9216)
 gemm_case("fc6_dgrad", B, 9216, 4096, tb=False)
@@ -87,4 +91,6 @@ conv_case("conv2", B, 27, 27, 96, 256, 5, 1, 2, 2)
 conv_case("conv3", B, 13, 13, 256, 384, 3, 1, 1, 1)
 conv_case("conv4", B, 13, 13, 384, 384, 3, 1, 1, 2)
 conv_case("conv5", B, 13, 13, 384, 256, 3, 1, 1, 2)
-json.dump(res, open("gpurun_out/bench_kernels.json", "w"), indent=1)
+conv_case("vgg_conv3_2", 64, 56, 56, 256, 256, 3, 1, 1, 1)
+json.dump(res, open("gpurun_out/bench_kernels_big%d.json" % BIG, "w"),
+          indent=1)

@@ -10,7 +10,6 @@ from __future__ import annotations
 
 from veles_amd.models.nn_units import GradientDescentBase
 from veles_amd import ops
-from veles_amd.ops import fp8
 
 __all__ = ["GradientDescent", "GDTanh", "GDRELU", "GDStrictRELU",
            "GDSigmoid", "GDSoftmax"]
@@ -25,11 +24,6 @@ class GradientDescent(GradientDescentBase):
         if fwd is None:
             raise AttributeError("%s: forward_unit is not set" % self)
         self.attach_params(fwd)
-
-    def init_unpickled(self):
-        super().init_unpickled()
-        self.fp8_sdy_ = None
-        self.dy8_ = None
 
     def run(self):
         fwd = self.forward
@@ -54,17 +48,10 @@ class GradientDescent(GradientDescentBase):
             ei = self.alloc_err_input(self.input.devmem.shape)
             aux, aux_act = self.aux_tensor()
             aux2 = None if aux is None else aux.reshape(B, -1)
-            if getattr(fwd, "fp8_", False):
-                # e5m2 err x e4m3 W^T on the fp8 MFMA kernel
-                if self.fp8_sdy_ is None:
-                    self.fp8_sdy_ = fp8.Scaler(self.torch_device, fp8.E5M2)
-                self.dy8_ = fp8.quantize(e2, self.fp8_sdy_, out=self.dy8_)
-                fp8.gemm(self.dy8_, self.fp8_sdy_, fp8.transpose(fwd.w8_),
-                         fwd.fp8_sw_, aux=aux2, aux_act=aux_act,
-                         out=ei.view(B, -1))
-            else:
-                ops.gemm(e2, fwd.weights_lp, trans_b=fwd.weights_transposed,
-                         out=ei.view(B, -1), aux=aux2, aux_act=aux_act)
+            # stays bf16 under float8 as well: an fp8 dgrad would need W^T
+            # materialised every step, which costs more than the GEMM
+            ops.gemm(e2, fwd.weights_lp, trans_b=fwd.weights_transposed,
+                     out=ei.view(B, -1), aux=aux2, aux_act=aux_act)
         self.report_gradients()
 
 

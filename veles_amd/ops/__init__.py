@@ -180,6 +180,12 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
     return out
 
 
+def set_gemm_big_tile(on):
+    """Enable / disable the 256x128 big-tile GEMM kernel for long-M GEMMs
+    (A/B switch for benchmarks; enabled by default)."""
+    _lib_call("hvk_set_gemm_big_tile", int(bool(on)))
+
+
 def linear_fwd(x, w, bias=None, act=0, out=None):
     """y[B][out] = act(x[B][in] @ w[out][in]^T + bias)."""
     return gemm(x, w, trans_b=True, bias=bias, act=act, out=out)

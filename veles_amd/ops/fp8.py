@@ -4,10 +4,11 @@ per-tensor delayed scaling (BASELINE config 5).
 GPU: ``csrc/kernels/gemm_fp8.hip`` - quantizers that record the tensor's amax
 on the device, and MFMA kernels on ``v_mfma_scale_f32_16x16x128_f8f6f4``
 (2x the bf16 rate) for the conv forward / backward-data and the
-fully-connected forward / backward-data GEMMs.  Weight gradients stay bf16
-(docs/OPS.md §FP8).  CPU: the same quantization in PyTorch (``float8_e4m3fn``
-/ ``float8_e5m2`` casts) followed by the float32 reference op, so CPU tests
-pin the GPU numerics up to accumulation order.
+fully-connected forward GEMMs.  Weight gradients and the fully-connected
+backward-data GEMM stay bf16 (docs/OPS.md §FP8).  CPU: the same quantization
+in PyTorch (``float8_e4m3fn`` / ``float8_e5m2`` casts) followed by the
+float32 reference op, so CPU tests pin the GPU numerics up to accumulation
+order.
 
 Scaling recipe (per tensor, no host synchronisation):
 
@@ -170,7 +171,7 @@ def _u8(t):
 
 
 def transpose(w8):
-    """[R][C] fp8 -> contiguous [C][R] (the FC dgrad B operand)."""
+    """[R][C] fp8 -> contiguous [C][R]."""
     return _u8(w8).t().contiguous().view(w8.dtype)
 
 
