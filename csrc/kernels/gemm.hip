@@ -63,7 +63,7 @@ struct DenseK {
     return c;
   }
   static constexpr bool kGlds = true;
-  __host__ __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
+  __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     return (c.ok && k < K) ? c.row + k : g_zero8;
   }
@@ -87,7 +87,7 @@ struct DenseMN {
   __device__ void group(int g) { p += (long long)g * gstride; }
   __device__ __forceinline__ Ctx col_ctx(int c) const { return Ctx{c}; }
   static constexpr bool kGlds = true;
-  __host__ __device__ bool dma_ok() const {
+  __device__ bool dma_ok() const {
     return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
   }
   __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int k) const {
@@ -140,7 +140,7 @@ struct ConvFwdA {
     return x[c.base + (ih * g.W + iw) * g.C + ch];
   }
   static constexpr bool kGlds = true;
-  __host__ __device__ bool dma_ok() const { return vec; }
+  __device__ bool dma_ok() const { return vec; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t t, ch, kh, kw;
@@ -204,7 +204,7 @@ struct ConvDgradA {
     return c.base + (oh * g.OW + ow) * g.OC;
   }
   static constexpr bool kGlds = true;
-  __host__ __device__ bool dma_ok() const { return vec; }
+  __device__ bool dma_ok() const { return vec; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t oc;
@@ -228,7 +228,7 @@ struct ConvDgradA {
 // to the common vectorised kernels)
 struct ConvDgradAS : ConvDgradA {
   static constexpr bool kGlds = false;
-  __host__ __device__ bool dma_ok() const { return false; }
+  __device__ bool dma_ok() const { return false; }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     uint16_t e[8];
@@ -264,7 +264,7 @@ struct ConvWgradB {
     return c;
   }
   static constexpr bool kGlds = true;
-  __host__ __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
+  __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return g_zero8;
     if (cx.ok == 2) return g_ones8;
@@ -334,7 +334,7 @@ struct RunGeom {
 
 struct ConvFwdRunA {
   static constexpr bool kGlds = false;
-  __host__ __device__ bool dma_ok() const { return false; }
+  __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
   RunGeom r;
@@ -381,7 +381,7 @@ struct ConvFwdRunA {
 // wgrad B for small-channel convs: MN-major, rows = pixels, cols = (kh, j)
 struct ConvWgradRunB {
   static constexpr bool kGlds = false;
-  __host__ __device__ bool dma_ok() const { return false; }
+  __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
   RunGeom r;
@@ -800,173 +800,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
 }
 
-
-// ---------------------------------------------------------------------------
-// Big-tile variant for GEMMs with a long M (conv forward / backward-data:
-// M = pixels) and a K-major A operand: 256 x 128 x 64 tile, 8 waves (4 x 2,
-// each 64 x 64 - the same fragment code as above), ONE workgroup per CU with
-// a 3-stage LDS-DMA ring (144 KiB).  Two K tiles stay in flight, so a single
-// barrier per K tile suffices: the buffer refilled at step kt was last read
-// at step kt-1, which every wave finished before passing step kt's barrier.
-// Per FLOP it moves 25 % fewer operand bytes than the 128 x 128 tile.
-constexpr int BMB = 256, NTB = 512, NSTG = 3;
-
-template <class LA, class LB, bool BKM>
-__global__ void __launch_bounds__(NTB, 1)
-gemm_big_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int tiles_n,
-                int tiles) {
-  constexpr int SA = BMB * BK;            // A stage (elements)
-  constexpr int SB = 128 * BK;            // B stage
-  constexpr int STG = SA + SB;
-  constexpr int OPER = NSTG * STG * 2;    // bytes
-  constexpr int LDC = 128 + 4;
-  constexpr int CT = BMB * LDC * 4;
-  constexpr int SMEM_BYTES = OPER > CT ? OPER : CT;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES / 2];
-
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = wgid % tiles;
-  const int gi = wgid / tiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  la.group(gi);
-  lb.group(gi);
-  const int m0 = tm * BMB, n0 = tn * 128;
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int trq = fr >> 2, trp = fr & 3;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto frag_k = [&](const uint16_t* s, int rowbase, int ks) -> bf16x8 {
-    int row = rowbase + fr;
-    int c = ks * 4 + fq;
-    return *(const bf16x8*)(s + row * 64 + ((c ^ (row & 7)) << 3));
-  };
-  auto frag_mn = [&](const uint16_t* s, int colbase, int ks) -> bf16x8 {
-    int k = ks * 32 + fq * 8 + trq;
-    int b = colbase >> 4;
-    const uint16_t* p0 = s + k * 128 + ((b ^ hk(k)) << 4) + trp * 4;
-    const uint16_t* p1 = s + (k + 4) * 128 + ((b ^ hk(k + 4)) << 4) + trp * 4;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, v);
-  };
-  auto compute = [&](const uint16_t* sA, const uint16_t* sB) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag_k(sA, wm * 64 + i * 16, ks);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (BKM) bfv[i] = frag_k(sB, wn * 64 + i * 16, ks);
-        else bfv[i] = frag_mn(sB, wn * 64 + i * 16, ks);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
-                                                              acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // DMA map: A 32 KiB = 32 instructions (8 rows x 128 B each), 4 per wave;
-  // B 16 KiB = 16 instructions, 2 per wave (K-major rows, or the 128-wide
-  // MN-major image of the 128 x 128 kernel)
-  constexpr int NIA = 4, NIB = 2;
-  const int w = __builtin_amdgcn_readfirstlane(wid);
-  typename LA::Ctx da[NIA];
-  typename LB::Ctx db[NIB];
-  int ka[NIA], kb[NIB];
-#pragma unroll
-  for (int i = 0; i < NIA; ++i) {
-    const int I = w * NIA + i;
-    const int row = 8 * I + (lane >> 3);
-    da[i] = la.row_ctx(m0 + row);
-    ka[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
-  }
-#pragma unroll
-  for (int i = 0; i < NIB; ++i) {
-    const int I = w * NIB + i;
-    if constexpr (BKM) {
-      const int row = 8 * I + (lane >> 3);
-      db[i] = lb.row_ctx(n0 + row);
-      kb[i] = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
-    } else {
-      int hkv = ((lane >> 4) & 3) | (((I >> 1) & 1) << 2);
-      int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
-      db[i] = lb.col_ctx(n0 + 8 * c);
-      kb[i] = 4 * I + (lane >> 4);
-    }
-  }
-  auto issue = [&](int k0, uint16_t* st) {
-#pragma unroll
-    for (int i = 0; i < NIA; ++i)
-      __builtin_amdgcn_global_load_lds(
-          (const void*)la.src(da[i], k0 + ka[i]),
-          (__attribute__((address_space(3))) void*)(st + (w * NIA + i) * 512),
-          16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < NIB; ++i)
-      __builtin_amdgcn_global_load_lds(
-          (const void*)lb.src(db[i], k0 + kb[i]),
-          (__attribute__((address_space(3))) void*)(st + SA + (w * NIB + i) * 512),
-          16, 0, 0);
-  };
-
-  const int nk = (K + BK - 1) / BK;
-  issue(0, smem);
-  if (nk > 1) issue(BK, smem + STG);
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + 2 < nk) {
-      int nxt = cur + 2 >= NSTG ? cur + 2 - NSTG : cur + 2;
-      issue((kt + 2) * BK, smem + nxt * STG);
-    }
-    compute(smem + cur * STG, smem + cur * STG + SA);
-    cur = cur + 1 == NSTG ? 0 : cur + 1;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  float* sC = (float*)smem;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int rb = wm * 64 + i * 16 + fq * 4;
-      int cc = wn * 64 + j * 16 + fr;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + cc] = acc[i][j][rr];
-    }
-  __syncthreads();
-  for (int q = t; q < BMB * 16; q += NTB) {
-    int row = q >> 4, c8 = (q & 15) * 8;
-    if (m0 + row >= M) continue;
-    const float4* src = (const float4*)(sC + row * LDC + c8);
-    float v[8];
-    float4 lo = src[0], hi = src[1];
-    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    epi.store8(gi, m0 + row, n0 + c8, v);
-  }
-}
-
-// 0: 128-row kernel only; 1: big-tile kernel where it applies (default)
-int g_big_tile = 1;
-
 // Tile width: 64 only when the 128-wide tile would waste more than 1/8 of
 // its columns (N = 48, 96, 192, 432); wide N keeps 128 so the A operand is
 // re-read by half as many column tiles (weight-gradient GEMMs, N = taps*C).
@@ -979,19 +812,6 @@ inline bool use_bn64(int N) {
 template <class LA, bool AK, class LB, bool BKM>
 hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                   int K, int splits, int groups, hipStream_t s) {
-  if constexpr (AK && LA::kGlds && LB::kGlds) {
-    // long-M GEMMs with a 128-wide-friendly N: the big-tile kernel
-    if (g_big_tile && splits <= 1 && !epi.atomic && !use_bn64(N) &&
-        (long long)M * groups >= 256LL * 512 && la.dma_ok() && lb.dma_ok()) {
-      const int tiles_m = (M + BMB - 1) / BMB, tiles_n = (N + 127) / 128;
-      const int tiles = tiles_m * tiles_n;
-      hipLaunchKernelGGL((gemm_big_kernel<LA, LB, BKM>),
-                         dim3((unsigned)((long long)tiles * groups)),
-                         dim3(NTB), 0, s, la, lb, epi, M, N, K, tiles_n,
-                         tiles);
-      return hipGetLastError();
-    }
-  }
   const bool n64 = use_bn64(N);
   const int bn = n64 ? 64 : 128;
   int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
@@ -1237,10 +1057,4 @@ HVK_API int hvk_conv_wgrad_run(const void* X, const void* dY, float* dW,
   }
   return (int)launch<DenseMN, false, ConvWgradRunB, false>(la, lb, e, OC, Nk, P,
                                                            splits, 1, s);
-}
-
-// A/B switch for the big-tile kernel (tools/bench_kernels.py)
-HVK_API int hvk_set_gemm_big_tile(int on) {
-  g_big_tile = on;
-  return 0;
 }

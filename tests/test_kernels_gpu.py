@@ -330,47 +330,3 @@ def test_solver_kernel(mode):
     close(s1g, s1c, 1e-5)
     close(lp.float(), wc, 1e-2)
 
-
-@pytest.mark.parametrize("big", [0, 1])
-@pytest.mark.parametrize("tb", [0, 1])
-def test_gemm_long_m_big_tile(big, tb):
-    # M * groups >= 256 * 512 selects the 256x128 3-stage kernel
-    M, N, K = 131072 + 77, 200, 136
-    a = rnd(M, K)
-    b = rnd(N, K, seed=1) if tb else rnd(K, N, seed=1)
-    bias = torch.randn(N)
-    ref = ops.gemm(a, b, trans_b=bool(tb), bias=bias, act=3,
-                   out_dtype=torch.float32)
-    ops.set_gemm_big_tile(big)
-    try:
-        got = ops.gemm(a.to(DEV), b.to(DEV), trans_b=bool(tb),
-                       bias=bias.to(DEV), act=3, out_dtype=torch.float32)
-        torch.cuda.synchronize()
-    finally:
-        ops.set_gemm_big_tile(1)
-    close(got, ref, 5e-3)
-
-
-@pytest.mark.parametrize("big", [0, 1])
-@pytest.mark.parametrize("cfg", [
-    (32, 64, 64, 16, 128, 3, 3, (1, 1), (1, 1, 1, 1), 1),
-    (16, 66, 66, 64, 256, 3, 3, (1, 1), (1, 1, 1, 1), 2),
-    (8, 130, 130, 32, 384, 5, 5, (2, 2), (2, 2, 2, 2), 1)])
-def test_conv_long_m_big_tile(big, cfg):
-    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
-    x = rnd(N, H, W, C)
-    w = rnd(OC, KH, KW, C // g, seed=1, scale=0.1)
-    b = torch.randn(OC)
-    OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
-    dy = rnd(N, OH, OW, OC, seed=2)
-    ref = ops.conv_fwd(x, w, b, sl, pad, g, 3)
-    refd = ops.conv_dgrad(dy, w, (N, H, W, C), sl, pad, g)
-    ops.set_gemm_big_tile(big)
-    try:
-        got = ops.conv_fwd(x.to(DEV), w.to(DEV), b.to(DEV), sl, pad, g, 3)
-        gotd = ops.conv_dgrad(dy.to(DEV), w.to(DEV), (N, H, W, C), sl, pad, g)
-        torch.cuda.synchronize()
-    finally:
-        ops.set_gemm_big_tile(1)
-    close(got, ref, 1e-2)
-    close(gotd, refd, 1e-2)

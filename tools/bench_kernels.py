@@ -18,8 +18,7 @@ import veles_amd.ops as ops  # noqa: E402
 dev = "cuda"
 BF = torch.bfloat16
 res = {}
-BIG = int(os.environ.get("HVK_BIG_TILE", "1"))
-ops.set_gemm_big_tile(BIG)
+TAG = os.environ.get("HVK_BENCH_TAG", "")
 
 
 def timeit(fn, n=20, w=3):
@@ -92,5 +91,5 @@ conv_case("conv3", B, 13, 13, 256, 384, 3, 1, 1, 1)
 conv_case("conv4", B, 13, 13, 384, 384, 3, 1, 1, 2)
 conv_case("conv5", B, 13, 13, 384, 256, 3, 1, 1, 2)
 conv_case("vgg_conv3_2", 64, 56, 56, 256, 256, 3, 1, 1, 1)
-json.dump(res, open("gpurun_out/bench_kernels_big%d.json" % BIG, "w"),
+json.dump(res, open("gpurun_out/bench_kernels%s.json" % TAG, "w"),
           indent=1)

@@ -15,6 +15,7 @@ right, bottom), sliding (x, y).
 """
 from __future__ import annotations
 
+import os
 import struct
 
 import torch
@@ -178,12 +179,6 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         r = r * act_bwd_ref(aux.float(), aux_act)
     out.copy_(r.to(out.dtype))
     return out
-
-
-def set_gemm_big_tile(on):
-    """Enable / disable the 256x128 big-tile GEMM kernel for long-M GEMMs
-    (A/B switch for benchmarks; enabled by default)."""
-    _lib_call("hvk_set_gemm_big_tile", int(bool(on)))
 
 
 def linear_fwd(x, w, bias=None, act=0, out=None):
@@ -446,7 +441,15 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     return dw
 
 
-def wgrad_splits(P, M, N, groups, target_blocks=2048):
+# 512 blocks (2 per CU) measured best on AlexNet b512 (72.7k img/s vs 71.6k
+# at 2048 and 69.0k at 4096: fewer splits = fewer f32 atomics)
+_WGRAD_BLOCKS = int(os.environ.get("HVK_WGRAD_BLOCKS", "512"))
+
+
+def wgrad_splits(P, M, N, groups, target_blocks=None):
+    """Pixel (K) splits of a weight-gradient GEMM: enough blocks to fill the
+    256 CUs, few enough that the f32 atomic reduction stays small."""
+    target_blocks = target_blocks or _WGRAD_BLOCKS
     tiles = ((M + 127) // 128) * ((N + 127) // 128) * groups
     splits = max(1, min(target_blocks // max(tiles, 1), P // 512))
     return splits

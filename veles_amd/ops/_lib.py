@@ -56,7 +56,6 @@ _SIGS = {
     "hvk_pool_bwd": [P, P, P] + [I] * 13 + [P, I, P],
     "hvk_lrn_fwd": [P, P, L, I, I, F, F, F, P],
     "hvk_lrn_bwd": [P, P, P, L, I, I, F, F, F, P, I, P],
-    "hvk_set_gemm_big_tile": [I],
     # fp8 (csrc/kernels/gemm_fp8.hip)
     "hvk_fp8_quant": [P, I, L, P, I, P, I, F, I, P],
     "hvk_fp8_amax": [P, I, L, P, I, P],
