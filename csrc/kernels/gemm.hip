@@ -678,8 +678,11 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         if (kt + 1 < nk) {
           issue(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * SA,
                 smem + 2 * SA + (cur ^ 1) * SB);
+          // leave exactly the next tile's DMAs (NIA + NIB) in flight
           if constexpr (NIA + NIB == 8)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else if constexpr (NIA + NIB == 7)
+            asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
           else
             asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         } else {
@@ -800,20 +803,24 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
 }
 
-// Tile width: 64 only when the 128-wide tile would waste more than 1/8 of
-// its columns (N = 48, 96, 192, 432); wide N keeps 128 so the A operand is
-// re-read by half as many column tiles (weight-gradient GEMMs, N = taps*C).
-inline bool use_bn64(int N) {
-  int w128 = (N + 127) / 128 * 128 - N;
-  int w64 = (N + 63) / 64 * 64 - N;
-  return w64 < w128 && w128 * 8 > N;
+// Tile width: 128 unless it wastes more than 1/8 of the columns; then the
+// width among {96 (K-major B only), 64} that wastes least, the wider on a
+// tie (N = 96, 192: 96; N = 48: 64).  Wide N keeps 128 so the A operand is
+// re-read by as few column tiles as possible (weight-gradient GEMMs).
+inline int pick_bn(int N, bool allow96) {
+  auto waste = [&](int b) { return (N + b - 1) / b * b - N; };
+  if (waste(128) * 8 <= N) return 128;
+  int best = 128;
+  if (allow96 && waste(96) < waste(best)) best = 96;
+  if (waste(64) < waste(best)) best = 64;
+  return best;
 }
 
 template <class LA, bool AK, class LB, bool BKM>
 hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                   int K, int splits, int groups, hipStream_t s) {
-  const bool n64 = use_bn64(N);
-  const int bn = n64 ? 64 : 128;
+  // a 96-wide MN-major B has no register-staged path (12 chunks per row)
+  const int bn = pick_bn(N, BKM);
   int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
   if (splits < 1) splits = 1;
   int k_split = (K + splits - 1) / splits;
@@ -821,14 +828,24 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   splits = (K + k_split - 1) / k_split;
   const int tiles = tiles_m * tiles_n;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  if (n64)
+  if (bn == 64)
     hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64>), grid, dim3(NTHR), 0,
                        s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
                        splits);
-  else
+  else if constexpr (BKM) {
+    if (bn == 96)
+      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 96>), grid, dim3(NTHR),
+                         0, s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
+                         splits);
+    else
+      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128>), grid,
+                         dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
+                         tiles_n, tiles, splits);
+  } else {
     hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128>), grid, dim3(NTHR), 0,
                        s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
                        splits);
+  }
   return hipGetLastError();
 }
 

@@ -102,7 +102,13 @@ class TrivialAcceleratedUnit(AcceleratedUnit):
 
 class DeviceBenchmark(AcceleratedUnit):
     """C = A*B square GEMM timing (reference accelerated_units.py:705-824);
-    returns ``1000/dt`` ("computing power") or the mean seconds."""
+    returns ``1000/dt`` ("computing power") or the mean seconds.
+
+    ``dtype`` "float32" / "float64" times the exact-precision MFMA SGEMM /
+    DGEMM at ``precision_level`` 0/1/2 - the reference's only published
+    device numbers are SGEMM/DGEMM 3001^3 at these levels
+    (devices/device_infos.json); default: the device compute
+    dtype (bf16 MFMA GEMM on the MI355X)."""
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
@@ -110,32 +116,52 @@ class DeviceBenchmark(AcceleratedUnit):
         self.repeats = int(kwargs.get("repeats", 10))
         self.dry_run_first = kwargs.get("dry_run_first", True)
         self.return_time = kwargs.get("return_time", False)
+        self.dtype = kwargs.get("dtype")
+        self.precision_level = kwargs.get("precision_level")
 
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
         import torch
         n = self.size
         g = torch.Generator().manual_seed(1)
-        a = torch.rand(n, n, generator=g) - 0.5
-        b = torch.rand(n, n, generator=g) - 0.5
-        self.a_ = a.to(self.torch_device, self.compute_dtype)
-        self.b_ = b.to(self.torch_device, self.compute_dtype)
+        a = torch.rand(n, n, generator=g, dtype=torch.float64) - 0.5
+        b = torch.rand(n, n, generator=g, dtype=torch.float64) - 0.5
+        dt = getattr(torch, self.dtype) if self.dtype else self.compute_dtype
+        self.a_ = a.to(self.torch_device, dt)
+        self.b_ = b.to(self.torch_device, dt)
+        self.c_ = torch.empty(n, n, dtype=dt, device=self.torch_device)
+
+    def _gemm(self):
+        from veles_amd import ops
+        kw = {}
+        if self.a_.dtype in (torch_f32(), torch_f64()):
+            kw["precision_level"] = self.precision_level
+        ops.gemm(self.a_, self.b_, out=self.c_, **kw)
 
     def run(self):
-        from veles_amd import ops
         if self.dry_run_first:
-            ops.gemm(self.a_, self.b_)
+            self._gemm()
         if self.is_gpu:
             self.device_.sync()
         t0 = time.perf_counter()
         for _ in range(self.repeats):
-            ops.gemm(self.a_, self.b_)
+            self._gemm()
         if self.is_gpu:
             self.device_.sync()
         dt = (time.perf_counter() - t0) / self.repeats
         self.seconds = dt
         self.gflops = 2.0 * self.size ** 3 / dt / 1e9
         return dt if self.return_time else 1000.0 / dt
+
+
+def torch_f32():
+    import torch
+    return torch.float32
+
+
+def torch_f64():
+    import torch
+    return torch.float64
 
 
 class AcceleratedWorkflow(Workflow):

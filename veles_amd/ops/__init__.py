@@ -119,13 +119,19 @@ def act_bwd(dy, y, act, out=None):
 # --------------------------------------------------------------------- GEMM
 def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
          alpha=1.0, beta=0.0, bias=None, bias_mode="col", act=0, aux=None,
-         aux_act=0, accumulate=False, splits=1, bias_grad=None):
+         aux_act=0, accumulate=False, splits=1, bias_grad=None,
+         precision_level=None):
     """out[M][N] = act(alpha*op(a)@op(b) + beta*out + bias) * f'_aux(aux).
 
     ``accumulate``: out (float32) += alpha*op(a)@op(b) (+bias) - split-K
     partial sums are reduced with float atomics on the GPU.
     ``bias_grad`` (float32 [M], accumulate only): += alpha * row sums of
     op(a), computed by the same kernel (a ones column appended to op(b)).
+
+    float32 / float64 GPU operands run the exact-precision MFMA SGEMM /
+    DGEMM (csrc/kernels/gemm_f32.hip; alpha / beta / accumulate only) with
+    the reference's ``precision_level`` 0 (plain), 1 (Kahan) or 2 (TwoSum
+    multi-partial); default ``root.common.engine.precision_level``.
     """
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
@@ -141,9 +147,14 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         out_dtype = out_dtype or (torch.float32 if accumulate else a.dtype)
         out = (torch.zeros if accumulate else torch.empty)(
             M, N, dtype=out_dtype, device=dev)
+    if _gpu(a) and a.dtype in (torch.float32, torch.float64):
+        return _gemm_fx(a, b, trans_a, trans_b, out, M, N, K, alpha, beta,
+                        accumulate, precision_level, bias, act, aux,
+                        bias_grad)
     if _gpu(a):
         if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
-            raise TypeError("GPU gemm operands must be bfloat16")
+            raise TypeError("GPU gemm operands must be bfloat16 (or float32 "
+                            "/ float64 for the exact-precision GEMM)")
         for t in (a, b, out):
             if t.stride(-1) != 1:
                 raise ValueError("gemm operands must be row-major")
@@ -178,6 +189,32 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
     if aux is not None:
         r = r * act_bwd_ref(aux.float(), aux_act)
     out.copy_(r.to(out.dtype))
+    return out
+
+
+def _precision_level(level):
+    if level is not None:
+        return int(level)
+    from veles_amd.utils.config import root, get
+    return int(get(root.common.engine.precision_level, 0))
+
+
+def _gemm_fx(a, b, ta, tb, out, M, N, K, alpha, beta, accumulate, level,
+             bias, act, aux, bias_grad):
+    if bias is not None or act_code(act) or aux is not None or \
+            bias_grad is not None:
+        raise ValueError("the float32/float64 GEMM takes alpha/beta only")
+    if b.dtype != a.dtype or out.dtype != a.dtype:
+        raise TypeError("gemm: mixed %s / %s / %s operands" %
+                        (a.dtype, b.dtype, out.dtype))
+    for t in (a, b, out):
+        if t.stride(-1) != 1:
+            raise ValueError("gemm operands must be row-major")
+    name = "hvk_gemm_f32" if a.dtype == torch.float32 else "hvk_gemm_f64"
+    _lib_call(name, int(ta), int(tb), M, N, K, _p(a), a.stride(0), _p(b),
+              b.stride(0), _p(out), out.stride(0), float(alpha),
+              1.0 if accumulate else float(beta), _precision_level(level),
+              _s(a))
     return out
 
 

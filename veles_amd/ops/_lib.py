@@ -23,6 +23,7 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_longlong
 F = ctypes.c_float
+D = ctypes.c_double
 U = ctypes.c_uint
 
 _SIGS = {
@@ -56,6 +57,9 @@ _SIGS = {
     "hvk_pool_bwd": [P, P, P] + [I] * 13 + [P, I, P],
     "hvk_lrn_fwd": [P, P, L, I, I, F, F, F, P],
     "hvk_lrn_bwd": [P, P, P, L, I, I, F, F, F, P, I, P],
+    # exact-precision GEMMs (csrc/kernels/gemm_f32.hip)
+    "hvk_gemm_f32": [I, I, I, I, I, P, I, P, I, P, I, F, F, I, P],
+    "hvk_gemm_f64": [I, I, I, I, I, P, I, P, I, P, I, D, D, I, P],
     # fp8 (csrc/kernels/gemm_fp8.hip)
     "hvk_fp8_quant": [P, I, L, P, I, P, I, F, I, P],
     "hvk_fp8_amax": [P, I, L, P, I, P],
