@@ -803,15 +803,16 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
 }
 
-// Tile width: 128 unless it wastes more than 1/8 of the columns; then the
-// width among {96 (K-major B only), 64} that wastes least, the wider on a
-// tie (N = 96, 192: 96; N = 48: 64).  Wide N keeps 128 so the A operand is
-// re-read by as few column tiles as possible (weight-gradient GEMMs).
+// Tile width: 128 unless it wastes more than 1/8 of the columns; then 64,
+// or 96 for a single 96-wide column tile (K-major B only: AlexNet conv1,
+// N = 96, +16 % over 128).  N = 192 measured faster as 3 x 64 than as
+// 2 x 96 (conv4 fwd 598 vs 536 TF: the 96 tile holds 150+ VGPRs).  Wide N
+// keeps 128 so the A operand is re-read by as few column tiles as possible.
 inline int pick_bn(int N, bool allow96) {
   auto waste = [&](int b) { return (N + b - 1) / b * b - N; };
   if (waste(128) * 8 <= N) return 128;
   int best = 128;
-  if (allow96 && waste(96) < waste(best)) best = 96;
+  if (allow96 && N <= 96 && waste(96) < waste(best)) best = 96;
   if (waste(64) < waste(best)) best = 64;
   return best;
 }
