@@ -461,6 +461,160 @@ __global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
     *(uint4*)(dx + base + c0) = *(uint4*)o;
   }
 }
+
+// ---------------------------------------------------------------------------
+// LRN -> 3x3 max pooling fused (AlexNet norm1/pool1, norm2/pool2): the LRN
+// output is never written.  Forward: per pool output x 8 channels, the LRN
+// of the 9 window pixels is recomputed from x (24-channel halo loads) and
+// max-pooled; argmax is the offset into the (virtual) LRN output, i.e. the
+// same tensor geometry as x.  Backward: per input pixel x 8 channels, the
+// pool gradient of the 16 channels the LRN window needs is gathered from
+// the <= 2 x 2 covering windows, then the LRN backward of lrn_bwd_vec runs
+// on it - the pool-gradient tensor is never written either.
+__device__ __forceinline__ float lrn_s(const float* v, int c, int half,
+                                      float alpha, float k) {
+  float s = 0.f;
+#pragma unroll
+  for (int d = -4; d <= 4; ++d) {
+    const int idx = c + d;
+    const float t = (idx >= 0 && idx < 24) ? v[idx] : 0.f;
+    s += (d >= -half && d <= half) ? t * t : 0.f;
+  }
+  return k + alpha * s;
+}
+
+template <int half>
+__global__ void lrn_pool3_fwd_kernel(const uint16_t* __restrict__ x,
+                                     uint16_t* __restrict__ y,
+                                     int* __restrict__ argmax, int N, int H,
+                                     int W, int C, int OH, int OW, int sy,
+                                     int sx, float alpha, float beta, float k,
+                                     FastDiv fCV, FastDiv fOW, FastDiv fOH) {
+  const int CV = C >> 3;
+  const int total = N * OH * OW * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
+    const int c0 = (int)cvu * 8;
+    const int h0 = (int)ohu * sy, w0 = (int)owu * sx;
+    const long long img = (long long)nu * H * W * C;
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { best[q] = -INFINITY; bi[q] = -1; }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int h = h0 + i / 3, w = w0 + i % 3;
+      if (h >= H || w >= W) continue;
+      const int off = (h * W + w) * C;
+      float v[24];
+      load24(x + img + off, c0, C, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float s = lrn_s(v, 8 + q, half, alpha, k);
+        const float yv = v[8 + q] * exp2f(-beta * __log2f(s));
+        if (bi[q] < 0 || yv > best[q]) { best[q] = yv; bi[q] = off; }
+      }
+    }
+    uint16_t o[8];
+    int a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[q] = f2bf(best[q]);
+      a[q] = (int)(img + bi[q]) + c0 + q;
+    }
+    const long long yo = (long long)pix * C + c0;
+    *(uint4*)(y + yo) = *(const uint4*)o;
+    *(int4*)(argmax + yo) = make_int4(a[0], a[1], a[2], a[3]);
+    *(int4*)(argmax + yo + 4) = make_int4(a[4], a[5], a[6], a[7]);
+  }
+}
+
+template <int half>
+__global__ void lrn_pool3_bwd_kernel(const uint16_t* __restrict__ x,
+                                     const uint16_t* __restrict__ dp,
+                                     const int* __restrict__ argmax,
+                                     uint16_t* __restrict__ dx, int N, int H,
+                                     int W, int C, int OH, int OW, int sy,
+                                     int sx, float alpha, float beta, float k,
+                                     const uint16_t* aux, int aux_act,
+                                     FastDiv fCV, FastDiv fW, FastDiv fH,
+                                     FastDiv fSy, FastDiv fSx) {
+  const int CV = C >> 3;
+  const int total = N * H * W * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, wu, nu, hu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fW, t, wu);
+    fdivmod(t, fH, nu, hu);
+    const int c0 = (int)cvu * 8;
+    const long long base = (long long)pix * C;
+    // covering windows (3x3, stride >= 2): at most 2 x 2
+    const int oh1 = min(OH - 1, (int)fdiv(hu, fSy));
+    const int ow1 = min(OW - 1, (int)fdiv(wu, fSx));
+    int yo[4];
+    bool ok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oh = oh1 - (i >> 1), ow = ow1 - (i & 1);
+      ok[i] = oh >= 0 && ow >= 0 && (int)hu - oh * sy < 3 &&
+              (int)wu - ow * sx < 3 && (int)hu >= oh * sy &&
+              (int)wu >= ow * sx;
+      yo[i] = (((int)nu * OH + max(oh, 0)) * OW + max(ow, 0)) * C;
+    }
+    // g[j] = pool gradient at channel c0 - 8 + j (j < 24), zero outside C
+    float g[24];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) g[j] = 0.f;
+#pragma unroll
+    for (int part = 0; part < 3; ++part) {
+      const int cb = c0 - 8 + part * 8;
+      if (cb < 0 || cb >= C) continue;
+      const int xo = (int)base + cb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (!ok[i]) continue;
+        const uint4 gv = *(const uint4*)(dp + yo[i] + cb);
+        const int4 a0 = *(const int4*)(argmax + yo[i] + cb);
+        const int4 a1 = *(const int4*)(argmax + yo[i] + cb + 4);
+        const uint16_t* gh = (const uint16_t*)&gv;
+        const int am[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          g[part * 8 + q] += am[q] == xo + q ? bf2f(gh[q]) : 0.f;
+      }
+    }
+    float xv[24];
+    load24(x + base, c0, C, xv);
+    // t_j = g_j x_j s_j^(-beta-1), j in [c0-4, c0+12)
+    float tj[16], sb[8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float s = lrn_s(xv, 4 + j, half, alpha, k);
+      const float ls = __log2f(s);
+      tj[j] = g[4 + j] * xv[4 + j] * exp2f((-beta - 1.f) * ls);
+      if (j >= 4 && j < 12) sb[j - 4] = exp2f(-beta * ls);
+    }
+    float a[8];
+    if (aux) load8(aux + base + c0, a);
+    uint16_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float acc = 0.f;
+#pragma unroll
+      for (int d = -4; d <= 4; ++d)
+        acc += (d >= -half && d <= half) ? tj[4 + q + d] : 0.f;
+      float v = g[8 + q] * sb[q] - 2.f * alpha * beta * xv[8 + q] * acc;
+      if (aux) v *= act_bwd(a[q], aux_act);
+      o[q] = f2bf(v);
+    }
+    *(uint4*)(dx + base + c0) = *(const uint4*)o;
+  }
+}
 }  // namespace
 
 HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
@@ -571,5 +725,52 @@ HVK_API int hvk_lrn_bwd(const void* x, const void* dy, void* dx, long long P,
   hipLaunchKernelGGL(lrn_bwd_kernel, dim3(grid_for(P, 4)), dim3(256), 0, s,
                      (const uint16_t*)x, (const uint16_t*)dy, (uint16_t*)dx, P,
                      C, n, alpha, beta, k, (const uint16_t*)aux, aux_act);
+  return (int)hipGetLastError();
+}
+
+// Fused LRN (across channels) -> 3x3 max pooling (no padding, stride >= 2),
+// C % 8 == 0, n / 2 <= 4.  y / argmax as hvk_pool_fwd applied to lrn(x).
+HVK_API int hvk_lrn_pool_fwd(const void* x, void* y, int* argmax, int N,
+                             int H, int W, int C, int OH, int OW, int sy,
+                             int sx, int n, float alpha, float beta, float k,
+                             hipStream_t s) {
+  if (C % 8 || n / 2 > 4 || sy < 2 || sx < 2 || ((uintptr_t)x & 15) ||
+      ((uintptr_t)y & 15) || ((uintptr_t)argmax & 15) ||
+      (long long)N * H * W * C >= (1ll << 31))
+    return -1;
+  const long long total = (long long)N * OH * OW * (C / 8);
+  const int h = n / 2;
+  auto kf = h == 0 ? lrn_pool3_fwd_kernel<0> : h == 1 ? lrn_pool3_fwd_kernel<1>
+          : h == 2 ? lrn_pool3_fwd_kernel<2> : h == 3 ? lrn_pool3_fwd_kernel<3>
+                   : lrn_pool3_fwd_kernel<4>;
+  hipLaunchKernelGGL(kf, dim3(grid_for(total)), dim3(256), 0, s,
+                     (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C, OH,
+                     OW, sy, sx, alpha, beta, k, make_fastdiv(C / 8),
+                     make_fastdiv(OW), make_fastdiv(OH));
+  return (int)hipGetLastError();
+}
+
+// dx = lrn_bwd(x, pool_bwd(dp, argmax)) [* f'(aux)] in one pass
+HVK_API int hvk_lrn_pool_bwd(const void* x, const void* dp, const int* argmax,
+                             void* dx, int N, int H, int W, int C, int OH,
+                             int OW, int sy, int sx, int n, float alpha,
+                             float beta, float k, const void* aux,
+                             int aux_act, hipStream_t s) {
+  if (C % 8 || n / 2 > 4 || sy < 2 || sx < 2 || ((uintptr_t)x & 15) ||
+      ((uintptr_t)dp & 15) || ((uintptr_t)dx & 15) ||
+      ((uintptr_t)argmax & 15) || ((uintptr_t)aux & 15) ||
+      (long long)N * H * W * C >= (1ll << 31))
+    return -1;
+  const long long total = (long long)N * H * W * (C / 8);
+  const int h = n / 2;
+  auto kb = h == 0 ? lrn_pool3_bwd_kernel<0> : h == 1 ? lrn_pool3_bwd_kernel<1>
+          : h == 2 ? lrn_pool3_bwd_kernel<2> : h == 3 ? lrn_pool3_bwd_kernel<3>
+                   : lrn_pool3_bwd_kernel<4>;
+  hipLaunchKernelGGL(kb, dim3(grid_for(total)), dim3(256), 0, s,
+                     (const uint16_t*)x, (const uint16_t*)dp, argmax,
+                     (uint16_t*)dx, N, H, W, C, OH, OW, sy, sx, alpha, beta, k,
+                     (const uint16_t*)aux, aux_act, make_fastdiv(C / 8),
+                     make_fastdiv(W), make_fastdiv(H), make_fastdiv(sy),
+                     make_fastdiv(sx));
   return (int)hipGetLastError();
 }

@@ -330,3 +330,25 @@ def test_solver_kernel(mode):
     close(s1g, s1c, 1e-5)
     close(lp.float(), wc, 1e-2)
 
+
+
+@pytest.mark.parametrize("shape", [(2, 27, 27, 96), (3, 13, 13, 16),
+                                   (2, 55, 55, 96)])
+def test_lrn_pool_fused(shape):
+    n, alpha, beta, k = 5, 1e-4 / 5, 0.75, 1.0
+    x = rnd(*shape, scale=3.0)
+    xg = x.to(DEV)
+    y, am = ops.lrn_pool_fwd(xg, n, alpha, beta, k, 3, 3, (2, 2))
+    yr, amr = ops.lrn_pool_fwd(x, n, alpha, beta, k, 3, 3, (2, 2))
+    torch.cuda.synchronize()
+    close(y, yr, 1e-2)
+    # argmax may differ only where two window values tie in fp32 vs bf16
+    assert (am.cpu() != amr).float().mean().item() < 1e-3
+    dp = rnd(*y.shape, seed=5)
+    aux = rnd(*shape, seed=6)
+    dx = ops.lrn_pool_bwd(xg, dp.to(DEV), am, n, alpha, beta, k, 3, 3,
+                          (2, 2), aux=aux.to(DEV), aux_act=3)
+    dxr = ops.lrn_pool_bwd(x, dp, am.cpu(), n, alpha, beta, k, 3, 3, (2, 2),
+                           aux=aux, aux_act=3)
+    torch.cuda.synchronize()
+    close(dx, dxr, 2e-2)

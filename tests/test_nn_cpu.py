@@ -115,3 +115,32 @@ def test_package_export_roundtrip(tmp_path):
     assert c["units"][0]["links"] == [1]
     w = c["units"][0]["data"]["weights"]
     assert w.startswith("@") and w.endswith("100x784")
+
+
+def test_lrn_pool_fusion_matches_unfused_cpu():
+    """AlexNet norm/pool pairs run fused; one training step gives the same
+    weights as the unfused graph (CPU reference composition)."""
+    from veles_amd.models.normalization_units import LRNormalizerForward
+    layers = [
+        {"type": "conv_str", "->": {"n_kernels": 16, "kx": 3, "ky": 3,
+                                    "padding": 1},
+         "<-": {"learning_rate": 0.01}},
+        {"type": "norm", "->": {"n": 5, "alpha": 1e-3, "beta": 0.75,
+                                "k": 1.0}},
+        {"type": "max_pooling", "->": {"kx": 3, "ky": 3, "sliding": 2}},
+        {"type": "softmax", "->": {"output_sample_shape": 10},
+         "<-": {"learning_rate": 0.01}}]
+    from veles_amd.prng import random_generator
+    ws = []
+    for fuse in (True, False):
+        torch.manual_seed(0)
+        random_generator.get().seed(1234)
+        wf = build(layers, lengths=(0, 0, 40), mb=20, epochs=None,
+                   fuse_lrn_pool=fuse)
+        wf.decision.fail_iterations = None
+        wf.initialize(device=Device(backend="cpu"))
+        lrn = [f for f in wf.forwards if isinstance(f, LRNormalizerForward)]
+        assert lrn[0].fused == fuse
+        wf.run_steps(2)
+        ws.append(wf.forwards[0].weights_master.clone())
+    assert torch.allclose(ws[0], ws[1], atol=1e-6)

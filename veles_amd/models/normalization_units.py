@@ -1,6 +1,11 @@
 """Local response normalisation across channels (Znicz ``norm``;
 docs/OPS.md §LRN): y_c = x_c * (k + alpha * sum_{|c'-c|<=n/2} x_c'^2)^-beta.
-One wave per NHWC pixel, channels staged in LDS (``hvk_lrn_fwd/bwd``)."""
+Vectorised over 8 channels of an NHWC pixel (``hvk_lrn_fwd/bwd``).
+
+When a 3x3 max pooling follows (AlexNet norm1/pool1, norm2/pool2) the
+StandardWorkflow links them (``fused_into``) and the pooling units run the
+fused kernels (``hvk_lrn_pool_fwd/bwd``): the LRN output and the pool
+gradient are never materialised, and these units' runs become no-ops."""
 from __future__ import annotations
 
 from veles_amd.accelerated_units import AcceleratedUnit
@@ -27,6 +32,7 @@ class LRNormalizerForward(AcceleratedUnit, _LRNParams):
         super().__init__(workflow, **kwargs)
         self._lrn_kwargs(kwargs)
         self.output = Array(shallow_pickle=True)
+        self.fused_into = None  # the max pooling unit that computes us
         self.demand("input")
 
     @property
@@ -45,8 +51,15 @@ class LRNormalizerForward(AcceleratedUnit, _LRNParams):
             tuple(self.input.shape), dtype=x.dtype if x is not None else
             self.compute_dtype, device=self.torch_device)
 
+    @property
+    def fused(self):
+        p = self.fused_into
+        return p is not None and getattr(p, "lrn_fused_active_", False)
+
     def run(self):
         import torch
+        if self.fused:
+            return
         x = self.input.devmem
         y = self.output.devmem
         if y is None or y.shape != x.shape or y.dtype != x.dtype or \
@@ -63,6 +76,9 @@ class LRNormalizerBackward(GradientDescentBase, _LRNParams):
         self._lrn_kwargs(kwargs)
 
     def run(self):
+        fwd = self.forward
+        if fwd is not None and getattr(fwd, "fused", False):
+            return  # err_input written by the fused pooling backward
         x = self.input.devmem
         ei = self.alloc_err_input(tuple(x.shape))
         aux, aux_act = self.aux_tensor()

@@ -39,7 +39,12 @@ class Pooling(AcceleratedUnit):
         self.sliding = (s, s) if isinstance(s, int) else tuple(s)
         self.output = Array(shallow_pickle=True)
         self.input_offset = Array(shallow_pickle=True)
+        self.fused_lrn = None  # LRN unit computed by this pooling (fused)
         self.demand("input")
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.lrn_fused_active_ = False
 
     @property
     def activation(self):
@@ -67,8 +72,19 @@ class Pooling(AcceleratedUnit):
         self.input_offset.devmem = torch.zeros(B, OH, OW, C,
                                                dtype=torch.int32,
                                                device=self.torch_device)
+        lrn = self.fused_lrn
+        self.lrn_fused_active_ = lrn is not None and self.MODE == "max" and \
+            len(tuple(self.input.shape)) == 4 and \
+            ops.lrn_pool_fusable(C, lrn.n, self.ky, self.kx, self.sliding)
 
     def run(self):
+        if self.lrn_fused_active_:
+            lrn = self.fused_lrn
+            ops.lrn_pool_fwd(lrn.input.devmem, lrn.n, lrn.alpha, lrn.beta,
+                             lrn.k, self.ky, self.kx, self.sliding,
+                             out=self.output.devmem,
+                             argmax=self.input_offset.devmem)
+            return
         x = self._in()
         B, H, W, C = x.shape
         OH, OW = ops.pool_out_size(H, W, self.ky, self.kx, self.sliding[1],
@@ -250,10 +266,23 @@ class GDPooling(GradientDescentBase):
         self.ky = int(kwargs.get("ky", 2))
         s = kwargs.get("sliding", (self.kx, self.ky))
         self.sliding = (s, s) if isinstance(s, int) else tuple(s)
+        self.fused_lrn_gd = None  # GD unit of a fused LRN below
         self.demand("input_offset")
 
     def run(self):
         err = self.err_output.devmem
+        fwd = self.forward
+        if fwd is not None and getattr(fwd, "lrn_fused_active_", False):
+            # LRN -> pool fused backward straight into the LRN GD unit's
+            # err_input (its own run is a no-op)
+            lrn, lgd = fwd.fused_lrn, self.fused_lrn_gd
+            x = lrn.input.devmem
+            ei = lgd.alloc_err_input(tuple(x.shape))
+            aux, aux_act = lgd.aux_tensor()
+            ops.lrn_pool_bwd(x, err, self.input_offset.devmem, lrn.n,
+                             lrn.alpha, lrn.beta, lrn.k, self.ky, self.kx,
+                             self.sliding, aux=aux, aux_act=aux_act, out=ei)
+            return
         x = self.input.devmem
         shape = tuple(x.shape) if x.dim() == 4 else tuple(x.shape) + (1,)
         ei = self.alloc_err_input(shape)

@@ -161,6 +161,8 @@ class StandardWorkflow(AcceleratedWorkflow):
         self.loader_name = kwargs.get("loader_name")
         self.loader_config = dict(_cfg(kwargs.get("loader_config")))
         self.loss_function = kwargs.get("loss_function", "softmax")
+        # LRN -> 3x3 max pooling pairs as one fused kernel each way
+        self.fuse_lrn_pool = kwargs.get("fuse_lrn_pool", True)
         self.decision_config = dict(_cfg(kwargs.get("decision_config")))
         self.snapshotter_config = kwargs.get("snapshotter_config")
         if self.snapshotter_config is not None:
@@ -399,6 +401,14 @@ class StandardWorkflow(AcceleratedWorkflow):
                     getattr(gds[i - 1], "own_derivative", False):
                 gds[i].fuse_from(below, act)
                 gds[i - 1].own_derivative = False
+        # LRN -> max pooling pairs run as one fused kernel each way
+        for i in range(n - 1):
+            lrn, pool = self.forwards[i], self.forwards[i + 1]
+            if isinstance(lrn, LRNormalizerForward) and \
+                    type(pool) is MaxPooling and self.fuse_lrn_pool:
+                lrn.fused_into = pool
+                pool.fused_lrn = lrn
+                gds[i + 1].fused_lrn_gd = gds[i]
         self.gds = gds
         return gds[0]
 

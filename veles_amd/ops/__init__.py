@@ -664,6 +664,54 @@ def lrn_bwd(x, dy, n=5, alpha=1e-4, beta=0.75, k=2.0, aux=None, aux_act=0,
     return out
 
 
+# ------------------------------------------------------- fused LRN -> pool
+def lrn_pool_fusable(C, n, ky, kx, sliding):
+    """Shapes the fused LRN -> 3x3 max-pool kernels take."""
+    sx, sy = sliding
+    return C % 8 == 0 and n // 2 <= 4 and ky == 3 and kx == 3 and \
+        sx >= 2 and sy >= 2
+
+
+def lrn_pool_fwd(x, n, alpha, beta, k, ky, kx, sliding, out=None,
+                 argmax=None):
+    """max_pool(lrn(x)) without materialising lrn(x); ``argmax`` indexes the
+    (virtual) LRN output, i.e. x's geometry."""
+    sx, sy = sliding
+    N, H, W, C = x.shape
+    OH, OW = pool_out_size(H, W, ky, kx, sy, sx)
+    if out is None:
+        out = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
+    if argmax is None:
+        argmax = torch.empty(N, OH, OW, C, dtype=torch.int32, device=x.device)
+    if _gpu(x):
+        _lib_call("hvk_lrn_pool_fwd", _p(x), _p(out), _p(argmax), N, H, W, C,
+                  OH, OW, sy, sx, n, float(alpha), float(beta), float(k),
+                  _s(x))
+        return out, argmax
+    y = lrn_fwd(x.float(), n, alpha, beta, k)
+    return pool_fwd(y, ky, kx, sliding, "max", out=out, argmax=argmax)
+
+
+def lrn_pool_bwd(x, dp, argmax, n, alpha, beta, k, ky, kx, sliding,
+                 aux=None, aux_act=0, out=None):
+    """lrn_bwd(x, pool_bwd(dp)) [* f'(aux)] without materialising the pool
+    gradient."""
+    sx, sy = sliding
+    N, H, W, C = x.shape
+    _, OH, OW, _ = dp.shape
+    aux_act = act_code(aux_act)
+    if out is None:
+        out = torch.empty_like(x)
+    if _gpu(x):
+        _lib_call("hvk_lrn_pool_bwd", _p(x), _p(dp), _p(argmax), _p(out), N,
+                  H, W, C, OH, OW, sy, sx, n, float(alpha), float(beta),
+                  float(k), _p(aux), aux_act, _s(x))
+        return out
+    g = pool_bwd(dp.float(), argmax, tuple(x.shape), ky, kx, sliding, "max")
+    return lrn_bwd(x, g, n, alpha, beta, k, aux=aux, aux_act=aux_act,
+                   out=out)
+
+
 # --------------------------------------------------------------- evaluators
 def softmax_ce(logits, labels, *, scale=None, err=None, probs=None,
                max_idx=None, metrics=None, confusion=None):
