@@ -28,6 +28,8 @@ def _kind(arg):
         return _lib.L
     if a.startswith("float"):
         return _lib.F
+    if a.startswith("double"):
+        return _lib.D
     if a.startswith(("unsigned", "uint32_t")):
         return _lib.U
     return _lib.I
