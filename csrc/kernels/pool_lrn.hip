@@ -381,6 +381,29 @@ __device__ __forceinline__ void load24(const uint16_t* row, int c0, int C,
   load8(row + c0, d + 8);
   if (c0 + 8 < C) load8(row + c0 + 8, d + 16);
 }
+__device__ __forceinline__ void load4(const uint16_t* p, float* d) {
+  const uint2 v = *(const uint2*)p;
+  d[0] = __uint_as_float(v.x << 16);
+  d[1] = __uint_as_float(v.x & 0xffff0000u);
+  d[2] = __uint_as_float(v.y << 16);
+  d[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+// d[k] = row[c0 - 8 + k] for the channels an LRN of half-width `half` over
+// channels [c0 - half, c0 + 8 + half) reads (zero outside [0, C)): 16
+// channels (8 B + 16 B + 8 B) when half <= 2, else the full 24.
+template <int half>
+__device__ __forceinline__ void loadx(const uint16_t* row, int c0, int C,
+                                      float* d) {
+  if (half > 2) {
+    load24(row, c0, C, d);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 24; ++q) d[q] = 0.f;
+  if (c0 >= 8) load4(row + c0 - 4, d + 4);
+  load8(row + c0, d + 8);
+  if (c0 + 8 < C) load4(row + c0 + 8, d + 16);
+}
 template <int half>
 __global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
                                    int C, float alpha, float beta,
@@ -511,7 +534,7 @@ __global__ void lrn_pool3_fwd_kernel(const uint16_t* __restrict__ x,
       if (h >= H || w >= W) continue;
       const int off = (h * W + w) * C;
       float v[24];
-      load24(x + img + off, c0, C, v);
+      loadx<half>(x + img + off, c0, C, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float s = lrn_s(v, 8 + q, half, alpha, k);
@@ -589,7 +612,7 @@ __global__ void lrn_pool3_bwd_kernel(const uint16_t* __restrict__ x,
       }
     }
     float xv[24];
-    load24(x + base, c0, C, xv);
+    loadx<half>(x + base, c0, C, xv);
     // t_j = g_j x_j s_j^(-beta-1), j in [c0-4, c0+12)
     float tj[16], sb[8];
 #pragma unroll
@@ -613,6 +636,104 @@ __global__ void lrn_pool3_bwd_kernel(const uint16_t* __restrict__ x,
       o[q] = f2bf(v);
     }
     *(uint4*)(dx + base + c0) = *(const uint4*)o;
+  }
+}
+
+// Stride-2 specialisation of lrn_pool3_bwd_kernel: one thread per 2 x 2 input
+// pixel block x 8 channels.  With 3x3 / stride 2 windows the four windows
+// (i-1..i) x (j-1..j) cover the whole block (i, j), so each (window, 4-channel
+// chunk) of pool gradient + argmax is loaded once per block instead of once
+// per covering pixel and 8-channel part (~6x fewer vector-memory bytes; the
+// old kernel was texture-address bound, not HBM bound).  When aux is x itself
+// (ReLU below, derivative from the output) the activation derivative reuses
+// the x registers.
+template <int half>
+__global__ __launch_bounds__(256) void lrn_pool3s2_bwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
+    const int* __restrict__ argmax, uint16_t* __restrict__ dx, int N, int H,
+    int W, int C, int OH, int OW, float alpha, float beta, float k,
+    const uint16_t* aux, int aux_act, FastDiv fCV, FastDiv fBW,
+    FastDiv fBH) {
+  const int CV = C >> 3;
+  const int BH = (H + 1) >> 1, BW = (W + 1) >> 1;
+  const int total = N * BH * BW * CV;
+  const bool aux_x = aux == x;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t blk, cvu, t, bwu, nu, bhu;
+    fdivmod((uint32_t)e, fCV, blk, cvu);
+    fdivmod(blk, fBW, t, bwu);
+    fdivmod(t, fBH, nu, bhu);
+    const int c0 = (int)cvu * 8;
+    int po[4];
+    bool pv[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int hp = (int)bhu * 2 + (p >> 1), wp = (int)bwu * 2 + (p & 1);
+      pv[p] = hp < H && wp < W;
+      // argmax values are >= 0: an invalid pixel never matches
+      po[p] = pv[p] ? (((int)nu * H + hp) * W + wp) * C : -1;
+    }
+    // g[p][j]: pool gradient of pixel p at channel c0 - 4 + j
+    float g[4][16];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) g[p][j] = 0.f;
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const int oh = (int)bhu - 1 + (wi >> 1), ow = (int)bwu - 1 + (wi & 1);
+      if (oh < 0 || ow < 0 || oh >= OH || ow >= OW) continue;
+      const int yo = (((int)nu * OH + oh) * OW + ow) * C;
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) {
+        const int cb = c0 - 4 + ch * 4;
+        if (cb < 0 || cb >= C) continue;
+        float gf[4];
+        load4(dp + yo + cb, gf);
+        const int4 a4 = *(const int4*)(argmax + yo + cb);
+        const int am[4] = {a4.x - cb, a4.y - cb - 1, a4.z - cb - 2,
+                           a4.w - cb - 3};
+        // window (i-1+a, j-1+b) reaches pixel (ph, pw) of the block only if
+        // (a || !ph) && (b || !pw): 9 of the 16 (window, pixel) pairs
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          if (!((wi >> 1) || !(p >> 1)) || !((wi & 1) || !(p & 1))) continue;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            g[p][ch * 4 + q] += am[q] == po[p] ? gf[q] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (!pv[p]) continue;
+      float xv[24];
+      loadx<half>(x + po[p], c0, C, xv);
+      float tj[16], sb[8];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float s = lrn_s(xv, 4 + j, half, alpha, k);
+        const float ls = __log2f(s);
+        const float e1 = exp2f((-beta - 1.f) * ls);  // s^(-beta-1)
+        tj[j] = g[p][j] * xv[4 + j] * e1;
+        if (j >= 4 && j < 12) sb[j - 4] = e1 * s;  // s^-beta
+      }
+      float a[8];
+      if (aux && !aux_x) load8(aux + po[p] + c0, a);
+      uint16_t o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float acc = 0.f;
+#pragma unroll
+        for (int d = -4; d <= 4; ++d)
+          acc += (d >= -half && d <= half) ? tj[4 + q + d] : 0.f;
+        float v = g[p][4 + q] * sb[q] - 2.f * alpha * beta * xv[8 + q] * acc;
+        if (aux) v *= act_bwd(aux_x ? xv[8 + q] : a[q], aux_act);
+        o[q] = f2bf(v);
+      }
+      *(uint4*)(dx + po[p] + c0) = *(const uint4*)o;
+    }
   }
 }
 }  // namespace
@@ -761,8 +882,22 @@ HVK_API int hvk_lrn_pool_bwd(const void* x, const void* dp, const int* argmax,
       ((uintptr_t)argmax & 15) || ((uintptr_t)aux & 15) ||
       (long long)N * H * W * C >= (1ll << 31))
     return -1;
-  const long long total = (long long)N * H * W * (C / 8);
   const int h = n / 2;
+  if (sy == 2 && sx == 2) {
+    const int BH = (H + 1) / 2, BW = (W + 1) / 2;
+    const long long tb = (long long)N * BH * BW * (C / 8);
+    auto k2 = h == 0 ? lrn_pool3s2_bwd_kernel<0>
+            : h == 1 ? lrn_pool3s2_bwd_kernel<1>
+            : h == 2 ? lrn_pool3s2_bwd_kernel<2>
+            : h == 3 ? lrn_pool3s2_bwd_kernel<3> : lrn_pool3s2_bwd_kernel<4>;
+    hipLaunchKernelGGL(k2, dim3(grid_for(tb)), dim3(256), 0, s,
+                       (const uint16_t*)x, (const uint16_t*)dp, argmax,
+                       (uint16_t*)dx, N, H, W, C, OH, OW, alpha, beta, k,
+                       (const uint16_t*)aux, aux_act, make_fastdiv(C / 8),
+                       make_fastdiv(BW), make_fastdiv(BH));
+    return (int)hipGetLastError();
+  }
+  const long long total = (long long)N * H * W * (C / 8);
   auto kb = h == 0 ? lrn_pool3_bwd_kernel<0> : h == 1 ? lrn_pool3_bwd_kernel<1>
           : h == 2 ? lrn_pool3_bwd_kernel<2> : h == 3 ? lrn_pool3_bwd_kernel<3>
                    : lrn_pool3_bwd_kernel<4>;

@@ -332,23 +332,39 @@ def test_solver_kernel(mode):
 
 
 
-@pytest.mark.parametrize("shape", [(2, 27, 27, 96), (3, 13, 13, 16),
-                                   (2, 55, 55, 96)])
-def test_lrn_pool_fused(shape):
-    n, alpha, beta, k = 5, 1e-4 / 5, 0.75, 1.0
+@pytest.mark.parametrize("shape,stride,n,aux_mode", [
+    ((2, 27, 27, 96), 2, 5, "sep"), ((3, 13, 13, 16), 2, 5, "sep"),
+    ((2, 55, 55, 96), 2, 5, "sep"), ((2, 55, 55, 96), 2, 5, "x"),
+    ((2, 14, 12, 8), 2, 3, "none"), ((1, 16, 17, 24), 2, 9, "x"),
+    ((2, 20, 19, 32), 3, 5, "sep"), ((1, 15, 15, 40), 3, 7, "x")])
+def test_lrn_pool_fused(shape, stride, n, aux_mode):
+    """Fused LRN -> 3x3 max pool forward / backward against the fp32
+    reference; stride 2 runs the 2x2-block backward kernel, stride 3 the
+    per-pixel one; aux_mode "x" hits the aux-is-input (ReLU) shortcut."""
+    alpha, beta, k = 1e-4 / n, 0.75, 1.0
+    st = (stride, stride)
     x = rnd(*shape, scale=3.0)
+    if aux_mode == "x":
+        x = x.clamp_min(0.0)
     xg = x.to(DEV)
-    y, am = ops.lrn_pool_fwd(xg, n, alpha, beta, k, 3, 3, (2, 2))
-    yr, amr = ops.lrn_pool_fwd(x, n, alpha, beta, k, 3, 3, (2, 2))
+    y, am = ops.lrn_pool_fwd(xg, n, alpha, beta, k, 3, 3, st)
+    yr, amr = ops.lrn_pool_fwd(x, n, alpha, beta, k, 3, 3, st)
     torch.cuda.synchronize()
     close(y, yr, 1e-2)
     # argmax may differ only where two window values tie in fp32 vs bf16
     assert (am.cpu() != amr).float().mean().item() < 1e-3
     dp = rnd(*y.shape, seed=5)
-    aux = rnd(*shape, seed=6)
+    if aux_mode == "sep":
+        aux, auxg = rnd(*shape, seed=6), None
+        auxg = aux.to(DEV)
+    elif aux_mode == "x":
+        aux, auxg = x, xg
+    else:
+        aux = auxg = None
+    act = 3 if aux is not None else 0
     dx = ops.lrn_pool_bwd(xg, dp.to(DEV), am, n, alpha, beta, k, 3, 3,
-                          (2, 2), aux=aux.to(DEV), aux_act=3)
-    dxr = ops.lrn_pool_bwd(x, dp, am.cpu(), n, alpha, beta, k, 3, 3, (2, 2),
-                           aux=aux, aux_act=3)
+                          st, aux=auxg, aux_act=act)
+    dxr = ops.lrn_pool_bwd(x, dp, am.cpu(), n, alpha, beta, k, 3, 3, st,
+                           aux=aux, aux_act=act)
     torch.cuda.synchronize()
     close(dx, dxr, 2e-2)
