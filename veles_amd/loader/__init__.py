@@ -17,3 +17,7 @@ from veles_amd.loader.interactive import (  # noqa: F401
     InteractiveLoader, RestfulLoader)
 from veles_amd.loader.saver import (  # noqa: F401
     MinibatchesSaver, MinibatchesLoader)
+from veles_amd.loader.audio import (  # noqa: F401
+    FullBatchAudioLoader, TextLinesLoader, decode_audio)
+from veles_amd.loader.queue_loader import (  # noqa: F401
+    QueueLoader, QueueLoaderClient)
