@@ -67,13 +67,19 @@ class PoolEngine : public Engine {
     std::lock_guard<std::mutex> lk(mu_);
     futs_.push_back(pool_.Enqueue(std::move(fn)));
   }
+  // Tasks may schedule children (a unit fires its successors): drain until
+  // no task scheduled while waiting is left, or Wait() could return while a
+  // child is still queued.
   void Wait() override {
-    std::vector<std::future<void>> f;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      f.swap(futs_);
+    while (true) {
+      std::vector<std::future<void>> f;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        f.swap(futs_);
+      }
+      if (f.empty()) return;
+      for (auto& x : f) x.get();
     }
-    for (auto& x : f) x.get();
   }
 
  private:

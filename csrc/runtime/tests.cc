@@ -1,6 +1,7 @@
 // tests.cc - self-test binary of the native runtime (the reference's
 // libVeles/tests/ gtest suite: memory_optimizer, workflow_loader, units).
 //   veles_rt_tests [package.zip input.npy expected.npy [--gpu]]
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -104,6 +105,31 @@ static int TestPackage(const char* pkg, const char* in, const char* exp,
   return 0;
 }
 
+// Engine contract under concurrency (run under -fsanitize=thread by
+// tests/test_native_runtime.py): tasks that schedule children, Wait()
+// returning only after every descendant ran.
+static void TestEngines() {
+  for (int rep = 0; rep < 20; ++rep) {
+    auto eng = MakeThreadPoolEngine(4);
+    std::atomic<int> ran{0};
+    std::function<void(int)> fan;
+    Engine* e = eng.get();
+    fan = [&](int depth) {
+      ran.fetch_add(1);
+      if (depth < 4)
+        for (int c = 0; c < 3; ++c) e->Schedule([&fan, depth] { fan(depth + 1); });
+    };
+    e->Schedule([&fan] { fan(0); });
+    e->Wait();
+    EXPECT(ran.load() == 1 + 3 + 9 + 27 + 81);
+  }
+  auto ser = MakeSerialEngine();
+  int n = 0;
+  ser->Schedule([&n] { ++n; });
+  ser->Wait();
+  EXPECT(n == 1);
+}
+
 int main(int argc, char** argv) {
   (void)veles_rt_units_anchor;
   try {
@@ -111,6 +137,7 @@ int main(int argc, char** argv) {
     TestJson();
     TestNpy();
     TestFactory();
+    TestEngines();
     if (argc >= 4)
       TestPackage(argv[1], argv[2], argv[3],
                   argc > 4 && std::strcmp(argv[4], "--gpu") == 0);

@@ -77,6 +77,18 @@ def test_cpp_selftests():
     assert r.returncode == 0, r.stderr + r.stdout
 
 
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_cpp_selftests_under_host_sanitizers(kind):
+    """ASan+UBSan and TSan builds of the C++ self-tests (memory optimizer,
+    JSON / npy parsers, unit factory, thread-pool engine) must run clean."""
+    exe, env = rt.build_sanitized_tests(kind)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-4000:] + r.stdout
+    assert "OK 0" in r.stdout
+    assert "runtime error" not in r.stderr  # UBSan reports
+
+
 @pytest.mark.parametrize("fmt", ["zip", "tgz"])
 def test_native_forward_matches_python(tmp_path, fmt):
     wf = _trained_workflow()

@@ -33,7 +33,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-parameter",
          "-Wno-unused-result"]
 
-__all__ = ["build_runtime", "NativeWorkflow", "optimize_memory"]
+__all__ = ["build_runtime", "build_sanitized_tests", "NativeWorkflow",
+           "optimize_memory"]
 
 
 def _sources():
@@ -87,6 +88,39 @@ def build_runtime(force=False, verbose=False):
     if verbose:
         print("built", LIB)
     return LIB
+
+
+SANITIZERS = {"asan": "address,undefined", "tsan": "thread"}
+
+
+def build_sanitized_tests(kind="asan"):
+    """Host-sanitizer build of the C++ self-test binary:
+    ``asan`` = AddressSanitizer + UBSan, ``tsan`` = ThreadSanitizer over the
+    engine / thread-pool paths.  Host code only (``-fno-gpu-sanitize``):
+    GPU ASan / xnack runs are not available on the MI355X pool.  Returns
+    the binary path and the environment to run it with."""
+    from veles_amd.ops import build as kbuild
+    if not os.path.exists(kbuild.LIB):
+        kbuild.build()
+    out = os.path.join(HERE, "veles_rt_tests_" + kind)
+    srcs = sorted(s for s in glob.glob(os.path.join(SRC, "*.cc"))
+                  if os.path.basename(s) != "veles_infer.cc")
+    stamp = _digest(srcs + glob.glob(os.path.join(SRC, "*.h"))) + kind
+    if not (os.path.exists(out) and os.path.exists(out + ".stamp") and
+            open(out + ".stamp").read() == stamp):
+        opsdir = os.path.dirname(kbuild.LIB)
+        _run([HIPCC, "-O1", "-g", "-std=c++17", "-fno-omit-frame-pointer",
+              "-fsanitize=" + SANITIZERS[kind], "-fno-gpu-sanitize",
+              "-o", out] + srcs +
+             ["-L" + opsdir, "-lhvk", "-Wl,-rpath," + opsdir, "-lz"])
+        with open(out + ".stamp", "w") as f:
+            f.write(stamp)
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "verify_asan_link_order=0:detect_leaks=1:" \
+        "abort_on_error=0"
+    env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
+    env["TSAN_OPTIONS"] = "halt_on_error=1"
+    return out, env
 
 
 _lib = None
