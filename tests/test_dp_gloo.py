@@ -78,3 +78,63 @@ def test_dp_matches_single_process(tmp_path, layers_name):
     for k in w0.files:
         numpy.testing.assert_array_equal(w0[k], w1[k])
         numpy.testing.assert_allclose(w0[k], ws[k], rtol=1e-4, atol=1e-5)
+
+
+def _train_local(steps, monkeypatch, acc):
+    import torch
+    if acc > 1:
+        monkeypatch.setenv("VELES_AMD_DP_ACCUMULATE", str(acc))
+    else:
+        monkeypatch.delenv("VELES_AMD_DP_ACCUMULATE", raising=False)
+    torch.set_num_threads(1)
+    from veles_amd.prng import random_generator
+    for i in range(4):
+        random_generator.get(i).seed(1234 + i)
+    numpy.random.seed(1234)
+    torch.manual_seed(1234)
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow, zoo
+    import veles_amd.loader  # noqa: F401
+    wf = StandardWorkflow(
+        DummyLauncher(), loader_name="synthetic_images",
+        loader_config={"dataset": "mnist", "class_lengths": (0, 0, 400),
+                       "minibatch_size": 40,
+                       "normalization_type": "mean_disp"},
+        layers=zoo.mnist_fc(),
+        decision_config={"max_epochs": None, "fail_iterations": None})
+    wf.initialize(device=Device(backend="cpu"))
+    assert wf.loader.max_minibatch_size == 40 // acc
+    wf.run_steps(steps * acc)
+    return [f.weights_master.numpy().copy() for f in wf.forwards
+            if getattr(f, "_pw_", None) is not None]
+
+
+def test_gradient_accumulation_keeps_global_batch(monkeypatch):
+    """acc micro-steps of B/acc samples == one step of B samples: the
+    elastic-shrink path (parallel/launch.py ``shrink``) keeps the global
+    batch this way."""
+    ref = _train_local(3, monkeypatch, 1)
+    got = _train_local(3, monkeypatch, 2)
+    for a, b in zip(ref, got):
+        numpy.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_spawn_ranks_shrinks_after_failure(tmp_path):
+    """A rank that fails once is dropped on respawn; survivors accumulate
+    world0 / world1 micro-steps."""
+    import sys
+    from veles_amd.parallel.launch import spawn_ranks
+    script = tmp_path / "r.py"
+    script.write_text(
+        "import os, sys\n"
+        "w = int(os.environ['WORLD_SIZE']); r = int(os.environ['RANK'])\n"
+        "if w == 3 and r == 1: sys.exit(7)\n"
+        "open(os.path.join(%r, 'r%%d_w%%d' %% (r, w)), 'w').write(\n"
+        "    os.environ.get('VELES_AMD_DP_ACCUMULATE', '1') + ' ' +\n"
+        "    os.environ['VELES_AMD_DEVICE'])\n" % str(tmp_path))
+    rc = spawn_ranks("0-2", [sys.executable, str(script)], respawn=1,
+                     snapshot_dir=str(tmp_path), poll=0.05, shrink=True)
+    assert rc == 0
+    assert (tmp_path / "r0_w2").read_text() == "2 0"
+    assert (tmp_path / "r1_w2").read_text() == "2 2"

@@ -137,7 +137,8 @@ class Main(object):
             i = argv.index("--gpus")
             del argv[i:i + 2]
             return spawn_ranks(args.gpus, [sys.executable, "-m", "veles_amd"]
-                               + argv, respawn=args.respawn)
+                               + argv, respawn=args.respawn,
+                               shrink=args.respawn_shrink)
         self._setup_logging(args)
         if not args.workflow:
             make_parser().print_help()

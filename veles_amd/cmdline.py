@@ -71,6 +71,9 @@ def make_parser():
     p.add_argument("--respawn", type=int, default=0,
                    help="restart failed rank groups N times from the "
                         "latest snapshot")
+    p.add_argument("--respawn-shrink", action="store_true",
+                   help="on respawn, drop the failed ranks' GPUs and keep "
+                        "the global batch by gradient accumulation")
     p.add_argument("--trace-events", default="",
                    help="write a Chrome-trace JSON of unit events here")
     p.add_argument("--train-ratio", type=float, default=1.0)

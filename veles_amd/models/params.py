@@ -16,6 +16,8 @@ Master weights are float32; the compute copy is the device compute dtype
 """
 from __future__ import annotations
 
+import os
+
 import numpy
 
 __all__ = ["ParameterStore", "Param"]
@@ -67,7 +69,12 @@ class ParameterStore(object):
         self._solver_segs = None
         self._seg_key = None
         self.steps = 0
-        self.accumulate = 1
+        # micro-steps per optimizer step: > 1 after an elastic shrink keeps
+        # the global batch (parallel/launch.py ``shrink``)
+        from veles_amd.utils.config import root, get
+        self.accumulate = max(1, int(get(
+            root.common.engine.dp.accumulate,
+            os.environ.get("VELES_AMD_DP_ACCUMULATE", 1))))
         self._accum_count = 0
         # callables run after every applied update (e.g. ZeroFiller masks)
         self.post_update_hooks = []

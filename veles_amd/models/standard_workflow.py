@@ -19,6 +19,7 @@ is fused into gds[i]'s err_input kernel (see models/nn_units.py).
 """
 from __future__ import annotations
 
+import os
 import re
 
 from veles_amd.accelerated_units import AcceleratedWorkflow
@@ -441,6 +442,17 @@ class StandardWorkflow(AcceleratedWorkflow):
         if dp is not None:
             self.loader.rank = dp.rank
             self.loader.world_size = dp.world_size
+        # gradient accumulation (elastic shrink, parallel/launch.py): each
+        # micro-step serves 1/acc of the configured global minibatch, the
+        # optimizer steps once per acc micro-steps
+        from veles_amd.utils.config import root, get
+        acc = max(1, int(get(root.common.engine.dp.accumulate,
+                             os.environ.get("VELES_AMD_DP_ACCUMULATE", 1))))
+        ld = self.loader
+        full = getattr(ld, "full_minibatch_size", None) or \
+            ld.max_minibatch_size
+        ld.full_minibatch_size = full
+        ld.max_minibatch_size = -(-full // acc)
         return super().initialize(**kwargs)
 
     def run_steps(self, n):

@@ -74,21 +74,33 @@ def _kill_all(procs):
                 pass
 
 
-def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5):
+def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5,
+                shrink=False):
     """Run ``cmd`` once per device in ``spec`` ("0-7", "0,1", "4").
-    Returns the group's exit code (0 when every rank succeeded)."""
+    Returns the group's exit code (0 when every rank succeeded).
+
+    ``shrink``: on a respawn, leave out the device(s) whose rank failed and
+    keep the global batch by gradient accumulation - each survivor's
+    optimizer step accumulates ``VELES_AMD_DP_ACCUMULATE`` = original world
+    size / surviving world size micro-steps (rounded up when it does not
+    divide; a warning says so)."""
     devices = parse_device_spec(spec) if isinstance(spec, str) else list(spec)
+    world0 = len(devices)
     attempt = 0
     cmd = list(cmd)
+    env_extra = {}
     while True:
-        procs = _launch(devices, cmd, free_port())
+        procs = _launch(devices, cmd, free_port(), env_extra)
         failed = None
+        failed_ranks = []
         try:
             while True:
                 codes = [p.poll() for p in procs]
                 bad = [c for c in codes if c not in (None, 0)]
                 if bad:
                     failed = bad[0]
+                    failed_ranks = [i for i, c in enumerate(codes)
+                                    if c not in (None, 0)]
                     break
                 if all(c == 0 for c in codes):
                     return 0
@@ -109,5 +121,16 @@ def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5):
                 i = cmd.index("-w")
                 del cmd[i:i + 2]
             cmd = cmd[:3] + ["-w", snap] + cmd[3:]
-        print("[launch] rank failed with %s; respawn %d/%d from %s" %
-              (failed, attempt, respawn, snap), file=sys.stderr)
+        if shrink and 0 < len(failed_ranks) < len(devices):
+            devices = [d for i, d in enumerate(devices)
+                       if i not in failed_ranks]
+            acc = -(-world0 // len(devices))
+            if acc * len(devices) != world0:
+                print("[launch] %d ranks left of %d: global batch becomes "
+                      "%d/%d of the original" % (len(devices), world0,
+                                                  acc * len(devices), world0),
+                      file=sys.stderr)
+            env_extra = {"VELES_AMD_DP_ACCUMULATE": str(acc)}
+        print("[launch] rank(s) %s failed with %s; respawn %d/%d on %s "
+              "from %s" % (failed_ranks, failed, attempt, respawn, devices,
+                           snap), file=sys.stderr)

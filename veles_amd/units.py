@@ -28,6 +28,7 @@ compute stream (stream order = data-dependency order, no host sync needed).
 from __future__ import annotations
 
 import collections
+import os
 import threading
 import time
 import uuid
@@ -107,6 +108,28 @@ class _Scheduler(object):
         while pending:
             dst, src = pending.popleft()
             dst._check_gate_and_run(src)
+
+
+_ROCTX = [None, False]
+
+
+def _roctx():
+    """torch.cuda.nvtx (roctx on ROCm builds) when unit ranges are enabled
+    by ``root.common.trace.roctx`` or ``VELES_AMD_ROCTX=1``: each unit run
+    becomes a named range in ``rocprofv3 --marker-trace`` / the torch
+    profiler, next to the kernel trace."""
+    if not _ROCTX[1]:
+        _ROCTX[1] = True
+        on = root.common.trace.roctx is True or \
+            os.environ.get("VELES_AMD_ROCTX") == "1"
+        if on:
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    _ROCTX[0] = torch.cuda.nvtx
+            except ImportError:
+                pass
+    return _ROCTX[0]
 
 
 class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
@@ -502,7 +525,15 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
         t0 = time.perf_counter()
         if events.enabled:
             events.record(self.name, "begin")
-        type(self).run(self)
+        rng = _roctx()
+        if rng is not None:
+            rng.range_push(self.name)
+            try:
+                type(self).run(self)
+            finally:
+                rng.range_pop()
+        else:
+            type(self).run(self)
         dt = time.perf_counter() - t0
         if events.enabled:
             events.record(self.name, "end")
