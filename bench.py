@@ -56,7 +56,10 @@ def main():
         print("bench.py: --gpus %d but WORLD_SIZE=%d; launch with "
               "torch.distributed.run" % (args.gpus, world), file=sys.stderr)
     backend = "cpu" if args.cpu or not torch.cuda.is_available() else "hip"
-    dp = DataParallel(backend="gloo" if backend == "cpu" else "nccl")
+    # VELES_AMD_DP_BACKEND=gloo rehearses the multi-rank path with several
+    # ranks on one GPU (RCCL refuses two ranks on one device)
+    dp = DataParallel(backend=os.environ.get("VELES_AMD_DP_BACKEND") or
+                      ("gloo" if backend == "cpu" else "nccl"))
     if backend == "hip":
         torch.cuda.set_device(dp.local_rank % torch.cuda.device_count())
     device = Device(backend=backend)
