@@ -808,9 +808,22 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 // N = 96, +16 % over 128).  N = 192 measured faster as 3 x 64 than as
 // 2 x 96 (conv4 fwd 598 vs 536 TF: the 96 tile holds 150+ VGPRs).  Wide N
 // keeps 128 so the A operand is re-read by as few column tiles as possible.
+// The 128 tile is kept while it wastes at most N / div columns: div = 8 for
+// K-major B, 2 for MN-major B - a 64-wide MN-major B tile still DMAs the
+// 128-wide image (the upper half from the zero page), so it saves no fill
+// bandwidth and only adds tiles (AlexNet conv1 wgrad, N = 432: 126 -> 203 TF
+// at 128, step +1.5 %; profiles/gemm_experiments_r1.md §4).
+// HVK_BN_WASTE_DIV overrides both (A/B knob).
+inline int bn_waste_div(bool kmajor) {
+  static int d = [] {
+    const char* e = getenv("HVK_BN_WASTE_DIV");
+    return e ? atoi(e) : 0;
+  }();
+  return d > 0 ? d : (kmajor ? 8 : 2);
+}
 inline int pick_bn(int N, bool allow96) {
   auto waste = [&](int b) { return (N + b - 1) / b * b - N; };
-  if (waste(128) * 8 <= N) return 128;
+  if (waste(128) * bn_waste_div(allow96) <= N) return 128;
   int best = 128;
   if (allow96 && N <= 96 && waste(96) < waste(best)) best = 96;
   if (waste(64) < waste(best)) best = 64;
