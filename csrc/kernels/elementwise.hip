@@ -642,53 +642,71 @@ __global__ void solver_kernel(float* w, float* grad, float* s1, float* s2,
 // uint8 -> bf16 rows of any length (e.g. 227*227*3): 8 elements per lane,
 // unaligned 8-B loads / 16-B stores (gfx950 unaligned access), per-feature
 // mean / rdisp as float4 pairs; the row tail is scalar.
+template <int SPT>
 __global__ void fill_rows_u8_bf16_kernel(const uint8_t* __restrict__ src,
                                          const int* shuffled, int start,
-                                         int count, long long sample_size,
+                                         int count, int max_mb,
+                                         long long sample_size,
                                          const float* __restrict__ mean,
                                          const float* __restrict__ rdisp,
                                          uint16_t* __restrict__ dst,
                                          const int* labels, int* labels_out,
                                          int* idx_out) {
-  const int i = blockIdx.y;
-  const int sidx = i < count ? shuffled[start + i] : -1;
-  const uint8_t* in = src + (long long)(sidx < 0 ? 0 : sidx) * sample_size;
-  uint16_t* out = dst + (long long)i * sample_size;
+  // SPT samples per thread: the per-feature mean / rdisp (2 x 32 B per 8
+  // features) are loaded once and reused across the samples
+  const int i0 = blockIdx.y * SPT;
+  int sidx[SPT];
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int i = i0 + q;
+    sidx[q] = i < count ? shuffled[start + i] : -1;
+  }
   const long long nv = sample_size / 8;
   for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
        v < nv; v += (long long)gridDim.x * blockDim.x) {
     const long long j = v * 8;
-    uint16_t o[8];
-    if (sidx >= 0) {
-      uint8_t b[8];
-      __builtin_memcpy(b, in + j, 8);
-      float4 m0 = make_float4(0.f, 0.f, 0.f, 0.f), m1 = m0;
-      float4 r0 = make_float4(1.f, 1.f, 1.f, 1.f), r1 = r0;
-      if (mean) { m0 = ((const float4*)(mean + j))[0]; m1 = ((const float4*)(mean + j))[1]; }
-      if (rdisp) { r0 = ((const float4*)(rdisp + j))[0]; r1 = ((const float4*)(rdisp + j))[1]; }
-      const float mm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-      const float rr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    float4 m0 = make_float4(0.f, 0.f, 0.f, 0.f), m1 = m0;
+    float4 r0 = make_float4(1.f, 1.f, 1.f, 1.f), r1 = r0;
+    if (mean) { m0 = ((const float4*)(mean + j))[0]; m1 = ((const float4*)(mean + j))[1]; }
+    if (rdisp) { r0 = ((const float4*)(rdisp + j))[0]; r1 = ((const float4*)(rdisp + j))[1]; }
+    const float mm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+    const float rr[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    uint8_t b[SPT][8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = f2bf(((float)b[q] - mm[q]) * rr[q]);
-    } else {
+    for (int q = 0; q < SPT; ++q)
+      if (sidx[q] >= 0)
+        __builtin_memcpy(b[q], src + (long long)sidx[q] * sample_size + j, 8);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] = 0;
+    for (int q = 0; q < SPT; ++q) {
+      const int i = i0 + q;
+      if (i >= max_mb) break;
+      uint16_t o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = sidx[q] >= 0 ? f2bf(((float)b[q][e] - mm[e]) * rr[e]) : 0;
+      __builtin_memcpy(dst + (long long)i * sample_size + j, o, 16);
     }
-    __builtin_memcpy(out + j, o, 16);
   }
   if (blockIdx.x == 0) {
-    for (long long j = nv * 8 + threadIdx.x; j < sample_size; j += blockDim.x) {
-      float x = 0.f;
-      if (sidx >= 0) {
-        x = (float)in[j];
-        if (mean) x -= mean[j];
-        if (rdisp) x *= rdisp[j];
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+      const int i = i0 + q;
+      if (i >= max_mb) break;
+      const uint8_t* in = src + (long long)(sidx[q] < 0 ? 0 : sidx[q]) * sample_size;
+      uint16_t* out = dst + (long long)i * sample_size;
+      for (long long j = nv * 8 + threadIdx.x; j < sample_size; j += blockDim.x) {
+        float x = 0.f;
+        if (sidx[q] >= 0) {
+          x = (float)in[j];
+          if (mean) x -= mean[j];
+          if (rdisp) x *= rdisp[j];
+        }
+        out[j] = f2bf(x);
       }
-      out[j] = f2bf(x);
-    }
-    if (threadIdx.x == 0) {
-      if (labels_out) labels_out[i] = (sidx >= 0 && labels) ? labels[sidx] : -1;
-      if (idx_out) idx_out[i] = sidx;
+      if (threadIdx.x == 0) {
+        if (labels_out) labels_out[i] = (sidx[q] >= 0 && labels) ? labels[sidx[q]] : -1;
+        if (idx_out) idx_out[i] = sidx[q];
+      }
     }
   }
 }
@@ -758,9 +776,11 @@ HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
     long long gx = (sample_size / 8 + 255) / 256;
     if (gx > 1024) gx = 1024;
     if (gx < 1) gx = 1;
-    hipLaunchKernelGGL(fill_rows_u8_bf16_kernel, dim3((int)gx, max_mb),
-                       dim3(256), 0, s, (const uint8_t*)src, shuffled, start,
-                       count, sample_size, mean, rdisp, (uint16_t*)dst, labels,
+    constexpr int SPT = 4;
+    hipLaunchKernelGGL(fill_rows_u8_bf16_kernel<SPT>,
+                       dim3((int)gx, (max_mb + SPT - 1) / SPT), dim3(256), 0,
+                       s, (const uint8_t*)src, shuffled, start, count, max_mb,
+                       sample_size, mean, rdisp, (uint16_t*)dst, labels,
                        labels_out, idx_out);
   } else if (max_mb <= 65535) {
     long long gx = (sample_size + 1023) / 1024;

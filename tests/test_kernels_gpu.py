@@ -298,16 +298,28 @@ def test_col_sum_vectorised(C):
     close(ops.col_sum(x.to(DEV)), ops.col_sum(x), 1e-4)
 
 
-def test_fill_minibatch_odd_sample():
+@pytest.mark.parametrize("max_mb,count", [(8, 6), (7, 7), (5, 3), (1, 1)])
+def test_fill_minibatch_odd_sample(max_mb, count):
+    """Odd sample size (unaligned rows): the multi-sample row kernel, with a
+    minibatch that is not a multiple of its samples per thread and padded
+    rows (labels -1, indices -1, data 0)."""
     src = torch.randint(0, 256, (20, 227 * 3), dtype=torch.uint8)
+    lab = torch.randint(0, 10, (20,), dtype=torch.int32)
     sh = torch.randperm(20).to(torch.int32)
     mean, rd = torch.rand(681) * 100, torch.rand(681) * 0.01
-    d = torch.empty(8, 681, dtype=BF)
-    ops.fill_minibatch(src, sh, 2, 6, d, mean=mean, rdisp=rd)
-    dg = torch.empty(8, 681, dtype=BF, device=DEV)
-    ops.fill_minibatch(src.to(DEV), sh.to(DEV), 2, 6, dg, mean=mean.to(DEV),
-                       rdisp=rd.to(DEV))
+    d = torch.empty(max_mb, 681, dtype=BF)
+    lo = torch.empty(max_mb, dtype=torch.int32)
+    io = torch.empty(max_mb, dtype=torch.int32)
+    ops.fill_minibatch(src, sh, 2, count, d, mean=mean, rdisp=rd, labels=lab,
+                       labels_out=lo, idx_out=io)
+    dg = torch.full((max_mb, 681), 7.0, dtype=BF, device=DEV)
+    log = torch.empty_like(lo, device=DEV)
+    iog = torch.empty_like(io, device=DEV)
+    ops.fill_minibatch(src.to(DEV), sh.to(DEV), 2, count, dg,
+                       mean=mean.to(DEV), rdisp=rd.to(DEV),
+                       labels=lab.to(DEV), labels_out=log, idx_out=iog)
     close(dg, d, 1e-2)
+    assert torch.equal(log.cpu(), lo) and torch.equal(iog.cpu(), io)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
