@@ -1,6 +1,11 @@
 """Summarise a rocprofv3 --pmc counter_collection CSV per kernel config:
 wait / issue / active shares of wave cycles, MFMA busy share, LDS bank
-conflicts per LDS instruction (MI355X_MICROARCH.md, rocprofv3 PMC slots)."""
+conflicts per LDS instruction (MI355X_MICROARCH.md, rocprofv3 PMC slots).
+
+MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (kernel time x 2.4 GHz x 1024
+SIMDs): the counter sums over every SIMD (calibrated on this box:
+SQ_BUSY_CYCLES / (time x 2.4 GHz) = 30 ~ the 32 shader engines).  Under load
+the clock can sit below 2.4 GHz, so the figure is a lower bound."""
 import collections
 import csv
 import sys
@@ -20,7 +25,7 @@ def main(path, out, title):
             int(r["Start_Timestamp"])
     lines = ["# " + title, "",
              "| kernel | grid | ms (sum) | wait % | issue-stall % | active % "
-             "| MFMA busy % of busy | LDS conflict cyc / LDS inst |",
+             "| MFMA util % (of 1024 SIMDs x 2.4 GHz) | LDS conflict cyc / LDS inst |",
              "|---|---|---|---|---|---|---|---|"]
     items = []
     for k, d in agg.items():
@@ -28,13 +33,13 @@ def main(path, out, title):
         items.append((ns, k, d))
     for ns, k, d in sorted(items, key=lambda x: -x[0])[:25]:
         wc = d.get("SQ_WAVE_CYCLES", 0) or 1
-        busy = d.get("SQ_BUSY_CYCLES", 0) or 1
         lds = d.get("SQ_INSTS_LDS", 0) or 1
         lines.append("| %s | %s | %.3f | %.0f | %.0f | %.0f | %.0f | %.2f |" % (
             k[0], k[1], ns / 1e6, 100 * d.get("SQ_WAIT_ANY", 0) / wc,
             100 * d.get("SQ_WAIT_INST_ANY", 0) / wc,
             100 * d.get("SQ_ACTIVE_INST_ANY", 0) / wc,
-            100 * d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / busy,
+            100 * d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(ns * 2.4 * 1024,
+                                                             1),
             d.get("SQ_LDS_BANK_CONFLICT", 0) / lds))
     open(out, "w").write("\n".join(lines) + "\n")
 
