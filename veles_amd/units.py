@@ -499,6 +499,9 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
                     value.state = saved[key]
         if saved:
             self._saved_rg_states = saved
+        if not getattr(type(self), "DISABLE_INTERFACE_VERIFICATION", False):
+            from veles_amd.verified import Verified
+            Verified.verify_interface(self, IUnit)
         retry = type(self).initialize(self, **kwargs)
         for key, st in restore.items():
             getattr(self, key).state = st
