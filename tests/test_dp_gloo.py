@@ -138,3 +138,27 @@ def test_spawn_ranks_shrinks_after_failure(tmp_path):
     assert rc == 0
     assert (tmp_path / "r0_w2").read_text() == "2 0"
     assert (tmp_path / "r1_w2").read_text() == "2 2"
+
+
+def test_watchdog_kicked_by_decision_and_expires():
+    """--job-timeout: the decision unit's run kicks the watchdog; a stall
+    longer than the timeout fires on_expire (os._exit(124) by default)."""
+    import threading
+    import time
+    from veles_amd.parallel.faults import Watchdog
+
+    class Dec(object):
+        def run(self):
+            pass
+
+    class Wf(object):
+        decision = Dec()
+
+    fired = threading.Event()
+    wd = Watchdog(0.4, on_expire=fired.set).install(Wf)
+    for _ in range(6):
+        Wf.decision.run()
+        time.sleep(0.1)
+    assert not fired.is_set()
+    assert fired.wait(3.0)
+    wd.stop()

@@ -105,6 +105,10 @@ class Main(object):
         args = self.args
         if args.dry_run == "load":
             return
+        if args.job_timeout > 0:
+            from veles_amd.utils.config import root
+            root.common.engine.dp.timeout_s = max(60, int(args.job_timeout *
+                                                         60))
         dev = self.launcher.initialize()
         kwargs.setdefault("device", dev)
         self.workflow.initialize(**kwargs)
@@ -115,7 +119,13 @@ class Main(object):
         if args.fault_inject_prob > 0:
             from veles_amd.parallel.faults import FaultInjector
             FaultInjector(self.workflow, args.fault_inject_prob).install()
+        wd = None
+        if args.job_timeout > 0:
+            from veles_amd.parallel.faults import Watchdog
+            wd = Watchdog(args.job_timeout * 60.0).install(self.workflow)
         self.launcher.run()
+        if wd is not None:
+            wd.stop()
         self.launcher.finish()
         if args.dump_unit_attributes != "no":
             for u in self.workflow:

@@ -71,6 +71,9 @@ def make_parser():
     p.add_argument("--respawn", type=int, default=0,
                    help="restart failed rank groups N times from the "
                         "latest snapshot")
+    p.add_argument("--job-timeout", type=float, default=0.0,
+                   help="minutes a training step (or a collective) may "
+                        "take before the rank aborts for a respawn")
     p.add_argument("--respawn-shrink", action="store_true",
                    help="on respawn, drop the failed ranks' GPUs and keep "
                         "the global batch by gradient accumulation")

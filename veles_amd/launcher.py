@@ -84,7 +84,9 @@ class Launcher(Logger):
         if self.world_size > 1 and self.dp_ is None:
             from veles_amd.parallel.dp import DataParallel
             be = "gloo" if self.backend in ("cpu", "numpy") else None
-            self.dp_ = DataParallel(backend=be)
+            from veles_amd.utils.config import root, get
+            self.dp_ = DataParallel(backend=be, timeout_s=int(get(
+                root.common.engine.dp.timeout_s, 600)))
         if self.device is None:
             kw = {}
             if self.device_id not in (None, ""):

@@ -59,6 +59,23 @@ class Watchdog(object):
     def kick(self):
         self._last = time.time()
 
+    def install(self, workflow):
+        """Kick on every decision run (one per minibatch): a rank whose step
+        stalls longer than ``timeout`` exits 124 so the launcher can respawn
+        the group (the reference's per-slave job timeout, server.py:619-635,
+        ``--job-timeout``)."""
+        dec = getattr(workflow, "decision", None)
+        if dec is None:
+            return self
+        orig = dec.run
+        wd = self
+
+        def run_and_kick():
+            orig()
+            wd.kick()
+        dec.__dict__["run"] = run_and_kick
+        return self.start()
+
     def stop(self):
         self._stop.set()
 
