@@ -69,11 +69,15 @@ def test_alexnet_shapes_one_step_cpu():
     assert wf.param_store_.steps == 1
 
 
-def test_snapshot_and_exact_resume(tmp_path):
+@pytest.mark.parametrize("layers_name", ["mnist_fc", "lenet"])
+def test_snapshot_and_exact_resume(tmp_path, layers_name):
+    """Pickle snapshot + exact resume; lenet adds parameterless layers
+    (pooling) whose GD units pickle without weights."""
+    from veles_amd.models import zoo
     snap = {"prefix": "mnist", "directory": str(tmp_path), "interval": 1,
             "time_interval": 0, "compression": "gz"}
     root.common.disable.snapshotting = False
-    wf = build(mnist_fc(), epochs=2, snap=snap)
+    wf = build(getattr(zoo, layers_name)(), epochs=2, snap=snap)
     wf.initialize(device=Device(backend="cpu"))
     wf.run()
     files = sorted(os.listdir(tmp_path))

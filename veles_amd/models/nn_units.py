@@ -320,11 +320,11 @@ class GradientDescentBase(AcceleratedUnit):
 
     def __getstate__(self):
         fwd = getattr(self, "forward_unit", None)
-        if fwd is not None and fwd._pw_ is not None and \
-                fwd._pw_.mom is not None:
+        pw = getattr(fwd, "_pw_", None)  # parameterless layers: pooling...
+        if pw is not None and pw.mom is not None:
             self.accumulated_gradient_weights.reset(
-                fwd._pw_.mom.detach().float().cpu().numpy())
-            if fwd._pb_ is not None:
+                pw.mom.detach().float().cpu().numpy())
+            if getattr(fwd, "_pb_", None) is not None:
                 self.accumulated_gradient_bias.reset(
                     fwd._pb_.mom.detach().float().cpu().numpy())
         return super().__getstate__()
