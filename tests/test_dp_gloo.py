@@ -162,3 +162,56 @@ def test_watchdog_kicked_by_decision_and_expires():
     assert not fired.is_set()
     assert fired.wait(3.0)
     wd.stop()
+
+
+def test_spawn_ranks_multi_node_rank_layout(tmp_path):
+    """Two "nodes" of two ranks each on one host: global ranks 0-3 meet at
+    one rendezvous and each rank sees its node-local rank and device."""
+    import sys
+    import threading
+    from veles_amd.parallel.launch import spawn_ranks
+    script = tmp_path / "r.py"
+    script.write_text(
+        "import os\n"
+        "import torch.distributed as dist\n"
+        "import torch\n"
+        "dist.init_process_group('gloo')\n"
+        "t = torch.tensor([float(dist.get_rank())])\n"
+        "dist.all_reduce(t)\n"
+        "e = os.environ\n"
+        "open(os.path.join(%r, 'r' + e['RANK']), 'w').write(' '.join(\n"
+        "    [e['LOCAL_RANK'], e['WORLD_SIZE'], e['GROUP_RANK'],\n"
+        "     e['VELES_AMD_DEVICE'], str(int(t.item()))]))\n"
+        "dist.destroy_process_group()\n" % str(tmp_path))
+    port = _free_port()
+    rcs = [None, None]
+
+    def node(r):
+        rcs[r] = spawn_ranks("0,1", [sys.executable, str(script)],
+                             poll=0.05, nnodes=2, node_rank=r,
+                             master_addr="127.0.0.1", master_port=port)
+    ts = [threading.Thread(target=node, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert rcs == [0, 0]
+    for g in range(4):
+        assert (tmp_path / ("r%d" % g)).read_text() == "%d 4 %d %d 6" % (
+            g % 2, g // 2, g % 2)
+
+
+def test_multi_node_launch_validation_and_argv():
+    from veles_amd.__main__ import _strip_launch_flags
+    from veles_amd.parallel.launch import spawn_ranks
+    with pytest.raises(ValueError):
+        spawn_ranks("0", ["true"], nnodes=2, node_rank=0)
+    with pytest.raises(ValueError):
+        spawn_ranks("0", ["true"], nnodes=2, node_rank=2,
+                    master_addr="127.0.0.1", master_port=1)
+    with pytest.raises(ValueError):
+        spawn_ranks("0", ["true"], nnodes=2, node_rank=0, shrink=True,
+                    master_addr="127.0.0.1", master_port=1)
+    argv = ["wf.py", "-", "--gpus", "0-7", "--nnodes=2", "--node-rank", "1",
+            "--master-addr", "10.0.0.1", "--master-port=29500", "root.x=1"]
+    assert _strip_launch_flags(argv) == ["wf.py", "-", "root.x=1"]

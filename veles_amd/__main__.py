@@ -14,6 +14,29 @@ import sys
 __all__ = ["Main", "main"]
 
 
+_LAUNCH_FLAGS = ("--gpus", "--nnodes", "--node-rank", "--master-addr",
+                 "--master-port")
+
+
+def _strip_launch_flags(argv):
+    """The command line each spawned rank gets: the launcher's own flags
+    (``--gpus`` and the multi-node rendezvous) removed, both the
+    ``--flag value`` and ``--flag=value`` forms."""
+    out = []
+    skip = False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a in _LAUNCH_FLAGS:
+            skip = True
+            continue
+        if a.split("=", 1)[0] in _LAUNCH_FLAGS and "=" in a:
+            continue
+        out.append(a)
+    return out
+
+
 class Main(object):
     def __init__(self, argv=None):
         self.argv = sys.argv[1:] if argv is None else list(argv)
@@ -143,12 +166,13 @@ class Main(object):
             return 0
         if args.gpus and int(os.environ.get("WORLD_SIZE", "1")) == 1:
             from veles_amd.parallel.launch import spawn_ranks
-            argv = [a for a in self.argv]
-            i = argv.index("--gpus")
-            del argv[i:i + 2]
+            argv = _strip_launch_flags(self.argv)
             return spawn_ranks(args.gpus, [sys.executable, "-m", "veles_amd"]
                                + argv, respawn=args.respawn,
-                               shrink=args.respawn_shrink)
+                               shrink=args.respawn_shrink,
+                               nnodes=args.nnodes, node_rank=args.node_rank,
+                               master_addr=args.master_addr,
+                               master_port=args.master_port)
         self._setup_logging(args)
         if not args.workflow:
             make_parser().print_help()

@@ -64,6 +64,13 @@ def make_parser():
                    help="device id(s) / spec, e.g. 0 or 0-7 or 0,2x2")
     p.add_argument("--gpus", default="",
                    help="spawn one data-parallel rank per listed GPU")
+    p.add_argument("--nnodes", type=int, default=1,
+                   help="nodes in a multi-node --gpus job (each node runs "
+                        "the same command with its own --node-rank)")
+    p.add_argument("--node-rank", type=int, default=0)
+    p.add_argument("--master-addr", default=None,
+                   help="rendezvous host of global rank 0 (multi-node)")
+    p.add_argument("--master-port", type=int, default=None)
     p.add_argument("--force-cpu", default="",
                    help="comma-separated units pinned to the CPU")
     p.add_argument("--sync-run", action="store_true")

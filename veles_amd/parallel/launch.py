@@ -4,6 +4,12 @@ Replaces the reference's SSH/YARN node spawning and master/slave roles
 (veles/launcher.py:617-660, 808-842; server.py ``--respawn`` 637-655).  Each
 rank is a child process with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
 MASTER_PORT set (the torch.distributed.run contract, 127.0.0.1 rendezvous).
+Multi-node (``--nnodes N --node-rank R --master-addr A --master-port P``)
+replaces the reference's ``-n host/devs`` SSH node list and ``-m/-l``
+master/slave addresses (veles/launcher.py:199-262): every node runs this
+launcher for its own GPUs, global rank = R * local ranks + local rank, and
+all ranks rendezvous at A:P (RCCL over xGMI inside a node, the host network
+between nodes).
 Failure handling: if any rank dies, the whole group is terminated (a
 collective would otherwise hang until its timeout) and, with ``respawn > 0``,
 restarted from the newest ``*_current`` snapshot - the elastic-restart path
@@ -40,13 +46,18 @@ def latest_snapshot(directory):
     return max(cands, key=lambda c: os.path.getmtime(os.path.realpath(c)))
 
 
-def _launch(devices, cmd, port, env_extra=None):
+def _launch(devices, cmd, port, env_extra=None, nnodes=1, node_rank=0,
+            master_addr="127.0.0.1"):
     procs = []
     n = len(devices)
-    for rank, dev in enumerate(devices):
+    for local, dev in enumerate(devices):
         env = dict(os.environ)
-        env.update({"RANK": str(rank), "LOCAL_RANK": str(rank),
-                    "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+        env.update({"RANK": str(node_rank * n + local),
+                    "LOCAL_RANK": str(local),
+                    "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": str(node_rank),
+                    "WORLD_SIZE": str(n * nnodes),
+                    "MASTER_ADDR": master_addr,
                     "MASTER_PORT": str(port),
                     "VELES_AMD_DEVICE": str(dev)})
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -75,9 +86,18 @@ def _kill_all(procs):
 
 
 def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5,
-                shrink=False):
+                shrink=False, nnodes=1, node_rank=0, master_addr=None,
+                master_port=None):
     """Run ``cmd`` once per device in ``spec`` ("0-7", "0,1", "4").
     Returns the group's exit code (0 when every rank succeeded).
+
+    ``nnodes > 1``: this call is node ``node_rank`` of a job whose nodes
+    all list the same number of devices; ``master_addr``/``master_port``
+    (required) name the rendezvous of global rank 0.  A failure anywhere
+    ends every node's ranks (the survivors' collectives time out under
+    ``--job-timeout``), so each node's launcher respawns its group and the
+    job meets again at the same address.  Shrinking needs one launcher
+    for the whole job and is refused here.
 
     ``shrink``: on a respawn, leave out the device(s) whose rank failed and
     keep the global batch by gradient accumulation - each survivor's
@@ -86,11 +106,22 @@ def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5,
     divide; a warning says so)."""
     devices = parse_device_spec(spec) if isinstance(spec, str) else list(spec)
     world0 = len(devices)
+    if nnodes > 1:
+        if master_addr is None or master_port is None:
+            raise ValueError("multi-node launch needs master_addr and "
+                             "master_port")
+        if not 0 <= node_rank < nnodes:
+            raise ValueError("node_rank %d outside [0, %d)" %
+                             (node_rank, nnodes))
+        if shrink:
+            raise ValueError("--respawn-shrink is single-node only")
+    addr = master_addr or "127.0.0.1"
     attempt = 0
     cmd = list(cmd)
     env_extra = {}
     while True:
-        procs = _launch(devices, cmd, free_port(), env_extra)
+        procs = _launch(devices, cmd, master_port or free_port(), env_extra,
+                        nnodes, node_rank, addr)
         failed = None
         failed_ranks = []
         try:
