@@ -31,3 +31,12 @@ def test_sample_trains_one_epoch_cpu(name):
 @pytest.mark.parametrize("name", ["alexnet", "vgg16"])
 def test_big_sample_loads_cpu(name):
     cli("samples/%s.py" % name, "-", "-a", "cpu", "--dry-run", "load")
+
+
+def test_cli_html_help_and_plot_switches():
+    out = cli("--html-help")
+    assert out.lstrip().startswith("<!DOCTYPE html>")
+    assert "--master-addr" in out and "--no-graphics-client" in out
+    out = cli("samples/mnist_conv.py", "-", "-a", "cpu", "--dry-run", "load",
+              "--no-graphics-client", "-p", "", "--dump-config")
+    assert "plotting" in out

@@ -37,6 +37,22 @@ def _strip_launch_flags(argv):
     return out
 
 
+def _html_help(parser):
+    """``--html-help`` (reference cmdline.py:139-151): the argparse help as
+    a standalone HTML page, one table row per option."""
+    import html
+    rows = []
+    for act in parser._actions:
+        flags = ", ".join(act.option_strings) or act.dest
+        rows.append("<tr><td><code>%s</code></td><td>%s</td></tr>" % (
+            html.escape(flags), html.escape(act.help or "")))
+    return ("<!DOCTYPE html><html><head><meta charset=\"utf-8\">"
+            "<title>veles_amd command line</title></head><body>"
+            "<h1>python -m veles_amd</h1><pre>%s</pre><table>%s</table>"
+            "</body></html>" % (html.escape(parser.format_usage()),
+                                "".join(rows)))
+
+
 class Main(object):
     def __init__(self, argv=None):
         self.argv = sys.argv[1:] if argv is None else list(argv)
@@ -164,6 +180,9 @@ class Main(object):
         if args.version:
             print("veles_amd", __version__)
             return 0
+        if args.html_help:
+            print(_html_help(make_parser()))
+            return 0
         if args.gpus and int(os.environ.get("WORLD_SIZE", "1")) == 1:
             from veles_amd.parallel.launch import spawn_ranks
             argv = _strip_launch_flags(self.argv)
@@ -183,6 +202,10 @@ class Main(object):
         if args.force_cpu:
             root.common.engine.force_cpu = tuple(args.force_cpu.split(","))
         root.common.engine.sync_run = args.sync_run
+        if args.no_graphics_client or args.matplotlib_backend == "":
+            root.common.disable.plotting = True
+        elif args.matplotlib_backend:
+            root.common.plotting.backend = args.matplotlib_backend
         root.common.loader.train_ratio = args.train_ratio
         module = self._import_workflow(args.workflow)
         cfg = args.config

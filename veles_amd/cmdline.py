@@ -51,7 +51,12 @@ def make_parser():
     p.add_argument("-b", "--background", action="store_true")
     p.add_argument("-t", "--test", action="store_true",
                    help="test (inference) mode")
-    p.add_argument("-p", "--matplotlib-backend", default="")
+    p.add_argument("-p", "--matplotlib-backend", default=None,
+                   help="plot backend; '' disables every plotter")
+    p.add_argument("--no-graphics-client", action="store_true",
+                   help="disable every plotter")
+    p.add_argument("--html-help", action="store_true",
+                   help="print this help as an HTML page and exit")
     p.add_argument("--pdb-on-finish", action="store_true")
     p.add_argument("-s", "--stealth", action="store_true")
     p.add_argument("-f", "--log-file", default="")
