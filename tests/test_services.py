@@ -183,3 +183,21 @@ def test_cli_ensemble_train_and_test(tmp_path):
 
 
 _ = torch
+
+
+def test_prometheus_text_exposition():
+    from veles_amd.web_status import prometheus_text
+    st = {"time": 12.5, "rank": 3, "pid": 7, "epoch": 2,
+          "last_epoch": {"train_err": 0.25, "ok": True},
+          "units": {"conv1": 0.5, 'we"ird': 1.0},
+          "device_memory": {"allocated": 1024, "peak": 2048},
+          "workflow": "wf"}
+    txt = prometheus_text(st)
+    assert 'veles_amd_epoch{rank="3"} 2.0' in txt
+    assert 'veles_amd_last_epoch_train_err{rank="3"} 0.25' in txt
+    assert 'veles_amd_last_epoch_ok{rank="3"} 1.0' in txt
+    assert 'veles_amd_device_memory_peak{rank="3"} 2048.0' in txt
+    assert 'veles_amd_unit_run_seconds{rank="3",unit="conv1"} 0.5' in txt
+    assert "workflow" not in txt and "pid" not in txt
+    for line in txt.splitlines():
+        assert line.startswith("# TYPE ") or line.startswith("veles_amd_")

@@ -18,7 +18,43 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from veles_amd.units import Unit
 from veles_amd.utils.json_encoders import NumpyJSONEncoder
 
-__all__ = ["StatusReporter", "collect_status"]
+__all__ = ["StatusReporter", "collect_status", "prometheus_text"]
+
+
+def prometheus_text(st, prefix="veles_amd"):
+    """Prometheus text exposition (format 0.0.4) of one status record:
+    numeric scalars become gauges, per-unit run times one labelled gauge,
+    and every sample carries the rank label (a scrape target per rank)."""
+    import re
+    rank = st.get("rank", 0)
+    lines = []
+
+    def gauge(name, value, labels=""):
+        name = prefix + "_" + re.sub(r"[^a-zA-Z0-9_]", "_", name)
+        lab = 'rank="%s"%s' % (rank, labels)
+        lines.append("# TYPE %s gauge" % name)
+        lines.append("%s{%s} %r" % (name, lab, float(value)))
+
+    def walk(key, v):
+        if isinstance(v, bool):
+            gauge(key, int(v))
+        elif isinstance(v, (int, float)):
+            gauge(key, v)
+        elif isinstance(v, dict) and key != "units":
+            for k, x in v.items():
+                walk(key + "_" + str(k), x)
+    for k, v in st.items():
+        if k not in ("rank", "pid"):
+            walk(k, v)
+    units = st.get("units") or {}
+    if units:
+        name = prefix + "_unit_run_seconds"
+        lines.append("# TYPE %s gauge" % name)
+        for u, t in units.items():
+            lines.append('%s{rank="%s",unit="%s"} %r' % (
+                name, rank, str(u).replace("\\", "_").replace('"', "'"),
+                float(t)))
+    return "\n".join(lines) + "\n"
 
 
 def collect_status(wf):
@@ -74,6 +110,15 @@ class StatusReporter(Unit):
                 pass
 
             def do_GET(self):
+                if self.path.rstrip("/") == "/metrics":
+                    st = rep.records[-1] if rep.records else {}
+                    body = prometheus_text(st).encode()
+                    self.send_response(200)
+                    self.send_header("Content-Type",
+                                     "text/plain; version=0.0.4")
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return
                 if self.path.rstrip("/") not in ("/status", ""):
                     self.send_response(404)
                     self.end_headers()
