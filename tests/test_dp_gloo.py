@@ -215,3 +215,119 @@ def test_multi_node_launch_validation_and_argv():
     argv = ["wf.py", "-", "--gpus", "0-7", "--nnodes=2", "--node-rank", "1",
             "--master-addr", "10.0.0.1", "--master-port=29500", "root.x=1"]
     assert _strip_launch_flags(argv) == ["wf.py", "-", "root.x=1"]
+
+
+def _train_snap(rank, world, port, snapdir, steps):
+    import torch
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    from veles_amd.models import zoo
+    from veles_amd.parallel.dp import DataParallel
+    from veles_amd.utils.config import root
+    import veles_amd.loader  # noqa: F401
+    root.common.disable.snapshotting = False
+    dp = DataParallel(backend="gloo", timeout_s=60)
+    la = DummyLauncher()
+    la.dp_ = dp
+    # the clocks of the two ranks disagree as much as they can: rank 0
+    # always finds the interval elapsed, rank 1 never does.  The decision
+    # must still be collective (rank 0's), or rank 0 waits in the export
+    # barrier while rank 1 enters the next gradient all-reduce.
+    wf = StandardWorkflow(
+        la, loader_name="synthetic_images",
+        loader_config={"dataset": "mnist", "class_lengths": (0, 40, 80),
+                       "minibatch_size": 40,
+                       "normalization_type": "mean_disp"},
+        layers=zoo.mnist_fc(),
+        decision_config={"max_epochs": None, "fail_iterations": None},
+        snapshotter_config={"prefix": "dp", "directory": snapdir,
+                            "interval": 1, "compression": "",
+                            "time_interval": 0.0 if rank == 0 else 1e9})
+    wf.initialize(device=Device(backend="cpu"))
+    wf.run_steps(steps)
+    dp.barrier()
+    dp.shutdown()
+
+
+def test_dp_snapshotter_decision_is_collective(tmp_path):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_train_snap,
+                         args=(r, 2, port, str(tmp_path), 6))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0, 0]
+    snaps = [f for f in os.listdir(tmp_path) if f.startswith("dp_") and
+             "current" not in f]
+    assert snaps, "rank 0 wrote no snapshot"
+
+
+def test_multi_node_respawn_needs_shared_snapshot_dir(tmp_path, monkeypatch):
+    """Only global rank 0 writes snapshots; a node whose snapshot directory
+    is not shared with the others would resume stale state."""
+    import threading
+    from veles_amd.parallel.launch import check_shared_dir, spawn_ranks
+    monkeypatch.setenv("VELES_AMD_SHARED_DIR_TIMEOUT", "0.5")
+    # node 1 alone: node 0's marker never shows up -> refused before launch
+    with pytest.raises(ValueError, match="shared"):
+        spawn_ranks("0", ["true"], respawn=1, nnodes=2, node_rank=1,
+                    master_addr="127.0.0.1", master_port=1,
+                    snapshot_dir=str(tmp_path / "private"))
+    # both nodes see one directory: accepted
+    shared = str(tmp_path / "shared")
+    ok = [None, None]
+
+    def node(r):
+        ok[r] = check_shared_dir(shared, 2, r, "job", timeout=10)
+    ts = [threading.Thread(target=node, args=(r,)) for r in (0, 1)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(20)
+    assert ok == [True, True]
+
+
+def _digest_rank(rank, port, path, q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": "2",
+                       "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    from veles_amd.launcher import Launcher
+    la = Launcher(backend="cpu", snapshot_file=path % rank)
+    try:
+        la.initialize()
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, "mismatch" if "different snapshots" in str(e)
+               else str(e)))
+    la.dp_.shutdown()
+
+
+def test_ranks_must_resume_the_same_snapshot(tmp_path):
+    ctx = mp.get_context("spawn")
+    for same in (True, False):
+        for r in (0, 1):
+            (tmp_path / ("s%d" % r)).write_bytes(
+                b"snap" + (b"" if same else bytes([r])))
+        q = ctx.Queue()
+        port = _free_port()
+        ps = [ctx.Process(target=_digest_rank,
+                          args=(r, port, str(tmp_path / "s%d"), q))
+              for r in (0, 1)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(120)
+        res = dict(q.get(timeout=5) for _ in ps)
+        assert set(res.values()) == {"ok" if same else "mismatch"}

@@ -58,3 +58,42 @@ def test_forge_roundtrip(tmp_path):
         assert e.value.code == 404
     finally:
         srv.stop()
+
+
+@pytest.mark.parametrize("bad", [".", "..", ".hidden", "", "a/b", "../x"])
+def test_forge_rejects_dot_names(tmp_path, bad):
+    """'..' used to resolve to the store's parent: an upload wrote there and
+    a delete removed the whole store."""
+    from veles_amd.forge import ForgeStore
+    root = tmp_path / "store"
+    st = ForgeStore(str(root), tokens=["alice"])
+    (tmp_path / "keep.txt").write_text("k")
+    meta = {"name": bad, "workflow": "w.py", "configuration": "c.py",
+            "short_description": "d", "author": "a", "version": "1"}
+    import io
+    import tarfile
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w:gz") as t:
+        ti = tarfile.TarInfo("w.py")
+        ti.size = 0
+        t.addfile(ti, io.BytesIO(b""))
+    with pytest.raises(KeyError):
+        st.upload("alice", meta, buf.getvalue())
+    with pytest.raises(KeyError):
+        st.delete("alice", bad)
+    assert (tmp_path / "keep.txt").exists()
+    assert (root / "tokens.json").exists()
+    assert not (tmp_path / "manifest.json").exists()
+
+
+def test_forge_http_delete_dotdot(tmp_path):
+    srv = ForgeServer(str(tmp_path / "store"), tokens=["alice"])
+    srv.start()
+    try:
+        c = ForgeClient(srv.url)
+        with pytest.raises(urllib.error.HTTPError) as e:
+            c.delete("..", "alice")
+        assert e.value.code in (400, 403, 404)
+        assert (tmp_path / "store" / "tokens.json").exists()
+    finally:
+        srv.stop()

@@ -62,6 +62,35 @@ def test_downloader_missing_file_and_tar_escape(tmp_path):
         d.initialize()
 
 
+def test_unpack_rejects_symlink_chain(tmp_path):
+    """d/l -> .., d/l/m -> .., d/l/m/escaped.txt: every member passes a
+    realpath check taken before extraction, yet the file lands two levels
+    above the target.  Links are refused outright."""
+    src = tmp_path / "chain.tar"
+    with tarfile.open(src, "w") as t:
+        for name in ("d/l", "d/l/m"):
+            ti = tarfile.TarInfo(name)
+            ti.type = tarfile.SYMTYPE
+            ti.linkname = ".."
+            t.addfile(ti)
+        ti = tarfile.TarInfo("d/l/m/escaped.txt")
+        ti.size = 1
+        t.addfile(ti, io.BytesIO(b"z"))
+    out = tmp_path / "a" / "b" / "out"
+    out.mkdir(parents=True)
+    with pytest.raises(ValueError):
+        unpack(str(src), str(out))
+    assert not list(tmp_path.rglob("escaped.txt"))
+    hard = tmp_path / "hard.tar"
+    with tarfile.open(hard, "w") as t:
+        ti = tarfile.TarInfo("h")
+        ti.type = tarfile.LNKTYPE
+        ti.linkname = "../../etc/passwd"
+        t.addfile(ti)
+    with pytest.raises(ValueError):
+        unpack(str(hard), str(out))
+
+
 def test_decode_audio_widths(tmp_path):
     pcm = (numpy.arange(-50, 50, dtype=numpy.int16) * 300)
     _wav(tmp_path / "a.wav", pcm)

@@ -148,3 +148,25 @@ def test_lrn_pool_fusion_matches_unfused_cpu():
         wf.run_steps(2)
         ws.append(wf.forwards[0].weights_master.clone())
     assert torch.allclose(ws[0], ws[1], atol=1e-6)
+
+
+def test_segment_table_in_place_and_cache_bounded():
+    """A per-step LR policy must neither grow a cache nor move the device
+    table (_SEG_CACHE leaked one tensor per step)."""
+    import torch
+    from veles_amd import ops
+    t = ops.SegmentTable(torch.device("cpu"))
+    a = t.update(ops._pack_sgd_segs([(0, 64, 0.1, 0.0, 0.0, 0.9)]))
+    ptr = a.data_ptr()
+    for i in range(300):
+        b = t.update(ops._pack_sgd_segs([(0, 64, 0.1 * 0.99 ** i, 0.0, 0.0,
+                                          0.9)]))
+        assert b.data_ptr() == ptr
+    raw = ops._pack_sgd_segs([(0, 64, 0.5, 0.0, 0.0, 0.9)])
+    assert bytes(b[:len(raw)].numpy().tobytes()) != raw
+    b = t.update(raw)
+    assert bytes(b[:len(raw)].numpy().tobytes()) == raw
+    for i in range(500):
+        ops._segs_tensor(ops._pack_sgd_segs([(0, 8, float(i), 0, 0, 0)]),
+                         torch.device("cpu"))
+    assert len(ops._SEG_CACHE) <= ops._SEG_CACHE_MAX

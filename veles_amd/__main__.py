@@ -123,7 +123,8 @@ class Main(object):
             backend="cpu" if args.backend == "numpy" else args.backend,
             device_id=args.device or None,
             result_file=args.result_file or None, testing=args.test,
-            trace_events=args.trace_events or None, log_id=args.log_id)
+            trace_events=args.trace_events or None, log_id=args.log_id,
+            snapshot_file=args.snapshot or None)
         if args.snapshot:
             from veles_amd.snapshotter import SnapshotterToFile
             wf = SnapshotterToFile.import_(args.snapshot)

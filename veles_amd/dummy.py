@@ -36,6 +36,12 @@ class DummyLauncher(object):
     def add_ref(self, workflow):
         self.workflow = workflow
 
+    def __getstate__(self):
+        # process-local handles (the data-parallel group ``dp_``, streams)
+        # never enter a snapshot, as in Launcher.__getstate__
+        return {k: v for k, v in self.__dict__.items()
+                if not k.endswith("_")}
+
     def del_ref(self, unit):
         pass
 

@@ -44,7 +44,9 @@ __all__ = ["ForgeStore", "ForgeServer", "ForgeClient", "REQUIRED_FIELDS"]
 
 REQUIRED_FIELDS = ("name", "workflow", "configuration", "short_description",
                    "author", "version")
-_NAME = re.compile(r"^[A-Za-z0-9_.-]+$")
+# a name is one path component: it may not be empty, start with '.', or be
+# '.' / '..' (which would put the package at or above the store root)
+_NAME = re.compile(r"^[A-Za-z0-9_][A-Za-z0-9_.-]*$")
 
 
 def scramble(token):
@@ -89,7 +91,13 @@ class ForgeStore(object):
     def _dir(self, name):
         if not _NAME.match(name or ""):
             raise KeyError("bad package name %r" % name)
-        return os.path.join(self.root, name)
+        path = os.path.join(self.root, name)
+        # belt and braces: the package directory must be a direct child of
+        # the store root even if the root itself is reached via symlinks
+        if os.path.dirname(os.path.realpath(path)) != \
+                os.path.realpath(self.root):
+            raise KeyError("bad package name %r" % name)
+        return path
 
     def _manifest(self, name):
         p = os.path.join(self._dir(name), "manifest.json")

@@ -37,6 +37,7 @@ class Launcher(Logger):
         self.workflow = None
         self.device = None
         self.dp_ = None
+        self.snapshot_file = kwargs.get("snapshot_file")
         self.stopped = False
         self.start_time = time.time()
         self.world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,8 +95,23 @@ class Launcher(Logger):
                 ids = parse_device_spec(self.device_id)
                 kw["device_id"] = ids[self.rank % len(ids)]
             self.device = Device(backend=self.backend, **kw)
+        if self.dp_ is not None and self.snapshot_file:
+            self._check_same_snapshot()
         self.info("rank %d/%d on %s", self.rank, self.world_size, self.device)
         return self.device
+
+    def _check_same_snapshot(self):
+        """Every rank of a resumed data-parallel job must have restored the
+        same snapshot bytes: replicas that resume different epochs / loader
+        positions / momenta diverge and deadlock at the next epoch end."""
+        from veles_amd.parallel.launch import snapshot_digest
+        mine = snapshot_digest(self.snapshot_file)
+        allv = self.dp_.all_gather_object(mine)
+        if any(v != allv[0] for v in allv):
+            raise RuntimeError(
+                "ranks resumed from different snapshots %s (this rank: %s); "
+                "a multi-node job needs a shared snapshot directory" %
+                (allv, self.snapshot_file))
 
     def run(self):
         wf = self.workflow

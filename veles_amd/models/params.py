@@ -68,6 +68,7 @@ class ParameterStore(object):
         self._segs = None
         self._solver_segs = None
         self._seg_key = None
+        self._seg_table = None
         self.steps = 0
         # micro-steps per optimizer step: > 1 after an elastic shrink keeps
         # the global batch (parallel/launch.py ``shrink``)
@@ -237,18 +238,21 @@ class ParameterStore(object):
             for w in self._works:
                 w.wait()
         segs = self._cached_segments()
+        if segs and self._seg_table is None:
+            self._seg_table = ops.SegmentTable(self.master.device)
         if segs and self._solver_segs is not None:
             import torch
             if self.mom2 is None:
                 self.mom2 = torch.zeros_like(self.mom)
             ops.solver_update(self.master, self.grad, self.mom, self.mom2,
                               self._solver_segs, w_lp=self.lp,
-                              gscale=gscale / self.accumulate, zero_grad=True)
+                              gscale=gscale / self.accumulate, zero_grad=True,
+                              table=self._seg_table)
         elif segs:
             # the fused kernel also zeroes the gradient buffer
             ops.sgd_update(self.master, self.grad, self.mom, segs,
                            w_lp=self.lp, gscale=gscale / self.accumulate,
-                           zero_grad=True)
+                           zero_grad=True, table=self._seg_table)
         else:
             self.grad.zero_()
         self._works = []

@@ -782,31 +782,96 @@ def mse(y, target, *, scale=1.0, err=None, mse_out=None, metrics=None,
 
 # --------------------------------------------------------------- optimizer
 _SEG_CACHE = {}
+_SEG_CACHE_MAX = 64
 
 
-def _segs_tensor(segs, device):
-    key = (tuple(segs), str(device))
+def _pack_sgd_segs(segs):
+    return b"".join(struct.pack("<qqffff", int(b), int(e), float(lr),
+                                float(d), float(l1), float(m))
+                    for b, e, lr, d, l1, m in segs)
+
+
+def _pack_solver_segs(segs):
+    return b"".join(struct.pack(
+        "<qqffffifff", int(b), int(e), float(lr), float(d), float(l1),
+        float(m), int(mode), float(eps), float(rho), 0.0)
+        for b, e, lr, d, l1, m, mode, eps, rho in segs)
+
+
+def _segs_tensor(raw, device):
+    """Device copy of a packed segment table, from a BOUNDED cache (one-off
+    callers; a training loop whose learning rates move every step uses a
+    :class:`SegmentTable` instead)."""
+    key = (raw, str(device))
     t = _SEG_CACHE.get(key)
     if t is None:
-        raw = b"".join(struct.pack("<qqffff", int(b), int(e), float(lr),
-                                   float(d), float(l1), float(m))
-                       for b, e, lr, d, l1, m in segs)
         t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
-        if len(_SEG_CACHE) > 256:
-            _SEG_CACHE.clear()
+        if len(_SEG_CACHE) >= _SEG_CACHE_MAX:
+            _SEG_CACHE.pop(next(iter(_SEG_CACHE)))
         _SEG_CACHE[key] = t
     return t
 
 
-def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False):
+class SegmentTable(object):
+    """One persistent device buffer holding a packed segment table, updated
+    IN PLACE when the table changes (an LR policy such as ``exp`` changes it
+    every step).  The device address never moves - a captured HIP graph of
+    the train step keeps reading the current rates - and no device memory is
+    allocated per step.  Host staging goes through two pinned buffers, each
+    reused only after its previous stream-ordered copy has completed."""
+
+    def __init__(self, device):
+        self.device = device
+        self.dev = None
+        self._raw = None
+        self._pinned = [None, None]
+        self._events = [None, None]
+        self._slot = 0
+
+    def update(self, raw):
+        if raw == self._raw and self.dev is not None:
+            return self.dev
+        n = len(raw)
+        gpu = self.device.type == "cuda"
+        if self.dev is None or self.dev.numel() < n:
+            self.dev = torch.zeros(max(n, 64), dtype=torch.uint8,
+                                   device=self.device)
+            self._pinned = [None, None]
+        if not gpu:
+            self.dev[:n].copy_(torch.frombuffer(bytearray(raw),
+                                                dtype=torch.uint8))
+        else:
+            i = self._slot
+            self._slot ^= 1
+            if self._events[i] is not None:
+                self._events[i].synchronize()
+            if self._pinned[i] is None or self._pinned[i].numel() < n:
+                self._pinned[i] = torch.empty(self.dev.numel(),
+                                              dtype=torch.uint8,
+                                              pin_memory=True)
+            self._pinned[i][:n].copy_(torch.frombuffer(bytearray(raw),
+                                                       dtype=torch.uint8))
+            self.dev[:n].copy_(self._pinned[i][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._events[i] = ev
+        self._raw = raw
+        return self.dev
+
+
+def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
+               table=None):
     """Fused multi-segment SGD (flat float32 buffers).
 
     segs: [(begin, end, lr, weights_decay, l1_vs_l2, gradient_moment)]
       g = grad*gscale + decay*((1-l1)*w + l1*sign(w));  v = moment*v - lr*g;
-      w += v;  w_lp = bfloat16(w)"""
+      w += v;  w_lp = bfloat16(w)
+    table: optional :class:`SegmentTable` the packed segments are kept in."""
     n = w.numel()
     if _gpu(w):
-        st = _segs_tensor(segs, w.device)
+        raw = _pack_sgd_segs(segs)
+        st = table.update(raw) if table is not None else \
+            _segs_tensor(raw, w.device)
         fn = getattr(_lib.lib(), "hvk_sgd4")
         if mom is not None and fn(_p(w), _p(grad), _p(mom), _p(w_lp),
                                   _p(st), len(segs), n, float(gscale),
@@ -838,23 +903,16 @@ SOLVERS = {"momentum": 0, "adagrad": 1, "adadelta": 2, "rprop": 3}
 
 
 def solver_update(w, grad, s1, s2, segs, w_lp=None, gscale=1.0,
-                  zero_grad=False):
+                  zero_grad=False, table=None):
     """Fused multi-segment update with a solver per segment.
 
     segs: [(begin, end, lr, decay, l1_vs_l2, moment, mode, eps, rho)], modes
     in :data:`SOLVERS` (csrc/kernels/elementwise.hip ``solver_kernel``)."""
     n = w.numel()
     if _gpu(w):
-        key = ("solver", tuple(segs), str(w.device))
-        st = _SEG_CACHE.get(key)
-        if st is None:
-            raw = b"".join(struct.pack(
-                "<qqffffifff", int(b), int(e), float(lr), float(d), float(l1),
-                float(m), int(mode), float(eps), float(rho), 0.0)
-                for b, e, lr, d, l1, m, mode, eps, rho in segs)
-            st = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(
-                w.device)
-            _SEG_CACHE[key] = st
+        raw = _pack_solver_segs(segs)
+        st = table.update(raw) if table is not None else \
+            _segs_tensor(raw, w.device)
         _lib_call("hvk_solver", _p(w), _p(grad), _p(s1), _p(s2), _p(w_lp),
                   _p(st), len(segs), n, float(gscale), int(zero_grad), _s(w))
         return w

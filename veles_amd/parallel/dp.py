@@ -76,6 +76,18 @@ class DataParallel(object):
             dist.all_reduce(tensor, op=dist.ReduceOp.MAX)
         return tensor
 
+    def agree(self, flag, src=0):
+        """Rank ``src``'s boolean, on every rank (one tiny broadcast): for
+        decisions taken from a local clock that must be collective."""
+        if self.world_size <= 1:
+            return bool(flag)
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device()) \
+            if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.broadcast(t, src)
+        return bool(t.item())
+
     def broadcast_(self, tensor, src=0):
         if self.world_size > 1:
             dist.broadcast(tensor, src)

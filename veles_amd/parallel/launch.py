@@ -27,7 +27,8 @@ import time
 
 from veles_amd.backends import parse_device_spec
 
-__all__ = ["spawn_ranks", "free_port", "latest_snapshot"]
+__all__ = ["spawn_ranks", "free_port", "latest_snapshot",
+           "check_shared_dir", "snapshot_digest"]
 
 
 def free_port():
@@ -44,6 +45,46 @@ def latest_snapshot(directory):
     if not cands:
         return None
     return max(cands, key=lambda c: os.path.getmtime(os.path.realpath(c)))
+
+
+def snapshot_digest(path):
+    """(size, sha1) of a snapshot file: every rank of a resumed job must
+    have loaded the same bytes (Launcher.initialize checks it)."""
+    import hashlib
+    h = hashlib.sha1()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return os.path.getsize(path), h.hexdigest()
+
+
+def check_shared_dir(directory, nnodes, node_rank, tag, timeout=120.0,
+                     poll=0.2):
+    """Multi-node respawn resumes every node from ``directory``'s newest
+    ``*_current`` snapshot, which only global rank 0 writes: unless the
+    directory is shared by all nodes, nodes != 0 would resume from a stale
+    or no snapshot and diverge (momentum, epoch, loader position).  Each
+    node's launcher drops a marker named after the job ``tag`` and waits
+    until it sees the markers of all ``nnodes`` nodes; raises ValueError
+    when they do not all appear within ``timeout`` seconds."""
+    d = os.path.join(directory, ".veles_nodes", tag)
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "node%d" % node_rank), "w") as f:
+        f.write(socket.gethostname())
+    want = ["node%d" % i for i in range(nnodes)]
+    deadline = time.time() + timeout
+    while True:
+        have = set(os.listdir(d))
+        if all(w in have for w in want):
+            return True
+        if time.time() >= deadline:
+            missing = [w for w in want if w not in have]
+            raise ValueError(
+                "multi-node --respawn needs a snapshot directory shared by "
+                "every node: %s does not show %s after %.0f s (mount it on "
+                "all nodes or drop --respawn)" % (directory,
+                                                  ", ".join(missing), timeout))
+        time.sleep(poll)
 
 
 def _launch(devices, cmd, port, env_extra=None, nnodes=1, node_rank=0,
@@ -115,6 +156,12 @@ def spawn_ranks(spec, cmd, respawn=0, snapshot_dir=None, poll=0.5,
                              (node_rank, nnodes))
         if shrink:
             raise ValueError("--respawn-shrink is single-node only")
+        if respawn > 0:
+            from veles_amd.utils.config import root, get
+            check_shared_dir(
+                snapshot_dir or get(root.common.dirs.snapshots, "."), nnodes,
+                node_rank, "%s_%s" % (master_addr, master_port),
+                float(os.environ.get("VELES_AMD_SHARED_DIR_TIMEOUT", 120)))
     addr = master_addr or "127.0.0.1"
     attempt = 0
     cmd = list(cmd)

@@ -88,10 +88,18 @@ class SnapshotterBase(Unit, metaclass=SnapshotterRegistry):
         if self._skipped_counter < self.interval or self.skip:
             return
         self._skipped_counter = 0
-        if time.time() - self.time < self.time_interval:
+        # the run counter above is identical on every data-parallel rank;
+        # the wall clocks are not, so the time gate is decided by rank 0 and
+        # broadcast: every rank then enters (or skips) the barrier in
+        # export_if_rank0 together (a rank skipping it while another waits
+        # would pair the barrier with the next step's gradient all-reduce)
+        due = time.time() - self.time >= self.time_interval
+        dp = self._dp()
+        if dp is not None and dp.world_size > 1:
+            due = dp.agree(due)
+        if not due:
             return
         self.export_if_rank0()
-        self.time = time.time()
         return True
 
     def stop(self):
@@ -100,13 +108,21 @@ class SnapshotterBase(Unit, metaclass=SnapshotterRegistry):
             self._skipped_counter = 0
             self.export_if_rank0()
 
-    def export_if_rank0(self):
+    def _dp(self):
         from veles_amd.parallel import find_dp
-        dp = find_dp(self)
+        return find_dp(self)
+
+    def export_if_rank0(self):
+        dp = self._dp()
         if dp is not None and dp.world_size > 1:
             dp.barrier()
         if _rank() == 0:
             self.export()
+        if dp is not None and dp.world_size > 1:
+            # nobody starts the next interval before the file is complete,
+            # and every rank restarts its interval clock at the same point
+            dp.barrier()
+        self.time = time.time()
 
     def export(self):
         raise NotImplementedError
