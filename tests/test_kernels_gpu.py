@@ -28,7 +28,8 @@ def close(gpu, ref, tol):
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(17, 1999, 231), (7, 9, 8), (9, 7, 800),
                                    (1, 1, 1), (256, 384, 512),
-                                   (1000, 100, 784)])
+                                   (1000, 100, 784), (640, 512, 1000),
+                                   (384, 640, 64), (200, 136, 96)])
 def test_gemm_layouts(ta, tb, M, N, K):
     a = rnd(K, M) if ta else rnd(M, K)
     b = rnd(N, K, seed=1) if tb else rnd(K, N, seed=1)
