@@ -49,6 +49,39 @@ __device__ __forceinline__ uint4 pack8(const uint16_t* e) {
 }
 
 // ---------------------------------------------------------------- loaders
+// Bits [lo, hi) of a 32-bit mask (clamped to [0, 32)).
+__device__ __forceinline__ uint32_t span_mask(int lo, int hi) {
+  lo = max(lo, 0);
+  hi = min(hi, 32);
+  if (hi <= lo) return 0u;
+  const uint32_t up = hi >= 32 ? 0xffffffffu : ((1u << hi) - 1u);
+  return up & ~((1u << lo) - 1u);
+}
+
+// Branch-free LDS-DMA addressing for the implicit-GEMM A operands ("fast"
+// loaders, kFast): a tile row's pixel offset and the kh / kw taps that stay
+// inside the image (two bit masks) are computed once per block; a lane's tap
+// (kh, kw, channel) once per K tile and shared by all its DMA slots (the
+// 16-B chunk of a lane has the same k in every slot).  Per slot and tile the
+// address is then one add, two mask tests and a select - the per-slot
+// divisions and divergent bounds branches of src() cost conv dgrad 35-45 %
+// and conv forward 15-20 % of its MFMA rate (profiles/gemm_experiments_r2.md
+// §3).
+// the per-slot state type of a fast MN-major B loader (int placeholder else)
+template <class L, bool F> struct DColOf { using type = int; };
+template <class L> struct DColOf<L, true> { using type = typename L::DCol; };
+
+struct DRow { int pix; uint32_t rm, cm; };
+struct DTap { int off; uint32_t kh, kw, ok; };
+// DMA source: p if bit 0 of v is set, else zp (the zero page by default).
+// The empty asm pins the address computation before the select: without it
+// hipcc sinks the 64-bit address math into an exec-mask branch per slot.
+__device__ __forceinline__ const uint16_t* pick_src(
+    const uint16_t* p, uint32_t v, const uint16_t* zp = g_zero8) {
+  asm("" : "+v"(p));
+  return (v & 1u) ? p : zp;
+}
+
 // K-major loader: rows = M (or N) index, 8-element chunks along K.
 struct DenseK {
   const uint16_t* p;
@@ -63,9 +96,11 @@ struct DenseK {
     return c;
   }
   static constexpr bool kGlds = true;
+  static constexpr bool kFast = false;
   __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
-    return (c.ok && k < K) ? c.row + k : g_zero8;
+    // bitwise condition: && made hipcc branch around the address
+    return pick_src(c.row + k, (c.ok != 0) & (k < K));
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -87,13 +122,15 @@ struct DenseMN {
   __device__ void group(int g) { p += (long long)g * gstride; }
   __device__ __forceinline__ Ctx col_ctx(int c) const { return Ctx{c}; }
   static constexpr bool kGlds = true;
+  static constexpr bool kFast = false;
   __device__ bool dma_ok() const {
     return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
   }
   __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int k) const {
-    if (k >= K) return g_zero8;
-    if (cx.c < cols) return p + (long long)k * ld + cx.c;
-    return cx.c == ones_col ? g_ones8 : g_zero8;
+    // branch-free: in range -> data, the ones column -> ones page, else zeros
+    const bool in = k < K;
+    const uint16_t* zp = (in & (cx.c == ones_col)) ? g_ones8 : g_zero8;
+    return pick_src(p + (long long)k * ld + cx.c, in & (cx.c < cols), zp);
   }
   __device__ __forceinline__ uint4 load(const Ctx& cx, int k) const {
     if (k >= K) return zero4();
@@ -140,7 +177,8 @@ struct ConvFwdA {
     return x[c.base + (ih * g.W + iw) * g.C + ch];
   }
   static constexpr bool kGlds = true;
-  __device__ bool dma_ok() const { return vec; }
+  static constexpr bool kFast = true;
+  __device__ bool dma_ok() const { return vec && g.KH <= 32 && g.KW <= 32; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t t, ch, kh, kw;
@@ -150,6 +188,33 @@ struct ConvFwdA {
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
       return g_zero8;
     return x + c.base + (ih * g.W + iw) * g.C + ch;
+  }
+  // fast DMA addressing: x + pix + off, kh in rm, kw in cm
+  __device__ __forceinline__ DRow drow(int m) const {
+    DRow r;
+    uint32_t mm = m < M ? m : 0, n, rem, oh, ow;
+    fdivmod(mm, g.fOHOW, n, rem);
+    fdivmod(rem, g.fOW, oh, ow);
+    const int ih0 = (int)oh * g.sy - g.pt, iw0 = (int)ow * g.sx - g.pl;
+    r.pix = (int)n * g.H * g.W * g.C + coff + (ih0 * g.W + iw0) * g.C;
+    r.rm = m < M ? span_mask(-ih0, g.H - ih0) : 0u;
+    r.cm = span_mask(-iw0, g.W - iw0);
+    return r;
+  }
+  __device__ __forceinline__ DTap dtap(int k) const {
+    DTap t;
+    t.ok = k < K ? 1u : 0u;
+    uint32_t tp, ch, kh, kw;
+    fdivmod(t.ok ? k : 0, g.fCg, tp, ch);
+    fdivmod(tp, g.fKW, kh, kw);
+    t.kh = kh;
+    t.kw = kw;
+    t.off = ((int)kh * g.W + (int)kw) * g.C + (int)ch;
+    return t;
+  }
+  __device__ __forceinline__ const uint16_t* dsrc(const DRow& r,
+                                                  const DTap& t) const {
+    return pick_src(x + (r.pix + t.off), t.ok & (r.rm >> t.kh) & (r.cm >> t.kw));
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -204,12 +269,43 @@ struct ConvDgradA {
     return c.base + (oh * g.OW + ow) * g.OC;
   }
   static constexpr bool kGlds = true;
-  __device__ bool dma_ok() const { return vec; }
+  // stride 1 only (strided dgrad: ConvDgradAStr)
+  static constexpr bool kFast = true;
+  __device__ bool dma_ok() const {
+    return vec && g.sy == 1 && g.sx == 1 && g.KH <= 32 && g.KW <= 32;
+  }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t oc;
     int off = tap(c, k, oc);
     return off < 0 ? g_zero8 : dy + off + oc;
+  }
+  // fast DMA addressing (stride 1): oh = hp - kh, ow = wp - kw
+  __device__ __forceinline__ DRow drow(int m) const {
+    DRow r;
+    uint32_t mm = m < M ? m : 0, n, rem, h, w;
+    fdivmod(mm, g.fHW, n, rem);
+    fdivmod(rem, g.fW, h, w);
+    const int hp = (int)h + g.pt, wp = (int)w + g.pl;
+    r.pix = (int)n * g.OH * g.OW * g.OC + coff + (hp * g.OW + wp) * g.OC;
+    r.rm = m < M ? span_mask(hp - g.OH + 1, hp + 1) : 0u;
+    r.cm = span_mask(wp - g.OW + 1, wp + 1);
+    return r;
+  }
+  __device__ __forceinline__ DTap dtap(int k) const {
+    DTap t;
+    t.ok = k < K ? 1u : 0u;
+    uint32_t tp, oc, kh, kw;
+    fdivmod(t.ok ? k : 0, g.fOCg, tp, oc);
+    fdivmod(tp, g.fKW, kh, kw);
+    t.kh = kh;
+    t.kw = kw;
+    t.off = (int)oc - ((int)kh * g.OW + (int)kw) * g.OC;
+    return t;
+  }
+  __device__ __forceinline__ const uint16_t* dsrc(const DRow& r,
+                                                  const DTap& t) const {
+    return pick_src(dy + (r.pix + t.off), t.ok & (r.rm >> t.kh) & (r.cm >> t.kw));
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -223,11 +319,18 @@ struct ConvDgradA {
   }
 };
 
+// strided dgrad: per-slot src() addressing (the tap must divide by stride)
+struct ConvDgradAStr : ConvDgradA {
+  static constexpr bool kFast = false;
+  __device__ bool dma_ok() const { return vec; }
+};
+
 // scalar-gather variant for OC % 8 != 0 (a separate instantiation: its
 // 8-tap loop pushes the loader struct into scratch, which must not happen
 // to the common vectorised kernels)
 struct ConvDgradAS : ConvDgradA {
   static constexpr bool kGlds = false;
+  static constexpr bool kFast = false;
   __device__ bool dma_ok() const { return false; }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -264,7 +367,48 @@ struct ConvWgradB {
     return c;
   }
   static constexpr bool kGlds = true;
+  // fast DMA addressing needs OH*OW >= BK (a running pixel position wraps
+  // into the next image at most once per K tile); else ConvWgradBGen
+  static constexpr bool kFast = true;
   __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
+  // per DMA slot: the column's tap (fixed) and a running pixel p with
+  // rem = p mod OH*OW and the image base, advanced by BK per tile - one
+  // division per slot and tile (rem -> oh, ow) instead of two, no branches
+  struct DCol { int ch, kh, kw; uint32_t kind; int p, rem, nbase; };
+  __device__ __forceinline__ DCol dcol(int kk, int p, bool zero) const {
+    DCol d;
+    d.kind = zero ? 0u : kk < KK ? 1u : ((ones && kk == KK) ? 2u : 0u);
+    uint32_t t, ch, kh, kw, n, rem;
+    fdivmod(d.kind == 1u ? kk : 0, g.fCg, t, ch);
+    fdivmod(t, g.fKW, kh, kw);
+    d.ch = coff + (int)ch;
+    d.kh = (int)kh - g.pt;
+    d.kw = (int)kw - g.pl;
+    d.p = p;
+    fdivmod((uint32_t)p, g.fOHOW, n, rem);
+    d.rem = (int)rem;
+    d.nbase = (int)n * g.H * g.W * g.C;
+    return d;
+  }
+  __device__ __forceinline__ const uint16_t* dsrc(const DCol& d) const {
+    uint32_t oh, ow;
+    fdivmod((uint32_t)d.rem, g.fOW, oh, ow);
+    const int ih = (int)oh * g.sy + d.kh, iw = (int)ow * g.sx + d.kw;
+    const uint32_t in = (d.p < K ? 1u : 0u);
+    const uint32_t v = in & (d.kind == 1u ? 1u : 0u) &
+                       ((unsigned)ih < (unsigned)g.H ? 1u : 0u) &
+                       ((unsigned)iw < (unsigned)g.W ? 1u : 0u);
+    const uint16_t* zp =
+        (in & (d.kind == 2u ? 1u : 0u)) ? g_ones8 : g_zero8;
+    return pick_src(x + (d.nbase + (ih * g.W + iw) * g.C + d.ch), v, zp);
+  }
+  __device__ __forceinline__ void dnext(DCol& d) const {
+    d.p += BK;
+    d.rem += BK;
+    const bool w = d.rem >= g.OH * g.OW;
+    d.rem -= w ? g.OH * g.OW : 0;
+    d.nbase += w ? g.H * g.W * g.C : 0;
+  }
   __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return g_zero8;
     if (cx.ok == 2) return g_ones8;
@@ -314,6 +458,11 @@ struct ConvWgradB {
 };
 
 
+// wgrad B for OH * OW < BK: per-slot src() addressing
+struct ConvWgradBGen : ConvWgradB {
+  static constexpr bool kFast = false;
+};
+
 // Small-channel convs (C % 8 != 0, groups == 1, e.g. AlexNet conv1 with
 // C = 3): K is re-laid out as (kh, j) with j < RUNP, where j < RUN = KW*C
 // indexes the CONTIGUOUS (kw, c) run of one input row and RUNP pads it to
@@ -334,6 +483,7 @@ struct RunGeom {
 
 struct ConvFwdRunA {
   static constexpr bool kGlds = false;
+  static constexpr bool kFast = false;
   __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
@@ -381,6 +531,7 @@ struct ConvFwdRunA {
 // wgrad B for small-channel convs: MN-major, rows = pixels, cols = (kh, j)
 struct ConvWgradRunB {
   static constexpr bool kGlds = false;
+  static constexpr bool kFast = false;
   __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
@@ -621,15 +772,23 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       constexpr int NIB = BKM ? BN_ / 32 : 4;
       const int w = __builtin_amdgcn_readfirstlane(wid);
       typename LA::Ctx da[NIA];
+      DRow fa[NIA];  // fast A loaders (K-major): per-slot row state
       typename LB::Ctx db[NIB];
+      constexpr bool FB = !BKM && LB::kFast;  // fast MN-major B (wgrad)
+      typename DColOf<LB, FB>::type fb[NIB];
       int ka[NIA], kb[NIB];
+      // the lane's chunk offset along K: the same in every A slot
+      const int kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
       // MN-major B at BN = 64: the DMA image keeps the 256-B rows of the
       // 128-wide layout; the chunks of columns >= 64 read the zero page
       bool bz[NIB];
 #pragma unroll
       for (int i = 0; i < NIA; ++i) {
         const int I = w * NIA + i;
-        if constexpr (AK) {
+        if constexpr (AK && LA::kFast) {
+          fa[i] = la.drow(m0 + 8 * I + (lane >> 3));
+          ka[i] = kc;
+        } else if constexpr (AK) {
           int row = 8 * I + (lane >> 3);
           int c = (lane & 7) ^ ((lane >> 3) & 7);
           da[i] = la.row_ctx(m0 + row);
@@ -653,24 +812,49 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
           int hkv = ((lane >> 4) & 3) | (((I >> 1) & 1) << 2);
           int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
           bz[i] = BN_ < 128 && 8 * c >= BN_;
-          db[i] = lb.col_ctx(n0 + (bz[i] ? 0 : 8 * c));
           kb[i] = 4 * I + (lane >> 4);
+          if constexpr (FB)
+            fb[i] = lb.dcol(n0 + 8 * c, kbeg + kb[i], bz[i]);
+          else
+            db[i] = lb.col_ctx(n0 + (bz[i] ? 0 : 8 * c));
         }
         if constexpr (BKM) bz[i] = false;
       }
       auto issue = [&](int k0, uint16_t* sA, uint16_t* sB) {
+        if constexpr (AK && LA::kFast) {
+          const DTap tp = la.dtap(k0 + kc);
 #pragma unroll
-        for (int i = 0; i < NIA; ++i)
-          __builtin_amdgcn_global_load_lds(
-              (const void*)la.src(da[i], k0 + ka[i]),
-              (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
-              16, 0, 0);
+          for (int i = 0; i < NIA; ++i)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)la.dsrc(fa[i], tp),
+                (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
+                16, 0, 0);
+        } else {
 #pragma unroll
-        for (int i = 0; i < NIB; ++i)
-          __builtin_amdgcn_global_load_lds(
-              (const void*)(bz[i] ? g_zero8 : lb.src(db[i], k0 + kb[i])),
-              (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 512),
-              16, 0, 0);
+          for (int i = 0; i < NIA; ++i)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)la.src(da[i], k0 + ka[i]),
+                (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
+                16, 0, 0);
+        }
+        if constexpr (FB) {
+          // k0 advances by BK per call: the slot state tracks it
+#pragma unroll
+          for (int i = 0; i < NIB; ++i) {
+            __builtin_amdgcn_global_load_lds(
+                (const void*)lb.dsrc(fb[i]),
+                (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 512),
+                16, 0, 0);
+            lb.dnext(fb[i]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NIB; ++i)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(bz[i] ? g_zero8 : lb.src(db[i], k0 + kb[i])),
+                (__attribute__((address_space(3))) void*)(sB + (w * NIB + i) * 512),
+                16, 0, 0);
+        }
       };
       issue(kbeg, smem, smem + 2 * SA);
       for (int kt = 0; kt < nk; ++kt) {
@@ -1013,6 +1197,12 @@ HVK_API int hvk_conv_dgrad_t(const void* dY, const void* Wt, void* dX, int N,
     return (int)launch<ConvDgradAS, true, DenseK, true>(ls, lb, e, M, g.Cg,
                                                         K, 1, groups, s);
   }
+  if (sy != 1 || sx != 1 || KH > 32 || KW > 32) {
+    ConvDgradAStr ls;
+    static_cast<ConvDgradA&>(ls) = la;
+    return (int)launch<ConvDgradAStr, true, DenseK, true>(ls, lb, e, M, g.Cg,
+                                                          K, 1, groups, s);
+  }
   return (int)launch<ConvDgradA, true, DenseK, true>(la, lb, e, M, g.Cg, K,
                                                      1, groups, s);
 }
@@ -1035,6 +1225,12 @@ HVK_API int hvk_conv_wgrad(const void* X, const void* dY, float* dW, int N,
   if (dbias) {
     e.ones_col = KK;
     e.bias_grad = dbias;
+  }
+  if (OH * OW < BK) {
+    ConvWgradBGen lg;
+    static_cast<ConvWgradB&>(lg) = lb;
+    return (int)launch<DenseMN, false, ConvWgradBGen, false>(
+        la, lg, e, g.OCg, Nk, P, splits, groups, s);
   }
   return (int)launch<DenseMN, false, ConvWgradB, false>(la, lb, e, g.OCg, Nk, P,
                                                         splits, groups, s);
