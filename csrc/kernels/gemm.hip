@@ -49,38 +49,16 @@ __device__ __forceinline__ uint4 pack8(const uint16_t* e) {
 }
 
 // ---------------------------------------------------------------- loaders
-// Bits [lo, hi) of a 32-bit mask (clamped to [0, 32)).
-__device__ __forceinline__ uint32_t span_mask(int lo, int hi) {
-  lo = max(lo, 0);
-  hi = min(hi, 32);
-  if (hi <= lo) return 0u;
-  const uint32_t up = hi >= 32 ? 0xffffffffu : ((1u << hi) - 1u);
-  return up & ~((1u << lo) - 1u);
+// DMA source: p if bit 0 of v is set, else zp (the zero page by default)
+// - see hvk::pick_ptr in conv_geom.h.
+__device__ __forceinline__ const uint16_t* pick_src(
+    const uint16_t* p, uint32_t v, const uint16_t* zp = g_zero8) {
+  return pick_ptr(p, v, zp);
 }
 
-// Branch-free LDS-DMA addressing for the implicit-GEMM A operands ("fast"
-// loaders, kFast): a tile row's pixel offset and the kh / kw taps that stay
-// inside the image (two bit masks) are computed once per block; a lane's tap
-// (kh, kw, channel) once per K tile and shared by all its DMA slots (the
-// 16-B chunk of a lane has the same k in every slot).  Per slot and tile the
-// address is then one add, two mask tests and a select - the per-slot
-// divisions and divergent bounds branches of src() cost conv dgrad 35-45 %
-// and conv forward 15-20 % of its MFMA rate (profiles/gemm_experiments_r2.md
-// §3).
 // the per-slot state type of a fast MN-major B loader (int placeholder else)
 template <class L, bool F> struct DColOf { using type = int; };
 template <class L> struct DColOf<L, true> { using type = typename L::DCol; };
-
-struct DRow { int pix; uint32_t rm, cm; };
-struct DTap { int off; uint32_t kh, kw, ok; };
-// DMA source: p if bit 0 of v is set, else zp (the zero page by default).
-// The empty asm pins the address computation before the select: without it
-// hipcc sinks the 64-bit address math into an exec-mask branch per slot.
-__device__ __forceinline__ const uint16_t* pick_src(
-    const uint16_t* p, uint32_t v, const uint16_t* zp = g_zero8) {
-  asm("" : "+v"(p));
-  return (v & 1u) ? p : zp;
-}
 
 // K-major loader: rows = M (or N) index, 8-element chunks along K.
 struct DenseK {
@@ -189,32 +167,14 @@ struct ConvFwdA {
       return g_zero8;
     return x + c.base + (ih * g.W + iw) * g.C + ch;
   }
-  // fast DMA addressing: x + pix + off, kh in rm, kw in cm
+  // fast DMA addressing (conv_geom.h): x + pix + off, kh in rm, kw in cm
   __device__ __forceinline__ DRow drow(int m) const {
-    DRow r;
-    uint32_t mm = m < M ? m : 0, n, rem, oh, ow;
-    fdivmod(mm, g.fOHOW, n, rem);
-    fdivmod(rem, g.fOW, oh, ow);
-    const int ih0 = (int)oh * g.sy - g.pt, iw0 = (int)ow * g.sx - g.pl;
-    r.pix = (int)n * g.H * g.W * g.C + coff + (ih0 * g.W + iw0) * g.C;
-    r.rm = m < M ? span_mask(-ih0, g.H - ih0) : 0u;
-    r.cm = span_mask(-iw0, g.W - iw0);
-    return r;
+    return fwd_drow(g, M, coff, m);
   }
-  __device__ __forceinline__ DTap dtap(int k) const {
-    DTap t;
-    t.ok = k < K ? 1u : 0u;
-    uint32_t tp, ch, kh, kw;
-    fdivmod(t.ok ? k : 0, g.fCg, tp, ch);
-    fdivmod(tp, g.fKW, kh, kw);
-    t.kh = kh;
-    t.kw = kw;
-    t.off = ((int)kh * g.W + (int)kw) * g.C + (int)ch;
-    return t;
-  }
+  __device__ __forceinline__ DTap dtap(int k) const { return fwd_dtap(g, K, k); }
   __device__ __forceinline__ const uint16_t* dsrc(const DRow& r,
                                                   const DTap& t) const {
-    return pick_src(x + (r.pix + t.off), t.ok & (r.rm >> t.kh) & (r.cm >> t.kw));
+    return pick_src(x + (r.pix + t.off), tap_ok(r, t));
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -280,32 +240,16 @@ struct ConvDgradA {
     int off = tap(c, k, oc);
     return off < 0 ? g_zero8 : dy + off + oc;
   }
-  // fast DMA addressing (stride 1): oh = hp - kh, ow = wp - kw
+  // fast DMA addressing (stride 1, conv_geom.h): oh = hp - kh, ow = wp - kw
   __device__ __forceinline__ DRow drow(int m) const {
-    DRow r;
-    uint32_t mm = m < M ? m : 0, n, rem, h, w;
-    fdivmod(mm, g.fHW, n, rem);
-    fdivmod(rem, g.fW, h, w);
-    const int hp = (int)h + g.pt, wp = (int)w + g.pl;
-    r.pix = (int)n * g.OH * g.OW * g.OC + coff + (hp * g.OW + wp) * g.OC;
-    r.rm = m < M ? span_mask(hp - g.OH + 1, hp + 1) : 0u;
-    r.cm = span_mask(wp - g.OW + 1, wp + 1);
-    return r;
+    return dgrad_drow(g, M, coff, m);
   }
   __device__ __forceinline__ DTap dtap(int k) const {
-    DTap t;
-    t.ok = k < K ? 1u : 0u;
-    uint32_t tp, oc, kh, kw;
-    fdivmod(t.ok ? k : 0, g.fOCg, tp, oc);
-    fdivmod(tp, g.fKW, kh, kw);
-    t.kh = kh;
-    t.kw = kw;
-    t.off = (int)oc - ((int)kh * g.OW + (int)kw) * g.OC;
-    return t;
+    return dgrad_dtap(g, K, k);
   }
   __device__ __forceinline__ const uint16_t* dsrc(const DRow& r,
                                                   const DTap& t) const {
-    return pick_src(dy + (r.pix + t.off), t.ok & (r.rm >> t.kh) & (r.cm >> t.kw));
+    return pick_src(dy + (r.pix + t.off), tap_ok(r, t));
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();

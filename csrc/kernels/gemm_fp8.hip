@@ -62,8 +62,10 @@ struct Dense8 {
     c.row = p + (long long)(c.ok ? r : 0) * ld;
     return c;
   }
+  static constexpr bool kFast = false;
   __device__ __forceinline__ const uint8_t* src(const Ctx& c, int k) const {
-    return (c.ok && k < K) ? c.row + k : g_zero16;
+    // bitwise condition + pinned address: no exec-mask branch per slot
+    return pick_ptr(c.row + k, (c.ok != 0) & (k < K), g_zero16);
   }
 };
 
@@ -95,6 +97,16 @@ struct ConvFwdA8 {
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W)
       return g_zero16;
     return x + c.base + (ih * g.W + iw) * g.C + ch;
+  }
+  // branch-free DMA addressing (conv_geom.h), as the bf16 ConvFwdA
+  static constexpr bool kFast = true;
+  __device__ __forceinline__ DRow drow(int m) const {
+    return fwd_drow(g, M, coff, m);
+  }
+  __device__ __forceinline__ DTap dtap(int k) const { return fwd_dtap(g, K, k); }
+  __device__ __forceinline__ const uint8_t* dsrc(const DRow& r,
+                                                 const DTap& t) const {
+    return pick_ptr(x + (r.pix + t.off), tap_ok(r, t), g_zero16);
   }
 };
 
@@ -132,6 +144,22 @@ struct ConvDgradA8 {
     if (oh >= g.OH || ow >= g.OW) return g_zero16;
     return dy + c.base + (oh * g.OW + ow) * g.OC + oc;
   }
+  // branch-free DMA addressing for stride 1 (strided: ConvDgradA8Str)
+  static constexpr bool kFast = true;
+  __device__ __forceinline__ DRow drow(int m) const {
+    return dgrad_drow(g, M, coff, m);
+  }
+  __device__ __forceinline__ DTap dtap(int k) const {
+    return dgrad_dtap(g, K, k);
+  }
+  __device__ __forceinline__ const uint8_t* dsrc(const DRow& r,
+                                                 const DTap& t) const {
+    return pick_ptr(dy + (r.pix + t.off), tap_ok(r, t), g_zero16);
+  }
+};
+
+struct ConvDgradA8Str : ConvDgradA8 {
+  static constexpr bool kFast = false;
 };
 
 // ---------------------------------------------------------------- epilogue
@@ -259,14 +287,20 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
   constexpr int NIB = SB / (NTHR * 16);   // 4 (BN 128) or 2 (BN 64)
   const int w = __builtin_amdgcn_readfirstlane(wid);
   typename LA::Ctx da[NIA];
+  DRow fa[NIA];  // fast A loaders: per-slot row state
   typename LB::Ctx db[NIB];
   int ka[NIA], kb[NIB];
+  // the lane's chunk offset along K (row & 7 == (lane >> 3) & 7 in every slot)
+  const int kc = 16 * ((lane & 7) ^ ((lane >> 3) & 7));
 #pragma unroll
   for (int i = 0; i < NIA; ++i) {
     const int I = w * NIA + i;
     const int row = 8 * I + (lane >> 3);
-    da[i] = la.row_ctx(m0 + row);
-    ka[i] = 16 * ((lane & 7) ^ (row & 7));
+    if constexpr (LA::kFast)
+      fa[i] = la.drow(m0 + row);
+    else
+      da[i] = la.row_ctx(m0 + row);
+    ka[i] = kc;
   }
 #pragma unroll
   for (int i = 0; i < NIB; ++i) {
@@ -276,12 +310,22 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
     kb[i] = 16 * ((lane & 7) ^ (row & 7));
   }
   auto issue = [&](int k0, uint8_t* sA, uint8_t* sB) {
+    if constexpr (LA::kFast) {
+      const DTap tp = la.dtap(k0 + kc);
 #pragma unroll
-    for (int i = 0; i < NIA; ++i)
-      __builtin_amdgcn_global_load_lds(
-          (const void*)la.src(da[i], k0 + ka[i]),
-          (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 1024),
-          16, 0, 0);
+      for (int i = 0; i < NIA; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)la.dsrc(fa[i], tp),
+            (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 1024),
+            16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NIA; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)la.src(da[i], k0 + ka[i]),
+            (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 1024),
+            16, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < NIB; ++i)
       __builtin_amdgcn_global_load_lds(
@@ -586,7 +630,9 @@ HVK_API int hvk_conv_fwd_fp8(const void* X, const void* Wt, const float* bias,
                              hipStream_t s) {
   ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
   const int M = N * OH * OW, K = KH * KW * g.Cg;
-  if ((g.Cg & 15) || (C & 15) || !al16(X) || !al16(Wt)) return -3;
+  if ((g.Cg & 15) || (C & 15) || !al16(X) || !al16(Wt) || KH > 32 ||
+      KW > 32)
+    return -3;
   ConvFwdA8 la{(const uint8_t*)X, g, M, K, 0};
   Dense8 lb{(const uint8_t*)Wt, (long long)g.OCg * K, g.OCg, K, K};
   Epi8 e = make_epi8(Y, OC, M, g.OCg, bias, act, nullptr, 0, 0, sxs, sws,
@@ -612,5 +658,10 @@ HVK_API int hvk_conv_dgrad_fp8(const void* dY, const void* Wt, void* dX,
   Epi8 e = make_epi8(dX, C, M, g.Cg, nullptr, 0, aux, C, aux_act, sds, sws,
                      hist, fmax_dy, fmax_w);
   e.gcol = g.Cg;
+  if (sy != 1 || sx != 1 || KH > 32 || KW > 32) {
+    ConvDgradA8Str ls;
+    static_cast<ConvDgradA8&>(ls) = la;
+    return (int)dispatch8(fdy, fw, ls, lb, e, M, g.Cg, K, groups, s);
+  }
   return (int)dispatch8(fdy, fw, la, lb, e, M, g.Cg, K, groups, s);
 }

@@ -203,10 +203,12 @@ def gemm(a8, sa, b8, sb, bias=None, act=0, aux=None, aux_act=0, out=None):
                     bias=bias, act=act, aux=aux, aux_act=aux_act, out=out)
 
 
-def fp8_conv_ok(C, OC, groups):
-    """Channel counts the fp8 implicit-GEMM loaders take (16-B chunks)."""
+def fp8_conv_ok(C, OC, groups, KH=1, KW=1):
+    """Geometry the fp8 implicit-GEMM loaders take: 16-B channel chunks, and
+    kernels of at most 32 taps per axis (the tap bit masks of the branch-free
+    forward addressing, conv_geom.h)."""
     return C % 16 == 0 and (C // groups) % 16 == 0 and OC % 16 == 0 and \
-        (OC // groups) % 16 == 0
+        (OC // groups) % 16 == 0 and KH <= 32 and KW <= 32
 
 
 def conv_fwd(x8, sx, w8, sw, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
