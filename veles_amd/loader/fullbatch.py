@@ -36,6 +36,13 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         self.validation_ratio = kwargs.get("validation_ratio", None)
         self.on_device = kwargs.get("on_device", True)
         self._affine = None
+        # export_affine (StandardWorkflow.link_meandispnorm): serve the raw
+        # data and publish the per-feature normalisation as ``mean`` /
+        # ``rdisp`` for a separate MeanDispNormalizer unit, as the
+        # reference's image loaders do, instead of folding it into the gather
+        self.export_affine = kwargs.get("export_affine", False)
+        self.mean = Array()
+        self.rdisp = Array()
 
     def init_unpickled(self):
         super().init_unpickled()
@@ -115,6 +122,7 @@ class FullBatchLoader(Loader, IFullBatchLoader):
             rdisp = numpy.broadcast_to(numpy.asarray(rdisp, numpy.float32),
                                        (feat,)).copy()
             self._affine = (mean, rdisp)
+            self._export_affine()
         else:
             # non-affine normalizer: normalise the resident data once
             d = data.astype(numpy.float32)
@@ -134,6 +142,15 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         feat = int(numpy.prod(self.sample_shape))
         self._affine = tuple(numpy.broadcast_to(
             numpy.asarray(a, numpy.float32), (feat,)).copy() for a in aff)
+        self._export_affine()
+
+    def _export_affine(self):
+        if not self.export_affine or self._affine is None:
+            return
+        shape = self.sample_shape
+        self.mean.reset(self._affine[0].reshape(shape).copy())
+        self.rdisp.reset(self._affine[1].reshape(shape).copy())
+        self._affine = None  # the gather serves raw samples
 
     def normalize_minibatch(self):
         pass  # folded into the gather

@@ -113,8 +113,10 @@ class DecisionGD(DecisionBase):
         self.epoch_n_err[cls] = m[0]
         self.epoch_n_err_pt[cls] = 100.0 * m[0] / n
         self.epoch_loss[cls] = m[1] / n
-        if cls == VALID and hasattr(self.evaluator, "take_confusion"):
-            self.evaluator.take_confusion()
+        if hasattr(self.evaluator, "take_confusion"):
+            self.evaluator.take_confusion(
+                cls, shown=cls == VALID or (cls == TRAIN and
+                                            self.class_lengths[VALID] == 0))
 
     def on_epoch_ended(self):
         has_valid = self.class_lengths[VALID] > 0

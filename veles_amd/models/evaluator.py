@@ -66,7 +66,11 @@ class EvaluatorSoftmax(EvaluatorBase):
         super().__init__(workflow, **kwargs)
         self.demand("labels")
         self.logits = None
+        # per class (test / validation / train) [true][predicted] counts of
+        # the last finished pass over that class; ``confusion_matrix`` shows
+        # the validation one (train when there is no validation set)
         self.confusion_matrix = Array()
+        self.confusion_matrixes = [None, None, None]
 
     def init_unpickled(self):
         super().init_unpickled()
@@ -88,20 +92,30 @@ class EvaluatorSoftmax(EvaluatorBase):
         conf = None
         if self.compute_confusion_matrix:
             if self.confusion_ is None:
-                self.confusion_ = torch.zeros(C, C, dtype=torch.int32,
+                self.confusion_ = torch.zeros(3, C, C, dtype=torch.int32,
                                               device=self.torch_device)
-            conf = self.confusion_
+            conf = self.confusion_[self.minibatch_class]
         gb = max(int(self.global_batch_size), 1)
         ops.softmax_ce(logits.reshape(B, C), self.labels.devmem,
                        scale=1.0 / gb if self.mean else 1.0, err=err,
                        metrics=m[self.minibatch_class], confusion=conf)
 
-    def take_confusion(self):
+    def take_confusion(self, cls, shown=True):
+        """The confusion counts of class ``cls`` since its last take (summed
+        over the data-parallel group); ``shown`` also publishes them as
+        ``confusion_matrix``.  Called by the decision at every class end."""
         if self.confusion_ is None:
             return None
-        c = self.confusion_.cpu().numpy().copy()
-        self.confusion_.zero_()
-        self.confusion_matrix.reset(c)
+        t = self.confusion_[cls]
+        from veles_amd.parallel import find_dp
+        dp = find_dp(self)
+        if dp is not None and dp.world_size > 1:
+            dp.all_reduce_sum(t)
+        c = t.cpu().numpy().copy()
+        t.zero_()
+        self.confusion_matrixes[cls] = c
+        if shown:
+            self.confusion_matrix.reset(c)
         return c
 
 

@@ -15,8 +15,9 @@ loaders block for the next request); otherwise one pass over the TEST set.
 from __future__ import annotations
 
 from veles_amd.models.standard_workflow import StandardWorkflow
+from veles_amd.units import Unit
 
-__all__ = ["ForwardWorkflow"]
+__all__ = ["ForwardWorkflow", "ForwardWorkflowExtractor"]
 
 
 class ForwardWorkflow(StandardWorkflow):
@@ -81,3 +82,55 @@ class ForwardWorkflow(StandardWorkflow):
                     dst.bias.reset(src.bias.mem.copy())
         fwd.loader.derive_from(trained.loader)
         return fwd
+
+
+class ForwardWorkflowExtractor(Unit):
+    """``StandardWorkflow.link_result_unit`` (reference docs
+    manualrst_veles_workflow_creation.rst:520-533): keeps an inference
+    workflow extracted from the training one - once training completes, or
+    at every epoch that improved the validation error
+    (``on_improvement=True``) - and optionally exports it as a libVeles-style
+    package (``package=path.zip|.tar.gz``, read by the native runtime).
+
+    Linked after the decision; the unit decides from ``decision.complete`` /
+    ``decision.improved`` itself, so it can sit on any branch of the cycle.
+    """
+    MAPPING = "forward_workflow_extractor"
+
+    def __init__(self, workflow, **kwargs):
+        kwargs.setdefault("view_group", "SERVICE")
+        super().__init__(workflow, **kwargs)
+        self.loader_name = kwargs.get("loader_name")
+        self.loader_config = kwargs.get("loader_config")
+        self.result_unit_factory = kwargs.get("result_unit_factory")
+        self.result_unit_config = kwargs.get("result_unit_config")
+        self.package = kwargs.get("package")
+        self.precision = kwargs.get("precision", 32)
+        self.on_improvement = kwargs.get("on_improvement", False)
+        self.extractions = 0
+        self.demand("decision")
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.forward_workflow_ = None
+
+    @property
+    def forward_workflow(self):
+        return self.forward_workflow_
+
+    def run(self):
+        d = self.decision
+        due = bool(d.improved) if self.on_improvement else bool(d.complete)
+        if not due:
+            return
+        wf = self.workflow
+        self.forward_workflow_ = wf.extract_forward_workflow(
+            self.loader_name, self.loader_config, self.result_unit_factory,
+            self.result_unit_config)
+        self.extractions += 1
+        if self.package:
+            self.forward_workflow_.package_export(
+                self.package, precision=self.precision,
+                archive_format="zip" if self.package.endswith(".zip")
+                else "tgz")
+            self.info("Exported the forward workflow to %s", self.package)

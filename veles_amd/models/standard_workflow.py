@@ -51,6 +51,7 @@ from veles_amd.models.channel_splitting import (
 from veles_amd.models.cutter import Cutter, GDCutter
 from veles_amd.models.deconv import Deconv, GDDeconv
 from veles_amd.models.rprop_all2all import RPropAll2All
+from veles_amd.models.standard_workflow_links import LinkBuilders
 from veles_amd.models.weights_zerofilling import GDZeroFiller, ZeroFiller
 from veles_amd.plumbing import Repeater
 from veles_amd.snapshotter import SnapshotterRegistry, SnapshotterToFile
@@ -146,11 +147,13 @@ def _cfg(v):
     return fix_contents(v) if isinstance(v, Config) else (v or {})
 
 
-class StandardWorkflow(AcceleratedWorkflow):
+class StandardWorkflow(LinkBuilders, AcceleratedWorkflow):
     """kwargs: layers | mcdnnic_topology (+mcdnnic_parameters), loader_name,
     loader_config, loss_function ("softmax"|"mse"), decision_config,
     snapshotter_config (None disables), lr_adjuster_config, evaluator_config,
-    testing."""
+    testing; configs of the optional builders (standard_workflow_links.py):
+    image_saver_config, data_saver_config, publisher_config,
+    result_unit_config."""
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
@@ -171,6 +174,9 @@ class StandardWorkflow(AcceleratedWorkflow):
         self.lr_adjuster_config = kwargs.get("lr_adjuster_config")
         self.evaluator_config = dict(_cfg(kwargs.get("evaluator_config")))
         self.testing = kwargs.get("testing", False)
+        for k in ("image_saver_config", "data_saver_config",
+                  "publisher_config", "result_unit_config"):
+            setattr(self, k, dict(_cfg(kwargs.get(k))))
         self.forwards = []
         self.gds = []
         self.snapshotter = None

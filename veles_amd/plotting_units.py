@@ -10,7 +10,23 @@ from veles_amd.plotter import Plotter
 
 __all__ = ["AccumulatingPlotter", "MatrixPlotter", "ImagePlotter",
            "ImmediatePlotter", "Histogram", "AutoHistogramPlotter",
-           "MultiHistogram", "TableMaxMin", "to_numpy"]
+           "MultiHistogram", "TableMaxMin", "Weights2D", "to_numpy",
+           "unit_weights"]
+
+# scalar reductions an AccumulatingPlotter can apply to an array input
+_REDUCE = {"max": numpy.max, "min": numpy.min, "mean": numpy.mean,
+           "norm": lambda a: float(numpy.sqrt(numpy.sum(a * a)))}
+
+
+def unit_weights(unit, name="weights"):
+    """The live weights of a forward unit: the device master copy of the
+    flat parameter store when it exists (``Array.mem`` is only synced for
+    snapshots), else the unit's Array."""
+    p = getattr(unit, {"weights": "_pw_", "bias": "_pb_"}.get(name, ""),
+                None)
+    if p is not None and p.master is not None:
+        return p.master
+    return getattr(unit, name)
 
 
 def to_numpy(v):
@@ -42,9 +58,15 @@ class AccumulatingPlotter(Plotter):
 
     def run(self):
         v = self.input
-        if self.input_field is not None:
-            v = v[self.input_field]
-        self.values.append(float(numpy.asarray(to_numpy(v)).reshape(-1)[0]))
+        if self.input_field in _REDUCE:
+            # a statistic of an array (min / max of an output, weight norm)
+            a = numpy.asarray(to_numpy(v), dtype=numpy.float64).reshape(-1)
+            self.values.append(float(_REDUCE[self.input_field](a)))
+        else:
+            if self.input_field is not None:
+                v = v[self.input_field]
+            self.values.append(float(numpy.asarray(
+                to_numpy(v)).reshape(-1)[0]))
         super().run()
 
     def draw(self, fig):
@@ -93,6 +115,12 @@ class ImagePlotter(Plotter):
         a = to_numpy(self.input)[:self.limit]
         if self.sample_shape is not None:
             a = a.reshape((len(a),) + tuple(self.sample_shape))
+        elif a.ndim == 2:
+            # flat samples (FC outputs): zero-padded square images
+            side = int(numpy.ceil(numpy.sqrt(a.shape[1])))
+            sq = numpy.zeros((len(a), side * side), a.dtype)
+            sq[:, :a.shape[1]] = a
+            a = sq.reshape(len(a), side, side)
         self.images_ = a
 
     def draw(self, fig):
@@ -205,8 +233,8 @@ class TableMaxMin(Plotter):
     def render(self):
         import os
         os.makedirs(self.directory, exist_ok=True)
-        fn = os.path.join(self.directory, "%s%s.txt" % (self.name_prefix,
-                                                       self.name))
+        fn = os.path.join(self.directory, "%s%s.txt" % (
+            self.name_prefix, self.name.replace(" ", "_")))
         with open(fn, "w") as f:
             f.write("%-24s %12s %12s %12s %12s\n" % ("name", "max", "min",
                                                       "mean", "std"))
@@ -214,3 +242,85 @@ class TableMaxMin(Plotter):
                 f.write("%-24s %12.6g %12.6g %12.6g %12.6g\n" % row)
         if fn not in self.files:
             self.files.append(fn)
+
+
+class Weights2D(Plotter):
+    """The first ``limit`` kernels / neurons of a layer's weights as images
+    (Znicz ``Weights2D``, ``link_weights_plotter``): conv kernels
+    [OC][KH][KW][C] are drawn as KHxKW(xC) images, fully-connected rows as
+    ``sample_shape`` images (the layer's input sample shape by default).
+
+    ``similar=True`` orders the neurons so that the most similar pairs
+    (cosine similarity of their weight rows) are adjacent - the
+    ``link_similar_weights_plotter`` view used to spot duplicated units.
+    The source is a forward unit; its live device weights are read at draw
+    time (``unit_weights``)."""
+    MAPPING = "weights_2d"
+
+    def __init__(self, workflow, **kwargs):
+        super().__init__(workflow, **kwargs)
+        self.limit = kwargs.get("limit", 64)
+        self.sample_shape = kwargs.get("sample_shape")
+        self.similar = kwargs.get("similar", False)
+        self.weights_name = kwargs.get("weights_name", "weights")
+        self.source_unit = kwargs.get("source_unit")
+
+    def collect(self):
+        w = numpy.asarray(to_numpy(unit_weights(self.source_unit,
+                                                self.weights_name)))
+        rows = w.reshape(w.shape[0], -1)
+        if self.similar and len(rows) > 1:
+            rows = rows[similarity_order(rows)]
+        rows = rows[:self.limit]
+        if w.ndim == 4:
+            imgs = rows.reshape((len(rows),) + w.shape[1:])
+        else:
+            shape = self.sample_shape
+            if shape is None:
+                inp = getattr(self.source_unit, "input", None)
+                shp = getattr(inp, "shape", None)
+                shape = tuple(shp[1:]) if shp is not None and \
+                    int(numpy.prod(shp[1:])) == rows.shape[1] else None
+            if shape is None:
+                side = int(numpy.ceil(numpy.sqrt(rows.shape[1])))
+                pad = numpy.zeros((len(rows), side * side), rows.dtype)
+                pad[:, :rows.shape[1]] = rows
+                rows, shape = pad, (side, side)
+            imgs = rows.reshape((len(rows),) + tuple(shape))
+        self.images_ = imgs
+
+    def draw(self, fig):
+        a = self.images_
+        n = len(a)
+        cols = int(numpy.ceil(numpy.sqrt(n)))
+        rows = int(numpy.ceil(n / max(cols, 1)))
+        for i in range(n):
+            ax = fig.add_subplot(rows, cols, i + 1)
+            img = a[i]
+            if img.ndim == 3 and img.shape[-1] not in (1, 3):
+                img = img[..., 0]
+            if img.ndim == 3 and img.shape[-1] == 1:
+                img = img[..., 0]
+            lo, hi = float(img.min()), float(img.max())
+            ax.imshow((img - lo) / (hi - lo + 1e-12), cmap="gray")
+            ax.axis("off")
+
+
+def similarity_order(rows):
+    """A greedy chain through the rows: start from the most similar pair
+    (cosine), then always append the row most similar to the chain's end."""
+    r = numpy.asarray(rows, dtype=numpy.float64)
+    nrm = numpy.linalg.norm(r, axis=1, keepdims=True)
+    u = r / numpy.where(nrm > 0, nrm, 1.0)
+    sim = u @ u.T
+    numpy.fill_diagonal(sim, -numpy.inf)
+    i, j = numpy.unravel_index(int(numpy.argmax(sim)), sim.shape)
+    order = [int(i), int(j)]
+    used = numpy.zeros(len(r), bool)
+    used[order] = True
+    while len(order) < len(r):
+        cand = numpy.where(used, -numpy.inf, sim[order[-1]])
+        k = int(numpy.argmax(cand))
+        order.append(k)
+        used[k] = True
+    return numpy.asarray(order)
