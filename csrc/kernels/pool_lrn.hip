@@ -736,7 +736,335 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_kernel(
     }
   }
 }
+// ---------------------------------------------------------------------------
+// Non-overlapping 2 x 2 / stride-2 pooling (VGG) WITHOUT an argmax tensor.
+// Forward: one thread per output pixel x 8 channels, four 16-B loads, one
+// 16-B store.  Backward recomputes the window's choice from the forward input
+// (the first maximum in window order, as the forward took it) and writes all
+// four input pixels of the window: it reads x + dy instead of dy + an int32
+// argmax as large as x / 2, and the forward writes no argmax at all.  Even H
+// and W only (every input pixel belongs to exactly one window).
+template <int MODE>
+__global__ __launch_bounds__(256) void pool2_fwd_kernel(
+    const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N, int H,
+    int W, int C, FastDiv fCV, FastDiv fOW, FastDiv fOH) {
+  const int CV = C >> 3, OH = H >> 1, OW = W >> 1;
+  const int total = N * OH * OW * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
+    const long long b = (((long long)nu * H + 2 * ohu) * W + 2 * owu) * C +
+                        cvu * 8;
+    uint4 v[4];
+    v[0] = *(const uint4*)(x + b);
+    v[1] = *(const uint4*)(x + b + C);
+    v[2] = *(const uint4*)(x + b + (long long)W * C);
+    v[3] = *(const uint4*)(x + b + (long long)W * C + C);
+    uint16_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float best = 0.f, key = -INFINITY, sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f = bf2f(((const uint16_t*)&v[i])[q]);
+        sum += f;
+        const float kf = MODE == POOL_MAXABS ? fabsf(f) : f;
+        if (i == 0 || kf > key) { key = kf; best = f; }
+      }
+      o[q] = f2bf(MODE == POOL_AVG ? 0.25f * sum : best);
+    }
+    *(uint4*)(y + (long long)pix * C + cvu * 8) = *(const uint4*)o;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void pool2_bwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+    uint16_t* __restrict__ dx, int N, int H, int W, int C,
+    const uint16_t* aux, int aux_act, FastDiv fCV, FastDiv fOW,
+    FastDiv fOH) {
+  const int CV = C >> 3, OH = H >> 1, OW = W >> 1;
+  const int total = N * OH * OW * CV;
+  const bool aux_x = aux == x;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
+    const long long b = (((long long)nu * H + 2 * ohu) * W + 2 * owu) * C +
+                        cvu * 8;
+    const long long off[4] = {b, b + C, b + (long long)W * C,
+                              b + (long long)W * C + C};
+    const uint4 g = *(const uint4*)(dy + (long long)pix * C + cvu * 8);
+    uint4 v[4], a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (MODE != POOL_AVG || aux_x) v[i] = *(const uint4*)(x + off[i]);
+      if (aux && !aux_x) a[i] = *(const uint4*)(aux + off[i]);
+    }
+    uint16_t o[4][8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float gq = bf2f(((const uint16_t*)&g)[q]);
+      int ch = 0;
+      if (MODE != POOL_AVG) {
+        float key = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float f = bf2f(((const uint16_t*)&v[i])[q]);
+          const float kf = MODE == POOL_MAXABS ? fabsf(f) : f;
+          if (i == 0 || kf > key) { key = kf; ch = i; }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float d = MODE == POOL_AVG ? 0.25f * gq : (i == ch ? gq : 0.f);
+        if (aux) {
+          const float av = bf2f(((const uint16_t*)(aux_x ? &v[i] : &a[i]))[q]);
+          d *= act_bwd(av, aux_act);
+        }
+        o[i][q] = f2bf(d);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(uint4*)(dx + off[i]) = *(const uint4*)o[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused LRN -> 3x3 / stride-2 max pooling with a ONE-BYTE argmax: the index
+// (0..8, row-major) of the chosen pixel inside its window instead of an int32
+// offset into x.  Forward writes 8 B of argmax per 8 channels instead of 32 B;
+// backward reads one 8-B chunk per 8 channels and compares it against the
+// window-local index a block pixel has in each of its 2 x 2 covering windows
+// (a compile-time constant per (window, pixel) pair).  The LRN loops only
+// evaluate the channels the window half-width needs.
+template <int half>
+__global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8_kernel(
+    const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+    uint8_t* __restrict__ argmax, int N, int H, int W, int C, int OH, int OW,
+    float alpha, float beta, float k, FastDiv fCV, FastDiv fOW, FastDiv fOH) {
+  const int CV = C >> 3;
+  const int total = N * OH * OW * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
+    const int c0 = (int)cvu * 8;
+    const int h0 = (int)ohu * 2, w0 = (int)owu * 2;
+    const uint16_t* img = x + (long long)nu * H * W * C;
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { best[q] = -INFINITY; bi[q] = 0; }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int h = h0 + i / 3, w = w0 + i % 3;
+      if (h >= H || w >= W) continue;
+      float v[24];
+      loadx<half>(img + (h * W + w) * C, c0, C, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float s = lrn_s(v, 8 + q, half, alpha, k);
+        const float yv = v[8 + q] * exp2f(-beta * __log2f(s));
+        if (i == 0 || yv > best[q]) { best[q] = yv; bi[q] = i; }
+      }
+    }
+    uint16_t o[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(best[q]);
+    const long long yo = (long long)pix * C + c0;
+    *(uint4*)(y + yo) = *(const uint4*)o;
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    *(uint2*)(argmax + yo) = a;
+  }
+}
+
+template <int half>
+__global__ __launch_bounds__(256) void lrn_pool3s2_bwd_u8_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
+    const uint8_t* __restrict__ argmax, uint16_t* __restrict__ dx, int N,
+    int H, int W, int C, int OH, int OW, float alpha, float beta, float k,
+    const uint16_t* aux, int aux_act, FastDiv fCV, FastDiv fBW,
+    FastDiv fBH) {
+  // g[p][j]: pool gradient of block pixel p at channel c0 - 8 + j; only
+  // j in [8 - half, 16 + half) is ever needed (the LRN window)
+  constexpr int JLO = 8 - half, JHI = 16 + half;
+  const int CV = C >> 3;
+  const int BH = (H + 1) >> 1, BW = (W + 1) >> 1;
+  const int total = N * BH * BW * CV;
+  const bool aux_x = aux == x;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t blk, cvu, t, bwu, nu, bhu;
+    fdivmod((uint32_t)e, fCV, blk, cvu);
+    fdivmod(blk, fBW, t, bwu);
+    fdivmod(t, fBH, nu, bhu);
+    const int c0 = (int)cvu * 8;
+    float g[4][24];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < 24; ++j) g[p][j] = 0.f;
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const int a = wi >> 1, b = wi & 1;
+      const int oh = (int)bhu - 1 + a, ow = (int)bwu - 1 + b;
+      if (oh < 0 || ow < 0 || oh >= OH || ow >= OW) continue;
+      const long long yo = (((long long)nu * OH + oh) * OW + ow) * C;
+#pragma unroll
+      for (int part = 0; part < 3; ++part) {
+        // channel chunk [c0 - 8 + 8 part, +8): skip chunks outside C and
+        // those the LRN window never reaches
+        if (8 * part + 8 <= JLO || 8 * part >= JHI) continue;
+        const int cb = c0 - 8 + 8 * part;
+        if (cb < 0 || cb >= C) continue;
+        const uint4 gv = *(const uint4*)(dp + yo + cb);
+        const uint2 av = *(const uint2*)(argmax + yo + cb);
+        const uint16_t* gh = (const uint16_t*)&gv;
+        const uint8_t* ah = (const uint8_t*)&av;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int r = 2 * (1 - a) + (p >> 1), c = 2 * (1 - b) + (p & 1);
+          if (r > 2 || c > 2) continue;  // pixel outside this window
+          const int kexp = r * 3 + c;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int j = 8 * part + q;
+            if (j < JLO || j >= JHI) continue;
+            g[p][j] += ah[q] == kexp ? bf2f(gh[q]) : 0.f;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int hp = (int)bhu * 2 + (p >> 1), wp = (int)bwu * 2 + (p & 1);
+      if (hp >= H || wp >= W) continue;
+      const long long po = (((long long)nu * H + hp) * W + wp) * C;
+      float xv[24];
+      loadx<half>(x + po, c0, C, xv);
+      // t_j = g_j x_j s_j^(-beta-1) for j in [8 - half, 16 + half)
+      float tj[24], sb[8];
+#pragma unroll
+      for (int j = JLO; j < JHI; ++j) {
+        const float s = lrn_s(xv, j, half, alpha, k);
+        const float e1 = exp2f((-beta - 1.f) * __log2f(s));  // s^(-beta-1)
+        tj[j] = g[p][j] * xv[j] * e1;
+        if (j >= 8 && j < 16) sb[j - 8] = e1 * s;  // s^-beta
+      }
+      float av8[8];
+      if (aux && !aux_x) load8(aux + po + c0, av8);
+      uint16_t o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float acc = 0.f;
+#pragma unroll
+        for (int d = -half; d <= half; ++d) acc += tj[8 + q + d];
+        float v = g[p][8 + q] * sb[q] - 2.f * alpha * beta * xv[8 + q] * acc;
+        if (aux) v *= act_bwd(aux_x ? xv[8 + q] : av8[q], aux_act);
+        o[q] = f2bf(v);
+      }
+      *(uint4*)(dx + po + c0) = *(const uint4*)o;
+    }
+  }
+}
 }  // namespace
+
+// 2 x 2 / stride-2 pooling without argmax (pool2_fwd_kernel): C % 8 == 0,
+// even H and W, 16-B aligned tensors; mode 0 max, 1 avg, 2 maxabs.
+HVK_API int hvk_pool2_fwd(const void* x, void* y, int N, int H, int W, int C,
+                          int mode, hipStream_t s) {
+  if (C % 8 || (H & 1) || (W & 1) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)y & 15) || (long long)N * H * W * C >= (1ll << 31))
+    return -1;
+  const long long total = (long long)N * (H / 2) * (W / 2) * (C / 8);
+  auto k = mode == POOL_AVG ? pool2_fwd_kernel<POOL_AVG>
+           : mode == POOL_MAXABS ? pool2_fwd_kernel<POOL_MAXABS>
+                                 : pool2_fwd_kernel<POOL_MAX>;
+  hipLaunchKernelGGL(k, dim3(grid_for(total)), dim3(256), 0, s,
+                     (const uint16_t*)x, (uint16_t*)y, N, H, W, C,
+                     make_fastdiv(C / 8), make_fastdiv(W / 2),
+                     make_fastdiv(H / 2));
+  return (int)hipGetLastError();
+}
+
+// dx of a 2 x 2 / stride-2 pooling, the choice recomputed from x (the
+// forward input); aux multiplies by act_bwd(aux) (aux may be x itself)
+HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
+                          int H, int W, int C, int mode, const void* aux,
+                          int aux_act, hipStream_t s) {
+  if (C % 8 || (H & 1) || (W & 1) || ((uintptr_t)x & 15) ||
+      ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || ((uintptr_t)aux & 15) ||
+      (long long)N * H * W * C >= (1ll << 31))
+    return -1;
+  const long long total = (long long)N * (H / 2) * (W / 2) * (C / 8);
+  auto k = mode == POOL_AVG ? pool2_bwd_kernel<POOL_AVG>
+           : mode == POOL_MAXABS ? pool2_bwd_kernel<POOL_MAXABS>
+                                 : pool2_bwd_kernel<POOL_MAX>;
+  hipLaunchKernelGGL(k, dim3(grid_for(total)), dim3(256), 0, s,
+                     (const uint16_t*)x, (const uint16_t*)dy, (uint16_t*)dx,
+                     N, H, W, C, (const uint16_t*)aux, aux_act,
+                     make_fastdiv(C / 8), make_fastdiv(W / 2),
+                     make_fastdiv(H / 2));
+  return (int)hipGetLastError();
+}
+
+// Fused LRN -> 3x3 stride-2 max pooling with a uint8 window-index argmax
+// (see lrn_pool3s2_fwd_u8_kernel).  C % 8 == 0, n / 2 <= 4.
+HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
+                                int H, int W, int C, int OH, int OW, int n,
+                                float alpha, float beta, float k,
+                                hipStream_t s) {
+  if (C % 8 || n / 2 > 4 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15) ||
+      ((uintptr_t)argmax & 7) || (long long)N * H * W * C >= (1ll << 31))
+    return -1;
+  const long long total = (long long)N * OH * OW * (C / 8);
+  const int h = n / 2;
+  auto kf = h == 0 ? lrn_pool3s2_fwd_u8_kernel<0>
+          : h == 1 ? lrn_pool3s2_fwd_u8_kernel<1>
+          : h == 2 ? lrn_pool3s2_fwd_u8_kernel<2>
+          : h == 3 ? lrn_pool3s2_fwd_u8_kernel<3>
+                   : lrn_pool3s2_fwd_u8_kernel<4>;
+  hipLaunchKernelGGL(kf, dim3(grid_for(total)), dim3(256), 0, s,
+                     (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N, H,
+                     W, C, OH, OW, alpha, beta, k, make_fastdiv(C / 8),
+                     make_fastdiv(OW), make_fastdiv(OH));
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
+                                const void* argmax, void* dx, int N, int H,
+                                int W, int C, int OH, int OW, int n,
+                                float alpha, float beta, float k,
+                                const void* aux, int aux_act, hipStream_t s) {
+  if (C % 8 || n / 2 > 4 || ((uintptr_t)x & 15) || ((uintptr_t)dp & 15) ||
+      ((uintptr_t)dx & 15) || ((uintptr_t)argmax & 7) ||
+      ((uintptr_t)aux & 15) || (long long)N * H * W * C >= (1ll << 31))
+    return -1;
+  const int h = n / 2;
+  const int BH = (H + 1) / 2, BW = (W + 1) / 2;
+  const long long tb = (long long)N * BH * BW * (C / 8);
+  auto k2 = h == 0 ? lrn_pool3s2_bwd_u8_kernel<0>
+          : h == 1 ? lrn_pool3s2_bwd_u8_kernel<1>
+          : h == 2 ? lrn_pool3s2_bwd_u8_kernel<2>
+          : h == 3 ? lrn_pool3s2_bwd_u8_kernel<3>
+                   : lrn_pool3s2_bwd_u8_kernel<4>;
+  hipLaunchKernelGGL(k2, dim3(grid_for(tb)), dim3(256), 0, s,
+                     (const uint16_t*)x, (const uint16_t*)dp,
+                     (const uint8_t*)argmax, (uint16_t*)dx, N, H, W, C, OH, OW,
+                     alpha, beta, k, (const uint16_t*)aux, aux_act,
+                     make_fastdiv(C / 8), make_fastdiv(BW), make_fastdiv(BH));
+  return (int)hipGetLastError();
+}
 
 HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
                          int W, int C, int OH, int OW, int ky, int kx, int sy,

@@ -373,6 +373,16 @@ def test_lrn_pool_fused(shape, stride, n, aux_mode):
     close(y, yr, 1e-2)
     # argmax may differ only where two window values tie in fp32 vs bf16
     assert (am.cpu() != amr).float().mean().item() < 1e-3
+    if stride == 2:
+        # the one-byte window-index format the AlexNet pair uses on the GPU
+        am8 = torch.zeros(am.shape, dtype=torch.uint8, device=DEV)
+        y8, _ = ops.lrn_pool_fwd(xg, n, alpha, beta, k, 3, 3, st,
+                                 argmax=am8)
+        torch.cuda.synchronize()
+        assert torch.equal(y8, y)
+        off8 = ops.window_index_to_offsets(am8, shape, 3, 3, st).cpu()
+        assert (off8 != amr).float().mean().item() < 1e-3
+        am = am8
     dp = rnd(*y.shape, seed=5)
     if aux_mode == "sep":
         aux, auxg = rnd(*shape, seed=6), None
@@ -388,3 +398,35 @@ def test_lrn_pool_fused(shape, stride, n, aux_mode):
                            aux=aux, aux_act=act)
     torch.cuda.synchronize()
     close(dx, dxr, 2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["max", "avg", "maxabs"])
+@pytest.mark.parametrize("aux_mode", ["none", "sep", "x"])
+def test_pool2_argmax_free(mode, aux_mode):
+    """2 x 2 / stride-2 pooling without an argmax tensor: the backward
+    recomputes the window's choice from x (pool2 kernels) - against the
+    argmax-based fp32 reference, with and without a fused activation
+    derivative (aux separate, or aux == x for ReLU below)."""
+    shape = (3, 14, 10, 24)
+    x = rnd(*shape, scale=2.0)
+    if aux_mode == "x":
+        x = x.clamp_min(0.0)
+    xg = x.to(DEV)
+    y = ops.pool2_fwd(xg, mode)
+    yr, am = ops.pool_fwd(x, 2, 2, (2, 2), mode)
+    torch.cuda.synchronize()
+    close(y, yr, 1e-2)
+    dy = rnd(*y.shape, seed=4)
+    aux = auxg = None
+    if aux_mode == "sep":
+        aux = rnd(*shape, seed=6)
+        auxg = aux.to(DEV)
+    elif aux_mode == "x":
+        aux, auxg = x, xg
+    act = 3 if aux is not None else 0
+    dx = ops.pool2_bwd(xg, dy.to(DEV), mode, aux=auxg, aux_act=act)
+    dxr = ops.pool_bwd(dy, am, shape, 2, 2, (2, 2), mode, aux=aux,
+                       aux_act=act)
+    torch.cuda.synchronize()
+    close(dx, dxr, 1e-2)

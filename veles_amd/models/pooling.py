@@ -40,11 +40,15 @@ class Pooling(AcceleratedUnit):
         self.output = Array(shallow_pickle=True)
         self.input_offset = Array(shallow_pickle=True)
         self.fused_lrn = None  # LRN unit computed by this pooling (fused)
+        # input_offset read by another unit (depooling): keep it in the flat
+        # int32 format
+        self.offsets_exported = False
         self.demand("input")
 
     def init_unpickled(self):
         super().init_unpickled()
         self.lrn_fused_active_ = False
+        self.argmax_free_ = False
 
     @property
     def activation(self):
@@ -69,13 +73,26 @@ class Pooling(AcceleratedUnit):
             else self.compute_dtype
         self.output.devmem = torch.zeros(B, OH, OW, C, dtype=dt,
                                          device=self.torch_device)
-        self.input_offset.devmem = torch.zeros(B, OH, OW, C,
-                                               dtype=torch.int32,
-                                               device=self.torch_device)
         lrn = self.fused_lrn
+        # non-overlapping 2 x 2 windows on the GPU: no argmax tensor at all,
+        # the GD unit recomputes the choice from the input (ops.pool2_bwd)
+        self.argmax_free_ = self.is_gpu and lrn is None and \
+            not self.offsets_exported and \
+            type(self) in (MaxPooling, AvgPooling, MaxAbsPooling) and \
+            ops.pool2_ok(shape, self.ky, self.kx, self.sliding)
+        if not self.argmax_free_:
+            self.input_offset.devmem = torch.zeros(B, OH, OW, C,
+                                                   dtype=torch.int32,
+                                                   device=self.torch_device)
         self.lrn_fused_active_ = lrn is not None and self.MODE == "max" and \
             len(tuple(self.input.shape)) == 4 and \
             ops.lrn_pool_fusable(C, lrn.n, self.ky, self.kx, self.sliding)
+        if self.lrn_fused_active_ and self.is_gpu and \
+                tuple(self.sliding) == (2, 2) and not self.offsets_exported:
+            # the fused pair keeps its argmax private: one byte per element
+            # (window-local index) instead of an int32 offset
+            self.input_offset.devmem = torch.zeros(
+                B, OH, OW, C, dtype=torch.uint8, device=self.torch_device)
 
     def run(self):
         if self.lrn_fused_active_:
@@ -86,6 +103,9 @@ class Pooling(AcceleratedUnit):
                              argmax=self.input_offset.devmem)
             return
         x = self._in()
+        if self.argmax_free_:
+            ops.pool2_fwd(x, self.MODE, out=self.output.devmem)
+            return
         B, H, W, C = x.shape
         OH, OW = ops.pool_out_size(H, W, self.ky, self.kx, self.sliding[1],
                                    self.sliding[0])
@@ -287,6 +307,9 @@ class GDPooling(GradientDescentBase):
         shape = tuple(x.shape) if x.dim() == 4 else tuple(x.shape) + (1,)
         ei = self.alloc_err_input(shape)
         aux, aux_act = self.aux_tensor()
+        if fwd is not None and getattr(fwd, "argmax_free_", False):
+            ops.pool2_bwd(x, err, self.MODE, aux=aux, aux_act=aux_act, out=ei)
+            return
         if aux is not None and aux.dim() == 3:
             aux = aux.unsqueeze(-1)
         ops.pool_bwd(err, self.input_offset.devmem

@@ -291,6 +291,7 @@ class StandardWorkflow(LinkBuilders, AcceleratedWorkflow):
                     raise ValueError("depooling without a pooling before it")
                 pool = pools.pop()
                 unit.link_attrs(pool, "input_offset")
+                pool.offsets_exported = True  # keep int32 flat offsets
                 unit.output_shape_source = pool.input
             elif isinstance(unit, (MaxPooling, MaxAbsPooling,
                                    StochasticPooling)) and \

@@ -620,6 +620,47 @@ def pool_bwd(dy, argmax, x_shape, ky, kx, sliding=None, mode="max",
     return out
 
 
+def pool2_ok(x_shape, ky, kx, sliding):
+    """Geometry of the argmax-free 2 x 2 / stride-2 pooling kernels."""
+    if len(x_shape) != 4:
+        return False
+    N, H, W, C = x_shape
+    return ky == 2 and kx == 2 and tuple(sliding) == (2, 2) and \
+        C % 8 == 0 and H % 2 == 0 and W % 2 == 0
+
+
+def pool2_fwd(x, mode="max", out=None):
+    """2 x 2 / stride-2 NHWC pooling that writes no argmax: ``pool2_bwd``
+    recomputes the window's choice from x."""
+    N, H, W, C = x.shape
+    m = POOL[mode]
+    if out is None:
+        out = torch.empty(N, H // 2, W // 2, C, dtype=x.dtype,
+                          device=x.device)
+    if _gpu(x):
+        _lib_call("hvk_pool2_fwd", _p(x), _p(out), N, H, W, C, m, _s(x))
+        return out
+    y, _ = pool_fwd(x, 2, 2, (2, 2), mode, out=out)
+    return y
+
+
+def pool2_bwd(x, dy, mode="max", aux=None, aux_act=0, out=None):
+    N, H, W, C = x.shape
+    m = POOL[mode]
+    aux_act = act_code(aux_act)
+    if out is None:
+        out = torch.empty_like(x, dtype=dy.dtype)
+    if _gpu(x):
+        _lib_call("hvk_pool2_bwd", _p(x), _p(dy), _p(out), N, H, W, C, m,
+                  _p(aux), aux_act, _s(x))
+        return out
+    am = None
+    if m != 1:
+        _, am = pool_fwd(x, 2, 2, (2, 2), mode)
+    return pool_bwd(dy, am, (N, H, W, C), 2, 2, (2, 2), mode, aux=aux,
+                    aux_act=aux_act, out=out)
+
+
 # --------------------------------------------------------------------- LRN
 def _lrn_ref(x, n, alpha, beta, k):
     x2 = x * x
@@ -672,10 +713,30 @@ def lrn_pool_fusable(C, n, ky, kx, sliding):
         sx >= 2 and sy >= 2
 
 
+def window_index_to_offsets(am, x_shape, ky, kx, sliding):
+    """A uint8 window-local argmax (0 .. ky*kx-1, row-major inside the pooling
+    window) -> flat int32 offsets into the NHWC input, the format of
+    ``pool_fwd``'s argmax (reference paths and tests)."""
+    sx, sy = sliding
+    N, H, W, C = x_shape
+    _, OH, OW, _ = am.shape
+    dev = am.device
+    a = am.long()
+    oh = torch.arange(OH, device=dev).view(1, OH, 1, 1)
+    ow = torch.arange(OW, device=dev).view(1, 1, OW, 1)
+    n = torch.arange(N, device=dev).view(N, 1, 1, 1)
+    c = torch.arange(C, device=dev).view(1, 1, 1, C)
+    h = oh * sy + a // kx
+    w = ow * sx + a % kx
+    return (((n * H + h) * W + w) * C + c).to(torch.int32)
+
+
 def lrn_pool_fwd(x, n, alpha, beta, k, ky, kx, sliding, out=None,
                  argmax=None):
     """max_pool(lrn(x)) without materialising lrn(x); ``argmax`` indexes the
-    (virtual) LRN output, i.e. x's geometry."""
+    (virtual) LRN output, i.e. x's geometry.  A uint8 ``argmax`` (GPU,
+    stride 2) holds the window-local index instead: 1 byte per element
+    (``window_index_to_offsets`` converts)."""
     sx, sy = sliding
     N, H, W, C = x.shape
     OH, OW = pool_out_size(H, W, ky, kx, sy, sx)
@@ -684,11 +745,27 @@ def lrn_pool_fwd(x, n, alpha, beta, k, ky, kx, sliding, out=None,
     if argmax is None:
         argmax = torch.empty(N, OH, OW, C, dtype=torch.int32, device=x.device)
     if _gpu(x):
+        if argmax.dtype == torch.uint8:
+            if (sx, sy) != (2, 2):
+                raise ValueError("uint8 window-index argmax: stride 2 only")
+            _lib_call("hvk_lrn_pool_fwd_u8", _p(x), _p(out), _p(argmax), N,
+                      H, W, C, OH, OW, n, float(alpha), float(beta), float(k),
+                      _s(x))
+            return out, argmax
         _lib_call("hvk_lrn_pool_fwd", _p(x), _p(out), _p(argmax), N, H, W, C,
                   OH, OW, sy, sx, n, float(alpha), float(beta), float(k),
                   _s(x))
         return out, argmax
     y = lrn_fwd(x.float(), n, alpha, beta, k)
+    if argmax.dtype == torch.uint8:
+        yo, off = pool_fwd(y, ky, kx, sliding, "max", out=out)
+        # window-local index of the chosen flat offset
+        hw = (off.long() // C)
+        h, w = (hw // W) % H, hw % W
+        oh = torch.arange(OH).view(1, OH, 1, 1)
+        ow = torch.arange(OW).view(1, 1, OW, 1)
+        argmax.copy_(((h - oh * sy) * kx + (w - ow * sx)).to(torch.uint8))
+        return yo, argmax
     return pool_fwd(y, ky, kx, sliding, "max", out=out, argmax=argmax)
 
 
@@ -703,10 +780,18 @@ def lrn_pool_bwd(x, dp, argmax, n, alpha, beta, k, ky, kx, sliding,
     if out is None:
         out = torch.empty_like(x)
     if _gpu(x):
+        if argmax.dtype == torch.uint8:
+            _lib_call("hvk_lrn_pool_bwd_u8", _p(x), _p(dp), _p(argmax),
+                      _p(out), N, H, W, C, OH, OW, n, float(alpha),
+                      float(beta), float(k), _p(aux), aux_act, _s(x))
+            return out
         _lib_call("hvk_lrn_pool_bwd", _p(x), _p(dp), _p(argmax), _p(out), N,
                   H, W, C, OH, OW, sy, sx, n, float(alpha), float(beta),
                   float(k), _p(aux), aux_act, _s(x))
         return out
+    if argmax.dtype == torch.uint8:
+        argmax = window_index_to_offsets(argmax, tuple(x.shape), ky, kx,
+                                         sliding)
     g = pool_bwd(dp.float(), argmax, tuple(x.shape), ky, kx, sliding, "max")
     return lrn_bwd(x, g, n, alpha, beta, k, aux=aux, aux_act=aux_act,
                    out=out)

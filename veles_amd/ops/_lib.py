@@ -59,6 +59,10 @@ _SIGS = {
     "hvk_lrn_bwd": [P, P, P, L, I, I, F, F, F, P, I, P],
     "hvk_lrn_pool_fwd": [P, P, P] + [I] * 9 + [F, F, F, P],
     "hvk_lrn_pool_bwd": [P, P, P, P] + [I] * 9 + [F, F, F, P, I, P],
+    "hvk_pool2_fwd": [P, P] + [I] * 5 + [P],
+    "hvk_pool2_bwd": [P, P, P] + [I] * 5 + [P, I, P],
+    "hvk_lrn_pool_fwd_u8": [P, P, P] + [I] * 7 + [F, F, F, P],
+    "hvk_lrn_pool_bwd_u8": [P, P, P, P] + [I] * 7 + [F, F, F, P, I, P],
     # exact-precision GEMMs (csrc/kernels/gemm_f32.hip)
     "hvk_gemm_f32": [I, I, I, I, I, P, I, P, I, P, I, F, F, I, P],
     "hvk_gemm_f64": [I, I, I, I, I, P, I, P, I, P, I, D, D, I, P],
