@@ -576,6 +576,49 @@ struct Epi {
     if (out_f32) ((float*)c)[idx] = v;
     else ((uint16_t*)c)[idx] = f2bf(v);
   }
+  // The common case, decided once per block (wave-uniform): no atomics,
+  // remaps, fused bias-gradient column or beta; per-column bias; 16-B
+  // aligned rows.  Then every 8-column chunk is one straight-line store.
+  __host__ __device__ bool fast_ok() const {
+    return !atomic && !run_in && ones_col < 0 && beta == 0.f &&
+           bias_mode != 2 && (ldc & 7) == 0 && (((uintptr_t)c) & 15) == 0 &&
+           (gcol & 7) == 0 &&
+           (bias_mode != 1 || (((uintptr_t)bias) & 15) == 0) &&
+           (!aux || ((ld_aux & 7) == 0 && (((uintptr_t)aux) & 15) == 0));
+  }
+  // fast_ok() and n + 8 <= N: one switch per chunk, vector bias / aux loads,
+  // packed bf16 conversion (v is scratch)
+  __device__ __forceinline__ void store8_fast(int gi, int m, int n,
+                                              float* v) const {
+    const int gm = m + gi * grow, gn = n + gi * gcol;
+    const long long idx = (long long)gm * ldc + gn;
+    if (alpha != 1.f) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= alpha;
+    }
+    if (bias_mode == 1) {
+      const float4 b0 = *(const float4*)(bias + gn);
+      const float4 b1 = *(const float4*)(bias + gn + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+    act_fwd8(v, act);
+    if (aux) {
+      const uint4 av = *(const uint4*)(aux + (long long)gm * ld_aux + gn);
+      const uint16_t* ah = (const uint16_t*)&av;
+      float a[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[q] = bf2f(ah[q]);
+      act_bwd_mul8(v, a, aux_act);
+    }
+    if (out_f32) {
+      float4* d = (float4*)((float*)c + idx);
+      d[0] = make_float4(v[0], v[1], v[2], v[3]);
+      d[1] = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      *(uint4*)((uint16_t*)c + idx) = pack_bf16x8(v);
+    }
+  }
   // 8 consecutive columns of one row: 16-B vector stores when possible
   __device__ void store8(int gi, int m, int n, const float* v) const {
     if (m >= M || n >= N) return;
@@ -919,6 +962,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     }
   __syncthreads();
   constexpr int CH = BN_ / 8;
+  const bool fast = epi.fast_ok();
   for (int q = t; q < BM * CH; q += NTHR) {
     int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
     if (m0 + row >= M) continue;
@@ -927,7 +971,10 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     float4 lo = src[0], hi = src[1];
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    epi.store8(gi, m0 + row, n0 + c8, v);
+    if (fast && n0 + c8 + 8 <= epi.N)
+      epi.store8_fast(gi, m0 + row, n0 + c8, v);
+    else
+      epi.store8(gi, m0 + row, n0 + c8, v);
   }
 }
 
@@ -1040,6 +1087,22 @@ __global__ void im2col_kernel(const uint16_t* x, uint16_t* col, ConvGeom g,
   }
 }
 
+// Split-K finishing pass: C = epilogue(ws), ws the f32 sum of the K splits
+// (N % 8 == 0 and Epi::fast_ok(): one 8-column chunk per thread)
+__global__ void splitk_finish_kernel(const float* __restrict__ ws, int M,
+                                     int N, Epi e) {
+  const int CH = N >> 3;
+  const long long total = (long long)M * CH;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       q < total; q += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(q / CH), c8 = (int)(q - (long long)m * CH) * 8;
+    const float4* src = (const float4*)(ws + (long long)m * N + c8);
+    const float4 lo = src[0], hi = src[1];
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    e.store8_fast(0, m, c8, v);
+  }
+}
+
 }  // namespace
 
 // col[M][Kp] = im2col(X) for a single-group conv (Kp = round_up(KH*KW*C, 8))
@@ -1098,6 +1161,36 @@ HVK_API int hvk_gemm(int transA, int transB, int M, int N, int K,
     err = launch<DenseMN, false, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
   }
   return (int)err;
+}
+
+// Split-K GEMM for shapes with too few output tiles to fill 256 CUs (the FC
+// layers at batch 512: fc6 forward is 4 x 32 tiles of 128 x 128): the K range
+// is split `splits` ways, the partial products are summed by f32 atomics into
+// the workspace ws[M][N] (zeroed here), then one pass applies alpha, the
+// per-column bias, the activation and the aux derivative and casts to C.
+// Same arguments as hvk_gemm minus beta / accumulate / bias_grad; N % 8 == 0
+// and 16-B aligned C / bias / aux rows (-4 otherwise: use hvk_gemm).
+HVK_API int hvk_gemm_splitk(int transA, int transB, int M, int N, int K,
+                            const void* A, int lda, const void* B, int ldb,
+                            void* C, int ldc, int out_f32, float alpha,
+                            const float* bias, int act, const void* aux,
+                            int ld_aux, int aux_act, int splits, float* ws,
+                            hipStream_t s) {
+  Epi e = make_epi(C, ldc, M, N, out_f32, 0, alpha, 0.f, bias, 1, act, aux,
+                   ld_aux, aux_act);
+  if (N % 8 || !e.fast_ok() || ((uintptr_t)ws & 15) || splits < 2) return -4;
+  hipError_t err = hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), s);
+  if (err != hipSuccess) return (int)err;
+  const int rc = hvk_gemm(transA, transB, M, N, K, A, lda, B, ldb, ws, N, 1,
+                          1, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0, splits,
+                          nullptr, s);
+  if (rc) return rc;
+  const long long total = (long long)M * (N / 8);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(splitk_finish_kernel, dim3((int)blocks), dim3(256), 0, s,
+                     (const float*)ws, M, N, e);
+  return (int)hipGetLastError();
 }
 
 // Y[n][oh][ow][oc] = act(sum X*W + bias); X NHWC bf16, W [OC][KH][KW][C/g]

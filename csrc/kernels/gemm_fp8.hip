@@ -191,8 +191,10 @@ __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
     if (vec) {
       uint4 av = *(const uint4*)(e.aux + (long long)m * e.ld_aux + gn);
       const uint16_t* ah = (const uint16_t*)&av;
+      float y[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) a[q] = act_bwd(bf2f(ah[q]), e.aux_act);
+      for (int q = 0; q < 8; ++q) y[q] = bf2f(ah[q]);
+      act_bwd_mul8(a, y, e.aux_act);  // a = act_bwd(y), one switch
     } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q)
@@ -203,19 +205,27 @@ __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
   }
   float o[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float t = v[q] * alpha;
-    if (e.bias && n + q < e.N) t += e.bias[gn + q];
-    if (e.act) t = act_fwd(t, e.act);
-    o[q] = t * a[q];
+  for (int q = 0; q < 8; ++q) o[q] = v[q] * alpha;
+  if (e.bias) {
+    if (vec && (((uintptr_t)(e.bias + gn)) & 15) == 0) {
+      const float4 b0 = *(const float4*)(e.bias + gn);
+      const float4 b1 = *(const float4*)(e.bias + gn + 4);
+      o[0] += b0.x; o[1] += b0.y; o[2] += b0.z; o[3] += b0.w;
+      o[4] += b1.x; o[5] += b1.y; o[6] += b1.z; o[7] += b1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (n + q < e.N) o[q] += e.bias[gn + q];
+    }
+  }
+  // one switch per chunk (act_fwd8); a[] already holds act_bwd(aux)
+  act_fwd8(o, e.act);
+  if (e.aux) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] *= a[q];
   }
   if (vec) {
-    uint4 w;
-    w.x = f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-    w.y = f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-    w.z = f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-    w.w = f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
-    *(uint4*)(e.c + idx) = w;
+    *(uint4*)(e.c + idx) = pack_bf16x8(o);
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q)

@@ -25,6 +25,19 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+// two floats -> packed bf16 pair (lo = a) in ONE v_cvt_pk_bf16_f32 (RNE,
+// NaN-preserving); a per-element cast + shift/or costs three instructions
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ uint4 pack_bf16x8(const float* v) {
+  return make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                    pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -74,6 +87,32 @@ __device__ __forceinline__ float act_fwd(float x, int act) {
     default: return x;
   }
 }
+// act_fwd over 8 values with ONE switch on the (wave-uniform) code: the
+// per-element switch of an unrolled loop costs a branch ladder per element
+__device__ __forceinline__ void act_fwd8(float* v, int act) {
+  switch (act) {
+    case ACT_LINEAR: return;
+    case ACT_STRICT_RELU:
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : 0.f;
+      return;
+    case ACT_TANH:
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = 1.7159f * tanhf(0.6666f * v[q]);
+      return;
+    case ACT_RELU:
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        v[q] = v[q] > 15.f ? v[q] : log1pf(__expf(v[q]));
+      return;
+    case ACT_SIGMOID:
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = 1.f / (1.f + __expf(-v[q]));
+      return;
+    default:
+      return;
+  }
+}
 // derivative expressed through the activation OUTPUT y
 __device__ __forceinline__ float act_bwd(float y, int act) {
   switch (act) {
@@ -85,4 +124,22 @@ __device__ __forceinline__ float act_bwd(float y, int act) {
   }
 }
 
+}  // namespace hvk
+
+namespace hvk {
+// v[q] *= act_bwd(y[q], act) for 8 values, one switch (see act_fwd8)
+__device__ __forceinline__ void act_bwd_mul8(float* v, const float* y,
+                                             int act) {
+  switch (act) {
+    case ACT_LINEAR: return;
+    case ACT_STRICT_RELU:
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= y[q] > 0.f ? 1.f : 0.f;
+      return;
+    default:
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= act_bwd(y[q], act);
+      return;
+  }
+}
 }  // namespace hvk

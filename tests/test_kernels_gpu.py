@@ -64,6 +64,27 @@ def test_gemm_epilogue_bias_act_aux():
         close(got, ref, 5e-3)
 
 
+@pytest.mark.parametrize("tb", [1, 0])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_gemm_auto_splitk_epilogue(tb, out_dtype):
+    """Few output tiles and a long K (the FC layers at batch 512) take the
+    split-K path (hvk_gemm_splitk: f32 atomics into a workspace, then one
+    epilogue pass): bias, activation and aux derivative against fp32."""
+    M, N, K = 256, 1000, 4096
+    assert ops.auto_splitk(M, N, K, torch.empty(M, N, device=DEV)) > 1
+    a, w = rnd(M, K), rnd(N, K, seed=2) if tb else rnd(K, N, seed=2)
+    bias = torch.randn(N)
+    aux = rnd(M, N, seed=3)
+    for act in (0, 1, 3, 4):
+        ref = ops.gemm(a, w, trans_b=bool(tb), bias=bias, act=act, aux=aux,
+                       aux_act=3, out_dtype=torch.float32)
+        got = ops.gemm(a.to(DEV), w.to(DEV), trans_b=bool(tb),
+                       bias=bias.to(DEV), act=act, aux=aux.to(DEV),
+                       aux_act=3, out_dtype=out_dtype)
+        close(got.float(), ref, 1e-2 if out_dtype == torch.bfloat16 else
+              5e-3)
+
+
 def test_gemm_splitk_accumulate():
     M, N, K = 96, 200, 4096
     a, b = rnd(K, M), rnd(K, N, seed=4)

@@ -165,6 +165,17 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
             raise ValueError("split-K requires accumulate=True")
         if bias_grad is not None and (trans_b or not accumulate):
             raise ValueError("bias_grad needs accumulate=True, trans_b=False")
+        sk = 0 if accumulate or beta != 0.0 else \
+            auto_splitk(M, N, K, out, bias, aux)
+        if sk > 1:
+            ws = torch.empty(M * N, dtype=torch.float32, device=dev)
+            _lib_call("hvk_gemm_splitk", int(trans_a), int(trans_b), M, N, K,
+                      _p(a), a.stride(0), _p(b), b.stride(0), _p(out),
+                      out.stride(0), int(out.dtype == torch.float32),
+                      float(alpha), _p(bias), act, _p(aux),
+                      0 if aux is None else aux.stride(0), aux_act, sk,
+                      _p(ws), _s(a))
+            return out
         _lib_call("hvk_gemm", int(trans_a), int(trans_b), M, N, K, _p(a),
                   a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0),
                   int(out.dtype == torch.float32), atomic, float(alpha),
@@ -190,6 +201,27 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         r = r * act_bwd_ref(aux.float(), aux_act)
     out.copy_(r.to(out.dtype))
     return out
+
+
+_SPLITK_ENV = os.environ.get("HVK_SPLITK")
+
+
+def auto_splitk(M, N, K, out, bias=None, aux=None):
+    """K splits for a GEMM whose 128 x 128 output tiles cannot fill the
+    MI355X's 256 CUs twice over (the FC layers at batch 512): enough splits
+    for ~512 workgroups, each keeping >= 1024 of K.  0 = no split (shape or
+    alignment not taken by hvk_gemm_splitk).  HVK_SPLITK=0 disables."""
+    if _SPLITK_ENV == "0":
+        return 0
+    tiles = -(-M // 128) * -(-N // 128)
+    if tiles >= 256 or K < 2048 or N % 8:
+        return 0
+    if out.stride(0) % 8 or out.data_ptr() % 16 or \
+            (bias is not None and bias.data_ptr() % 16) or \
+            (aux is not None and (aux.stride(0) % 8 or aux.data_ptr() % 16)):
+        return 0
+    sk = min(-(-512 // tiles), K // 1024)
+    return sk if sk > 1 else 0
 
 
 def _precision_level(level):

@@ -29,6 +29,8 @@ U = ctypes.c_uint
 _SIGS = {
     "hvk_gemm": [I, I, I, I, I, P, I, P, I, P, I, I, I, F, F, P, I, I, P, I, I,
                  I, P, P],
+    "hvk_gemm_splitk": [I, I, I, I, I, P, I, P, I, P, I, I, F, P, I, P, I, I,
+                        I, P, P],
     "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
     "hvk_conv_dgrad_t": [P, P, P] + [I] * 14 + [P, I, P],
     "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P, P],
