@@ -117,6 +117,34 @@ __device__ __forceinline__ uint32_t tap_ok(const DRow& r, const DTap& t) {
   return t.ok & (r.rm >> t.kh) & (r.cm >> t.kw);
 }
 
+// LDS-DMA through a buffer descriptor (buffer_load_dwordx4 ... lds): 32-bit
+// byte offsets instead of 64-bit addresses, and the hardware bounds check
+// replaces the zero page - a lane whose offset is kBufOOB reads zeros
+// (verified on gfx950: tools/probes/buffer_lds_oob.hip).  Tensors must span
+// less than 2 GiB from the descriptor base (loaders' buf_ok()).
+constexpr uint32_t kBufOOB = 0x80000000u;
+constexpr long long kBufMaxBytes = (1ll << 31) - 64;
+// The base is read through readfirstlane so that hipcc can PROVE the
+// descriptor wave-uniform; otherwise it wraps every buffer op in a waterfall
+// loop (cdna_hip_programming.md T20 - seen here on the 128-wide conv kernel).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t dma_rsrc(const void* base) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  void* p = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)kBufOOB,
+                                           0x00020000);
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds,
+                                      uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+// byte offset of element `off` if bit 0 of v is set, else kBufOOB
+__device__ __forceinline__ uint32_t buf_off(int off, uint32_t v) {
+  return (v & 1u) ? (uint32_t)off * 2u : kBufOOB;
+}
+
 // Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md T1):
 // consecutive logical workgroup ids land on one XCD (private L2).
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

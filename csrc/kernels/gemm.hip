@@ -75,10 +75,20 @@ struct DenseK {
   }
   static constexpr bool kGlds = true;
   static constexpr bool kFast = false;
+  static constexpr bool kBuf = true;
   __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     // bitwise condition: && made hipcc branch around the address
     return pick_src(c.row + k, (c.ok != 0) & (k < K));
+  }
+  // buffer DMA: descriptor at the (group) base, per-slot row byte offset
+  bool buf_ok(int groups) const {
+    return ((long long)(rows - 1) * ld + K) * 2 +
+               (long long)(groups - 1) * gstride * 2 < kBufMaxBytes;
+  }
+  __device__ const void* dbase() const { return p; }
+  __device__ __forceinline__ uint32_t row_voff(int r) const {
+    return r < rows ? (uint32_t)r * (uint32_t)ld * 2u : kBufOOB;
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -101,6 +111,8 @@ struct DenseMN {
   __device__ __forceinline__ Ctx col_ctx(int c) const { return Ctx{c}; }
   static constexpr bool kGlds = true;
   static constexpr bool kFast = false;
+  static constexpr bool kBuf = false;
+  bool buf_ok(int) const { return false; }
   __device__ bool dma_ok() const {
     return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
   }
@@ -175,6 +187,15 @@ struct ConvFwdA {
   __device__ __forceinline__ const uint16_t* dsrc(const DRow& r,
                                                   const DTap& t) const {
     return pick_src(x + (r.pix + t.off), tap_ok(r, t));
+  }
+  static constexpr bool kBuf = true;
+  bool buf_ok(int) const {
+    return (long long)g.N * g.H * g.W * g.C * 2 < kBufMaxBytes;
+  }
+  __device__ const void* dbase() const { return x; }
+  __device__ __forceinline__ uint32_t dvoff(const DRow& r,
+                                            const DTap& t) const {
+    return buf_off(r.pix + t.off, tap_ok(r, t));
   }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -251,6 +272,15 @@ struct ConvDgradA {
                                                   const DTap& t) const {
     return pick_src(dy + (r.pix + t.off), tap_ok(r, t));
   }
+  static constexpr bool kBuf = true;
+  bool buf_ok(int) const {
+    return (long long)g.N * g.OH * g.OW * g.OC * 2 < kBufMaxBytes;
+  }
+  __device__ const void* dbase() const { return dy; }
+  __device__ __forceinline__ uint32_t dvoff(const DRow& r,
+                                            const DTap& t) const {
+    return buf_off(r.pix + t.off, tap_ok(r, t));
+  }
   __device__ __forceinline__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     if (vec) {
@@ -266,6 +296,8 @@ struct ConvDgradA {
 // strided dgrad: per-slot src() addressing (the tap must divide by stride)
 struct ConvDgradAStr : ConvDgradA {
   static constexpr bool kFast = false;
+  static constexpr bool kBuf = false;
+  bool buf_ok(int) const { return false; }
   __device__ bool dma_ok() const { return vec; }
 };
 
@@ -275,6 +307,8 @@ struct ConvDgradAStr : ConvDgradA {
 struct ConvDgradAS : ConvDgradA {
   static constexpr bool kGlds = false;
   static constexpr bool kFast = false;
+  static constexpr bool kBuf = false;
+  bool buf_ok(int) const { return false; }
   __device__ bool dma_ok() const { return false; }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
@@ -314,6 +348,8 @@ struct ConvWgradB {
   // fast DMA addressing needs OH*OW >= BK (a running pixel position wraps
   // into the next image at most once per K tile); else ConvWgradBGen
   static constexpr bool kFast = true;
+  static constexpr bool kBuf = false;
+  bool buf_ok(int) const { return false; }
   __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
   // per DMA slot: the column's tap (fixed) and a running pixel p with
   // rem = p mod OH*OW and the image base, advanced by BK per tile - one
@@ -428,6 +464,8 @@ struct RunGeom {
 struct ConvFwdRunA {
   static constexpr bool kGlds = false;
   static constexpr bool kFast = false;
+  static constexpr bool kBuf = false;
+  bool buf_ok(int) const { return false; }
   __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
@@ -476,6 +514,8 @@ struct ConvFwdRunA {
 struct ConvWgradRunB {
   static constexpr bool kGlds = false;
   static constexpr bool kFast = false;
+  static constexpr bool kBuf = false;
+  bool buf_ok(int) const { return false; }
   __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
@@ -664,9 +704,16 @@ struct Epi {
   }
 };
 
+// the buffer descriptor of a loader's tensor (BUF kernels; unused else)
+template <class L, bool B>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const L& l) {
+  if constexpr (B) return dma_rsrc(l.dbase());
+  else return dma_rsrc(nullptr);
+}
+
 __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
-template <class LA, bool AK, class LB, bool BKM, int BN_>
+template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF>
 __global__ void __launch_bounds__(NTHR, 2)
 gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
             int tiles_n, int tiles, int splits) {
@@ -766,6 +813,12 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       int ka[NIA], kb[NIB];
       // the lane's chunk offset along K: the same in every A slot
       const int kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
+      // BUF (K-major loaders, tensors < 2 GiB): LDS-DMA through buffer
+      // descriptors - a per-slot 32-bit byte offset instead of a 64-bit
+      // address, and kBufOOB lanes read zeros (no zero-page select)
+      const __amdgpu_buffer_rsrc_t ra = rsrc_of<LA, BUF>(la);
+      const __amdgpu_buffer_rsrc_t rb = rsrc_of<LB, BUF>(lb);
+      uint32_t va[NIA], vb[NIB];
       // MN-major B at BN = 64: the DMA image keeps the 256-B rows of the
       // 128-wide layout; the chunks of columns >= 64 read the zero page
       bool bz[NIB];
@@ -774,6 +827,9 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         const int I = w * NIA + i;
         if constexpr (AK && LA::kFast) {
           fa[i] = la.drow(m0 + 8 * I + (lane >> 3));
+          ka[i] = kc;
+        } else if constexpr (AK && BUF) {
+          va[i] = la.row_voff(m0 + 8 * I + (lane >> 3));
           ka[i] = kc;
         } else if constexpr (AK) {
           int row = 8 * I + (lane >> 3);
@@ -790,7 +846,10 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 #pragma unroll
       for (int i = 0; i < NIB; ++i) {
         const int I = w * NIB + i;
-        if constexpr (BKM) {
+        if constexpr (BKM && BUF) {
+          vb[i] = lb.row_voff(n0 + 8 * I + (lane >> 3));
+          kb[i] = kc;
+        } else if constexpr (BKM) {
           int row = 8 * I + (lane >> 3);
           int c = (lane & 7) ^ ((lane >> 3) & 7);
           db[i] = lb.row_ctx(n0 + row);
@@ -808,7 +867,19 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         if constexpr (BKM) bz[i] = false;
       }
       auto issue = [&](int k0, uint16_t* sA, uint16_t* sB) {
-        if constexpr (AK && LA::kFast) {
+        // the K-major lanes' byte offset along K and its validity (BUF)
+        const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
+        if constexpr (AK && LA::kFast && BUF) {
+          const DTap tp = la.dtap(k0 + kc);
+#pragma unroll
+          for (int i = 0; i < NIA; ++i)
+            dma16(ra, sA + (w * NIA + i) * 512, la.dvoff(fa[i], tp));
+        } else if constexpr (AK && BUF) {
+          const bool kin = k0 + kc < la.K;
+#pragma unroll
+          for (int i = 0; i < NIA; ++i)
+            dma16(ra, sA + (w * NIA + i) * 512, kin ? va[i] + kbyte : kBufOOB);
+        } else if constexpr (AK && LA::kFast) {
           const DTap tp = la.dtap(k0 + kc);
 #pragma unroll
           for (int i = 0; i < NIA; ++i)
@@ -824,7 +895,12 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
                 (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
                 16, 0, 0);
         }
-        if constexpr (FB) {
+        if constexpr (BKM && BUF) {
+          const bool kin = k0 + kc < lb.K;
+#pragma unroll
+          for (int i = 0; i < NIB; ++i)
+            dma16(rb, sB + (w * NIB + i) * 512, kin ? vb[i] + kbyte : kBufOOB);
+        } else if constexpr (FB) {
           // k0 advances by BK per call: the slot state tracks it
 #pragma unroll
           for (int i = 0; i < NIB; ++i) {
@@ -1005,6 +1081,31 @@ inline int pick_bn(int N, bool allow96) {
   return best;
 }
 
+template <class LA, bool AK, class LB, bool BKM, bool BUF>
+hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
+                     int K, int k_split, int tiles_n, int tiles, int splits,
+                     int bn, dim3 grid, hipStream_t s) {
+  if (bn == 64)
+    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64, BUF>), grid,
+                       dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
+                       tiles_n, tiles, splits);
+  else if constexpr (BKM) {
+    if (bn == 96)
+      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 96, BUF>), grid,
+                         dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
+                         tiles_n, tiles, splits);
+    else
+      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF>), grid,
+                         dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
+                         tiles_n, tiles, splits);
+  } else {
+    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF>), grid,
+                       dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
+                       tiles_n, tiles, splits);
+  }
+  return hipGetLastError();
+}
+
 template <class LA, bool AK, class LB, bool BKM>
 hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                   int K, int splits, int groups, hipStream_t s) {
@@ -1017,25 +1118,15 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   splits = (K + k_split - 1) / k_split;
   const int tiles = tiles_m * tiles_n;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  if (bn == 64)
-    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64>), grid, dim3(NTHR), 0,
-                       s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
-                       splits);
-  else if constexpr (BKM) {
-    if (bn == 96)
-      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 96>), grid, dim3(NTHR),
-                         0, s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
-                         splits);
-    else
-      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128>), grid,
-                         dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
-                         tiles_n, tiles, splits);
-  } else {
-    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128>), grid, dim3(NTHR), 0,
-                       s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
-                       splits);
+  if constexpr (LA::kBuf && LB::kBuf && AK && BKM) {
+    if (la.buf_ok(groups) && lb.buf_ok(groups))
+      return launch_bn<LA, AK, LB, BKM, true>(la, lb, epi, M, N, K, k_split,
+                                              tiles_n, tiles, splits, bn,
+                                              grid, s);
   }
-  return hipGetLastError();
+  return launch_bn<LA, AK, LB, BKM, false>(la, lb, epi, M, N, K, k_split,
+                                           tiles_n, tiles, splits, bn, grid,
+                                           s);
 }
 
 
