@@ -111,8 +111,19 @@ struct DenseMN {
   __device__ __forceinline__ Ctx col_ctx(int c) const { return Ctx{c}; }
   static constexpr bool kGlds = true;
   static constexpr bool kFast = false;
-  static constexpr bool kBuf = false;
-  bool buf_ok(int) const { return false; }
+  // buffer DMA only without the ones column (its page is another tensor)
+  static constexpr bool kBuf = true;
+  bool buf_ok(int groups) const {
+    return ones_col < 0 &&
+           ((long long)(K - 1) * ld + cols) * 2 +
+                   (long long)(groups - 1) * gstride * 2 < kBufMaxBytes;
+  }
+  __device__ const void* dbase() const { return p; }
+  // byte offset of chunk column c in k-row kr (kBufOOB past the columns)
+  __device__ __forceinline__ uint32_t col_voff(int c, int kr) const {
+    return c < cols ? ((uint32_t)kr * (uint32_t)ld + (uint32_t)c) * 2u
+                    : kBufOOB;
+  }
   __device__ bool dma_ok() const {
     return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
   }
@@ -587,7 +598,7 @@ struct Epi {
   int ones_col;    // column routed to bias_grad[m] (fused bias gradient)
   float* bias_grad;
   int run_in, run_out;  // column remap n = kh*run_in + j -> kh*run_out + j
-  __device__ void store(int gi, int m, int n, float v) const {
+  __device__ __forceinline__ void store(int gi, int m, int n, float v) const {
     if (m >= M || n >= N) return;
     if (n == ones_col) {
       atomicAdd(bias_grad + m + gi * grow, v * alpha);
@@ -616,12 +627,14 @@ struct Epi {
     if (out_f32) ((float*)c)[idx] = v;
     else ((uint16_t*)c)[idx] = f2bf(v);
   }
-  // The common case, decided once per block (wave-uniform): no atomics,
-  // remaps, fused bias-gradient column or beta; per-column bias; 16-B
-  // aligned rows.  Then every 8-column chunk is one straight-line store.
-  __host__ __device__ bool fast_ok() const {
-    return !atomic && !run_in && ones_col < 0 && beta == 0.f &&
-           bias_mode != 2 && (ldc & 7) == 0 && (((uintptr_t)c) & 15) == 0 &&
+  // The common case, decided once per block (wave-uniform): no atomics or
+  // remaps, per-column bias, 16-B aligned rows.  Then every 8-column chunk
+  // (except one holding the fused bias-gradient column) is one straight-line
+  // store; beta != 0 adds beta * C (the gradient accumulation of an unsplit
+  // weight-gradient GEMM: read-modify-write instead of f32 atomics).
+  __host__ __device__ __forceinline__ bool fast_ok() const {
+    return !atomic && !run_in && bias_mode != 2 && (ldc & 7) == 0 &&
+           (((uintptr_t)c) & 15) == 0 &&
            (gcol & 7) == 0 &&
            (bias_mode != 1 || (((uintptr_t)bias) & 15) == 0) &&
            (!aux || ((ld_aux & 7) == 0 && (((uintptr_t)aux) & 15) == 0));
@@ -635,6 +648,22 @@ struct Epi {
     if (alpha != 1.f) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] *= alpha;
+    }
+    if (beta != 0.f) {
+      float o[8];
+      if (out_f32) {
+        const float4* d = (const float4*)((const float*)c + idx);
+        const float4 lo = d[0], hi = d[1];
+        o[0] = lo.x; o[1] = lo.y; o[2] = lo.z; o[3] = lo.w;
+        o[4] = hi.x; o[5] = hi.y; o[6] = hi.z; o[7] = hi.w;
+      } else {
+        const uint4 ov = *(const uint4*)((const uint16_t*)c + idx);
+        const uint16_t* oh = (const uint16_t*)&ov;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o[q] = bf2f(oh[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += beta * o[q];
     }
     if (bias_mode == 1) {
       const float4 b0 = *(const float4*)(bias + gn);
@@ -660,7 +689,8 @@ struct Epi {
     }
   }
   // 8 consecutive columns of one row: 16-B vector stores when possible
-  __device__ void store8(int gi, int m, int n, const float* v) const {
+  __device__ __forceinline__ void store8(int gi, int m, int n,
+                                         const float* v) const {
     if (m >= M || n >= N) return;
     int gm = m + gi * grow, gn = n + gi * gcol;
     long long idx = (long long)gm * ldc + gn;
@@ -813,11 +843,13 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       int ka[NIA], kb[NIB];
       // the lane's chunk offset along K: the same in every A slot
       const int kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
-      // BUF (K-major loaders, tensors < 2 GiB): LDS-DMA through buffer
+      // BUF (loaders with kBuf, tensors < 2 GiB): LDS-DMA through buffer
       // descriptors - a per-slot 32-bit byte offset instead of a 64-bit
       // address, and kBufOOB lanes read zeros (no zero-page select)
-      const __amdgpu_buffer_rsrc_t ra = rsrc_of<LA, BUF>(la);
-      const __amdgpu_buffer_rsrc_t rb = rsrc_of<LB, BUF>(lb);
+      // per operand: BUF kernels use buffers for every loader that can
+      constexpr bool BA = BUF && LA::kBuf, BB = BUF && LB::kBuf;
+      const __amdgpu_buffer_rsrc_t ra = rsrc_of<LA, BA>(la);
+      const __amdgpu_buffer_rsrc_t rb = rsrc_of<LB, BB>(lb);
       uint32_t va[NIA], vb[NIB];
       // MN-major B at BN = 64: the DMA image keeps the 256-B rows of the
       // 128-wide layout; the chunks of columns >= 64 read the zero page
@@ -828,7 +860,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         if constexpr (AK && LA::kFast) {
           fa[i] = la.drow(m0 + 8 * I + (lane >> 3));
           ka[i] = kc;
-        } else if constexpr (AK && BUF) {
+        } else if constexpr (AK && BA) {
           va[i] = la.row_voff(m0 + 8 * I + (lane >> 3));
           ka[i] = kc;
         } else if constexpr (AK) {
@@ -839,14 +871,17 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         } else {
           int hkv = ((lane >> 4) & 3) | (((I >> 1) & 1) << 2);
           int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
-          da[i] = la.col_ctx(m0 + 8 * c);
           ka[i] = 4 * I + (lane >> 4);
+          if constexpr (BA)
+            va[i] = la.col_voff(m0 + 8 * c, ka[i]);
+          else
+            da[i] = la.col_ctx(m0 + 8 * c);
         }
       }
 #pragma unroll
       for (int i = 0; i < NIB; ++i) {
         const int I = w * NIB + i;
-        if constexpr (BKM && BUF) {
+        if constexpr (BKM && BB) {
           vb[i] = lb.row_voff(n0 + 8 * I + (lane >> 3));
           kb[i] = kc;
         } else if constexpr (BKM) {
@@ -861,6 +896,8 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
           kb[i] = 4 * I + (lane >> 4);
           if constexpr (FB)
             fb[i] = lb.dcol(n0 + 8 * c, kbeg + kb[i], bz[i]);
+          else if constexpr (BB)
+            vb[i] = bz[i] ? kBufOOB : lb.col_voff(n0 + 8 * c, kb[i]);
           else
             db[i] = lb.col_ctx(n0 + (bz[i] ? 0 : 8 * c));
         }
@@ -869,12 +906,12 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       auto issue = [&](int k0, uint16_t* sA, uint16_t* sB) {
         // the K-major lanes' byte offset along K and its validity (BUF)
         const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
-        if constexpr (AK && LA::kFast && BUF) {
+        if constexpr (AK && LA::kFast && BA) {
           const DTap tp = la.dtap(k0 + kc);
 #pragma unroll
           for (int i = 0; i < NIA; ++i)
             dma16(ra, sA + (w * NIA + i) * 512, la.dvoff(fa[i], tp));
-        } else if constexpr (AK && BUF) {
+        } else if constexpr (AK && BA) {
           const bool kin = k0 + kc < la.K;
 #pragma unroll
           for (int i = 0; i < NIA; ++i)
@@ -887,6 +924,13 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
                 (const void*)la.dsrc(fa[i], tp),
                 (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
                 16, 0, 0);
+        } else if constexpr (!AK && BA) {
+          // MN-major: the k-row advance is one uniform byte offset per tile
+          const uint32_t kadv = (uint32_t)k0 * (uint32_t)la.ld * 2u;
+#pragma unroll
+          for (int i = 0; i < NIA; ++i)
+            dma16(ra, sA + (w * NIA + i) * 512,
+                  k0 + ka[i] < la.K ? va[i] + kadv : kBufOOB);
         } else {
 #pragma unroll
           for (int i = 0; i < NIA; ++i)
@@ -895,11 +939,17 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
                 (__attribute__((address_space(3))) void*)(sA + (w * NIA + i) * 512),
                 16, 0, 0);
         }
-        if constexpr (BKM && BUF) {
+        if constexpr (BKM && BB) {
           const bool kin = k0 + kc < lb.K;
 #pragma unroll
           for (int i = 0; i < NIB; ++i)
             dma16(rb, sB + (w * NIB + i) * 512, kin ? vb[i] + kbyte : kBufOOB);
+        } else if constexpr (!BKM && BB) {
+          const uint32_t kadv = (uint32_t)k0 * (uint32_t)lb.ld * 2u;
+#pragma unroll
+          for (int i = 0; i < NIB; ++i)
+            dma16(rb, sB + (w * NIB + i) * 512,
+                  k0 + kb[i] < lb.K ? vb[i] + kadv : kBufOOB);
         } else if constexpr (FB) {
           // k0 advances by BK per call: the slot state tracks it
 #pragma unroll
@@ -1047,7 +1097,8 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     float4 lo = src[0], hi = src[1];
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    if (fast && n0 + c8 + 8 <= epi.N)
+    if (fast && n0 + c8 + 8 <= epi.N &&
+        (epi.ones_col < 0 || n0 + c8 + 8 <= epi.ones_col))
       epi.store8_fast(gi, m0 + row, n0 + c8, v);
     else
       epi.store8(gi, m0 + row, n0 + c8, v);
@@ -1107,6 +1158,12 @@ hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
 }
 
 template <class LA, bool AK, class LB, bool BKM>
+hipError_t launch_sel(const LA& la, const LB& lb, const Epi& epi, int M,
+                      int N, int K, int k_split, int tiles_n, int tiles,
+                      int splits, int groups, int bn, dim3 grid,
+                      hipStream_t s);
+
+template <class LA, bool AK, class LB, bool BKM>
 hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                   int K, int splits, int groups, hipStream_t s) {
   // a 96-wide MN-major B has no register-staged path (12 chunks per row)
@@ -1118,8 +1175,27 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   splits = (K + k_split - 1) / k_split;
   const int tiles = tiles_m * tiles_n;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  if constexpr (LA::kBuf && LB::kBuf && AK && BKM) {
-    if (la.buf_ok(groups) && lb.buf_ok(groups))
+  if (epi.atomic && splits == 1) {
+    // an unsplit accumulate writes every element once: read-modify-write in
+    // the staged epilogue instead of one f32 atomic per element (the FC
+    // weight gradients at batch 512 were bound by the atomic rate)
+    Epi e = epi;
+    e.atomic = 0;
+    e.beta = 1.f;
+    return launch_sel<LA, AK, LB, BKM>(la, lb, e, M, N, K, k_split, tiles_n,
+                                       tiles, splits, groups, bn, grid, s);
+  }
+  return launch_sel<LA, AK, LB, BKM>(la, lb, epi, M, N, K, k_split, tiles_n,
+                                     tiles, splits, groups, bn, grid, s);
+}
+
+template <class LA, bool AK, class LB, bool BKM>
+hipError_t launch_sel(const LA& la, const LB& lb, const Epi& epi, int M,
+                      int N, int K, int k_split, int tiles_n, int tiles,
+                      int splits, int groups, int bn, dim3 grid,
+                      hipStream_t s) {
+  if constexpr (LA::kBuf || LB::kBuf) {
+    if ((!LA::kBuf || la.buf_ok(groups)) && (!LB::kBuf || lb.buf_ok(groups)))
       return launch_bn<LA, AK, LB, BKM, true>(la, lb, epi, M, N, K, k_split,
                                               tiles_n, tiles, splits, bn,
                                               grid, s);

@@ -38,7 +38,10 @@ def main():
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 512
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     cases = [("gemm_8192", lambda: gemm(8192, 8192, 8192)),
-             ("fc6_fwd", lambda: gemm(B, 4096, 9216))]
+             ("fc6_fwd", lambda: gemm(B, 4096, 9216)),
+             ("fc6_dgrad", lambda: gemm(B, 9216, 4096, tb=False)),
+             ("fc6_wgrad", lambda: gemm(4096, 9216, B, ta=True, tb=False)),
+             ("fc7_fwd", lambda: gemm(B, 4096, 4096))]
     layers = {"conv1s2d": None,
               "conv2": (B, 27, 27, 96, 256, 5, 1, 2, 2),
               "conv3": (B, 13, 13, 256, 384, 3, 1, 1, 1),
