@@ -75,7 +75,9 @@ def main():
                        "normalization_type": "mean_disp",
                        "generate_on_device": backend == "hip"},
         layers=layers_fn(), decision_config={"max_epochs": None,
-                                             "fail_iterations": None})
+                                             "fail_iterations": None},
+        # capture the forward / backward segments inside the warmup steps
+        graph_warmup=max(0, min(2, args.warmup - 1)))
     wf.initialize(device=device)
 
     def sync():
@@ -124,7 +126,11 @@ def main():
                           "per_gpu_batch": args.batch, "seq_len": None,
                           "parallelism": "dp%d" % dp.world_size,
                           "image": shape, "grad_allreduce":
-                          "bucketed RCCL, overlapped with backward"}}
+                          "bucketed RCCL, overlapped with backward",
+                          "hip_graphs": [
+                              "%s:%d captured/%d replayed" % (
+                                  s.name, s.captures, s.replays)
+                              for s in getattr(wf, "graph_segments_", [])]}}
         print(json.dumps(out), flush=True)
         if args.profile_json:
             with open(args.profile_json, "w") as f:

@@ -424,9 +424,13 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x, uint32_t seed) {
   x ^= x >> 16;
   return x;
 }
+// seed_dev (optional): the seed is read from device memory instead, so a
+// captured HIP graph draws a fresh mask every replay (hvk_seed_advance).
 __global__ void dropout_kernel(const void* x, int xdt, void* y, int ydt,
                                long long n, uint32_t seed, uint32_t thresh,
-                               float scale, uint8_t* mask_out) {
+                               float scale, uint8_t* mask_out,
+                               const uint32_t* seed_dev) {
+  if (seed_dev) seed = __builtin_amdgcn_readfirstlane(seed_dev[0]);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     bool keep = hash32((uint32_t)i, seed) >= thresh;
@@ -914,7 +918,31 @@ HVK_API int hvk_dropout(const void* x, int xdt, void* y, int ydt, long long n,
   uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
   float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
-                     y, ydt, n, seed, thresh, scale, (uint8_t*)mask_out);
+                     y, ydt, n, seed, thresh, scale, (uint8_t*)mask_out,
+                     (const uint32_t*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// dropout with the seed in device memory (graph-safe: the forward unit
+// advances it with hvk_seed_advance inside the captured step)
+HVK_API int hvk_dropout_dev(const void* x, int xdt, void* y, int ydt,
+                            long long n, const void* seed_dev, float p,
+                            void* mask_out, hipStream_t s) {
+  uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
+                     y, ydt, n, 0u, thresh, scale, (uint8_t*)mask_out,
+                     (const uint32_t*)seed_dev);
+  return (int)hipGetLastError();
+}
+
+// seed <- hash(seed + 1): a per-step seed sequence that lives on the device
+__global__ void seed_advance_kernel(uint32_t* seed) {
+  if (threadIdx.x == 0) seed[0] = hash32(seed[0] + 1u, 0x2545F491u);
+}
+HVK_API int hvk_seed_advance(void* seed, hipStream_t s) {
+  hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, s,
+                     (uint32_t*)seed);
   return (int)hipGetLastError();
 }
 

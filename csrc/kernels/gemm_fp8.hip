@@ -552,8 +552,11 @@ __global__ void fp8_amax_kernel(const void* x, long long n, float* st,
 
 // history[idx] = current amax (or every slot when fill), current = 0; one
 // thread per scaler of a [count][hist + 1] state block
+// step (optional): the history slot is step % hist read from device memory
+// (graph-safe roll; the registry advances the counter after the launch)
 __global__ void fp8_roll_kernel(float* states, int count, int hist, int idx,
-                                int fill) {
+                                int fill, const int* step) {
+  if (step) idx = __builtin_amdgcn_readfirstlane(step[0]) % hist;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= count) return;
   float* st = states + (long long)s * (hist + 1);
@@ -610,7 +613,15 @@ HVK_API int hvk_fp8_roll(float* states, int count, int hist, int idx,
                          int fill, hipStream_t s) {
   if (count <= 0) return 0;
   hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
-                     states, count, hist, idx, fill);
+                     states, count, hist, idx, fill, (const int*)nullptr);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_fp8_roll_dev(float* states, int count, int hist,
+                             const void* step, hipStream_t s) {
+  if (count <= 0) return 0;
+  hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
+                     states, count, hist, 0, 0, (const int*)step);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,212 @@
+"""GraphSegment dispatch (veles_amd/graphs.py) on the CPU: a host-side
+recorder stands in for HIP-graph capture - while "capturing", launches are
+recorded instead of executed, and replay() executes the recording - so the
+warmup / capture / replay / invalidation / failure state machine is pinned
+without a GPU (the real capture is covered by tests/test_graphs_gpu.py)."""
+import pytest
+import torch
+
+from veles_amd.graphs import GraphSegment
+from veles_amd.memory import Array
+
+_ACTIVE = []
+
+
+def launch(fn):
+    if _ACTIVE:
+        _ACTIVE[-1].ops.append(fn)
+    else:
+        fn()
+
+
+class FakeGraph(object):
+    def __init__(self):
+        self.ops = []
+
+    def replay(self):
+        for fn in self.ops:
+            fn()
+
+
+class _Ctx(object):
+    def __init__(self, g):
+        self.g = g
+
+    def __enter__(self):
+        _ACTIVE.append(self.g)
+
+    def __exit__(self, *exc):
+        _ACTIVE.remove(self.g)
+
+
+class Recording(GraphSegment):
+    @staticmethod
+    def new_graph():
+        g = FakeGraph()
+        return g, _Ctx(g)
+
+
+class U(object):
+    """A unit whose run() does host work (log) + 'device' work (count)."""
+
+    def __init__(self, name, log, dev, fail_in_capture=False):
+        self.name = name
+        self.log = log
+        self.dev = dev
+        self.fail_in_capture = fail_in_capture
+        self.output = Array()
+
+    def run(self):
+        if self.fail_in_capture and _ACTIVE:
+            raise RuntimeError("operation not permitted when capturing")
+        self.log.append(self.name)
+        launch(lambda: self.dev.__setitem__(self.name,
+                                            self.dev.get(self.name, 0) + 1))
+
+
+def _pass(seg):
+    for u in seg.units:
+        seg.run_unit(u)
+
+
+def _make(warmup=2, **kw):
+    log, dev = [], {}
+    units = [U("a", log, dev), U("b", log, dev, **kw), U("c", log, dev)]
+    key = [("train", 8)]
+    hooks = {"pre": 0, "replay": 0}
+    inp = Array()
+    inp.devmem = torch.zeros(2)
+    seg = Recording("t", units, lambda: key[0], lambda: [inp], warmup=warmup,
+                    pre_hooks=[lambda: hooks.__setitem__("pre",
+                                                         hooks["pre"] + 1)],
+                    replay_hooks=[lambda: hooks.__setitem__(
+                        "replay", hooks["replay"] + 1)])
+    return seg, log, dev, key, hooks, inp
+
+
+def test_warmup_capture_replay():
+    seg, log, dev, key, hooks, _ = _make()
+    for _ in range(2):
+        _pass(seg)
+    assert log == list("abcabc") and dev == {"a": 2, "b": 2, "c": 2}
+    assert seg.captures == 0
+    _pass(seg)  # captured: host code runs, the device work runs ONCE
+    assert log == list("abc" * 3)
+    assert dev == {"a": 3, "b": 3, "c": 3}
+    assert seg.captures == 1 and hooks["replay"] == 0
+    for _ in range(4):
+        _pass(seg)  # replays: no host code, device work every pass
+    assert log == list("abc" * 3)
+    assert dev == {"a": 7, "b": 7, "c": 7}
+    assert seg.replays == 4 and hooks["replay"] == 4
+    assert hooks["pre"] == 7  # every eligible pass
+
+
+def test_new_key_warms_up_and_captures_separately():
+    seg, log, dev, key, hooks, _ = _make(warmup=1)
+    for _ in range(3):
+        _pass(seg)
+    assert seg.captures == 1 and seg.replays == 1
+    key[0] = ("valid", 8)
+    _pass(seg)  # eager warmup of the new key
+    assert seg.captures == 1 and log[-3:] == list("abc")
+    _pass(seg)
+    assert seg.captures == 2 and set(seg.graphs) == {("train", 8),
+                                                     ("valid", 8)}
+    key[0] = ("train", 8)
+    n = len(log)
+    _pass(seg)
+    assert len(log) == n and seg.replays == 2
+    assert dev["a"] == 6
+
+
+def test_key_none_runs_eagerly():
+    seg, log, dev, key, hooks, _ = _make(warmup=0)
+    key[0] = None
+    for _ in range(3):
+        _pass(seg)
+    assert seg.captures == 0 and log == list("abc" * 3)
+    assert hooks["pre"] == 0
+
+
+def test_moved_input_drops_the_graph():
+    seg, log, dev, key, hooks, inp = _make(warmup=1)
+    for _ in range(3):
+        _pass(seg)
+    assert seg.replays == 1
+    inp.devmem = torch.ones(2)  # the loader swapped its buffer
+    _pass(seg)  # graph dropped, eager warmup again
+    assert seg.replays == 1 and log[-3:] == list("abc")
+    _pass(seg)
+    assert seg.captures == 2
+    _pass(seg)
+    assert seg.replays == 2
+    assert dev["a"] == 6
+
+
+def test_failed_capture_reruns_eagerly_and_pins_the_key():
+    seg, log, dev, key, hooks, _ = _make(warmup=1, fail_in_capture=True)
+    _pass(seg)
+    _pass(seg)  # capture attempt: b fails -> a, b re-run eagerly, c eager
+    assert seg.failures == 1 and seg.captures == 0
+    assert dev == {"a": 2, "b": 2, "c": 2}
+    assert key[0] in seg.eager_keys and not _ACTIVE
+    _pass(seg)
+    assert dev == {"a": 3, "b": 3, "c": 3} and seg.replays == 0
+
+
+def test_replay_reattaches_recorded_tensors():
+    seg, log, dev, key, hooks, _ = _make(warmup=1)
+    b = seg.units[1]
+    t_train, t_valid = torch.zeros(3), torch.zeros(4)
+    orig = U.run
+
+    def run_alias(self):
+        orig(self)
+        if self.name == "b":
+            self.output.devmem = t_train if key[0][0] == "train" \
+                else t_valid
+    U.run = run_alias
+    try:
+        for _ in range(2):
+            _pass(seg)  # train: warmup + capture
+        key[0] = ("valid", 8)
+        for _ in range(2):
+            _pass(seg)
+        assert b.output.devmem is t_valid
+        key[0] = ("train", 8)
+        _pass(seg)  # replay restores what the train capture left
+        assert b.output.devmem is t_train
+    finally:
+        U.run = orig
+
+
+def test_unsafe_unit_keeps_segment_eager():
+    log, dev = [], {}
+    u = U("x", log, dev)
+    u.graph_safe = False
+    seg = Recording("t", [U("a", log, dev), u], lambda: 1, warmup=0)
+    for _ in range(3):
+        _pass(seg)
+    assert seg.captures == 0 and log == list("ax" * 3)
+
+
+def test_install_is_noop_on_cpu():
+    from veles_amd.graphs import install_step_graphs
+
+    class WF(object):
+        device = None
+    assert install_step_graphs(WF()) == []
+
+
+@pytest.mark.parametrize("seed", [0, 1, 12345, 2 ** 31 - 1, 2 ** 32 - 1])
+def test_seed_advance_reference(seed):
+    from veles_amd import ops
+    t = torch.tensor([seed - (1 << 32) if seed >= (1 << 31) else seed],
+                     dtype=torch.int32)
+    ops.seed_advance(t)
+    assert int(t[0]) & 0xFFFFFFFF == ops.seed_advance_ref(seed)
+    x = torch.randn(1000)
+    y1 = ops.dropout(x, 0.3, None, seed_dev=t)
+    y2 = ops.dropout(x, 0.3, int(t[0]) & 0xFFFFFFFF)
+    assert torch.equal(y1, y2)

@@ -1,0 +1,115 @@
+"""HIP-graph capture of the train step (veles_amd/graphs.py) on an MI355X:
+the same StandardWorkflow trained with the forward / backward segments
+captured and replayed must match the eager run (up to the f32 atomics'
+summation order), replays must really advance the device-side dropout seed
+and fp8 history, and the host bookkeeping of skipped units must hold."""
+import numpy
+import pytest
+import torch
+
+from veles_amd.utils.config import root
+
+pytestmark = pytest.mark.gpu
+
+G = {"learning_rate": 0.02, "gradient_moment": 0.9, "weights_decay": 1e-4}
+LAYERS = [
+    {"type": "conv_str", "->": {"n_kernels": 32, "kx": 3, "ky": 3,
+                                "padding": 1}, "<-": dict(G)},
+    {"type": "norm", "alpha": 1e-4, "beta": 0.75, "n": 5, "k": 2},
+    {"type": "max_pooling", "->": {"kx": 3, "ky": 3, "sliding": 2}},
+    {"type": "conv_relu", "->": {"n_kernels": 64, "kx": 3, "ky": 3,
+                                 "padding": 1}, "<-": dict(G)},
+    {"type": "max_pooling", "->": {"kx": 2, "ky": 2, "sliding": 2}},
+    {"type": "all2all_relu", "->": {"output_sample_shape": 256},
+     "<-": dict(G)},
+    {"type": "dropout", "dropout_ratio": 0.5},
+    {"type": "softmax", "->": {"output_sample_shape": 10}, "<-": dict(G)}]
+
+
+def _train(graphs, steps, precision="bfloat16", layers=LAYERS):
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    from veles_amd.prng import random_generator
+    import veles_amd.loader  # noqa: F401
+    old = (root.common.engine.graphs, root.common.engine.precision_type)
+    root.common.engine.graphs = graphs
+    root.common.engine.precision_type = precision
+    try:
+        random_generator.get().seed(1234)
+        numpy.random.seed(1234)
+        torch.manual_seed(0)
+        wf = StandardWorkflow(
+            DummyLauncher(), loader_name="synthetic_images",
+            loader_config={"dataset": "mnist", "class_lengths": (0, 128, 640),
+                           "minibatch_size": 64, "normalization_type":
+                           "mean_disp", "seed": 7, "noise": 110.0},
+            layers=layers, decision_config={"max_epochs": None,
+                                            "fail_iterations": None})
+        wf.initialize(device=Device(backend="hip"))
+        wf.run_steps(steps)
+        torch.cuda.synchronize()
+        return wf
+    finally:
+        root.common.engine.graphs, root.common.engine.precision_type = old
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+def test_graphed_training_matches_eager():
+    steps = 25  # 2.5 epochs: TRAIN and VALID keys, captures + replays
+    eager = _train(False, steps)
+    graphed = _train(True, steps)
+    assert not getattr(eager, "graph_segments_", [])
+    fwd, bwd = graphed.graph_segments_
+    assert fwd.captures == 2 and bwd.captures == 1  # (TRAIN, VALID) / TRAIN
+    assert fwd.failures == 0 and bwd.failures == 0
+    assert bwd.replays >= steps - 4 and fwd.replays >= steps - 4
+    assert graphed.param_store_.steps == eager.param_store_.steps == steps
+    # same trajectory (the f32 atomics of split-K / weight gradients sum in
+    # a different order run to run: a tolerance, not bit equality)
+    assert _rel(graphed.param_store_.master, eager.param_store_.master) < 2e-2
+    he, hg = eager.decision.history, graphed.decision.history
+    assert len(he) == len(hg) >= 2
+    for a, b in zip(he, hg):
+        assert abs(a["validation_loss"] - b["validation_loss"]) < \
+            0.05 * abs(a["validation_loss"]) + 1e-3
+    # the replayed dropout advanced its device seed once per TRAIN step
+    from veles_amd import ops
+    drop = [u for u in graphed.forwards if type(u).__name__ ==
+            "DropoutForward"][0]
+    s = drop.seed & 0xFFFFFFFF
+    for _ in range(steps):
+        s = ops.seed_advance_ref(s)
+    assert int(drop.seed_dev_.cpu()[0]) & 0xFFFFFFFF == s
+
+
+def test_graph_replay_is_faster_for_a_small_step():
+    """The point of capture: a small network's step is host-bound eagerly
+    (one Python dispatch per kernel); a replay is one graph launch."""
+    import time
+    small = [dict(LAYERS[0]), LAYERS[2], dict(LAYERS[5]), LAYERS[7]]
+    res = {}
+    for graphs in (False, True):
+        wf = _train(graphs, 6, layers=small)
+        wf.run_steps(5)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wf.run_steps(30)
+        torch.cuda.synchronize()
+        res[graphs] = time.perf_counter() - t0
+    print("eager %.2f ms/step, graphed %.2f ms/step" % (
+        res[False] / 30 * 1e3, res[True] / 30 * 1e3))
+    assert res[True] < res[False]
+
+
+def test_graphed_fp8_rolls_the_history():
+    from veles_amd.ops import fp8
+    steps = 12
+    wf = _train(True, steps, precision="float8")
+    fwd, bwd = wf.graph_segments_
+    assert bwd.replays > 0 and bwd.failures == 0 and fwd.failures == 0
+    r = fp8.registry(torch.device("cuda", torch.cuda.current_device()))
+    assert int(r.step_dev.cpu()[0]) == r.step

@@ -1,0 +1,331 @@
+"""HIP-graph capture of the static parts of a training step.
+
+The reference runs every unit's kernels through per-launch Python / OpenCL
+calls (``AcceleratedUnit.execute_kernel``, accelerated_units.py:436-455) and
+its native runtime plans one arena per workflow (libVeles
+src/workflow.cc:44-161); SURVEY §2.6 / §7.4 ask for the MI355X equivalent:
+"HIP-graph capture of the static train step".  Here a :class:`GraphSegment`
+is a run of consecutive units whose ``run()`` only enqueues device work:
+
+* the forward segment: every forward unit + the evaluator;
+* the backward segment: every GD unit (err_input / weight-gradient kernels
+  and the fused update launched by the last one).
+
+The unit graph still drives the step (loader, decision, snapshotter, LR
+policy stay eager Python between the segments).  For each segment and each
+*key* (minibatch class and size, testing flag) the first ``warmup`` passes
+run eagerly (lazy allocations, fp8 history priming, split-K workspaces),
+the next pass runs inside ``torch.cuda.graph`` capture and is then replayed
+once, and every later pass with that key is ONE ``hipGraphLaunch`` - the
+segment's units are skipped on the host.  What makes a replay correct:
+
+* kernel arguments that change per step live on the device: the dropout
+  seed sequence (``hvk_seed_advance``), the fp8 history slot
+  (``hvk_fp8_roll_dev``), the SGD segment table (refreshed by a pre-replay
+  hook, ``ParameterStore.refresh_table``, never captured);
+* the external inputs of a segment (the loader's minibatch buffers) are
+  checked by identity before every replay - a moved buffer drops the graph;
+* the device tensors the segment's Arrays point at are recorded at capture
+  and re-attached on replay (a unit may alias ``output`` to ``input``
+  depending on the key, e.g. dropout on non-TRAIN minibatches), and every
+  tensor the graph touches is kept alive as long as the graph;
+* host bookkeeping of skipped units runs as replay hooks
+  (``ParameterStore.replayed_step``).
+
+A unit class that cannot be captured sets ``graph_safe = False`` (e.g.
+stochastic pooling: a torch.Generator seeded from the host per minibatch);
+any such unit in a segment keeps that segment eager.  A capture that fails
+(an op that synchronises, an unsupported call) re-runs the pass eagerly and
+pins that key to eager mode.  Multi-rank steps (RCCL collectives inside the
+backward) and gradient accumulation stay eager (``graph_safe`` of the
+parameter store).  Disable with ``root.common.engine.graphs = False`` or
+``VELES_AMD_GRAPHS=0``.
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+__all__ = ["GraphSegment", "graphs_enabled", "install_step_graphs"]
+
+_log = logging.getLogger("graphs")
+
+
+def graphs_enabled():
+    from veles_amd.utils.config import root, get
+    env = os.environ.get("VELES_AMD_GRAPHS")
+    if env is not None:
+        return env not in ("0", "false", "False", "")
+    return bool(get(root.common.engine.graphs, True))
+
+
+def _arrays_of(unit):
+    from veles_amd.memory import Array
+    return [v for v in vars(unit).values() if isinstance(v, Array)]
+
+
+class _Captured(object):
+    __slots__ = ("graph", "key", "inputs", "arrays", "keep")
+
+    def __init__(self, graph, key, inputs):
+        self.graph = graph
+        self.key = key
+        self.inputs = inputs      # [(Array, tensor)] checked before replay
+        self.arrays = []          # [(Array, tensor)] re-attached on replay
+        self.keep = []            # tensors the graph reads / writes
+
+    def inputs_ok(self):
+        for arr, t in self.inputs:
+            if arr._devmem is not t:
+                return False
+        return True
+
+    def restore(self):
+        for arr, t in self.arrays:
+            if arr._devmem is not t:
+                arr.devmem = t
+            elif arr._state != 0 and t is not None and t.is_cuda:
+                arr._state = 0
+
+
+class GraphSegment(object):
+    """Capture / replay of ``units`` (run consecutively, head first).
+
+    key_fn() -> hashable key of the pass, or None to run it eagerly.
+    inputs_fn() -> Arrays produced outside the segment that it reads.
+    pre_hooks run before every replay or capture (eagerly); replay_hooks
+    after every replay, in place of the skipped units' host bookkeeping."""
+
+    MAX_GRAPHS = 8
+
+    def __init__(self, name, units, key_fn, inputs_fn=None, warmup=2,
+                 pre_hooks=(), replay_hooks=()):
+        self.name = name
+        self.units = list(units)
+        self.head = self.units[0]
+        self.tail = self.units[-1]
+        self.key_fn = key_fn
+        self.inputs_fn = inputs_fn or (lambda: [])
+        self.warmup = warmup
+        self.pre_hooks = list(pre_hooks)
+        self.replay_hooks = list(replay_hooks)
+        self.graphs = {}
+        self.seen = {}
+        self.eager_keys = set()
+        self.mode = None
+        self.cur = None
+        self.ctx = None
+        self.pos = 0
+        self.captures = 0
+        self.replays = 0
+        self.failures = 0
+        self.safe = all(getattr(u, "graph_safe", True) for u in self.units)
+        for u in self.units:
+            u.graph_segment_ = self
+
+    def uninstall(self):
+        self.drop()
+        for u in self.units:
+            if getattr(u, "graph_segment_", None) is self:
+                u.graph_segment_ = None
+
+    def drop(self, key=None):
+        if key is None:
+            self.graphs.clear()
+        else:
+            self.graphs.pop(key, None)
+
+    # -- per-unit dispatch (Unit.do_run) ---------------------------------
+    def run_unit(self, unit):
+        if unit is self.head:
+            self._begin()
+        mode = self.mode
+        if mode == "replay":
+            if unit is self.tail:
+                self.mode = None
+            return
+        self.pos += 1
+        try:
+            type(unit).run(unit)
+        except BaseException as e:
+            if mode == "capture":
+                self._capture_failed(unit, e)
+                return
+            self.mode = None
+            raise
+        if unit is self.tail:
+            self._end()
+
+    def _begin(self):
+        if self.mode == "capture":  # a previous pass never reached the tail
+            self._abort_capture()
+        self.mode = "eager"
+        self.pos = 0
+        if not self.safe:
+            return
+        key = self.key_fn()
+        if key is None or key in self.eager_keys:
+            return
+        for h in self.pre_hooks:
+            h()
+        g = self.graphs.get(key)
+        if g is not None:
+            if g.inputs_ok():
+                g.graph.replay()
+                g.restore()
+                for h in self.replay_hooks:
+                    h()
+                self.replays += 1
+                self.mode = "replay"
+                return
+            _log.info("%s: inputs of graph %r moved, recapturing",
+                      self.name, key)
+            self.drop(key)
+            self.seen[key] = 0
+        n = self.seen.get(key, 0)
+        if n < self.warmup or len(self.graphs) >= self.MAX_GRAPHS:
+            self.seen[key] = n + 1
+            return
+        graph, ctx = self.new_graph()
+        self.cur = _Captured(graph, key, [(a, a._devmem)
+                                          for a in self.inputs_fn()])
+        self.ctx = ctx
+        self.ctx.__enter__()
+        self.mode = "capture"
+
+    @staticmethod
+    def new_graph():
+        """(graph with .replay(), capture context manager).  Tests swap in a
+        host-side recorder; on the GPU it is torch's HIP graph + capture
+        on a side stream with a private memory pool."""
+        import torch
+        graph = torch.cuda.CUDAGraph()
+        return graph, torch.cuda.graph(graph)
+
+    def _end(self):
+        if self.mode == "capture":
+            cur, ctx = self.cur, self.ctx
+            self.cur = self.ctx = None
+            try:
+                ctx.__exit__(None, None, None)
+            except Exception as e:  # noqa: BLE001 - capture_end failed
+                self._pin_eager(cur.key, e)
+                self.mode = None
+                self._rerun_eager(len(self.units))
+                return
+            self._record(cur)
+            self.graphs[cur.key] = cur
+            self.captures += 1
+            cur.graph.replay()  # capture records; this pass still has to run
+        self.mode = None
+
+    def _record(self, cur):
+        import torch
+        from veles_amd import ops
+        seen = set()
+        for u in self.units:
+            for a in _arrays_of(u):
+                if id(a) in seen:
+                    continue
+                seen.add(id(a))
+                cur.arrays.append((a, a._devmem))
+            for v in vars(u).values():
+                if isinstance(v, torch.Tensor):
+                    cur.keep.append(v)
+        cur.keep.extend(t for _, t in cur.arrays if t is not None)
+        # op-level workspaces / cached segment tensors the graph baked in
+        cur.keep.extend(ops._WS.values())
+        cur.keep.extend(ops._SEG_CACHE.values())
+
+    def _abort_capture(self):
+        ctx, cur = self.ctx, self.cur
+        self.ctx = self.cur = None
+        if ctx is not None:
+            try:
+                ctx.__exit__(None, None, None)
+            except Exception:  # noqa: BLE001
+                pass
+        if cur is not None:
+            self._pin_eager(cur.key, RuntimeError("capture interrupted"))
+
+    def _capture_failed(self, unit, exc):
+        key = self.cur.key if self.cur is not None else None
+        self._abort_capture()
+        if key is not None:
+            self._pin_eager(key, exc)
+        self.failures += 1
+        # nothing captured has executed: run this pass for real, eagerly
+        self.mode = "eager"
+        self._rerun_eager(self.pos)
+        if unit is self.tail:
+            self.mode = None
+
+    def _pin_eager(self, key, exc):
+        self.eager_keys.add(key)
+        self.graphs.pop(key, None)
+        _log.warning("%s: graph capture of %r failed (%s); this key runs "
+                     "eagerly", self.name, key, exc)
+
+    def _rerun_eager(self, upto):
+        for u in self.units[:upto]:
+            type(u).run(u)
+
+
+def _is_chain(units):
+    """True when the units run strictly one after another (no other unit
+    can run - and be captured - between the head and the tail)."""
+    for a, b in zip(units, units[1:]):
+        if set(a._links_to) != {b} or set(b._links_from) != {a}:
+            return False
+    return True
+
+
+def _full_key(wf):
+    ld = wf.loader
+    return (int(ld.minibatch_class), int(ld.minibatch_size),
+            bool(getattr(wf, "testing", False)))
+
+
+def install_step_graphs(wf, warmup=2):
+    """Attach forward / backward GraphSegments to a StandardWorkflow whose
+    device is a GPU.  Returns the installed segments (empty if disabled)."""
+    for seg in getattr(wf, "graph_segments_", None) or []:
+        seg.uninstall()
+    wf.graph_segments_ = []
+    dev = getattr(wf, "device", None)
+    if not graphs_enabled() or dev is None or not getattr(dev, "is_gpu",
+                                                          False):
+        return []
+    ld = wf.loader
+    ev = getattr(wf, "evaluator", None)
+    fwd_units = list(wf.forwards) + ([ev] if ev is not None else [])
+    if not fwd_units:
+        return []
+
+    def inputs():
+        out = []
+        for name in ("minibatch_data", "minibatch_labels",
+                     "minibatch_targets"):
+            a = getattr(ld, name, None)
+            if a is not None and getattr(a, "_devmem", None) is not None:
+                out.append(a)
+        return out
+
+    segs = []
+    if _is_chain(fwd_units):
+        segs.append(GraphSegment("forward", fwd_units,
+                                 lambda: _full_key(wf), inputs,
+                                 warmup=warmup))
+    gds = [g for g in reversed(getattr(wf, "gds", []) or []) if g is not None]
+    store = getattr(wf, "param_store_", None)
+    if gds and store is not None and _is_chain(gds):
+        def bkey():
+            if not store.graph_safe():
+                return None
+            return _full_key(wf)
+        segs.append(GraphSegment(
+            "backward", gds, bkey, inputs, warmup=warmup,
+            pre_hooks=[store.refresh_table],
+            replay_hooks=[store.replayed_step]))
+    wf.graph_segments_ = segs
+    return segs

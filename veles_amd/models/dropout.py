@@ -56,11 +56,27 @@ class DropoutForward(AcceleratedUnit):
             self.active_ = False
             return
         self.active_ = True
-        self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
         y = self.output.devmem
         if y is None or y is x or y.shape != x.shape or y.dtype != x.dtype:
             self.output.devmem = y = torch.empty_like(x)
+        if x.is_cuda:
+            # the seed sequence lives on the device (seeded once from the
+            # unit's reproducible generator): no host value enters the
+            # kernel arguments, so a captured step replays with fresh masks
+            sd = self.seed_dev_
+            if sd is None or sd.device != x.device:
+                self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
+                self.seed_dev_ = sd = torch.tensor(
+                    [self.seed], dtype=torch.int32, device=x.device)
+            ops.seed_advance(sd)
+            ops.dropout(x, self.dropout_ratio, None, out=y, seed_dev=sd)
+            return
+        self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
         ops.dropout(x, self.dropout_ratio, self.seed, out=y)
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.seed_dev_ = None
 
 
 class DropoutBackward(GradientDescentBase):
@@ -77,7 +93,9 @@ class DropoutBackward(GradientDescentBase):
             out = err
         else:
             ei = self.alloc_err_input(tuple(err.shape))
-            out = ops.dropout(err, fwd.dropout_ratio, fwd.seed, out=ei)
+            out = ops.dropout(err, fwd.dropout_ratio, fwd.seed, out=ei,
+                              seed_dev=getattr(fwd, "seed_dev_", None)
+                              if err.is_cuda else None)
         aux, aux_act = self.aux_tensor()
         if aux is not None:
             ei = self.alloc_err_input(tuple(err.shape))

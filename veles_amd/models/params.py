@@ -268,6 +268,40 @@ class ParameterStore(object):
             hook()
         return True
 
+    # -- HIP-graph replay support (veles_amd/graphs.py) ----------------------
+    def graph_safe(self):
+        """A captured backward may contain the update only when one step is
+        one launch sequence: no gradient accumulation over micro-steps and
+        no collectives (multi-rank steps run eagerly)."""
+        return self.accumulate == 1 and (
+            self.dp is None or self.dp.world_size <= 1)
+
+    def refresh_table(self):
+        """Bring the device segment table up to date BEFORE a replay or a
+        capture: the captured update reads rates from the table's fixed
+        address, and the upload itself must never be captured."""
+        from veles_amd import ops
+        segs = self._cached_segments()
+        if not segs or self.master is None or not self.master.is_cuda:
+            return
+        if self._seg_table is None:
+            self._seg_table = ops.SegmentTable(self.master.device)
+        if self._solver_segs is not None:
+            self._seg_table.update(ops._pack_solver_segs(self._solver_segs))
+        else:
+            self._seg_table.update(ops._pack_sgd_segs(segs))
+
+    def replayed_step(self):
+        """Host bookkeeping of one update whose kernels ran in a graph."""
+        self._works = []
+        self._launched = set()
+        self._ready.clear()
+        self._accum_count = 0
+        self.steps += 1
+        if self.device is not None and getattr(self.device, "fp8", False):
+            from veles_amd.ops import fp8
+            fp8.registry(self.device.torch_device).step += 1
+
     def sync_host(self):
         """Copy master weights back into each Param.host (for snapshots)."""
         for p in self.params:

@@ -144,6 +144,8 @@ class StochasticPooling(Pooling):
     MAPPING = "stochastic_pooling"
     MODE = "max"
     USE_ABS = False
+    # a host-seeded torch.Generator per minibatch: not HIP-graph capturable
+    graph_safe = False
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)

@@ -174,6 +174,8 @@ class StandardWorkflow(LinkBuilders, AcceleratedWorkflow):
         self.lr_adjuster_config = kwargs.get("lr_adjuster_config")
         self.evaluator_config = dict(_cfg(kwargs.get("evaluator_config")))
         self.testing = kwargs.get("testing", False)
+        # eager passes per (class, batch size) before a segment is captured
+        self.graph_warmup = int(kwargs.get("graph_warmup", 2))
         for k in ("image_saver_config", "data_saver_config",
                   "publisher_config", "result_unit_config"):
             setattr(self, k, dict(_cfg(kwargs.get(k))))
@@ -460,7 +462,11 @@ class StandardWorkflow(LinkBuilders, AcceleratedWorkflow):
             ld.max_minibatch_size
         ld.full_minibatch_size = full
         ld.max_minibatch_size = -(-full // acc)
-        return super().initialize(**kwargs)
+        res = super().initialize(**kwargs)
+        # forward / backward HIP-graph segments (GPU only; veles_amd/graphs)
+        from veles_amd.graphs import install_step_graphs
+        install_step_graphs(self, warmup=self.graph_warmup)
+        return res
 
     def run_steps(self, n):
         """Run exactly ``n`` more TRAIN minibatches (benchmarks / tests)."""

@@ -1088,12 +1088,21 @@ def dropout_mask_ref(n, seed, p):
     return h >= thresh
 
 
-def dropout(x, p, seed, out=None):
+def dropout(x, p, seed, out=None, seed_dev=None):
     """y = x * keep / (1-p) with a counter-based mask (same seed -> same mask:
-    the backward pass calls this on dy)."""
+    the backward pass calls this on dy).  ``seed_dev``: a 1-element int32
+    device tensor holding the seed instead (graph-safe, see
+    :func:`seed_advance`); ``seed`` is then ignored."""
     if out is None:
         out = torch.empty_like(x)
+    if seed_dev is not None and not _gpu(x):
+        seed = int(seed_dev.reshape(-1)[0]) & 0xFFFFFFFF
     if _gpu(x):
+        if seed_dev is not None:
+            _lib_call("hvk_dropout_dev", _p(x), DT[x.dtype], _p(out),
+                      DT[out.dtype], x.numel(), _p(seed_dev), float(p), None,
+                      _s(x))
+            return out
         _lib_call("hvk_dropout", _p(x), DT[x.dtype], _p(out), DT[out.dtype],
                   x.numel(), int(seed) & 0xFFFFFFFF, float(p), None, _s(x))
         return out
@@ -1101,6 +1110,24 @@ def dropout(x, p, seed, out=None):
     scale = 1.0 / (1.0 - p) if p < 1 else 0.0
     out.copy_((x.float() * keep * scale).to(out.dtype))
     return out
+
+
+def seed_advance_ref(seed):
+    """Host mirror of hvk_seed_advance: seed <- hash32(seed + 1)."""
+    i = torch.tensor([(int(seed) + 1) & 0xFFFFFFFF], dtype=torch.int64)
+    return int(_hash32(i, 0x2545F491)[0])
+
+
+def seed_advance(seed_dev):
+    """Advance a device-resident dropout seed (int32 [1]) in place - a
+    stream-ordered kernel, so a captured step draws a new mask every
+    replay."""
+    if _gpu(seed_dev):
+        _lib_call("hvk_seed_advance", _p(seed_dev), _s(seed_dev))
+        return seed_dev
+    v = seed_advance_ref(int(seed_dev.reshape(-1)[0]) & 0xFFFFFFFF)
+    seed_dev.fill_(v - (1 << 32) if v >= (1 << 31) else v)
+    return seed_dev
 
 
 # --------------------------------------------------------------------- RNG

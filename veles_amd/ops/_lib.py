@@ -48,6 +48,8 @@ _SIGS = {
     "hvk_act_fwd": [P, I, P, I, L, I, P],
     "hvk_act_bwd": [P, I, P, I, P, I, L, I, P],
     "hvk_dropout": [P, I, P, I, L, U, F, P, P],
+    "hvk_dropout_dev": [P, I, P, I, L, P, F, P, P],
+    "hvk_seed_advance": [P, P],
     "hvk_xorshift1024star": [P, I, I, P, P],
     "hvk_xorshift128plus": [P, I, P, P],
     "hvk_u64_to_uniform": [P, P, L, F, F, P],
@@ -72,6 +74,7 @@ _SIGS = {
     "hvk_fp8_quant": [P, I, L, P, I, P, I, F, I, P],
     "hvk_fp8_amax": [P, I, L, P, I, P],
     "hvk_fp8_roll": [P, I, I, I, I, P],
+    "hvk_fp8_roll_dev": [P, I, I, P, P],
     "hvk_gemm_fp8": [I, I, I, P, I, I, P, I, I, P, I, P, I, P, I, I, P, P, I,
                      F, F, P],
     "hvk_conv_fwd_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F, P],

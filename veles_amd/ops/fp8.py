@@ -56,6 +56,7 @@ class _Registry(object):
         self.blocks = []
         self.used = 0
         self.step = 0
+        self.step_dev = None  # device mirror of ``step`` (GPU roll)
 
     def allocate(self):
         i = self.used
@@ -67,20 +68,32 @@ class _Registry(object):
         return self.blocks[i // _CHUNK][i % _CHUNK]
 
     def roll(self):
-        """End of step: current amax -> history slot; current = 0."""
+        """End of step: current amax -> history slot; current = 0.  On the
+        GPU the slot index comes from a device step counter advanced in the
+        same stream, so a captured HIP graph of the step rolls correctly on
+        every replay."""
         idx = self.step % HIST
+        gpu_step = None
         for bi, blk in enumerate(self.blocks):
             count = min(_CHUNK, self.used - bi * _CHUNK)
             if count <= 0:
                 break
             if blk.is_cuda:
-                _call("hvk_fp8_roll", blk.data_ptr(), count, HIST, idx, 0,
-                      _s(blk))
+                if gpu_step is None:
+                    if self.step_dev is None:
+                        self.step_dev = torch.full(
+                            (1,), self.step, dtype=torch.int32,
+                            device=blk.device)
+                    gpu_step = self.step_dev
+                _call("hvk_fp8_roll_dev", blk.data_ptr(), count, HIST,
+                      gpu_step.data_ptr(), _s(blk))
             else:
                 cur = blk[:count, HIST]
                 keep = cur > 0
                 blk[:count, idx] = torch.where(keep, cur, blk[:count, idx])
                 blk[:count, HIST] = 0
+        if gpu_step is not None:
+            gpu_step.add_(1)
         self.step += 1
 
 

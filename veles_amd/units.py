@@ -529,14 +529,18 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
         if events.enabled:
             events.record(self.name, "begin")
         rng = _roctx()
+        # a unit inside a captured HIP-graph segment (veles_amd/graphs.py)
+        # is dispatched by the segment: eager, captured or replayed
+        seg = self.__dict__.get("graph_segment_")
+        body = type(self).run if seg is None else seg.run_unit
         if rng is not None:
             rng.range_push(self.name)
             try:
-                type(self).run(self)
+                body(self)
             finally:
                 rng.range_pop()
         else:
-            type(self).run(self)
+            body(self)
         dt = time.perf_counter() - t0
         if events.enabled:
             events.record(self.name, "end")

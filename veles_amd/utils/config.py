@@ -188,6 +188,10 @@ root.common.update({
         "precision_level": 0,
         "device_id": None,
         "sync_run": False,
+        # Capture the forward and backward unit chains of the train step in
+        # HIP graphs on the GPU (veles_amd/graphs.py); VELES_AMD_GRAPHS=0
+        # overrides.
+        "graphs": True,
         "force_cpu": (),
         "thread_pool": {"minthreads": 2, "maxthreads": 2},
         "kernels": {
