@@ -139,6 +139,8 @@ CONVS = [
     (3, 10, 12, 128, 64, 1, 1, (1, 1), (0, 0, 0, 0), 1),
     (2, 12, 9, 32, 48, 3, 5, (1, 1), (2, 0, 1, 2), 2),
     (2, 16, 16, 48, 40, 3, 3, (2, 2), (1, 1, 1, 1), 1),
+    # LeNet conv2: output channels off the 8-grid (dgrad zero-pads them)
+    (4, 12, 12, 20, 50, 5, 5, (1, 1), (0, 0, 0, 0), 1),
 ]
 
 

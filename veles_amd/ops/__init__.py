@@ -428,9 +428,23 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
     if _gpu(dy):
         # weights permuted to [g][c][kh][kw][oc]: a dense K-major B operand
         OCg, Cg = OC // groups, C // groups
-        wt = _workspace(("dgrad_wt", id(w)), (groups, Cg, KH, KW, OCg),
-                        w.dtype, w.device)
-        wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1))
+        if groups == 1 and OC % 8:
+            # an output-channel count off the 16-byte grid (LeNet's 50)
+            # would force the per-element A loader (5x slower): zero-pad
+            # dy's and the weights' channel dimension to a multiple of 8
+            OCp = -(-OC // 8) * 8
+            wt = _workspace(("dgrad_wtp", id(w)), (1, C, KH, KW, OCp),
+                            w.dtype, w.device, zero=True)
+            wt[..., :OC].copy_(w.view(1, OC, KH, KW, C).permute(
+                0, 4, 2, 3, 1))
+            dyp = _workspace(("dgrad_dyp", N, OH, OW, OCp), (N, OH, OW, OCp),
+                             dy.dtype, dy.device, zero=True)
+            dyp[..., :OC].copy_(dy)
+            dy, OC = dyp, OCp
+        else:
+            wt = _workspace(("dgrad_wt", id(w)), (groups, Cg, KH, KW, OCg),
+                            w.dtype, w.device)
+            wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1))
         _lib_call("hvk_conv_dgrad_t", _p(dy), _p(wt), _p(out), N, H, W, C,
                   OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, _p(aux),
                   aux_act, _s(dy))
@@ -520,7 +534,7 @@ def wgrad_splits(P, M, N, groups, target_blocks=None):
     256 CUs, few enough that the f32 atomic reduction stays small."""
     target_blocks = target_blocks or _WGRAD_BLOCKS
     tiles = ((M + 127) // 128) * ((N + 127) // 128) * groups
-    splits = max(1, min(target_blocks // max(tiles, 1), P // 512))
+    splits = max(1, min(target_blocks // max(tiles, 1), P // 256))
     return splits
 
 
