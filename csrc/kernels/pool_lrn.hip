@@ -977,6 +977,139 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_u8_kernel(
     }
   }
 }
+
+// The same backward with the LRN window halo shared across lanes.  Lanes of a
+// wave hold consecutive 8-channel chunks of one 2 x 2 pixel block (64 / CV
+// whole blocks per wave, the last 64 % CV lanes idle), so the channels a
+// chunk's LRN window reaches beyond its own 8 - the squares x^2 for the
+// window sums and the t_j = g_j x_j s_j^(-beta-1) terms of the gradient sum -
+// are the neighbouring lanes' own values: one DPP wave shift each instead of
+// loading, pooling-gradient-gathering and exponentiating 2 * half extra
+// channels per pixel in every thread (the u8 kernel above does 12 channels'
+// worth of transcendentals per 8 outputs at n = 5, this one 8).  AlexNet
+// b512 on MI355X: conv1 0.337 -> 0.233 ms, conv2 0.215 -> 0.144 ms.  The
+// same layout for the FORWARD kernel measured slower (conv1 0.194 ->
+// 0.286 ms): its halo loads hit L1 and the DPP chains serialise 9 window
+// pixels, so the forward keeps the per-thread halo.
+__device__ __forceinline__ float lane_from_below(float v) {  // lane - 1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+      0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float lane_from_above(float v) {  // lane + 1
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+      0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
+
+template <int half>
+__global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
+    const uint8_t* __restrict__ argmax, uint16_t* __restrict__ dx, int N,
+    int H, int W, int C, int OH, int OW, float alpha, float beta, float k,
+    const uint16_t* aux, int aux_act, int bpw, int nblk, FastDiv fBW,
+    FastDiv fBH) {
+  const int CV = C >> 3;
+  const int lane = threadIdx.x & 63;
+  const int lb = lane / CV, cvu = lane - lb * CV;
+  const int c0 = cvu * 8;
+  const bool first = cvu == 0, last = cvu == CV - 1;
+  const bool aux_x = aux == x;
+  const int nwv = (nblk + bpw - 1) / bpw;
+  const int wstride = (gridDim.x * blockDim.x) >> 6;
+  // the loop bound is wave-uniform: every lane reaches every DPP
+  for (int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wv < nwv;
+       wv += wstride) {
+    const int blk = wv * bpw + lb;
+    const bool ok = lb < bpw && blk < nblk;
+    uint32_t t, bwu, nu, bhu;
+    fdivmod((uint32_t)(ok ? blk : 0), fBW, t, bwu);
+    fdivmod(t, fBH, nu, bhu);
+    float g[4][8];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g[p][q] = 0.f;
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const int a = wi >> 1, b = wi & 1;
+      const int oh = (int)bhu - 1 + a, ow = (int)bwu - 1 + b;
+      if (!ok || oh < 0 || ow < 0 || oh >= OH || ow >= OW) continue;
+      const long long yo = (((long long)nu * OH + oh) * OW + ow) * C + c0;
+      const uint4 gv = *(const uint4*)(dp + yo);
+      const uint2 av = *(const uint2*)(argmax + yo);
+      const uint16_t* gh = (const uint16_t*)&gv;
+      const uint8_t* ah = (const uint8_t*)&av;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int r = 2 * (1 - a) + (p >> 1), c = 2 * (1 - b) + (p & 1);
+        if (r > 2 || c > 2) continue;  // pixel outside this window
+        const int kexp = r * 3 + c;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) g[p][q] += ah[q] == kexp ? bf2f(gh[q]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int hp = (int)bhu * 2 + (p >> 1), wp = (int)bwu * 2 + (p & 1);
+      const bool pv = ok && hp < H && wp < W;
+      const long long po = (((long long)nu * H + hp) * W + wp) * C + c0;
+      float xv[8];
+      if (pv) {
+        load8(x + po, xv);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xv[q] = 0.f;
+      }
+      // squares of channels c0 - half .. c0 + 8 + half
+      float e[8 + 2 * half];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) e[half + q] = xv[q] * xv[q];
+#pragma unroll
+      for (int d = 0; d < half; ++d) {
+        const float lo = lane_from_below(e[8 + d]);   // its channel 8-half+d
+        const float hi = lane_from_above(e[half + d]);  // its channel d
+        e[d] = first ? 0.f : lo;
+        e[8 + half + d] = last ? 0.f : hi;
+      }
+      float sb[8], tj[8 + 2 * half];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float w = 0.f;
+#pragma unroll
+        for (int d = 0; d <= 2 * half; ++d) w += e[q + d];
+        const float sq = k + alpha * w;
+        const float e1 = exp2f((-beta - 1.f) * __log2f(sq));  // s^(-beta-1)
+        sb[q] = e1 * sq;                                     // s^-beta
+        tj[half + q] = g[p][q] * xv[q] * e1;
+      }
+#pragma unroll
+      for (int d = 0; d < half; ++d) {
+        const float lo = lane_from_below(tj[8 + d]);
+        const float hi = lane_from_above(tj[half + d]);
+        tj[d] = first ? 0.f : lo;
+        tj[8 + half + d] = last ? 0.f : hi;
+      }
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float acc = 0.f;
+#pragma unroll
+        for (int d = 0; d <= 2 * half; ++d) acc += tj[q + d];
+        v[q] = g[p][q] * sb[q] - 2.f * alpha * beta * xv[q] * acc;
+      }
+      if (aux && pv) {
+        float av8[8];
+        if (aux_x) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) av8[q] = xv[q];
+        } else {
+          load8(aux + po, av8);
+        }
+        act_bwd_mul8(v, av8, aux_act);
+      }
+      if (pv) *(uint4*)(dx + po) = pack_bf16x8(v);
+    }
+  }
+}
 }  // namespace
 
 // 2 x 2 / stride-2 pooling without argmax (pool2_fwd_kernel): C % 8 == 0,
@@ -1053,6 +1186,27 @@ HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
   const int h = n / 2;
   const int BH = (H + 1) / 2, BW = (W + 1) / 2;
   const long long tb = (long long)N * BH * BW * (C / 8);
+  static const bool dpp_on = [] {
+    const char* e = getenv("HVK_LRN_DPP");
+    return !(e && e[0] == '0');
+  }();
+  if (dpp_on && C / 8 <= 64 && h >= 1 && h <= 4) {
+    // whole 2 x 2 blocks per wave, their chunks on consecutive lanes
+    const int CV = C / 8, bpw = 64 / CV;
+    const long long nblk = (long long)N * BH * BW;
+    const long long waves = (nblk + bpw - 1) / bpw;
+    const long long blocks = std::min<long long>((waves + 3) / 4, 1 << 16);
+    auto kd = h == 1 ? lrn_pool3s2_bwd_dpp_kernel<1>
+            : h == 2 ? lrn_pool3s2_bwd_dpp_kernel<2>
+            : h == 3 ? lrn_pool3s2_bwd_dpp_kernel<3>
+                     : lrn_pool3s2_bwd_dpp_kernel<4>;
+    hipLaunchKernelGGL(kd, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const uint16_t*)x, (const uint16_t*)dp,
+                       (const uint8_t*)argmax, (uint16_t*)dx, N, H, W, C, OH,
+                       OW, alpha, beta, k, (const uint16_t*)aux, aux_act, bpw,
+                       (int)nblk, make_fastdiv(BW), make_fastdiv(BH));
+    return (int)hipGetLastError();
+  }
   auto k2 = h == 0 ? lrn_pool3s2_bwd_u8_kernel<0>
           : h == 1 ? lrn_pool3s2_bwd_u8_kernel<1>
           : h == 2 ? lrn_pool3s2_bwd_u8_kernel<2>

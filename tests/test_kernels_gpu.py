@@ -379,7 +379,11 @@ def test_solver_kernel(mode):
     ((2, 27, 27, 96), 2, 5, "sep"), ((3, 13, 13, 16), 2, 5, "sep"),
     ((2, 55, 55, 96), 2, 5, "sep"), ((2, 55, 55, 96), 2, 5, "x"),
     ((2, 14, 12, 8), 2, 3, "none"), ((1, 16, 17, 24), 2, 9, "x"),
-    ((2, 20, 19, 32), 3, 5, "sep"), ((1, 15, 15, 40), 3, 7, "x")])
+    ((2, 20, 19, 32), 3, 5, "sep"), ((1, 15, 15, 40), 3, 7, "x"),
+    # DPP-halo backward: 2 blocks per wave (C = 256), one (C = 512), and
+    # the per-thread fallback past 64 chunks (C = 528)
+    ((2, 27, 27, 256), 2, 5, "x"), ((1, 9, 9, 512), 2, 5, "sep"),
+    ((1, 7, 7, 528), 2, 5, "sep")])
 def test_lrn_pool_fused(shape, stride, n, aux_mode):
     """Fused LRN -> 3x3 max pool forward / backward against the fp32
     reference; stride 2 runs the 2x2-block backward kernel, stride 3 the
