@@ -936,6 +936,125 @@ HVK_API int hvk_dropout_dev(const void* x, int xdt, void* y, int ydt,
   return (int)hipGetLastError();
 }
 
+// ------------------------------------------------ input-derivative activations
+// The Znicz standalone activations whose derivative is a function of the
+// INPUT (docs/OPS.md §Activations): log (asinh), tanhlog (scaled tanh up to
+// |x| = D, logarithmic growth beyond, C1-continuous), sincos (sin on even,
+// cos on odd feature columns), mul (k x).  p = D for tanhlog, k for mul.
+enum { XACT_LOG = 1, XACT_TANHLOG = 2, XACT_SINCOS = 3, XACT_MUL = 4 };
+struct XactParams {
+  int kind;
+  float p, edge, slope;  // tanhlog: edge = f(D), slope = f'(D)
+};
+__device__ __forceinline__ XactParams xact_params(int kind, float p) {
+  XactParams q{kind, p, 0.f, 0.f};
+  if (kind == XACT_TANHLOG) {
+    const float t = tanhf(0.6666f * p);
+    q.edge = 1.7159f * t;
+    q.slope = 1.7159f * 0.6666f * (1.f - t * t);
+  }
+  return q;
+}
+__device__ __forceinline__ float xact_f(float x, const XactParams& q,
+                                        int odd) {
+  switch (q.kind) {
+    case XACT_LOG: return logf(x + sqrtf(x * x + 1.f));
+    case XACT_TANHLOG: {
+      const float a = fabsf(x);
+      if (a <= q.p) return 1.7159f * tanhf(0.6666f * x);
+      return copysignf(q.edge + q.slope * q.p * logf(a / q.p), x);
+    }
+    case XACT_SINCOS: return odd ? cosf(x) : sinf(x);
+    case XACT_MUL: return q.p * x;
+    default: return x;
+  }
+}
+__device__ __forceinline__ float xact_d(float x, const XactParams& q,
+                                        int odd) {
+  switch (q.kind) {
+    case XACT_LOG: return rsqrtf(x * x + 1.f);
+    case XACT_TANHLOG: {
+      const float a = fabsf(x);
+      if (a <= q.p) {
+        const float t = tanhf(0.6666f * x);
+        return 1.7159f * 0.6666f * (1.f - t * t);
+      }
+      return q.slope * q.p / a;
+    }
+    case XACT_SINCOS: return odd ? -sinf(x) : cosf(x);
+    case XACT_MUL: return q.p;
+    default: return 1.f;
+  }
+}
+// bwd = 0: y = f(x); bwd = 1: y = err * f'(x).  rowlen: features per sample
+// (sincos parity is the column's); 8 elements per thread when vec
+__global__ void xact_kernel(const void* x, int xdt, const void* err,
+                            int edt, void* y, int ydt, long long n, int kind,
+                            float p, long long rowlen, int bwd, int vec) {
+  const XactParams q = xact_params(kind, p);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  if (vec) {  // bf16, n % 8 == 0, 16-B aligned, even rowlen
+    for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+         v < n / 8; v += stride) {
+      float xv[8], o[8];
+      const uint4 xr = ((const uint4*)x)[v];
+      const uint16_t* xh = (const uint16_t*)&xr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = bf2f(xh[e]);
+      if (bwd) {
+        const uint4 er = ((const uint4*)err)[v];
+        const uint16_t* eh = (const uint16_t*)&er;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = bf2f(eh[e]) * xact_d(xv[e], q, e & 1);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = xact_f(xv[e], q, e & 1);
+      }
+      ((uint4*)y)[v] = pack_bf16x8(o);
+    }
+    return;
+  }
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += stride) {
+    const int odd = (int)((i % rowlen) & 1);
+    const float xv = ld_any(x, i, xdt);
+    st_any(y, i, ydt, bwd ? ld_any(err, i, edt) * xact_d(xv, q, odd)
+                          : xact_f(xv, q, odd));
+  }
+}
+
+HVK_API int hvk_xact(const void* x, int xdt, const void* err, int edt,
+                     void* y, int ydt, long long n, int kind, float p,
+                     long long rowlen, int bwd, hipStream_t s) {
+  if (kind < XACT_LOG || kind > XACT_MUL || rowlen < 1) return -1;
+  const int vec = xdt == DT_BF16 && ydt == DT_BF16 &&
+                  (!bwd || edt == DT_BF16) && n % 8 == 0 &&
+                  rowlen % 2 == 0 && ((uintptr_t)x & 15) == 0 &&
+                  ((uintptr_t)y & 15) == 0 &&
+                  (!bwd || ((uintptr_t)err & 15) == 0);
+  hipLaunchKernelGGL(xact_kernel, dim3(grid_for(vec ? n / 8 : n)), dim3(256),
+                     0, s, x, xdt, err, edt, y, ydt, n, kind, p, rowlen, bwd,
+                     vec);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------- gather
+// y[i] = x[idx[i]] (int32 indices; idx < 0 gives 0): the depooling backward
+__global__ void gather_kernel(const void* x, int xdt, const int* idx, void* y,
+                              int ydt, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int j = idx[i];
+    st_any(y, i, ydt, j >= 0 ? ld_any(x, j, xdt) : 0.f);
+  }
+}
+HVK_API int hvk_gather(const void* x, int xdt, const int* idx, void* y,
+                       int ydt, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
+                     idx, y, ydt, n);
+  return (int)hipGetLastError();
+}
+
 // seed <- hash(seed + 1): a per-step seed sequence that lives on the device
 __global__ void seed_advance_kernel(uint32_t* seed) {
   if (threadIdx.x == 0) seed[0] = hash32(seed[0] + 1u, 0x2545F491u);

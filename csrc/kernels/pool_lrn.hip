@@ -1112,6 +1112,86 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
 }
 }  // namespace
 
+// Stochastic pooling (Znicz stochastic_pooling / stochastic_abs_pooling):
+// each window element is drawn with probability w_i / sum(w), w = max(x, 0)
+// (|x| for abs), uniform over the window when sum(w) = 0; the uniform of
+// output element o is hash(o, seed) >> 8 / 2^24 (counter-based, the seed read
+// from device memory so a captured step draws fresh samples every replay).
+// Testing: the probability-weighted average, argmax = the most probable.
+// One thread per output element (channels fastest: coalesced).
+__device__ __forceinline__ uint32_t sp_hash(uint32_t x, uint32_t seed) {
+  x ^= seed * 0x9E3779B9u;
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__global__ void stochastic_pool_kernel(const uint16_t* __restrict__ x,
+                                       uint16_t* __restrict__ y,
+                                       int* __restrict__ argmax, int N, int H,
+                                       int W, int C, int OH, int OW, int ky,
+                                       int kx, int sy, int sx, int use_abs,
+                                       int train, const uint32_t* seed_dev,
+                                       FastDiv fC, FastDiv fOW, FastDiv fOH) {
+  const uint32_t seed = __builtin_amdgcn_readfirstlane(seed_dev[0]);
+  const long long total = (long long)N * OH * OW * C;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       o < total; o += (long long)gridDim.x * blockDim.x) {
+    uint32_t pix, c, t, ow, n, oh;
+    fdivmod((uint32_t)o, fC, pix, c);
+    fdivmod(pix, fOW, t, ow);
+    fdivmod(t, fOH, n, oh);
+    const int h0 = (int)oh * sy, w0 = (int)ow * sx;
+    const int h1 = min(h0 + ky, H), w1 = min(w0 + kx, W);
+    const long long img = (long long)n * H * W * C + c;
+    float tot = 0.f;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) {
+        const float v = bf2f(x[img + ((long long)h * W + w) * C]);
+        tot += use_abs ? fabsf(v) : fmaxf(v, 0.f);
+      }
+    const int cnt = (h1 - h0) * (w1 - w0);
+    const float inv = tot > 0.f ? 1.f / tot : 0.f;
+    const float uni = 1.f / (float)cnt;
+    const float u =
+        (float)(sp_hash((uint32_t)o, seed) >> 8) * (1.f / 16777216.f);
+    float cum = 0.f, out = 0.f, best = -1.f;
+    long long pick = -1;
+    bool taken = false;
+    for (int h = h0; h < h1; ++h)
+      for (int w = w0; w < w1; ++w) {
+        const long long off = img + ((long long)h * W + w) * C;
+        const float v = bf2f(x[off]);
+        const float pr = tot > 0.f ? (use_abs ? fabsf(v) : fmaxf(v, 0.f)) * inv
+                                   : uni;
+        if (train) {
+          cum += pr;
+          if (!taken && cum >= u) { taken = true; pick = off; out = v; }
+          if (!taken) { pick = off; out = v; }  // rounding: the last one
+        } else {
+          out += pr * v;
+          if (pr > best) { best = pr; pick = off; }
+        }
+      }
+    y[o] = f2bf(out);
+    argmax[o] = (int)pick;
+  }
+}
+
+HVK_API int hvk_stochastic_pool(const void* x, void* y, int* argmax, int N,
+                                int H, int W, int C, int OH, int OW, int ky,
+                                int kx, int sy, int sx, int use_abs, int train,
+                                const void* seed_dev, hipStream_t s) {
+  const long long total = (long long)N * OH * OW * C;
+  if ((long long)N * H * W * C >= (1ll << 31) || !seed_dev) return -1;
+  hipLaunchKernelGGL(stochastic_pool_kernel, dim3(grid_for(total)), dim3(256),
+                     0, s, (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W,
+                     C, OH, OW, ky, kx, sy, sx, use_abs, train,
+                     (const uint32_t*)seed_dev, make_fastdiv(C),
+                     make_fastdiv(OW), make_fastdiv(OH));
+  return (int)hipGetLastError();
+}
+
 // 2 x 2 / stride-2 pooling without argmax (pool2_fwd_kernel): C % 8 == 0,
 // even H and W, 16-B aligned tensors; mode 0 max, 1 avg, 2 maxabs.
 HVK_API int hvk_pool2_fwd(const void* x, void* y, int N, int H, int W, int C,

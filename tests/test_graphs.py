@@ -210,3 +210,26 @@ def test_seed_advance_reference(seed):
     y1 = ops.dropout(x, 0.3, None, seed_dev=t)
     y2 = ops.dropout(x, 0.3, int(t[0]) & 0xFFFFFFFF)
     assert torch.equal(y1, y2)
+
+
+def test_stochastic_pool_reference_draws():
+    """CPU reference of hvk_stochastic_pool: drawn values sit at the drawn
+    offsets, zero-probability elements are never drawn unless the window
+    is all non-positive, test mode is the probability-weighted average."""
+    from veles_amd import ops
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 6, 6, 4, generator=g)
+    y, am = ops.stochastic_pool(x, 2, 2, (2, 2), False, True, seed=7)
+    assert torch.equal(y.view(-1), x.view(-1)[am.view(-1).long()])
+    win = x.unfold(1, 2, 2).unfold(2, 2, 2)  # N, 3, 3, C, 2, 2
+    anypos = (win > 0).flatten(-2).any(-1)
+    assert bool(((y > 0) | ~anypos).all())
+    yt, _ = ops.stochastic_pool(x, 2, 2, (2, 2), False, False)
+    w = win.clamp(min=0).flatten(-2)
+    p = w / w.sum(-1, keepdim=True).clamp(min=1e-30)
+    p = torch.where(w.sum(-1, keepdim=True) > 0, p, torch.full_like(p, .25))
+    ref = (p * win.flatten(-2)).sum(-1)
+    assert torch.allclose(yt, ref, atol=1e-5)
+    # a different seed draws differently somewhere
+    y2, am2 = ops.stochastic_pool(x, 2, 2, (2, 2), False, True, seed=8)
+    assert not torch.equal(am, am2)

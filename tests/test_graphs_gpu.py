@@ -113,3 +113,27 @@ def test_graphed_fp8_rolls_the_history():
     assert bwd.replays > 0 and bwd.failures == 0 and fwd.failures == 0
     r = fp8.registry(torch.device("cuda", torch.cuda.current_device()))
     assert int(r.step_dev.cpu()[0]) == r.step
+
+
+def test_graphed_stochastic_and_input_derivative_units():
+    """Units that draw per step (stochastic pooling) or differentiate
+    through their input (log / sincos activations) replay correctly: the
+    graphed run follows the eager one."""
+    layers = [
+        {"type": "conv_str", "->": {"n_kernels": 16, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(G)},
+        {"type": "stochastic_pooling", "->": {"kx": 2, "ky": 2,
+                                              "sliding": 2}},
+        {"type": "activation_log"},
+        {"type": "all2all_tanh", "->": {"output_sample_shape": 64},
+         "<-": dict(G)},
+        {"type": "activation_sincos"},
+        {"type": "softmax", "->": {"output_sample_shape": 10}, "<-": dict(G)}]
+    steps = 15
+    eager = _train(False, steps, layers=layers)
+    graphed = _train(True, steps, layers=layers)
+    fwd, bwd = graphed.graph_segments_
+    assert fwd.failures == 0 and bwd.failures == 0 and bwd.replays > 0
+    assert _rel(graphed.param_store_.master, eager.param_store_.master) < 2e-2
+    sp = graphed.forwards[1]
+    assert sp.seed_dev_ is not None

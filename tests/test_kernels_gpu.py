@@ -457,3 +457,60 @@ def test_pool2_argmax_free(mode, aux_mode):
                        aux_act=act)
     torch.cuda.synchronize()
     close(dx, dxr, 1e-2)
+
+
+# ------------------------------------------ input-derivative activations
+@pytest.mark.parametrize("kind,p", [("log", 0.0), ("tanhlog", 0.9),
+                                    ("sincos", 0.0), ("mul", 1.7)])
+@pytest.mark.parametrize("shape", [(4, 64), (3, 5, 7)])  # vector / scalar
+def test_xact(kind, p, shape):
+    x = rnd(*shape, scale=2.0)
+    e = rnd(*shape, seed=3)
+    y = ops.xact(x.to(DEV), kind, p)
+    d = ops.xact(x.to(DEV), kind, p, err=e.to(DEV))
+    torch.cuda.synchronize()
+    close(y, ops.xact_ref(x, kind, p), 1e-2)
+    close(d, ops.xact_ref(x, kind, p, bwd=True, err=e), 1e-2)
+
+
+def test_gather():
+    x = rnd(5, 7, 9)
+    idx = torch.randint(-1, x.numel(), (3, 11), dtype=torch.int32)
+    g = ops.gather(x.to(DEV), idx.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(g.cpu(), ops.gather(x, idx))
+
+
+@pytest.mark.parametrize("shape,k,s", [((2, 9, 10, 16), 3, 2),
+                                       ((3, 8, 8, 5), 2, 2),
+                                       ((1, 7, 5, 3), 3, 3)])
+@pytest.mark.parametrize("use_abs", [False, True])
+@pytest.mark.parametrize("train", [True, False])
+def test_stochastic_pool(shape, k, s, use_abs, train):
+    x = rnd(*shape)
+    seed = torch.tensor([12345], dtype=torch.int32)
+    y, am = ops.stochastic_pool(x.to(DEV), k, k, (s, s), use_abs, train,
+                                seed_dev=seed.to(DEV))
+    yr, amr = ops.stochastic_pool(x, k, k, (s, s), use_abs, train, seed=12345)
+    torch.cuda.synchronize()
+    # the draw agrees except where a cumulative probability sits on u
+    assert (am.cpu() != amr).float().mean().item() < 2e-3
+    same = am.cpu() == amr
+    close(y.cpu()[same], yr[same], 1e-2)
+    if train:  # a drawn value is the input at the drawn offset
+        assert torch.equal(y.cpu().view(-1),
+                           x.view(-1)[am.cpu().view(-1).long()])
+
+
+def test_depooling_scatter_is_pool_backward():
+    """Depooling (scatter-add of pooled values to the argmax offsets) runs
+    as the max-pooling backward gather; compare with a plain index_put."""
+    x = rnd(2, 9, 9, 8)
+    y, am = ops.pool_fwd(x.to(DEV), 3, 3, (2, 2), "max")
+    v = rnd(*y.shape, seed=4)
+    out = ops.pool_bwd(v.to(DEV), am, x.shape, 3, 3, (2, 2), "max")
+    ref = torch.zeros(x.numel())
+    ref.index_put_((am.cpu().reshape(-1).long(),), v.float().reshape(-1),
+                   accumulate=True)
+    torch.cuda.synchronize()
+    close(out, ref.view(x.shape), 1e-2)

@@ -1,9 +1,11 @@
 """Standalone activation units (Znicz ``activation_*`` types).
 
 tanh / relu (softplus) / strict relu / sigmoid run as ``hvk_act_fwd`` /
-``hvk_act_bwd``.  log (y = log(x + sqrt(x^2 + 1)), i.e. asinh), tanhlog
-(tanh for |x| <= 1 region, log growth beyond - docs/OPS.md), sincos (even
-outputs sin, odd cos) and mul (y = k x) are composed from device tensor ops.
+``hvk_act_bwd`` (derivative through the output).  log (y = log(x +
+sqrt(x^2 + 1)), i.e. asinh), tanhlog (scaled tanh up to |x| = D, log growth
+beyond - docs/OPS.md), sincos (even feature columns sin, odd cos) and mul
+(y = k x) differentiate through the INPUT: ``hvk_xact`` forward and
+backward (ops.xact; float32 reference ops.xact_ref on the CPU).
 """
 from __future__ import annotations
 
@@ -53,15 +55,20 @@ class ActivationForward(AcceleratedUnit):
             self.output.devmem = y = torch.empty_like(x)
         return y
 
+    XACT = None  # input-derivative kind (ops.XACT)
+
+    def xact_param(self):
+        return 0.0
+
     def compute(self, x):
-        raise NotImplementedError
+        return ops.xact_ref(x, self.XACT, self.xact_param())
 
     def run(self):
         x = self.input.devmem
         if self.ACT:
             ops.act_fwd(x, self.ACT, out=self._alloc(x))
         else:
-            self._alloc(x).copy_(self.compute(x.float()).to(x.dtype))
+            ops.xact(x, self.XACT, self.xact_param(), out=self._alloc(x))
 
 
 class ActivationBackward(GradientDescentBase):
@@ -72,8 +79,14 @@ class ActivationBackward(GradientDescentBase):
         super().__init__(workflow, **kwargs)
         self.demand("output")
 
+    XACT = None
+
+    def xact_param(self):
+        return 0.0
+
     def derivative(self, x, y):
-        raise NotImplementedError
+        return ops.xact_ref(x, self.XACT, self.xact_param(), bwd=True,
+                            err=torch.ones_like(x))
 
     def run(self):
         err = self.err_output.devmem
@@ -81,9 +94,8 @@ class ActivationBackward(GradientDescentBase):
         if self.ACT:
             ops.act_bwd(err, self.output.devmem, self.ACT, out=ei)
         else:
-            d = self.derivative(self.input.devmem.float(),
-                                self.output.devmem.float())
-            ei.copy_((err.float() * d).to(ei.dtype))
+            ops.xact(self.input.devmem, self.XACT, self.xact_param(), out=ei,
+                     err=err)
         aux, aux_act = self.aux_tensor()
         if aux is not None:
             ops.act_bwd(ei, aux, aux_act, out=ei)
@@ -105,86 +117,61 @@ ForwardSigmoid, BackwardSigmoid = _pair("Sigmoid", 4, "sigmoid")
 
 class ForwardLog(ActivationForward):
     MAPPING = "activation_log"
-
-    def compute(self, x):
-        return torch.log(x + torch.sqrt(x * x + 1))
+    XACT = "log"
 
 
 class BackwardLog(ActivationBackward):
     MAPPING = "activation_log"
-
-    def derivative(self, x, y):
-        return 1.0 / torch.sqrt(x * x + 1)
+    XACT = "log"
 
 
 class ForwardTanhLog(ActivationForward):
     MAPPING = "activation_tanhlog"
+    XACT = "tanhlog"
     D = 0.9
 
-    def compute(self, x):
-        a = x.abs()
-        lin = 1.7159 * torch.tanh(0.6666 * x)
-        edge = 1.7159 * torch.tanh(torch.tensor(0.6666 * self.D))
-        slope = 1.7159 * 0.6666 * (1 - torch.tanh(
-            torch.tensor(0.6666 * self.D)) ** 2)
-        logp = torch.sign(x) * (edge + slope * self.D * torch.log(
-            a.clamp(min=self.D) / self.D))
-        return torch.where(a <= self.D, lin, logp)
+    def xact_param(self):
+        return self.D
 
 
 class BackwardTanhLog(ActivationBackward):
     MAPPING = "activation_tanhlog"
+    XACT = "tanhlog"
     D = 0.9
 
-    def derivative(self, x, y):
-        a = x.abs()
-        t = torch.tanh(0.6666 * x)
-        dlin = 1.7159 * 0.6666 * (1 - t * t)
-        slope = 1.7159 * 0.6666 * (1 - torch.tanh(
-            torch.tensor(0.6666 * self.D)) ** 2)
-        dlog = slope * self.D / a.clamp(min=self.D)
-        return torch.where(a <= self.D, dlin, dlog)
+    def xact_param(self):
+        return self.D
 
 
 class ForwardSinCos(ActivationForward):
     MAPPING = "activation_sincos"
-
-    def compute(self, x):
-        flat = x.reshape(x.shape[0], -1)
-        out = torch.empty_like(flat)
-        out[:, 0::2] = torch.sin(flat[:, 0::2])
-        out[:, 1::2] = torch.cos(flat[:, 1::2])
-        return out.view(x.shape)
+    XACT = "sincos"
 
 
 class BackwardSinCos(ActivationBackward):
     MAPPING = "activation_sincos"
-
-    def derivative(self, x, y):
-        flat = x.reshape(x.shape[0], -1)
-        d = torch.empty_like(flat)
-        d[:, 0::2] = torch.cos(flat[:, 0::2])
-        d[:, 1::2] = -torch.sin(flat[:, 1::2])
-        return d.view(x.shape)
+    XACT = "sincos"
 
 
 class ForwardMul(ActivationForward):
     MAPPING = "activation_mul"
+    XACT = "mul"
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
         self.factor = kwargs.get("factor", 1.0)
 
-    def compute(self, x):
-        return x * self.factor
+    def xact_param(self):
+        return float(self.factor)
 
 
 class BackwardMul(ActivationBackward):
     MAPPING = "activation_mul"
+    XACT = "mul"
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
         self.factor = kwargs.get("factor", 1.0)
 
-    def derivative(self, x, y):
-        return torch.full_like(x, self.factor)
+    def xact_param(self):
+        return float(self.factor)

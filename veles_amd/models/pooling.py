@@ -7,7 +7,9 @@ max / avg / maxabs run as ``hvk_pool_fwd`` (8 channels per lane) with the
 argmax offset kept for the backward GATHER (``hvk_pool_bwd``, deterministic,
 no atomics).  Stochastic variants draw the window element with probability
 proportional to its (absolute) value during training and use the weighted
-average at test time; they are composed from device tensor ops.
+average at test time (``hvk_stochastic_pool``, counter-based uniforms from a
+device-resident seed).  Depooling scatters through the same gather kernel
+(``hvk_pool_bwd``) and its backward is ``hvk_gather``.
 """
 from __future__ import annotations
 
@@ -144,59 +146,49 @@ class StochasticPooling(Pooling):
     MAPPING = "stochastic_pooling"
     MODE = "max"
     USE_ABS = False
-    # a host-seeded torch.Generator per minibatch: not HIP-graph capturable
-    graph_safe = False
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
         self.rand = kwargs.get("rand", random_generator.get())
         self.uniform_seed = 0
 
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.seed_dev_ = None
+
     def run(self):
         x = self._in()
         B, H, W, C = x.shape
-        kx, ky = self.kx, self.ky
-        sx, sy = self.sliding
-        OH, OW = ops.pool_out_size(H, W, ky, kx, sy, sx)
-        Hp, Wp = (OH - 1) * sy + ky, (OW - 1) * sx + kx
-        xf = x.float()
-        pad = torch.zeros(B, Hp, Wp, C, device=x.device)
-        pad[:, :H, :W] = xf
-        valid = torch.zeros(B, Hp, Wp, C, device=x.device, dtype=torch.bool)
-        valid[:, :H, :W] = True
-        idx = torch.full((B, Hp, Wp, C), -1, dtype=torch.long, device=x.device)
-        idx[:, :H, :W] = torch.arange(B * H * W * C, device=x.device).view(
-            B, H, W, C)
-        vals, ids, oks = [], [], []
-        for dy in range(ky):
-            for dx in range(kx):
-                sl = (slice(None), slice(dy, dy + (OH - 1) * sy + 1, sy),
-                      slice(dx, dx + (OW - 1) * sx + 1, sx))
-                vals.append(pad[sl])
-                ids.append(idx[sl])
-                oks.append(valid[sl])
-        v = torch.stack(vals, -1)
-        i = torch.stack(ids, -1)
-        ok = torch.stack(oks, -1)
-        w = (v.abs() if self.USE_ABS else v.clamp(min=0)) * ok
-        tot = w.sum(-1, keepdim=True)
-        prob = torch.where(tot > 0, w / tot.clamp(min=1e-30),
-                           ok.float() / ok.float().sum(-1, keepdim=True))
-        testing = bool(getattr(self.workflow, "testing", False))
-        if testing:
-            y = (prob * v).sum(-1)
-            choice = prob.argmax(-1, keepdim=True)
-        else:
-            g = torch.Generator(device=x.device)
-            g.manual_seed(int(self.rand.randint(0, 2 ** 31 - 1)))
-            u = torch.rand(prob.shape[:-1] + (1,), generator=g,
-                           device=x.device)
-            choice = (prob.cumsum(-1) < u).sum(-1, keepdim=True).clamp(
-                max=prob.shape[-1] - 1)
-            y = v.gather(-1, choice).squeeze(-1)
-        self.output.devmem = y.to(x.dtype)
-        self.input_offset.devmem = i.gather(-1, choice).squeeze(-1).to(
-            torch.int32)
+        OH, OW = ops.pool_out_size(H, W, self.ky, self.kx, self.sliding[1],
+                                   self.sliding[0])
+        y = self.output.devmem
+        if y is None or tuple(y.shape) != (B, OH, OW, C) or \
+                y.dtype != x.dtype or y.device != x.device:
+            self.output.devmem = y = torch.zeros(B, OH, OW, C, dtype=x.dtype,
+                                                 device=x.device)
+        off = self.input_offset.devmem
+        if off is None or tuple(off.shape) != (B, OH, OW, C) or \
+                off.dtype != torch.int32 or off.device != x.device:
+            self.input_offset.devmem = off = torch.zeros(
+                B, OH, OW, C, dtype=torch.int32, device=x.device)
+        train = not bool(getattr(self.workflow, "testing", False))
+        if x.is_cuda:
+            # device-resident seed sequence (graph-safe, like dropout)
+            sd = self.seed_dev_
+            if sd is None or sd.device != x.device:
+                self.uniform_seed = int(self.rand.randint(0, 2 ** 31 - 1))
+                self.seed_dev_ = sd = torch.tensor(
+                    [self.uniform_seed], dtype=torch.int32, device=x.device)
+            if train:
+                ops.seed_advance(sd)
+            ops.stochastic_pool(x, self.ky, self.kx, self.sliding,
+                                self.USE_ABS, train, seed_dev=sd, out=y,
+                                argmax=off)
+            return
+        if train:
+            self.uniform_seed = int(self.rand.randint(0, 2 ** 31 - 1))
+        ops.stochastic_pool(x, self.ky, self.kx, self.sliding, self.USE_ABS,
+                            train, seed=self.uniform_seed, out=y, argmax=off)
 
 
 class StochasticAbsPooling(StochasticPooling):
@@ -209,13 +201,24 @@ class StochasticPoolingDepooling(StochasticPooling):
     shape, zeros except at the sampled positions)."""
     MAPPING = "stochastic_pool_depool"
 
+    def initialize(self, device=None, **kwargs):
+        super().initialize(device=device, **kwargs)
+        self.pooled_ = None
+
     def run(self):
-        super().run()
+        # pool into a private buffer, then scatter the drawn values back to
+        # the input geometry (the pooling backward's gather kernel)
         x = self._in()
-        out = torch.zeros(x.numel(), dtype=x.dtype, device=x.device)
-        out.index_put_((self.input_offset.devmem.reshape(-1).long(),),
-                       self.output.devmem.reshape(-1), accumulate=False)
-        self.output.devmem = out.view(x.shape)
+        out = self.output.devmem
+        if out is None or tuple(out.shape) != tuple(x.shape) or \
+                out.dtype != x.dtype or out.device != x.device:
+            out = torch.zeros(x.shape, dtype=x.dtype, device=x.device)
+        self.output.devmem = self.pooled_
+        super().run()
+        self.pooled_ = self.output.devmem
+        ops.pool_bwd(self.pooled_, self.input_offset.devmem, tuple(x.shape),
+                     self.ky, self.kx, self.sliding, "max", out=out)
+        self.output.devmem = out
 
 
 class StochasticAbsPoolingDepooling(StochasticPoolingDepooling):
@@ -241,12 +244,30 @@ class Depooling(AcceleratedUnit):
                                          device=x.device)
 
     def run(self):
+        # a scatter-add of x to the recorded offsets IS the max-pooling
+        # backward's gather (hvk_pool_bwd, no atomics) given the pooling's
+        # window geometry; without it, a device scatter
         x = self.input.devmem
         src = self.output_shape_source.devmem
-        out = torch.zeros(src.numel(), dtype=x.dtype, device=x.device)
-        out.index_put_((self.input_offset.devmem.reshape(-1).long(),),
-                       x.reshape(-1), accumulate=True)
-        self.output.devmem = out.view(src.shape)
+        out = self.output.devmem
+        if out is None or tuple(out.shape) != tuple(src.shape) or \
+                out.dtype != x.dtype:
+            out = torch.zeros(tuple(src.shape), dtype=x.dtype,
+                              device=x.device)
+        geo = getattr(self, "geometry", None)
+        shape4 = tuple(src.shape) if src.dim() == 4 else \
+            tuple(src.shape) + (1,)
+        if geo is not None:
+            ky, kx, sliding = geo
+            ops.pool_bwd(x.reshape(x.shape[0], x.shape[1], x.shape[2], -1),
+                         self.input_offset.devmem, shape4, ky, kx, sliding,
+                         "max", out=out.view(shape4))
+        else:
+            flat = torch.zeros(src.numel(), dtype=x.dtype, device=x.device)
+            flat.index_put_((self.input_offset.devmem.reshape(-1).long(),),
+                            x.reshape(-1), accumulate=True)
+            out.copy_(flat.view(src.shape))
+        self.output.devmem = out
 
 
 class GDDepooling(GradientDescentBase):
@@ -257,9 +278,10 @@ class GDDepooling(GradientDescentBase):
         if not self.need_err_input:
             return
         fwd = self.forward
-        off = fwd.input_offset.devmem.reshape(-1).long()
-        err = self.err_output.devmem.reshape(-1)
-        self.err_input.devmem = err[off].view(self.input.devmem.shape)
+        off = fwd.input_offset.devmem
+        ei = self.alloc_err_input(tuple(self.input.devmem.shape),
+                                  self.err_output.devmem.dtype)
+        ops.gather(self.err_output.devmem, off, out=ei.view(off.shape))
 
 
 class GDPoolDepool(GradientDescentBase):
@@ -272,10 +294,14 @@ class GDPoolDepool(GradientDescentBase):
             return
         fwd = self.forward
         err = self.err_output.devmem
-        off = fwd.input_offset.devmem.reshape(-1).long()
-        ei = torch.zeros(err.numel(), dtype=err.dtype, device=err.device)
-        ei[off] = err.reshape(-1)[off]
-        self.err_input.devmem = ei.view(err.shape)
+        off = fwd.input_offset.devmem
+        # err passes at the drawn positions: gather there, scatter back
+        g = ops.gather(err, off)
+        ei = self.alloc_err_input(tuple(err.shape), err.dtype)
+        ops.pool_bwd(g, off, tuple(err.shape) if err.dim() == 4 else
+                     tuple(err.shape) + (1,), fwd.ky, fwd.kx, fwd.sliding,
+                     "max", out=ei.view(tuple(err.shape) if err.dim() == 4
+                                        else tuple(err.shape) + (1,)))
 
 
 class GDPooling(GradientDescentBase):

@@ -295,6 +295,7 @@ class StandardWorkflow(LinkBuilders, AcceleratedWorkflow):
                 unit.link_attrs(pool, "input_offset")
                 pool.offsets_exported = True  # keep int32 flat offsets
                 unit.output_shape_source = pool.input
+                unit.geometry = (pool.ky, pool.kx, tuple(pool.sliding))
             elif isinstance(unit, (MaxPooling, MaxAbsPooling,
                                    StochasticPooling)) and \
                     not isinstance(unit, StochasticPoolingDepooling):

@@ -101,6 +101,76 @@ def act_fwd(x, act, out=None):
     return out
 
 
+XACT = {"log": 1, "tanhlog": 2, "sincos": 3, "mul": 4}
+
+
+def xact_ref(x, kind, p=0.0, bwd=False, err=None):
+    """float32 reference of hvk_xact: activations whose derivative is a
+    function of the input x (log = asinh, tanhlog, sincos, mul)."""
+    kind = XACT.get(kind, kind)
+    x = x.float()
+    if kind == 1:
+        d = torch.rsqrt(x * x + 1) if bwd else torch.log(
+            x + torch.sqrt(x * x + 1))
+    elif kind == 2:
+        a = x.abs()
+        t = torch.tanh(torch.tensor(0.6666 * p))
+        edge, slope = 1.7159 * t, 1.7159 * 0.6666 * (1 - t * t)
+        th = torch.tanh(0.6666 * x)
+        if bwd:
+            d = torch.where(a <= p, 1.7159 * 0.6666 * (1 - th * th),
+                            slope * p / a.clamp(min=p))
+        else:
+            d = torch.where(a <= p, 1.7159 * th, torch.sign(x) * (
+                edge + slope * p * torch.log(a.clamp(min=p) / p)))
+    elif kind == 3:
+        flat = x.reshape(x.shape[0] if x.dim() > 1 else 1, -1)
+        odd = (torch.arange(flat.shape[1], device=x.device) % 2 == 1)
+        if bwd:
+            d = torch.where(odd, -torch.sin(flat), torch.cos(flat))
+        else:
+            d = torch.where(odd, torch.cos(flat), torch.sin(flat))
+        d = d.view(x.shape)
+    elif kind == 4:
+        d = torch.full_like(x, p) if bwd else x * p
+    else:
+        raise ValueError("unknown activation %r" % kind)
+    return err.float() * d if bwd else d
+
+
+def xact(x, kind, p=0.0, out=None, err=None):
+    """y = f(x) (err None) or y = err * f'(x) for the input-derivative
+    activations (``XACT``); ``hvk_xact`` on the GPU."""
+    kind = XACT.get(kind, kind)
+    bwd = err is not None
+    if out is None:
+        out = torch.empty_like(err if bwd else x)
+    if _gpu(x):
+        rowlen = x[0].numel() if x.dim() > 1 else x.numel()
+        _lib_call("hvk_xact", _p(x), DT[x.dtype], _p(err),
+                  DT[err.dtype] if bwd else 0, _p(out), DT[out.dtype],
+                  x.numel(), int(kind), float(p), max(1, int(rowlen)),
+                  int(bwd), _s(x))
+        return out
+    out.copy_(xact_ref(x, kind, p, bwd, err).to(out.dtype))
+    return out
+
+
+def gather(x, idx, out=None):
+    """out[i] = x.flat[idx.flat[i]] (int32 indices; negative -> 0)."""
+    if out is None:
+        out = torch.empty(idx.shape, dtype=x.dtype, device=x.device)
+    if _gpu(x):
+        _lib_call("hvk_gather", _p(x), DT[x.dtype], _p(idx), _p(out),
+                  DT[out.dtype], idx.numel(), _s(x))
+        return out
+    i = idx.reshape(-1).long()
+    v = x.reshape(-1)[i.clamp(min=0)]
+    v = torch.where(i >= 0, v, torch.zeros_like(v))
+    out.copy_(v.view(out.shape))
+    return out
+
+
 def act_bwd(dy, y, act, out=None):
     """dx = dy * f'(y) (derivative expressed through the output y)."""
     act = act_code(act)
@@ -630,6 +700,90 @@ def pool_fwd(x, ky, kx, sliding=None, mode="max", out=None, argmax=None):
     out.copy_(y.to(out.dtype))
     if idx is not None:
         argmax.copy_(idx)
+    return out, argmax
+
+
+def stochastic_pool_u(n, seed, device="cpu"):
+    """The uniforms hvk_stochastic_pool draws: (hash32(o, seed) >> 8) / 2^24
+    for output element o."""
+    o = torch.arange(n, dtype=torch.int64, device=device)
+    return (_hash32(o, int(seed) & 0xFFFFFFFF) >> 8).float() / 16777216.0
+
+
+def stochastic_pool(x, ky, kx, sliding=None, use_abs=False, train=True,
+                    seed=0, seed_dev=None, out=None, argmax=None):
+    """Stochastic pooling (NHWC): train - draw a window element with
+    probability max(x, 0) / sum (|x| for use_abs; uniform when the sum is 0);
+    test - the probability-weighted average.  Returns (y, argmax) with the
+    flat input offset of the drawn (most probable) element.  GPU:
+    ``hvk_stochastic_pool`` with the seed in device memory (``seed_dev``,
+    int32 [1]); the CPU reference draws the same uniforms."""
+    sx, sy = sliding or (kx, ky)
+    N, H, W, C = x.shape
+    OH, OW = pool_out_size(H, W, ky, kx, sy, sx)
+    if out is None:
+        out = torch.empty(N, OH, OW, C, dtype=x.dtype, device=x.device)
+    if argmax is None:
+        argmax = torch.empty(N, OH, OW, C, dtype=torch.int32, device=x.device)
+    if _gpu(x):
+        if seed_dev is None:
+            seed_dev = torch.tensor([int(seed) & 0x7FFFFFFF],
+                                    dtype=torch.int32, device=x.device)
+        _lib_call("hvk_stochastic_pool", _p(x), _p(out), _p(argmax), N, H, W,
+                  C, OH, OW, ky, kx, sy, sx, int(bool(use_abs)),
+                  int(bool(train)), _p(seed_dev), _s(x))
+        return out, argmax
+    if seed_dev is not None:
+        seed = int(seed_dev.reshape(-1)[0]) & 0xFFFFFFFF
+    xf = x.float().cpu()
+    Hp, Wp = (OH - 1) * sy + ky, (OW - 1) * sx + kx
+    pad = torch.zeros(N, Hp, Wp, C)
+    pad[:, :H, :W] = xf
+    ok = torch.zeros(N, Hp, Wp, C, dtype=torch.bool)
+    ok[:, :H, :W] = True
+    idx = torch.full((N, Hp, Wp, C), -1, dtype=torch.long)
+    idx[:, :H, :W] = torch.arange(N * H * W * C).view(N, H, W, C)
+    vals, oks, ids = [], [], []
+    for dy in range(ky):
+        for dx in range(kx):
+            sl = (slice(None), slice(dy, dy + (OH - 1) * sy + 1, sy),
+                  slice(dx, dx + (OW - 1) * sx + 1, sx))
+            vals.append(pad[sl])
+            oks.append(ok[sl])
+            ids.append(idx[sl])
+    w = [(v.abs() if use_abs else v.clamp(min=0)) * o
+         for v, o in zip(vals, oks)]
+    tot = torch.zeros_like(vals[0])
+    cnt = torch.zeros_like(vals[0])
+    for wi, o in zip(w, oks):  # sequential, as the kernel sums
+        tot = tot + wi
+        cnt = cnt + o.float()
+    inv = torch.where(tot > 0, 1.0 / tot.clamp(min=1e-38),
+                      torch.zeros_like(tot))
+    uni = 1.0 / cnt
+    prs = [torch.where(tot > 0, wi * inv, uni) * o for wi, o in zip(w, oks)]
+    y = torch.zeros_like(tot)
+    pick = torch.full(tot.shape, -1, dtype=torch.long)
+    if train:
+        u = stochastic_pool_u(tot.numel(), seed).view(tot.shape)
+        cum = torch.zeros_like(tot)
+        taken = torch.zeros(tot.shape, dtype=torch.bool)
+        for v, pr, o, i in zip(vals, prs, oks, ids):
+            cum = cum + pr
+            hit = o & ~taken & (cum >= u)
+            fall = o & ~taken & ~hit
+            y = torch.where(hit | fall, v, y)
+            pick = torch.where(hit | fall, i, pick)
+            taken = taken | hit
+    else:
+        best = torch.full(tot.shape, -1.0)
+        for v, pr, o, i in zip(vals, prs, oks, ids):
+            y = y + pr * v
+            better = o & (pr > best)
+            best = torch.where(better, pr, best)
+            pick = torch.where(better, i, pick)
+    out.copy_(y.to(out.dtype))
+    argmax.copy_(pick.to(torch.int32))
     return out, argmax
 
 

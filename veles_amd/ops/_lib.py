@@ -50,6 +50,8 @@ _SIGS = {
     "hvk_dropout": [P, I, P, I, L, U, F, P, P],
     "hvk_dropout_dev": [P, I, P, I, L, P, F, P, P],
     "hvk_seed_advance": [P, P],
+    "hvk_xact": [P, I, P, I, P, I, L, I, F, L, I, P],
+    "hvk_gather": [P, I, P, P, I, L, P],
     "hvk_xorshift1024star": [P, I, I, P, P],
     "hvk_xorshift128plus": [P, I, P, P],
     "hvk_u64_to_uniform": [P, P, L, F, F, P],
@@ -64,6 +66,7 @@ _SIGS = {
     "hvk_lrn_pool_fwd": [P, P, P] + [I] * 9 + [F, F, F, P],
     "hvk_lrn_pool_bwd": [P, P, P, P] + [I] * 9 + [F, F, F, P, I, P],
     "hvk_pool2_fwd": [P, P] + [I] * 5 + [P],
+    "hvk_stochastic_pool": [P, P, P] + [I] * 12 + [P, P],
     "hvk_pool2_bwd": [P, P, P] + [I] * 5 + [P, I, P],
     "hvk_lrn_pool_fwd_u8": [P, P, P] + [I] * 7 + [F, F, F, P],
     "hvk_lrn_pool_bwd_u8": [P, P, P, P] + [I] * 7 + [F, F, F, P, I, P],
