@@ -514,3 +514,22 @@ def test_depooling_scatter_is_pool_backward():
                    accumulate=True)
     torch.cuda.synchronize()
     close(out, ref.view(x.shape), 1e-2)
+
+
+@pytest.mark.parametrize("shape,k,pad", [((3, 227, 227, 3), 11, (0, 0, 0, 0)),
+                                         ((1, 35, 33, 3), 11, (2, 1, 2, 1)),
+                                         ((2, 19, 21, 3), 8, (3, 2, 0, 0))])
+def test_space_to_depth(shape, k, pad):
+    """Row-staged space-to-depth (s = 4, C = 3) against a padded view."""
+    x = rnd(*shape)
+    y = ops.space_to_depth(x.to(DEV), 4, k, k, pad)
+    torch.cuda.synchronize()
+    N, H, W, C = shape
+    _, H2, W2, C2 = y.shape
+    pl, pt = pad[0], pad[1]
+    xp = torch.zeros(N, H2 * 4, W2 * 4, C, dtype=x.dtype)
+    h1, w1 = min(H, H2 * 4 - pt), min(W, W2 * 4 - pl)
+    xp[:, pt:pt + h1, pl:pl + w1] = x[:, :h1, :w1]
+    ref = xp.view(N, H2, 4, W2, 4, C).permute(0, 1, 3, 2, 4, 5).reshape(
+        N, H2, W2, 16 * C)
+    assert torch.equal(y.cpu(), ref)
