@@ -597,11 +597,13 @@ struct Epi {
   float* preact;   // optional f32 copy of the pre-activation (unused = null)
   int ones_col;    // column routed to bias_grad[m] (fused bias gradient)
   float* bias_grad;
+  int bias_store;  // 1: the bias-gradient column is stored, not added
   int run_in, run_out;  // column remap n = kh*run_in + j -> kh*run_out + j
   __device__ __forceinline__ void store(int gi, int m, int n, float v) const {
     if (m >= M || n >= N) return;
     if (n == ones_col) {
-      atomicAdd(bias_grad + m + gi * grow, v * alpha);
+      if (bias_store) bias_grad[m + gi * grow] = v * alpha;
+      else atomicAdd(bias_grad + m + gi * grow, v * alpha);
       return;
     }
     if (run_in) {
@@ -1175,6 +1177,34 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   splits = (K + k_split - 1) / k_split;
   const int tiles = tiles_m * tiles_n;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
+  if (epi.atomic == 2 && splits == 1) {
+    // gradient OVERWRITE (the step's only contribution to C): plain stores,
+    // no read of C, the bias-gradient column stored too - the optimizer
+    // then needs no zeroing pass over the gradient buffer
+    Epi e = epi;
+    e.atomic = 0;
+    e.beta = 0.f;
+    e.bias_store = 1;
+    return launch_sel<LA, AK, LB, BKM>(la, lb, e, M, N, K, k_split, tiles_n,
+                                       tiles, splits, groups, bn, grid, s);
+  }
+  if (epi.atomic == 2) {
+    // overwrite with split-K: zero C (and the bias gradient), then add
+    if (groups != 1) return hipErrorInvalidValue;
+    const int ncols = epi.ones_col >= 0 ? epi.ones_col : epi.N;
+    hipError_t z = hipMemset2DAsync(
+        epi.c, (size_t)epi.ldc * (epi.out_f32 ? 4 : 2), 0,
+        (size_t)ncols * (epi.out_f32 ? 4 : 2), (size_t)epi.M, s);
+    if (z != hipSuccess) return z;
+    if (epi.bias_grad) {
+      z = hipMemsetAsync(epi.bias_grad, 0, (size_t)epi.M * 4, s);
+      if (z != hipSuccess) return z;
+    }
+    Epi e = epi;
+    e.atomic = 1;
+    return launch_sel<LA, AK, LB, BKM>(la, lb, e, M, N, K, k_split, tiles_n,
+                                       tiles, splits, groups, bn, grid, s);
+  }
   if (epi.atomic && splits == 1) {
     // an unsplit accumulate writes every element once: read-modify-write in
     // the staged epilogue instead of one f32 atomic per element (the FC
@@ -1216,6 +1246,7 @@ Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
   e.aux = (const uint16_t*)aux; e.ld_aux = ld_aux; e.aux_act = aux_act;
   e.grow = 0; e.gcol = 0; e.preact = nullptr;
   e.ones_col = -1; e.bias_grad = nullptr; e.run_in = 0; e.run_out = 0;
+  e.bias_store = 0;
   return e;
 }
 

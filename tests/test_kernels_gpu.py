@@ -533,3 +533,22 @@ def test_space_to_depth(shape, k, pad):
     ref = xp.view(N, H2, 4, W2, 4, C).permute(0, 1, 3, 2, 4, 5).reshape(
         N, H2, W2, 16 * C)
     assert torch.equal(y.cpu(), ref)
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("with_bias", [False, True])
+def test_gemm_overwrite_gradient(splits, with_bias):
+    """accumulate="overwrite": the weight-gradient GEMM writes (and the
+    fused bias-gradient column stores) instead of adding - whatever the
+    buffers held before; split-K zeroes first."""
+    M, N, K = 200, 136, 1024
+    a, b = rnd(K, M), rnd(K, N, seed=1)
+    out = torch.full((M, N), 7.0, device=DEV)
+    bg = torch.full((M,), -3.0, device=DEV) if with_bias else None
+    ops.gemm(a.to(DEV), b.to(DEV), trans_a=True, out=out,
+             accumulate="overwrite", splits=splits, bias_grad=bg)
+    torch.cuda.synchronize()
+    ref = a.float().t() @ b.float()
+    close(out, ref, 1e-2)
+    if with_bias:
+        close(bg, a.float().sum(0), 1e-2)

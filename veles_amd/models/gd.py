@@ -17,6 +17,7 @@ __all__ = ["GradientDescent", "GDTanh", "GDRELU", "GDStrictRELU",
 
 class GradientDescent(GradientDescentBase):
     MAPPING = "all2all"
+    OVERWRITES_GRADS = True  # see ParameterStore.overwrite
 
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
@@ -36,14 +37,17 @@ class GradientDescent(GradientDescentBase):
             x = x.to(e2.dtype)
         pw, pb = fwd._pw_, fwd._pb_
         bg = None if pb is None else pb.grad
+        # the step's only contribution: write, not read-modify-write
+        ow = self.store_.overwrite
+        mode = "overwrite" if ow else True
         if not fwd.weights_transposed:
             # grad_W and grad_b (ones column) from one GEMM
-            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=True,
+            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode,
                      bias_grad=bg)
         else:
-            ops.gemm(x, e2, trans_a=True, out=pw.grad, accumulate=True)
+            ops.gemm(x, e2, trans_a=True, out=pw.grad, accumulate=mode)
             if bg is not None:
-                ops.col_sum(e2, out=bg, accumulate=True)
+                ops.col_sum(e2, out=bg, accumulate=not ow)
         if self.need_err_input:
             ei = self.alloc_err_input(self.input.devmem.shape)
             aux, aux_act = self.aux_tensor()

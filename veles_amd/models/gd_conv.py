@@ -18,6 +18,7 @@ __all__ = ["GradientDescentConv", "GDTanhConv", "GDRELUConv",
 
 class GradientDescentConv(GradientDescentBase):
     MAPPING = "conv"
+    OVERWRITES_GRADS = True  # zeroes its own span, then accumulates
 
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
@@ -41,6 +42,10 @@ class GradientDescentConv(GradientDescentBase):
         if x.dtype != err.dtype:
             x = x.to(err.dtype)
         pw, pb = fwd._pw_, fwd._pb_
+        if self.store_.overwrite:
+            # the update no longer zeroes the gradient buffer: the split-K
+            # atomics of this layer start from its own zeroed span
+            self.store_.zero_grads((pw, pb))
         # weight AND bias gradients from one implicit-GEMM launch
         ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,
                        fwd.grouping, col=getattr(fwd, "col_", None),

@@ -79,6 +79,10 @@ class ParameterStore(object):
         self._accum_count = 0
         # callables run after every applied update (e.g. ZeroFiller masks)
         self.post_update_hooks = []
+        # every gradient is WRITTEN once per step by its GD unit (no zeroing
+        # pass in the update, no read-modify-write in the FC weight-gradient
+        # GEMMs); decided at finalize (see overwrite_ok)
+        self.overwrite = False
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -140,6 +144,7 @@ class ParameterStore(object):
         if self.lp is not None:
             self.lp.copy_(self.master)
         self._build_buckets(order)
+        self.overwrite = self.overwrite_ok()
         self.finalized = True
         for p in order:
             if hasattr(p.owner, "on_params_finalized"):
@@ -163,6 +168,27 @@ class ParameterStore(object):
         for i, b in enumerate(self.buckets):
             for p in b:
                 p.bucket = i
+
+    def overwrite_ok(self):
+        """Gradients may be overwritten instead of accumulated when one step
+        is one contribution per parameter (no micro-step accumulation) and
+        every GD unit declares it writes its gradients whole
+        (``OVERWRITES_GRADS``)."""
+        import os as _os
+        if _os.environ.get("VELES_AMD_GRAD_OVERWRITE", "1") == "0":
+            return False
+        gds = [p.gd for p in self.params if p.gd is not None]
+        return self.accumulate == 1 and bool(gds) and all(
+            getattr(g, "OVERWRITES_GRADS", False) for g in gds)
+
+    def zero_grads(self, params):
+        """Zero the gradients of ``params`` (one fill over their span)."""
+        ps = [p for p in params if p is not None and p.offset is not None]
+        if not ps:
+            return
+        lo = min(p.offset for p in ps)
+        hi = max(p.offset + p.size for p in ps)
+        self.grad[lo:hi].zero_()
 
     def bucket_view(self, i):
         b = self.buckets[i]
@@ -246,14 +272,17 @@ class ParameterStore(object):
                 self.mom2 = torch.zeros_like(self.mom)
             ops.solver_update(self.master, self.grad, self.mom, self.mom2,
                               self._solver_segs, w_lp=self.lp,
-                              gscale=gscale / self.accumulate, zero_grad=True,
+                              gscale=gscale / self.accumulate,
+                              zero_grad=not self.overwrite,
                               table=self._seg_table)
         elif segs:
-            # the fused kernel also zeroes the gradient buffer
+            # the fused kernel also zeroes the gradient buffer (unless every
+            # gradient is overwritten next step anyway)
             ops.sgd_update(self.master, self.grad, self.mom, segs,
                            w_lp=self.lp, gscale=gscale / self.accumulate,
-                           zero_grad=True, table=self._seg_table)
-        else:
+                           zero_grad=not self.overwrite,
+                           table=self._seg_table)
+        elif not self.overwrite:
             self.grad.zero_()
         self._works = []
         self._launched = set()

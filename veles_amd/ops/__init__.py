@@ -197,6 +197,9 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
     partial sums are reduced with float atomics on the GPU.
     ``bias_grad`` (float32 [M], accumulate only): += alpha * row sums of
     op(a), computed by the same kernel (a ones column appended to op(b)).
+    ``accumulate="overwrite"``: out (and bias_grad) := the product instead
+    of +=, written without reading out - a weight gradient that is the
+    step's only contribution (no zeroing pass needed before it).
 
     float32 / float64 GPU operands run the exact-precision MFMA SGEMM /
     DGEMM (csrc/kernels/gemm_f32.hip; alpha / beta / accumulate only) with
@@ -217,10 +220,11 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         out_dtype = out_dtype or (torch.float32 if accumulate else a.dtype)
         out = (torch.zeros if accumulate else torch.empty)(
             M, N, dtype=out_dtype, device=dev)
+    overwrite = accumulate == "overwrite"
     if _gpu(a) and a.dtype in (torch.float32, torch.float64):
         return _gemm_fx(a, b, trans_a, trans_b, out, M, N, K, alpha, beta,
-                        accumulate, precision_level, bias, act, aux,
-                        bias_grad)
+                        accumulate and not overwrite, precision_level, bias,
+                        act, aux, bias_grad)
     if _gpu(a):
         if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
             raise TypeError("GPU gemm operands must be bfloat16 (or float32 "
@@ -230,7 +234,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
                 raise ValueError("gemm operands must be row-major")
         if accumulate and out.dtype != torch.float32:
             raise TypeError("accumulate requires a float32 output")
-        atomic = 1 if accumulate else 0
+        atomic = 2 if overwrite else (1 if accumulate else 0)
         if splits > 1 and not accumulate:
             raise ValueError("split-K requires accumulate=True")
         if bias_grad is not None and (trans_b or not accumulate):
@@ -259,6 +263,11 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
     if bias is not None:
         r = r + (bias.float().view(1, -1) if bm == 1 else
                  bias.float().view(-1, 1))
+    if overwrite:
+        out.copy_(r.to(out.dtype))
+        if bias_grad is not None:
+            bias_grad.copy_(alpha * A.sum(1))
+        return out
     if accumulate:
         out += r.to(out.dtype)
         if bias_grad is not None:
