@@ -36,8 +36,9 @@ A unit class that cannot be captured sets ``graph_safe = False`` (e.g.
 stochastic pooling: a torch.Generator seeded from the host per minibatch);
 any such unit in a segment keeps that segment eager.  A capture that fails
 (an op that synchronises, an unsupported call) re-runs the pass eagerly and
-pins that key to eager mode.  Multi-rank steps (RCCL collectives inside the
-backward) and gradient accumulation stay eager (``graph_safe`` of the
+pins that key to eager mode.  Multi-rank workflows are not captured at
+all (RCCL collectives and the process group's watchdog thread), and
+gradient accumulation keeps the backward eager (``graph_safe`` of the
 parameter store).  Disable with ``root.common.engine.graphs = False`` or
 ``VELES_AMD_GRAPHS=0``.
 """
@@ -200,7 +201,10 @@ class GraphSegment(object):
         on a side stream with a private memory pool."""
         import torch
         graph = torch.cuda.CUDAGraph()
-        return graph, torch.cuda.graph(graph)
+        # thread-local: helper threads (thread pool, a process group's
+        # watchdog) may keep making stream / event calls during the capture
+        return graph, torch.cuda.graph(graph,
+                                       capture_error_mode="thread_local")
 
     def _end(self):
         if self.mode == "capture":
@@ -295,6 +299,12 @@ def install_step_graphs(wf, warmup=2):
     dev = getattr(wf, "device", None)
     if not graphs_enabled() or dev is None or not getattr(dev, "is_gpu",
                                                           False):
+        return []
+    # multi-rank steps stay eager: the collectives and their watchdog are
+    # not captured, and a large-batch data-parallel step is GPU-bound anyway
+    from veles_amd.parallel import find_dp
+    dp = find_dp(wf)
+    if dp is not None and dp.world_size > 1:
         return []
     ld = wf.loader
     ev = getattr(wf, "evaluator", None)
