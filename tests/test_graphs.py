@@ -233,3 +233,29 @@ def test_stochastic_pool_reference_draws():
     # a different seed draws differently somewhere
     y2, am2 = ops.stochastic_pool(x, 2, 2, (2, 2), False, True, seed=8)
     assert not torch.equal(am, am2)
+
+
+def test_gradient_buckets_keep_a_small_tail():
+    """Buckets follow the backward order (the flat buffer is in reverse
+    registration order); the last bucket - the one no backward work can
+    hide - holds only the layers finishing last (<= tail_bucket_mb)."""
+    import numpy
+    from veles_amd.models.params import ParameterStore
+
+    class Owner(object):
+        pass
+    st = ParameterStore(None)
+    sizes = [("conv1", 34848), ("conv2", 307200), ("conv3", 884736),
+             ("conv4", 663552), ("conv5", 442368), ("fc6", 37748736),
+             ("fc7", 16777216), ("fc8", 4096000)]
+    for name, n in sizes:
+        o = Owner()
+        o.name = name
+        st.register(o, "weights", numpy.zeros(n, numpy.float32))
+    st.finalize()
+    names = [[p.owner.name for p in b] for b in st.buckets]
+    assert names[0] == ["fc8", "fc7"] and names[1] == ["fc6"]
+    assert names[-1] == ["conv2", "conv1"]  # 1.3 MB tail
+    assert sum(p.size for p in st.buckets[-1]) * 4 <= 2 << 20
+    assert [p for b in st.buckets for p in b] == sorted(
+        st.params, key=lambda p: p.offset)

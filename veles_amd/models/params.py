@@ -165,6 +165,19 @@ class ParameterStore(object):
                 cur, size = [], 0
         if cur:
             self.buckets.append(cur)
+        # the last bucket can only start reducing when the whole backward
+        # is done: keep it to the layers that finish last (AlexNet: conv2 +
+        # conv1, 1.4 MB) so conv5..conv3 reduce under their backward
+        tail_cap = int(get(root.common.engine.dp.tail_bucket_mb, 2) *
+                       (1 << 20) / 4)
+        last = self.buckets[-1] if self.buckets else []
+        if len(last) > 1:
+            tail, size = [], 0
+            while len(last) > 1 and size + last[-1].size <= tail_cap:
+                size += last[-1].size
+                tail.insert(0, last.pop())
+            if tail:
+                self.buckets.append(tail)
         for i, b in enumerate(self.buckets):
             for p in b:
                 p.bucket = i

@@ -206,6 +206,9 @@ root.common.update({
             # point: 32-64 MB buckets keep every link busy; see
             # docs/PARALLEL.md for the derivation.
             "bucket_mb": 32,
+            # MB of the last bucket (the layers whose gradients come last):
+            # the only all-reduce that cannot overlap the backward pass
+            "tail_bucket_mb": 2,
             "overlap": True,
             "grad_dtype": "float32",
             "timeout_s": 600,
