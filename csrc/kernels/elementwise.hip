@@ -247,7 +247,8 @@ struct SgdSeg {
 };
 __global__ void sgd4_kernel(float4* w, float4* grad, float4* mom,
                             uint2* w_lp, const SgdSeg* segs, int nseg,
-                            long long total4, float gscale, int zero_grad) {
+                            long long total4, float gscale,
+                            long long zero_from) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
        i < total4; i += (long long)gridDim.x * blockDim.x) {
     long long e = i * 4;
@@ -277,7 +278,9 @@ __global__ void sgd4_kernel(float4* w, float4* grad, float4* mom,
     }
     w[i] = wv;
     if (mom) mom[i] = mv;
-    if (zero_grad) grad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // gradients at and past zero_from (a 64-aligned parameter offset) are
+    // cleared for the next step's split-K atomics
+    if (e >= zero_from) grad[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (w_lp) {
       uint2 o;
       o.x = f2bf(wp[0]) | ((uint32_t)f2bf(wp[1]) << 16);
@@ -589,7 +592,8 @@ struct SolverSeg {
 };
 __global__ void solver_kernel(float* w, float* grad, float* s1, float* s2,
                               uint16_t* w_lp, const SolverSeg* segs, int nseg,
-                              long long total, float gscale, int zero_grad) {
+                              long long total, float gscale,
+                              long long zero_from) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
        i < total; i += (long long)gridDim.x * blockDim.x) {
     int lo = 0, hi = nseg - 1;
@@ -637,7 +641,7 @@ __global__ void solver_kernel(float* w, float* grad, float* s1, float* s2,
       }
       w[i] = wi;
     }
-    if (zero_grad) grad[i] = 0.f;
+    if (i >= zero_from) grad[i] = 0.f;
     if (w_lp) w_lp[i] = f2bf(wi);
   }
 }
@@ -833,23 +837,23 @@ HVK_API int hvk_mse(const void* y, int y_dt, const void* t, int t_dt, int B,
 
 HVK_API int hvk_sgd4(float* w, float* grad, float* mom, void* w_lp,
                      const void* segs, int nseg, long long total, float gscale,
-                     int zero_grad, hipStream_t s) {
+                     long long zero_from, hipStream_t s) {
   if (total % 4 || ((uintptr_t)w & 15) || ((uintptr_t)grad & 15) ||
       ((uintptr_t)mom & 15) || ((uintptr_t)w_lp & 7))
     return -1;
   hipLaunchKernelGGL(sgd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, s,
                      (float4*)w, (float4*)grad, (float4*)mom, (uint2*)w_lp,
-                     (const SgdSeg*)segs, nseg, total / 4, gscale, zero_grad);
+                     (const SgdSeg*)segs, nseg, total / 4, gscale, zero_from);
   return (int)hipGetLastError();
 }
 
 HVK_API int hvk_solver(float* w, float* grad, float* s1, float* s2,
                        void* w_lp, const void* segs, int nseg,
-                       long long total, float gscale, int zero_grad,
+                       long long total, float gscale, long long zero_from,
                        hipStream_t s) {
   hipLaunchKernelGGL(solver_kernel, dim3(grid_for(total)), dim3(256), 0, s, w,
                      grad, s1, s2, (uint16_t*)w_lp, (const SolverSeg*)segs,
-                     nseg, total, gscale, zero_grad);
+                     nseg, total, gscale, zero_from);
   return (int)hipGetLastError();
 }
 
@@ -1123,6 +1127,73 @@ HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
                      st, (const uint16_t*)x, (uint16_t*)y, H, W, C, s, pt, pl,
                      H2, W2, make_fastdiv(s), make_fastdiv(W2),
                      make_fastdiv(H2), runs);
+  return (int)hipGetLastError();
+}
+
+// Space-to-depth weights: w [OC][KH][KW][C] -> w2 [OC][KH2][KW2][s][s][C],
+// w2[o][a][b][dy][dx][c] = w[o][a*s+dy][b*s+dx][c] (0 past KH / KW): the
+// stride-1 conv on the space-to-depth image equals the strided conv on x.
+__global__ void s2d_weights_kernel(const uint16_t* __restrict__ w,
+                                   uint16_t* __restrict__ w2, int OC, int KH,
+                                   int KW, int C, int s, int KH2, int KW2) {
+  const long long total = (long long)OC * KH2 * KW2 * s * s * C;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       q < total; q += (long long)gridDim.x * blockDim.x) {
+    long long r = q;
+    const int c = (int)(r % C); r /= C;
+    const int dx = (int)(r % s); r /= s;
+    const int dy = (int)(r % s); r /= s;
+    const int b = (int)(r % KW2); r /= KW2;
+    const int a = (int)(r % KH2);
+    const int o = (int)(r / KH2);
+    const int kh = a * s + dy, kw = b * s + dx;
+    w2[q] = (kh < KH && kw < KW)
+                ? w[(((long long)o * KH + kh) * KW + kw) * C + c]
+                : (uint16_t)0;
+  }
+}
+
+// The inverse fold of the weight gradient: dw[o][kh][kw][c] += dw2[o][kh/s]
+// [kw/s][kh%s][kw%s][c]; clear = 1 zeroes all of dw2 (padded taps too), so
+// the next step's split-K atomics start from zeros without a memset.
+__global__ void s2d_grad_fold_kernel(float* __restrict__ dw2,
+                                     float* __restrict__ dw, int OC, int KH,
+                                     int KW, int C, int s, int KH2, int KW2,
+                                     int clear) {
+  const long long total = (long long)OC * KH2 * KW2 * s * s * C;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       q < total; q += (long long)gridDim.x * blockDim.x) {
+    long long r = q;
+    const int c = (int)(r % C); r /= C;
+    const int dx = (int)(r % s); r /= s;
+    const int dy = (int)(r % s); r /= s;
+    const int b = (int)(r % KW2); r /= KW2;
+    const int a = (int)(r % KH2);
+    const int o = (int)(r / KH2);
+    const int kh = a * s + dy, kw = b * s + dx;
+    const float v = dw2[q];
+    if (kh < KH && kw < KW)
+      dw[(((long long)o * KH + kh) * KW + kw) * C + c] += v;
+    if (clear) dw2[q] = 0.f;
+  }
+}
+
+HVK_API int hvk_s2d_weights(const void* w, void* w2, int OC, int KH, int KW,
+                            int C, int s, hipStream_t st) {
+  const int KH2 = (KH + s - 1) / s, KW2 = (KW + s - 1) / s;
+  const long long total = (long long)OC * KH2 * KW2 * s * s * C;
+  hipLaunchKernelGGL(s2d_weights_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     st, (const uint16_t*)w, (uint16_t*)w2, OC, KH, KW, C, s,
+                     KH2, KW2);
+  return (int)hipGetLastError();
+}
+
+HVK_API int hvk_s2d_grad_fold(float* dw2, float* dw, int OC, int KH, int KW,
+                              int C, int s, int clear, hipStream_t st) {
+  const int KH2 = (KH + s - 1) / s, KW2 = (KW + s - 1) / s;
+  const long long total = (long long)OC * KH2 * KW2 * s * s * C;
+  hipLaunchKernelGGL(s2d_grad_fold_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     st, dw2, dw, OC, KH, KW, C, s, KH2, KW2, clear);
   return (int)hipGetLastError();
 }
 

@@ -1287,15 +1287,19 @@ __global__ void im2col_kernel(const uint16_t* x, uint16_t* col, ConvGeom g,
 
 // Split-K finishing pass: C = epilogue(ws), ws the f32 sum of the K splits
 // (N % 8 == 0 and Epi::fast_ok(): one 8-column chunk per thread)
-__global__ void splitk_finish_kernel(const float* __restrict__ ws, int M,
-                                     int N, Epi e) {
+__global__ void splitk_finish_kernel(float* __restrict__ ws, int M, int N,
+                                     Epi e, int clear) {
   const int CH = N >> 3;
   const long long total = (long long)M * CH;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
        q < total; q += (long long)gridDim.x * blockDim.x) {
     const int m = (int)(q / CH), c8 = (int)(q - (long long)m * CH) * 8;
-    const float4* src = (const float4*)(ws + (long long)m * N + c8);
+    float4* src = (float4*)(ws + (long long)m * N + c8);
     const float4 lo = src[0], hi = src[1];
+    if (clear) {  // leave the workspace zeroed for the next split-K GEMM
+      src[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     e.store8_fast(0, m, c8, v);
   }
@@ -1368,17 +1372,21 @@ HVK_API int hvk_gemm(int transA, int transB, int M, int N, int K,
 // per-column bias, the activation and the aux derivative and casts to C.
 // Same arguments as hvk_gemm minus beta / accumulate / bias_grad; N % 8 == 0
 // and 16-B aligned C / bias / aux rows (-4 otherwise: use hvk_gemm).
+// ws_zero = 1: ws is all zeros on entry and is left all zeros (the finishing
+// pass clears what it read) - no memset launch per GEMM.
 HVK_API int hvk_gemm_splitk(int transA, int transB, int M, int N, int K,
                             const void* A, int lda, const void* B, int ldb,
                             void* C, int ldc, int out_f32, float alpha,
                             const float* bias, int act, const void* aux,
                             int ld_aux, int aux_act, int splits, float* ws,
-                            hipStream_t s) {
+                            int ws_zero, hipStream_t s) {
   Epi e = make_epi(C, ldc, M, N, out_f32, 0, alpha, 0.f, bias, 1, act, aux,
                    ld_aux, aux_act);
   if (N % 8 || !e.fast_ok() || ((uintptr_t)ws & 15) || splits < 2) return -4;
-  hipError_t err = hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), s);
-  if (err != hipSuccess) return (int)err;
+  if (!ws_zero) {
+    hipError_t err = hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), s);
+    if (err != hipSuccess) return (int)err;
+  }
   const int rc = hvk_gemm(transA, transB, M, N, K, A, lda, B, ldb, ws, N, 1,
                           1, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0, splits,
                           nullptr, s);
@@ -1387,7 +1395,7 @@ HVK_API int hvk_gemm_splitk(int transA, int transB, int M, int N, int K,
   long long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(splitk_finish_kernel, dim3((int)blocks), dim3(256), 0, s,
-                     (const float*)ws, M, N, e);
+                     ws, M, N, e, ws_zero);
   return (int)hipGetLastError();
 }
 

@@ -13,7 +13,7 @@ int hvk_gemm_splitk(int transA, int transB, int M, int N, int K,
                     const void* A, int lda, const void* B, int ldb, void* C,
                     int ldc, int out_f32, float alpha, const float* bias,
                     int act, const void* aux, int ld_aux, int aux_act,
-                    int splits, float* ws, hipStream_t s);
+                    int splits, float* ws, int ws_zero, hipStream_t s);
 int hvk_conv_fwd(const void* X, const void* W, const float* bias, void* Y,
                  int N, int H, int Wd, int C, int OC, int KH, int KW, int sy,
                  int sx, int pt, int pl, int OH, int OW, int groups, int act,

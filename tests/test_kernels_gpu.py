@@ -254,6 +254,23 @@ def test_sgd_and_colsum():
     close(ops.col_sum(x.to(DEV)), ops.col_sum(x), 1e-4)
 
 
+@pytest.mark.parametrize("zero", [True, False, 5056])
+def test_sgd_zero_tail(zero):
+    """zero_grad=True clears the whole gradient after the update, an int
+    offset only grad[offset:] (the split-K layers' tail), False nothing."""
+    n = 10048
+    w, g, m = torch.randn(n), torch.randn(n), torch.randn(n)
+    segs = [(0, 5056, 0.1, 0.0, 0.0, 0.9), (5056, n, 0.2, 0.0, 0.0, 0.5)]
+    gg = g.to(DEV)
+    ops.sgd_update(w.to(DEV), gg, m.to(DEV), segs,
+                   w_lp=torch.empty(n, dtype=BF, device=DEV), zero_grad=zero)
+    gc = g.clone()
+    ops.sgd_update(w, gc, m, segs, zero_grad=zero)
+    zf = 0 if zero is True else (n if zero is False else zero)
+    assert torch.equal(gg.cpu(), gc)
+    assert torch.equal(gc[:zf], g[:zf]) and not gc[zf:].any()
+
+
 def test_dropout_mask_matches_reference():
     x = torch.randn(12345)
     y = ops.dropout(x, 0.4, 1234)
@@ -321,6 +338,11 @@ def test_conv_im2col_path_fwd_and_wgrad():
     ops.conv_wgrad(x.to(DEV), dy.to(DEV), dgot, (s, s), (0, 0, 0, 0), 1,
                    col=ws["col"])
     close(dgot, dref, 1e-2)
+    # the space-to-depth gradient workspace clears itself in the fold: a
+    # second accumulation adds exactly one more gradient
+    ops.conv_wgrad(x.to(DEV), dy.to(DEV), dgot, (s, s), (0, 0, 0, 0), 1,
+                   col=ws["col"])
+    close(dgot, 2 * dref, 1e-2)
 
 
 @pytest.mark.parametrize("C", [96, 256, 8])
@@ -383,7 +405,9 @@ def test_solver_kernel(mode):
     # DPP-halo backward: 2 blocks per wave (C = 256), one (C = 512), and
     # the per-thread fallback past 64 chunks (C = 528)
     ((2, 27, 27, 256), 2, 5, "x"), ((1, 9, 9, 512), 2, 5, "sep"),
-    ((1, 7, 7, 528), 2, 5, "sep")])
+    ((1, 7, 7, 528), 2, 5, "sep"),
+    # row-marching forward: two 64-lane column groups (OW = 66)
+    ((1, 11, 133, 16), 2, 5, "x")])
 def test_lrn_pool_fused(shape, stride, n, aux_mode):
     """Fused LRN -> 3x3 max pool forward / backward against the fp32
     reference; stride 2 runs the 2x2-block backward kernel, stride 3 the

@@ -18,7 +18,8 @@ __all__ = ["GradientDescentConv", "GDTanhConv", "GDRELUConv",
 
 class GradientDescentConv(GradientDescentBase):
     MAPPING = "conv"
-    OVERWRITES_GRADS = True  # zeroes its own span, then accumulates
+    OVERWRITES_GRADS = True  # starts from a zeroed span, then accumulates
+    ZEROED_BY_UPDATE = True  # the fused update clears the span for it
 
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
@@ -42,9 +43,11 @@ class GradientDescentConv(GradientDescentBase):
         if x.dtype != err.dtype:
             x = x.to(err.dtype)
         pw, pb = fwd._pw_, fwd._pb_
-        if self.store_.overwrite:
-            # the update no longer zeroes the gradient buffer: the split-K
-            # atomics of this layer start from its own zeroed span
+        if self.store_.overwrite and not all(
+                self.store_.cleared_by_update(p) for p in (pw, pb)
+                if p is not None):
+            # the split-K atomics of this layer start from its own zeroed
+            # span (normally the update already cleared it: zero_tail)
             self.store_.zero_grads((pw, pb))
         # weight AND bias gradients from one implicit-GEMM launch
         ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,

@@ -83,6 +83,7 @@ class ParameterStore(object):
         # pass in the update, no read-modify-write in the FC weight-gradient
         # GEMMs); decided at finalize (see overwrite_ok)
         self.overwrite = False
+        self.zero_tail = 0
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -145,6 +146,16 @@ class ParameterStore(object):
             self.lp.copy_(self.master)
         self._build_buckets(order)
         self.overwrite = self.overwrite_ok()
+        # overwrite mode: the update clears the gradients of the split-K
+        # layers (``ZEROED_BY_UPDATE`` GDs, laid out last) after reading them,
+        # so those layers need no zeroing launch of their own before their
+        # atomics (one pass fused into the update instead of one per layer)
+        self.zero_tail = self.total
+        if self.overwrite:
+            tail = [p.offset for p in order if p.gd is not None and
+                    getattr(p.gd, "ZEROED_BY_UPDATE", False)]
+            if tail:
+                self.zero_tail = min(tail)
         self.finalized = True
         for p in order:
             if hasattr(p.owner, "on_params_finalized"):
@@ -193,6 +204,11 @@ class ParameterStore(object):
         gds = [p.gd for p in self.params if p.gd is not None]
         return self.accumulate == 1 and bool(gds) and all(
             getattr(g, "OVERWRITES_GRADS", False) for g in gds)
+
+    def cleared_by_update(self, p):
+        """True when the update clears ``p``'s gradient after every step."""
+        return (self.overwrite and p is not None and p.offset is not None and
+                p.offset >= self.zero_tail)
 
     def zero_grads(self, params):
         """Zero the gradients of ``params`` (one fill over their span)."""
@@ -286,17 +302,19 @@ class ParameterStore(object):
             ops.solver_update(self.master, self.grad, self.mom, self.mom2,
                               self._solver_segs, w_lp=self.lp,
                               gscale=gscale / self.accumulate,
-                              zero_grad=not self.overwrite,
+                              zero_grad=self._zero_arg(),
                               table=self._seg_table)
         elif segs:
             # the fused kernel also zeroes the gradient buffer (unless every
             # gradient is overwritten next step anyway)
             ops.sgd_update(self.master, self.grad, self.mom, segs,
                            w_lp=self.lp, gscale=gscale / self.accumulate,
-                           zero_grad=not self.overwrite,
+                           zero_grad=self._zero_arg(),
                            table=self._seg_table)
         elif not self.overwrite:
             self.grad.zero_()
+        elif self.zero_tail < self.total:
+            self.grad[self.zero_tail:].zero_()
         self._works = []
         self._launched = set()
         self._ready.clear()
@@ -309,6 +327,10 @@ class ParameterStore(object):
         for hook in self.post_update_hooks:
             hook()
         return True
+
+    def _zero_arg(self):
+        # everything (accumulating GDs) or the split-K tail (overwrite mode)
+        return True if not self.overwrite else self.zero_tail
 
     # -- HIP-graph replay support (veles_amd/graphs.py) ----------------------
     def graph_safe(self):

@@ -242,13 +242,16 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         sk = 0 if accumulate or beta != 0.0 else \
             auto_splitk(M, N, K, out, bias, aux)
         if sk > 1:
-            ws = torch.empty(M * N, dtype=torch.float32, device=dev)
+            # a persistent, self-clearing f32 workspace per size (zeroed once;
+            # the finishing pass zeroes what it reads)
+            ws = _workspace(("splitk_ws", M * N), (M * N,), torch.float32,
+                            dev, zero=True)
             _lib_call("hvk_gemm_splitk", int(trans_a), int(trans_b), M, N, K,
                       _p(a), a.stride(0), _p(b), b.stride(0), _p(out),
                       out.stride(0), int(out.dtype == torch.float32),
                       float(alpha), _p(bias), act, _p(aux),
                       0 if aux is None else aux.stride(0), aux_act, sk,
-                      _p(ws), _s(a))
+                      _p(ws), 1, _s(a))
             return out
         _lib_call("hvk_gemm", int(trans_a), int(trans_b), M, N, K, _p(a),
                   a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0),
@@ -406,13 +409,20 @@ def space_to_depth(x, s, KH, KW, padding):
 
 
 def _s2d_weights(w, s):
+    """[OC][KH][KW][C] -> the space-to-depth weights [OC][KH2][KW2][s*s*C]
+    (taps past KH / KW zero) in one kernel."""
     OC, KH, KW, C = w.shape
     KH2, KW2 = -(-KH // s), -(-KW // s)
-    wp = _workspace(("s2dw", id(w)), (OC, KH2 * s, KW2 * s, C), w.dtype,
-                    w.device, zero=True)
+    w2 = _workspace(("s2dw", id(w)), (OC, KH2, KW2, s * s * C), w.dtype,
+                    w.device)
+    if _gpu(w) and w.dtype == torch.bfloat16 and w.is_contiguous():
+        _lib_call("hvk_s2d_weights", _p(w), _p(w2), OC, KH, KW, C, s, _s(w))
+        return w2
+    wp = torch.zeros(OC, KH2 * s, KW2 * s, C, dtype=w.dtype, device=w.device)
     wp[:, :KH, :KW].copy_(w)   # taps past KH/KW stay zero
-    return wp.view(OC, KH2, s, KW2, s, C).permute(0, 1, 3, 2, 4, 5) \
-        .reshape(OC, KH2, KW2, s * s * C)
+    w2.copy_(wp.view(OC, KH2, s, KW2, s, C).permute(0, 1, 3, 2, 4, 5)
+             .reshape(OC, KH2, KW2, s * s * C))
+    return w2
 
 
 def im2col(x, KH, KW, sliding, padding, out=None):
@@ -558,17 +568,22 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
                 space_to_depth(x, s2, KH, KW, padding)
             H2, W2, C2 = x2.shape[1], x2.shape[2], x2.shape[3]
             KH2, KW2 = -(-KH // s2), -(-KW // s2)
+            # self-clearing workspace: zeroed once, cleared again by the fold
             dw2 = _workspace(("s2dg", dw.data_ptr()), (OC, KH2, KW2, C2),
-                             torch.float32, dw.device)
-            dw2.zero_()
+                             torch.float32, dw.device, zero=True)
             sp = splits or wgrad_splits(N * OH * OW, OC, KH2 * KW2 * C2 + 1,
                                         1)
             _lib_call("hvk_conv_wgrad", _p(x2), _p(dy), _p(dw2), N, H2, W2,
                       C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, int(sp),
                       _p(dbias), _s(x))
+            if dw.is_contiguous():
+                _lib_call("hvk_s2d_grad_fold", _p(dw2), _p(dw), OC, KH, KW, C,
+                          s2, 1, _s(x))
+                return dw
             full = dw2.view(OC, KH2, KW2, s2, s2, C).permute(
                 0, 1, 3, 2, 4, 5).reshape(OC, KH2 * s2, KW2 * s2, C)
             dw += full[:, :KH, :KW]
+            dw2.zero_()
             return dw
         if isinstance(col, S2DImage):
             col = None
@@ -1153,6 +1168,16 @@ class SegmentTable(object):
         return self.dev
 
 
+def _zero_from(zero_grad, n):
+    """Offset from which an update clears the gradients: True -> 0 (all),
+    False / None -> n (none), an int -> that offset (the split-K tail)."""
+    if zero_grad is None or zero_grad is False:
+        return n
+    if zero_grad is True:
+        return 0
+    return max(0, min(int(zero_grad), n))
+
+
 def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
                table=None):
     """Fused multi-segment SGD (flat float32 buffers).
@@ -1160,8 +1185,11 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
     segs: [(begin, end, lr, weights_decay, l1_vs_l2, gradient_moment)]
       g = grad*gscale + decay*((1-l1)*w + l1*sign(w));  v = moment*v - lr*g;
       w += v;  w_lp = bfloat16(w)
+    zero_grad: True clears the whole gradient after reading it, an int
+    offset clears only grad[offset:] (see :func:`_zero_from`).
     table: optional :class:`SegmentTable` the packed segments are kept in."""
     n = w.numel()
+    zf = _zero_from(zero_grad, n)
     if _gpu(w):
         raw = _pack_sgd_segs(segs)
         st = table.update(raw) if table is not None else \
@@ -1169,12 +1197,12 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
         fn = getattr(_lib.lib(), "hvk_sgd4")
         if mom is not None and fn(_p(w), _p(grad), _p(mom), _p(w_lp),
                                   _p(st), len(segs), n, float(gscale),
-                                  int(zero_grad), _s(w)) == 0:
+                                  zf, _s(w)) == 0:
             return w
         _lib_call("hvk_sgd", _p(w), _p(grad), _p(mom), _p(w_lp), _p(st),
                   len(segs), n, float(gscale), _s(w))
-        if zero_grad:
-            grad.zero_()
+        if zf < n:
+            grad[zf:].zero_()
         return w
     for b, e, lr, d, l1, m in segs:
         ws = w[b:e]
@@ -1188,8 +1216,8 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
         ws += v
     if w_lp is not None:
         w_lp.copy_(w.to(w_lp.dtype))
-    if zero_grad:
-        grad.zero_()
+    if zf < n:
+        grad[zf:].zero_()
     return w
 
 
@@ -1203,12 +1231,13 @@ def solver_update(w, grad, s1, s2, segs, w_lp=None, gscale=1.0,
     segs: [(begin, end, lr, decay, l1_vs_l2, moment, mode, eps, rho)], modes
     in :data:`SOLVERS` (csrc/kernels/elementwise.hip ``solver_kernel``)."""
     n = w.numel()
+    zf = _zero_from(zero_grad, n)
     if _gpu(w):
         raw = _pack_solver_segs(segs)
         st = table.update(raw) if table is not None else \
             _segs_tensor(raw, w.device)
         _lib_call("hvk_solver", _p(w), _p(grad), _p(s1), _p(s2), _p(w_lp),
-                  _p(st), len(segs), n, float(gscale), int(zero_grad), _s(w))
+                  _p(st), len(segs), n, float(gscale), zf, _s(w))
         return w
     for b, e, lr, d, l1, m, mode, eps, rho in segs:
         ws = w[b:e]
@@ -1241,8 +1270,8 @@ def solver_update(w, grad, s1, s2, segs, w_lp=None, gscale=1.0,
             ws += a
     if w_lp is not None:
         w_lp.copy_(w.to(w_lp.dtype))
-    if zero_grad:
-        grad.zero_()
+    if zf < n:
+        grad[zf:].zero_()
     return w
 
 

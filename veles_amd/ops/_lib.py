@@ -30,7 +30,7 @@ _SIGS = {
     "hvk_gemm": [I, I, I, I, I, P, I, P, I, P, I, I, I, F, F, P, I, I, P, I, I,
                  I, P, P],
     "hvk_gemm_splitk": [I, I, I, I, I, P, I, P, I, P, I, I, F, P, I, P, I, I,
-                        I, P, P],
+                        I, P, I, P],
     "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
     "hvk_conv_dgrad_t": [P, P, P] + [I] * 14 + [P, I, P],
     "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P, P],
@@ -42,7 +42,7 @@ _SIGS = {
     "hvk_softmax_ce": [P, I, I, I, P, F, P, I, P, P, P, P, P],
     "hvk_mse": [P, I, P, I, I, I, F, P, I, P, P, I, P],
     "hvk_sgd": [P, P, P, P, P, I, L, F, P],
-    "hvk_sgd4": [P, P, P, P, P, I, L, F, I, P],
+    "hvk_sgd4": [P, P, P, P, P, I, L, F, L, P],
     "hvk_col_sum": [P, I, I, I, P, F, P],
     "hvk_row_sum": [P, I, I, I, P, F, P],
     "hvk_act_fwd": [P, I, P, I, L, I, P],
@@ -57,8 +57,10 @@ _SIGS = {
     "hvk_u64_to_uniform": [P, P, L, F, F, P],
     "hvk_join": [P, P, I, I, P, I, P],
     "hvk_cast": [P, I, P, I, L, F, P],
-    "hvk_solver": [P, P, P, P, P, P, I, L, F, I, P],
+    "hvk_solver": [P, P, P, P, P, P, I, L, F, L, P],
     "hvk_space_to_depth": [P, P] + [I] * 9 + [P],
+    "hvk_s2d_weights": [P, P] + [I] * 5 + [P],
+    "hvk_s2d_grad_fold": [P, P] + [I] * 6 + [P],
     "hvk_pool_fwd": [P, P, P] + [I] * 13 + [P],
     "hvk_pool_bwd": [P, P, P] + [I] * 13 + [P, I, P],
     "hvk_lrn_fwd": [P, P, L, I, I, F, F, F, P],
