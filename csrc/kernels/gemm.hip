@@ -10,7 +10,8 @@
 // the (absent) Znicz conv/all2all/gd kernels.
 //
 // Block tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 =
-// 4x4 MFMA 16x16 tiles.  Operands are register-staged global->LDS (async
+// 4x4 MFMA 16x16 tiles - or, for most LDS-DMA shapes, 512 threads = 8 waves
+// (2x4, each 64x32) on the same tile and LDS footprint (see want_w8).  Operands are register-staged global->LDS (async
 // STAGE split: next tile's global loads are issued before this tile's MFMAs,
 // written to the other LDS buffer after them), double buffered, one barrier
 // per K-tile.  LDS images:
@@ -20,6 +21,8 @@
 //            b ^ h(k), h(k) = (k&3) | ((k>>3)&1)<<2 -> ds_read_b64_tr_b16
 //            transposed fragment reads conflict-free
 // Grid x is remapped so that consecutive output tiles share one XCD's L2.
+#include <type_traits>
+
 #include "conv_geom.h"
 
 using namespace hvk;
@@ -76,7 +79,7 @@ struct DenseK {
   static constexpr bool kGlds = true;
   static constexpr bool kFast = false;
   static constexpr bool kBuf = true;
-  __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
+  __host__ __device__ bool dma_ok() const { return vec && (K & 7) == 0; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     // bitwise condition: && made hipcc branch around the address
     return pick_src(c.row + k, (c.ok != 0) & (k < K));
@@ -124,7 +127,7 @@ struct DenseMN {
     return c < cols ? ((uint32_t)kr * (uint32_t)ld + (uint32_t)c) * 2u
                     : kBufOOB;
   }
-  __device__ bool dma_ok() const {
+  __host__ __device__ bool dma_ok() const {
     return vec && (cols & 7) == 0 && (ones_col < 0 || (ones_col & 7) == 0);
   }
   __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int k) const {
@@ -179,7 +182,7 @@ struct ConvFwdA {
   }
   static constexpr bool kGlds = true;
   static constexpr bool kFast = true;
-  __device__ bool dma_ok() const { return vec && g.KH <= 32 && g.KW <= 32; }
+  __host__ __device__ bool dma_ok() const { return vec && g.KH <= 32 && g.KW <= 32; }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return g_zero8;
     uint32_t t, ch, kh, kw;
@@ -263,7 +266,7 @@ struct ConvDgradA {
   static constexpr bool kGlds = true;
   // stride 1 only (strided dgrad: ConvDgradAStr)
   static constexpr bool kFast = true;
-  __device__ bool dma_ok() const {
+  __host__ __device__ bool dma_ok() const {
     return vec && g.sy == 1 && g.sx == 1 && g.KH <= 32 && g.KW <= 32;
   }
   __device__ __forceinline__ const uint16_t* src(const Ctx& c, int k) const {
@@ -309,7 +312,7 @@ struct ConvDgradAStr : ConvDgradA {
   static constexpr bool kFast = false;
   static constexpr bool kBuf = false;
   bool buf_ok(int) const { return false; }
-  __device__ bool dma_ok() const { return vec; }
+  __host__ __device__ bool dma_ok() const { return vec; }
 };
 
 // scalar-gather variant for OC % 8 != 0 (a separate instantiation: its
@@ -320,7 +323,7 @@ struct ConvDgradAS : ConvDgradA {
   static constexpr bool kFast = false;
   static constexpr bool kBuf = false;
   bool buf_ok(int) const { return false; }
-  __device__ bool dma_ok() const { return false; }
+  __host__ __device__ bool dma_ok() const { return false; }
   __device__ uint4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero4();
     uint16_t e[8];
@@ -361,7 +364,7 @@ struct ConvWgradB {
   static constexpr bool kFast = true;
   static constexpr bool kBuf = false;
   bool buf_ok(int) const { return false; }
-  __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
+  __host__ __device__ bool dma_ok() const { return vec && (KK & 7) == 0; }
   // per DMA slot: the column's tap (fixed) and a running pixel p with
   // rem = p mod OH*OW and the image base, advanced by BK per tile - one
   // division per slot and tile (rem -> oh, ow) instead of two, no branches
@@ -477,7 +480,7 @@ struct ConvFwdRunA {
   static constexpr bool kFast = false;
   static constexpr bool kBuf = false;
   bool buf_ok(int) const { return false; }
-  __device__ bool dma_ok() const { return false; }
+  __host__ __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
   RunGeom r;
@@ -527,7 +530,7 @@ struct ConvWgradRunB {
   static constexpr bool kFast = false;
   static constexpr bool kBuf = false;
   bool buf_ok(int) const { return false; }
-  __device__ bool dma_ok() const { return false; }
+  __host__ __device__ bool dma_ok() const { return false; }
   const uint16_t* x;
   ConvGeom g;
   RunGeom r;
@@ -745,11 +748,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const L& l) {
 
 __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
-template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF>
-__global__ void __launch_bounds__(NTHR, 2)
+// W8: 8 waves (2 x 4, each 64 x BN/4) per 128 x BN block instead of 4 (2 x 2,
+// each 64 x BN/2): twice the waves per CU at the same LDS footprint, for
+// latency cover; LDS-DMA loaders only, BN 64 / 128.
+template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF, bool W8>
+__global__ void __launch_bounds__(W8 ? 512 : NTHR, 2)
 gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
             int tiles_n, int tiles, int splits) {
-  constexpr int NB = BN_ / 32;          // B chunks per thread / MFMA n-tiles
+  constexpr int NW = W8 ? 8 : 4;        // waves per block
+  constexpr int NT = NW * 64;           // threads per block
+  constexpr int WNC = NW / 2;           // waves along N
+  constexpr int NB = BN_ / (16 * WNC);  // MFMA n-tiles per wave
+  static_assert(!W8 || BN_ % 64 == 0, "W8 needs BN 64 / 128");
   constexpr int CPR = BN_ / 8;          // MN-major B: chunks per k-row
   constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
   // operand double buffers (64 KiB); reused as the f32 C tile (with a
@@ -778,7 +788,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   lb.group(gi);
   const int m0 = tm * BM, n0 = tn * BN_;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WNC, wn = wid % WNC;
 
   const int fr = lane & 15, fq = lane >> 4;
   const int trq = fr >> 2, trp = fr & 3;
@@ -815,8 +825,8 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        if constexpr (BKM) bfv[i] = frag_k(sB, wn * (BN_ / 2) + i * 16, ks);
-        else bfv[i] = frag_mn(sB, wn * (BN_ / 2) + i * 16, ks);
+        if constexpr (BKM) bfv[i] = frag_k(sB, wn * (BN_ / WNC) + i * 16, ks);
+        else bfv[i] = frag_mn(sB, wn * (BN_ / WNC) + i * 16, ks);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -834,8 +844,8 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     if (la.dma_ok() && lb.dma_ok()) {
       // ---- LDS-DMA pipeline (global_load_lds_dwordx4): the next tile's
       // loads stay in flight across the barrier; one counted vmcnt per tile.
-      constexpr int NIA = 4;               // DMA instructions / wave (A)
-      constexpr int NIB = BKM ? BN_ / 32 : 4;
+      constexpr int NIA = 16 / NW;         // DMA instructions / wave (A)
+      constexpr int NIB = BKM ? BN_ / (8 * NW) : 16 / NW;
       const int w = __builtin_amdgcn_readfirstlane(wid);
       typename LA::Ctx da[NIA];
       DRow fa[NIA];  // fast A loaders (K-major): per-slot row state
@@ -978,12 +988,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
           issue(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * SA,
                 smem + 2 * SA + (cur ^ 1) * SB);
           // leave exactly the next tile's DMAs (NIA + NIB) in flight
-          if constexpr (NIA + NIB == 8)
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          else if constexpr (NIA + NIB == 7)
-            asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIA + NIB) : "memory");
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -997,7 +1002,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       done = true;
     }
   }
-  if (!done) {
+  if constexpr (!W8) if (!done) {
   typename LA::Ctx ca[4];
   typename LB::Ctx cb[4];
   if constexpr (AK) {
@@ -1070,7 +1075,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         int mb = m0 + wm * 64 + i * 16 + fq * 4;
-        int n = n0 + wn * (BN_ / 2) + j * 16 + fr;
+        int n = n0 + wn * (BN_ / WNC) + j * 16 + fr;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) epi.store(gi, mb + rr, n, acc[i][j][rr]);
       }
@@ -1084,14 +1089,14 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       int rb = wm * 64 + i * 16 + fq * 4;
-      int cc = wn * (BN_ / 2) + j * 16 + fr;
+      int cc = wn * (BN_ / WNC) + j * 16 + fr;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + cc] = acc[i][j][rr];
     }
   __syncthreads();
   constexpr int CH = BN_ / 8;
   const bool fast = epi.fast_ok();
-  for (int q = t; q < BM * CH; q += NTHR) {
+  for (int q = t; q < BM * CH; q += NT) {
     int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
     if (m0 + row >= M) continue;
     const float4* src = (const float4*)(sC + row * LDC + c8);
@@ -1134,25 +1139,60 @@ inline int pick_bn(int N, bool allow96) {
   return best;
 }
 
+// GEMM schedule selector (A/B knob, hvk_set_gemm_variant or the
+// HVK_GEMM_VARIANT environment variable): 0 = 4-wave blocks everywhere,
+// 1 = 8-wave blocks wherever they apply (LDS-DMA loaders, BN 64 / 128),
+// default (-1) = 8-wave blocks except for conv backward-data.  Measured on
+// the AlexNet / VGG shapes (profiles/gemm_experiments_r2.md §6): 8 waves
+// per block (4 per SIMD) lift the weight gradients 9-13 % and the FC GEMMs
+// 4-7 %, the forward convs 0-4 %; backward-data loses 1-2 %.
+int g_gemm_variant = -1;
+
+template <class LA, class LB>
+bool want_w8(const LA& la, const LB& lb, int bn) {
+  static const int env = [] {
+    const char* e = getenv("HVK_GEMM_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  const int v = g_gemm_variant >= 0 ? g_gemm_variant : env;
+  if (v == 0 || !(LA::kGlds && LB::kGlds) || (bn != 64 && bn != 128) ||
+      !la.dma_ok() || !lb.dma_ok())
+    return false;
+  return v == 1 || !std::is_base_of<ConvDgradA, LA>::value;
+}
+
 template <class LA, bool AK, class LB, bool BKM, bool BUF>
 hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles_n, int tiles, int splits,
                      int bn, dim3 grid, hipStream_t s) {
+  if constexpr (LA::kGlds && LB::kGlds) {
+    if (want_w8(la, lb, bn)) {
+      if (bn == 64)
+        hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64, BUF, true>), grid,
+                           dim3(512), 0, s, la, lb, epi, M, N, K, k_split,
+                           tiles_n, tiles, splits);
+      else
+        hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF, true>),
+                           grid, dim3(512), 0, s, la, lb, epi, M, N, K,
+                           k_split, tiles_n, tiles, splits);
+      return hipGetLastError();
+    }
+  }
   if (bn == 64)
-    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64, BUF>), grid,
+    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64, BUF, false>), grid,
                        dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
                        tiles_n, tiles, splits);
   else if constexpr (BKM) {
     if (bn == 96)
-      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 96, BUF>), grid,
+      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 96, BUF, false>), grid,
                          dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
                          tiles_n, tiles, splits);
     else
-      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF>), grid,
+      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF, false>), grid,
                          dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
                          tiles_n, tiles, splits);
   } else {
-    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF>), grid,
+    hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 128, BUF, false>), grid,
                        dim3(NTHR), 0, s, la, lb, epi, M, N, K, k_split,
                        tiles_n, tiles, splits);
   }
@@ -1306,6 +1346,8 @@ __global__ void splitk_finish_kernel(float* __restrict__ ws, int M, int N,
 }
 
 }  // namespace
+
+HVK_API void hvk_set_gemm_variant(int v) { g_gemm_variant = v; }
 
 // col[M][Kp] = im2col(X) for a single-group conv (Kp = round_up(KH*KW*C, 8))
 HVK_API int hvk_im2col(const void* X, void* col, int N, int H, int W, int C,
