@@ -234,11 +234,17 @@ __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
 }
 
 // ------------------------------------------------------------------ kernel
-template <class LA, class LB, int BN_, int FA, int FB>
-__global__ void __launch_bounds__(NTHR, 2)
+// W8: 8 waves (2 x 4, each 64 x BN/4) instead of 4 (2 x 2) on the same tile
+// and LDS footprint - more waves per SIMD for latency cover (the bf16
+// kernel's measurement: profiles/gemm_experiments_r2.md §6).
+template <class LA, class LB, int BN_, int FA, int FB, bool W8>
+__global__ void __launch_bounds__(W8 ? 512 : NTHR, 2)
 gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
                 int tiles) {
-  constexpr int NB = BN_ / 32;            // MFMA n-tiles per wave
+  constexpr int NW = W8 ? 8 : 4;          // waves per block
+  constexpr int NT = NW * 64;
+  constexpr int WNC = NW / 2;             // waves along N
+  constexpr int NB = BN_ / (16 * WNC);    // MFMA n-tiles per wave
   constexpr int SA = BM * BK;             // bytes per A stage
   constexpr int SB = BN_ * BK;            // bytes per B stage
   constexpr int OPER = 2 * (SA + SB);
@@ -255,7 +261,7 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
   lb.group(gi);
   const int m0 = tm * BM, n0 = tn * BN_;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WNC, wn = wid % WNC;
   const int fr = lane & 15, fq = lane >> 4;
 
   f32x4 acc[4][NB];
@@ -282,7 +288,7 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = frag(sA, wm * 64 + i * 16);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) bfv[j] = frag(sB, wn * (BN_ / 2) + j * 16);
+    for (int j = 0; j < NB; ++j) bfv[j] = frag(sB, wn * (BN_ / WNC) + j * 16);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -293,8 +299,8 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
 
   // LDS-DMA issue map: instruction I of a stage covers rows 8I..8I+7; lane
   // -> row 8I + (lane >> 3), LDS slot (lane & 7) holds chunk slot ^ (row & 7)
-  constexpr int NIA = SA / (NTHR * 16);   // 4
-  constexpr int NIB = SB / (NTHR * 16);   // 4 (BN 128) or 2 (BN 64)
+  constexpr int NIA = SA / (NT * 16);     // 4 (2 at W8)
+  constexpr int NIB = SB / (NT * 16);     // 4 (BN 128) or 2 (BN 64); half at W8
   const int w = __builtin_amdgcn_readfirstlane(wid);
   typename LA::Ctx da[NIA];
   DRow fa[NIA];  // fast A loaders: per-slot row state
@@ -350,10 +356,8 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
     const int cur = kt & 1;
     if (kt + 1 < nk) {
       issue((kt + 1) * BK, smem + (cur ^ 1) * SA, smem + 2 * SA + (cur ^ 1) * SB);
-      if constexpr (NIA + NIB == 8)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      // leave exactly the next tile's DMAs in flight
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIA + NIB) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -374,13 +378,13 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int rb = wm * 64 + i * 16 + fq * 4;
-      const int cc = wn * (BN_ / 2) + j * 16 + fr;
+      const int cc = wn * (BN_ / WNC) + j * 16 + fr;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + cc] = acc[i][j][rr];
     }
   __syncthreads();
   constexpr int CH = BN_ / 8;
-  for (int q = t; q < BM * CH; q += NTHR) {
+  for (int q = t; q < BM * CH; q += NT) {
     const int row = q / CH, c8 = (q - row * CH) * 8;
     if (m0 + row >= M) continue;
     const float4* src = (const float4*)(sC + row * LDC + c8);
@@ -406,11 +410,25 @@ hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
   const int tiles = tiles_m * tiles_n;
   dim3 grid((unsigned)((long long)tiles * groups));
+  // 8-wave blocks unless HVK_FP8_W8=0 (A/B knob)
+  static const bool w8 = [] {
+    const char* v = getenv("HVK_FP8_W8");
+    return !(v && v[0] == '0');
+  }();
+  if (w8) {
+    if (n64)
+      hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB, true>), grid,
+                         dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
+    else
+      hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB, true>), grid,
+                         dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
+    return hipGetLastError();
+  }
   if (n64)
-    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB>), grid, dim3(NTHR),
-                       0, s, la, lb, e, M, N, K, tiles_n, tiles);
+    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB, false>), grid,
+                       dim3(NTHR), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
   else
-    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB>), grid,
+    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB, false>), grid,
                        dim3(NTHR), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
   return hipGetLastError();
 }
