@@ -1141,8 +1141,8 @@ inline int pick_bn(int N, bool allow96) {
 
 // GEMM schedule selector (A/B knob, hvk_set_gemm_variant or the
 // HVK_GEMM_VARIANT environment variable): 0 = 4-wave blocks everywhere,
-// 1 = 8-wave blocks wherever they apply (LDS-DMA loaders, BN 64 / 128),
-// default (-1) = 8-wave blocks except for conv backward-data.  Measured on
+// default (-1) = 8-wave blocks for the LDS-DMA loaders at BN 64 / 128
+// except conv backward-data.  Measured on
 // the AlexNet / VGG shapes (profiles/gemm_experiments_r2.md §6): 8 waves
 // per block (4 per SIMD) lift the weight gradients 9-13 % and the FC GEMMs
 // 4-7 %, the forward convs 0-4 %; backward-data loses 1-2 %.
@@ -1165,7 +1165,9 @@ template <class LA, bool AK, class LB, bool BKM, bool BUF>
 hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles_n, int tiles, int splits,
                      int bn, dim3 grid, hipStream_t s) {
-  if constexpr (LA::kGlds && LB::kGlds) {
+  // (backward-data never runs 8-wave: not instantiated, half the compile)
+  if constexpr (LA::kGlds && LB::kGlds &&
+                !std::is_base_of<ConvDgradA, LA>::value) {
     if (want_w8(la, lb, bn)) {
       if (bn == 64)
         hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, 64, BUF, true>), grid,
