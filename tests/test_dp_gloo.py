@@ -17,12 +17,17 @@ def _free_port():
     return p
 
 
-def _train(rank, world, port, out, steps, layers_name):
+def _train(rank, world, port, out, steps, layers_name, bucket_mb=None,
+           overlap="1", backend="cpu"):
     import torch
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world),
                        "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port)})
+    os.environ["VELES_AMD_DP_OVERLAP_UPDATE"] = overlap
     torch.set_num_threads(1)
+    from veles_amd.utils.config import root
+    if bucket_mb is not None:
+        root.common.engine.dp.bucket_mb = bucket_mb
     from veles_amd.backends import Device
     from veles_amd.dummy import DummyLauncher
     from veles_amd.models import StandardWorkflow
@@ -40,23 +45,35 @@ def _train(rank, world, port, out, steps, layers_name):
                        "normalization_type": "mean_disp"},
         layers=getattr(zoo, layers_name)(),
         decision_config={"max_epochs": None, "fail_iterations": None})
-    wf.initialize(device=Device(backend="cpu"))
+    wf.initialize(device=Device(backend=backend))
     wf.run_steps(steps)
-    w = [f.weights_master.numpy().copy() for f in wf.forwards
+    if backend != "cpu":
+        torch.cuda.synchronize()
+    w = [f.weights_master.cpu().numpy().copy() for f in wf.forwards
          if getattr(f, "_pw_", None) is not None]
     numpy.savez(out % rank, *w)
     if dp is not None:
+        st = wf.param_store_
+        # small buckets: several per-bucket updates on the overlap path
+        assert bucket_mb is None or len(st.buckets) >= 2, len(st.buckets)
+        assert st._overlap == (overlap != "0")
         dp.shutdown()
 
 
-@pytest.mark.parametrize("layers_name", ["mnist_fc", "lenet"])
-def test_dp_matches_single_process(tmp_path, layers_name):
+@pytest.mark.parametrize("layers_name,bucket_mb,overlap", [
+    ("mnist_fc", None, "1"), ("lenet", None, "1"), ("lenet", 0.05, "1"),
+    ("mnist_fc", 0.02, "0")])
+def test_dp_matches_single_process(tmp_path, layers_name, bucket_mb,
+                                   overlap):
+    """Per-bucket updates (overlapped with the backward on a GPU side
+    stream) and the single fused update give the same weights."""
     steps = 6
     out = str(tmp_path / "w%d.npz")
     port = _free_port()
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=_train, args=(r, 2, port, out, steps,
-                                               layers_name))
+                                               layers_name, bucket_mb,
+                                               overlap))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -78,6 +95,41 @@ def test_dp_matches_single_process(tmp_path, layers_name):
     for k in w0.files:
         numpy.testing.assert_array_equal(w0[k], w1[k])
         numpy.testing.assert_allclose(w0[k], ws[k], rtol=1e-4, atol=1e-5)
+
+
+def _run_ranks(world, out, steps, layers_name, bucket_mb, overlap, backend):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_train, args=(r, world, port, out, steps,
+                                               layers_name, bucket_mb,
+                                               overlap, backend))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+
+
+@pytest.mark.gpu
+def test_dp_overlapped_update_on_gpu(tmp_path):
+    """Two ranks on the GPU (gloo carries the collectives; RCCL refuses two
+    ranks on one device): the per-bucket updates on the side stream, which
+    wait on each bucket's all-reduce while the backward continues, end with
+    the same weights as the single fused update after the backward, and
+    both ranks agree bit for bit."""
+    steps = 5
+    ov = str(tmp_path / "ov%d.npz")
+    fu = str(tmp_path / "fu%d.npz")
+    _run_ranks(2, ov, steps, "lenet", 0.05, "1", "hip")
+    _run_ranks(2, fu, steps, "lenet", 0.05, "0", "hip")
+    a0, a1, b0 = (numpy.load(ov % 0), numpy.load(ov % 1), numpy.load(fu % 0))
+    for k in a0.files:
+        assert numpy.isfinite(a0[k]).all()
+        numpy.testing.assert_array_equal(a0[k], a1[k])
+        # split-K f32 atomics make runs differ in the last bits; a stale
+        # or raced bucket update would differ by a whole update (~1e-3)
+        numpy.testing.assert_allclose(a0[k], b0[k], rtol=1e-4, atol=1e-6)
 
 
 def _train_local(steps, monkeypatch, acc):

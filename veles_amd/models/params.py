@@ -84,6 +84,10 @@ class ParameterStore(object):
         # GEMMs); decided at finalize (see overwrite_ok)
         self.overwrite = False
         self.zero_tail = 0
+        # multi-rank: per-bucket updates on a side stream (_overlap_update)
+        self._overlap = None
+        self._upd_stream = None
+        self._bucket_tables = {}
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -238,9 +242,73 @@ class ParameterStore(object):
             if i in self._launched:
                 continue
             if all(id(p) in self._ready for p in b):
-                self._launched.add(i)
-                self._works.append(self.dp.all_reduce_async(
-                    self.bucket_view(i)))
+                self._launch_bucket(i)
+
+    def _launch_bucket(self, i):
+        self._launched.add(i)
+        work = self.dp.all_reduce_async(self.bucket_view(i))
+        self._works.append(work)
+        if self._overlap_update():
+            self._bucket_update(i, work)
+
+    # -- per-bucket update overlapped with the backward (multi-rank) ---------
+    def _overlap_update(self):
+        """Multi-rank plain-SGD steps update each bucket as soon as ITS
+        all-reduce is done, on a side stream, while the layers below are
+        still in backward (AlexNet: the 58 M classifier parameters, 0.22 ms
+        of the 0.24 ms update, leave the critical path).  Off for solver
+        segments (adagrad / adadelta / rprop), gradient accumulation and
+        ``VELES_AMD_DP_OVERLAP_UPDATE=0``."""
+        if self._overlap is None:
+            self._overlap = (
+                self.dp is not None and self.dp.world_size > 1 and
+                self.accumulate == 1 and
+                os.environ.get("VELES_AMD_DP_OVERLAP_UPDATE", "1") != "0")
+        if not self._overlap:
+            return False
+        self._cached_segments()
+        return self._solver_segs is None
+
+    def _bucket_span(self, i):
+        """[lo, hi) of bucket i's update: from its first parameter to the
+        next bucket's (the last bucket to ``total``), so the spans tile the
+        store and stay 16-B aligned for the vector update kernel."""
+        lo = self.buckets[i][0].offset
+        hi = self.buckets[i + 1][0].offset if i + 1 < len(self.buckets) \
+            else self.total
+        return lo, hi
+
+    def _bucket_update(self, i, work):
+        import torch
+        from veles_amd import ops
+        lo, hi = self._bucket_span(i)
+        segs = []
+        for b, e, lr, d, l1, m in self._cached_segments():
+            b, e = max(b, lo), min(e, hi)
+            if b < e:
+                segs.append((b - lo, e - lo, lr, d, l1, m))
+        if not segs:
+            work.wait()
+            return
+        zf = True if not self.overwrite else max(0, self.zero_tail - lo)
+        tables = self._bucket_tables
+        if i not in tables:
+            tables[i] = ops.SegmentTable(self.master.device)
+        lp = self.lp[lo:hi] if self.lp is not None else None
+        args = (self.master[lo:hi], self.grad[lo:hi], self.mom[lo:hi], segs)
+        kw = {"w_lp": lp, "zero_grad": zf, "table": tables[i]}
+        if not self.master.is_cuda:
+            work.wait()
+            ops.sgd_update(*args, **kw)
+            return
+        if self._upd_stream is None:
+            self._upd_stream = torch.cuda.Stream(device=self.master.device)
+        # the side stream waits for this bucket's collective (which itself
+        # waited for the compute stream at launch); its writes to the bf16
+        # copy cannot race the forward, which finished before that point
+        with torch.cuda.stream(self._upd_stream):
+            work.wait()
+            ops.sgd_update(*args, **kw)
 
     def all_ready(self):
         return len(self._ready) >= len([p for p in self.params
@@ -284,18 +352,28 @@ class ParameterStore(object):
         if self._accum_count < self.accumulate:
             self._ready.clear()
             return False
+        overlapped = False
         if self.dp is not None and self.dp.world_size > 1:
             # buckets not launched yet (e.g. params without GD) go now
             for i in range(len(self.buckets)):
                 if i not in self._launched:
-                    self._works.append(self.dp.all_reduce_async(
-                        self.bucket_view(i)))
-            for w in self._works:
-                w.wait()
-        segs = self._cached_segments()
+                    self._launch_bucket(i)
+            overlapped = self._overlap_update()
+            if not overlapped:
+                for w in self._works:
+                    w.wait()
+            elif self._upd_stream is not None:
+                # every bucket was updated on the side stream: the next
+                # forward (compute stream) reads the new weights after it
+                import torch
+                torch.cuda.current_stream(self.master.device).wait_stream(
+                    self._upd_stream)
+        segs = [] if overlapped else self._cached_segments()
         if segs and self._seg_table is None:
             self._seg_table = ops.SegmentTable(self.master.device)
-        if segs and self._solver_segs is not None:
+        if overlapped:
+            pass  # updated bucket by bucket (``_bucket_update``)
+        elif segs and self._solver_segs is not None:
             import torch
             if self.mom2 is None:
                 self.mom2 = torch.zeros_like(self.mom)
