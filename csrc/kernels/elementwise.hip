@@ -847,6 +847,24 @@ HVK_API int hvk_sgd4(float* w, float* grad, float* mom, void* w_lp,
   return (int)hipGetLastError();
 }
 
+// The same update on at most `max_blocks` workgroups (grid-stride): a
+// data-parallel bucket update running on a side stream next to the backward
+// GEMMs takes a few CUs instead of every free slot on the chip.
+HVK_API int hvk_sgd4_grid(float* w, float* grad, float* mom, void* w_lp,
+                          const void* segs, int nseg, long long total,
+                          float gscale, long long zero_from, int max_blocks,
+                          hipStream_t s) {
+  if (total % 4 || ((uintptr_t)w & 15) || ((uintptr_t)grad & 15) ||
+      ((uintptr_t)mom & 15) || ((uintptr_t)w_lp & 7) || max_blocks < 1)
+    return -1;
+  int g = grid_for(total / 4);
+  if (g > max_blocks) g = max_blocks;
+  hipLaunchKernelGGL(sgd4_kernel, dim3(g), dim3(256), 0, s, (float4*)w,
+                     (float4*)grad, (float4*)mom, (uint2*)w_lp,
+                     (const SgdSeg*)segs, nseg, total / 4, gscale, zero_from);
+  return (int)hipGetLastError();
+}
+
 HVK_API int hvk_solver(float* w, float* grad, float* s1, float* s2,
                        void* w_lp, const void* segs, int nseg,
                        long long total, float gscale, long long zero_from,

@@ -121,7 +121,7 @@ def test_dp_overlapped_update_on_gpu(tmp_path):
     steps = 5
     ov = str(tmp_path / "ov%d.npz")
     fu = str(tmp_path / "fu%d.npz")
-    _run_ranks(2, ov, steps, "lenet", 0.05, "1", "hip")
+    _run_ranks(2, ov, steps, "lenet", 0.05, "force", "hip")
     _run_ranks(2, fu, steps, "lenet", 0.05, "0", "hip")
     a0, a1, b0 = (numpy.load(ov % 0), numpy.load(ov % 1), numpy.load(fu % 0))
     for k in a0.files:

@@ -304,7 +304,7 @@ def install_step_graphs(wf, warmup=2):
     # not captured, and a large-batch data-parallel step is GPU-bound anyway
     from veles_amd.parallel import find_dp
     dp = find_dp(wf)
-    if dp is not None and dp.world_size > 1:
+    if dp is not None and getattr(dp, "multi", dp.world_size > 1):
         return []
     ld = wf.loader
     ev = getattr(wf, "evaluator", None)

@@ -88,6 +88,10 @@ class ParameterStore(object):
         self._overlap = None
         self._upd_stream = None
         self._bucket_tables = {}
+        # workgroups of a side-stream bucket update (0: the full grid); one
+        # per CU measured best (profiles/dp_overlap_update_r2.md)
+        self._upd_blocks = int(os.environ.get("VELES_AMD_DP_UPDATE_BLOCKS",
+                                              "256"))
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -234,7 +238,7 @@ class ParameterStore(object):
         """Called by a GD unit once its gradients are enqueued."""
         for p in params:
             self._ready.add(id(p))
-        if self.dp is None or self.dp.world_size <= 1:
+        if not self._multi():
             return
         if self._accum_count + 1 < self.accumulate:
             return
@@ -260,10 +264,14 @@ class ParameterStore(object):
         segments (adagrad / adadelta / rprop), gradient accumulation and
         ``VELES_AMD_DP_OVERLAP_UPDATE=0``."""
         if self._overlap is None:
+            mode = os.environ.get("VELES_AMD_DP_OVERLAP_UPDATE", "1")
+            gpu = self.master is not None and self.master.is_cuda
+            # a host-blocking wait (gloo on GPU tensors) would stall the
+            # backward's launches at every bucket: only when forced
             self._overlap = (
-                self.dp is not None and self.dp.world_size > 1 and
-                self.accumulate == 1 and
-                os.environ.get("VELES_AMD_DP_OVERLAP_UPDATE", "1") != "0")
+                self._multi() and self.accumulate == 1 and mode != "0" and
+                (mode == "force" or not gpu or
+                 not getattr(self.dp, "host_blocking_wait", False)))
         if not self._overlap:
             return False
         self._cached_segments()
@@ -296,7 +304,8 @@ class ParameterStore(object):
             tables[i] = ops.SegmentTable(self.master.device)
         lp = self.lp[lo:hi] if self.lp is not None else None
         args = (self.master[lo:hi], self.grad[lo:hi], self.mom[lo:hi], segs)
-        kw = {"w_lp": lp, "zero_grad": zf, "table": tables[i]}
+        kw = {"w_lp": lp, "zero_grad": zf, "table": tables[i],
+              "max_blocks": self._upd_blocks}
         if not self.master.is_cuda:
             work.wait()
             ops.sgd_update(*args, **kw)
@@ -353,7 +362,7 @@ class ParameterStore(object):
             self._ready.clear()
             return False
         overlapped = False
-        if self.dp is not None and self.dp.world_size > 1:
+        if self._multi():
             # buckets not launched yet (e.g. params without GD) go now
             for i in range(len(self.buckets)):
                 if i not in self._launched:
@@ -415,8 +424,12 @@ class ParameterStore(object):
         """A captured backward may contain the update only when one step is
         one launch sequence: no gradient accumulation over micro-steps and
         no collectives (multi-rank steps run eagerly)."""
-        return self.accumulate == 1 and (
-            self.dp is None or self.dp.world_size <= 1)
+        return self.accumulate == 1 and not self._multi()
+
+    def _multi(self):
+        """Gradients go through collectives (``DataParallel.multi``)."""
+        dp = self.dp
+        return dp is not None and getattr(dp, "multi", dp.world_size > 1)
 
     def refresh_table(self):
         """Bring the device segment table up to date BEFORE a replay or a

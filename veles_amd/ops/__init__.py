@@ -1179,7 +1179,7 @@ def _zero_from(zero_grad, n):
 
 
 def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
-               table=None):
+               table=None, max_blocks=None):
     """Fused multi-segment SGD (flat float32 buffers).
 
     segs: [(begin, end, lr, weights_decay, l1_vs_l2, gradient_moment)]
@@ -1187,13 +1187,19 @@ def sgd_update(w, grad, mom, segs, w_lp=None, gscale=1.0, zero_grad=False,
       w += v;  w_lp = bfloat16(w)
     zero_grad: True clears the whole gradient after reading it, an int
     offset clears only grad[offset:] (see :func:`_zero_from`).
-    table: optional :class:`SegmentTable` the packed segments are kept in."""
+    table: optional :class:`SegmentTable` the packed segments are kept in.
+    max_blocks: cap on the GPU grid (a side-stream update next to compute)."""
     n = w.numel()
     zf = _zero_from(zero_grad, n)
     if _gpu(w):
         raw = _pack_sgd_segs(segs)
         st = table.update(raw) if table is not None else \
             _segs_tensor(raw, w.device)
+        if mom is not None and max_blocks:
+            fn = getattr(_lib.lib(), "hvk_sgd4_grid")
+            if fn(_p(w), _p(grad), _p(mom), _p(w_lp), _p(st), len(segs), n,
+                  float(gscale), zf, int(max_blocks), _s(w)) == 0:
+                return w
         fn = getattr(_lib.lib(), "hvk_sgd4")
         if mom is not None and fn(_p(w), _p(grad), _p(mom), _p(w_lp),
                                   _p(st), len(segs), n, float(gscale),

@@ -43,6 +43,7 @@ _SIGS = {
     "hvk_mse": [P, I, P, I, I, I, F, P, I, P, P, I, P],
     "hvk_sgd": [P, P, P, P, P, I, L, F, P],
     "hvk_sgd4": [P, P, P, P, P, I, L, F, L, P],
+    "hvk_sgd4_grid": [P, P, P, P, P, I, L, F, L, I, P],
     "hvk_col_sum": [P, I, I, I, P, F, P],
     "hvk_row_sum": [P, I, I, I, P, F, P],
     "hvk_act_fwd": [P, I, P, I, L, I, P],

@@ -40,7 +40,13 @@ class DataParallel(object):
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         self.backend = backend
         self.device = device
-        if self.world_size > 1 and not dist.is_initialized():
+        # VELES_AMD_DP_SOLO_COLLECTIVES=1 at world size 1: a one-rank process
+        # group that runs the whole multi-rank gradient path (bucketed
+        # all-reduces, per-bucket updates, eager steps) - the RCCL stream
+        # semantics of that path measured on a single GPU
+        self.solo = self.world_size == 1 and os.environ.get(
+            "VELES_AMD_DP_SOLO_COLLECTIVES", "0") == "1"
+        if (self.world_size > 1 or self.solo) and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
             kw = {}
@@ -50,14 +56,26 @@ class DataParallel(object):
             dist.init_process_group(
                 backend, rank=self.rank, world_size=self.world_size,
                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-        self.group = dist.group.WORLD if self.world_size > 1 else None
+        self.group = dist.group.WORLD if self.multi else None
 
     @property
     def is_master(self):
         return self.rank == 0
 
+    @property
+    def multi(self):
+        """True when gradients go through collectives (several ranks, or a
+        solo process group)."""
+        return self.world_size > 1 or self.solo
+
+    @property
+    def host_blocking_wait(self):
+        """gloo's ``Work.wait()`` blocks the host until the collective is
+        done; RCCL's only makes the current stream wait on it."""
+        return self.backend != "nccl"
+
     def all_reduce_async(self, tensor):
-        if self.world_size <= 1:
+        if not self.multi:
             return _Done()
         return dist.all_reduce(tensor, op=dist.ReduceOp.SUM, async_op=True)
 
@@ -108,7 +126,7 @@ class DataParallel(object):
         return out
 
     def shutdown(self):
-        if self.world_size > 1 and dist.is_initialized():
+        if self.multi and dist.is_initialized():
             dist.destroy_process_group()
 
     def __getstate__(self):
