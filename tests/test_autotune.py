@@ -1,0 +1,116 @@
+"""Device tuning table (veles_amd/ops/autotune.py): JSON round trip, lookups
+overriding the built-in split-K heuristics per shape, call recording, and on
+the GPU a tuning pass whose choices keep the numerics."""
+import json
+
+import pytest
+import torch
+
+from veles_amd import ops
+from veles_amd.ops import autotune
+
+
+@pytest.fixture
+def tab(tmp_path, monkeypatch):
+    t = autotune.TuningTable(str(tmp_path / "gfx950.json"))
+    monkeypatch.setattr(autotune, "_TABLE", t)
+    monkeypatch.setattr(autotune, "_ENABLED", True)
+    return t
+
+
+def test_table_round_trip_and_bad_files(tmp_path):
+    p = str(tmp_path / "t.json")
+    t = autotune.TuningTable(p)
+    assert t.entries == {} and t.get("wgrad:1:2:3:1") is None
+    t.set(autotune.key("wgrad", 1, 2, 3, 1), 8, 10.5, 4, 12.0)
+    t.data["device"] = {"name": "x"}
+    t.save()
+    u = autotune.TuningTable(p)
+    assert u.get("wgrad:1:2:3:1") == 8
+    assert u.entries["wgrad:1:2:3:1"]["default_us"] == 12.0
+    assert u.data["device"]["name"] == "x"
+    for bad in ("{not json", json.dumps({"format": 99, "entries": {}}),
+                json.dumps([1, 2])):
+        with open(p, "w") as f:
+            f.write(bad)
+        v = autotune.TuningTable(p)
+        assert v.entries == {}   # ignored, built-in defaults apply
+
+
+def test_wgrad_split_lookup_and_recording(tab):
+    x = torch.zeros(2, 9, 9, 16)
+    dy = torch.zeros(2, 7, 7, 32)
+    dw = torch.zeros(32, 3, 3, 16)
+    shape = (2 * 7 * 7, 32, 3 * 3 * 16 + 1, 1)
+    default = ops.wgrad_splits(*shape)
+    autotune.record(True)
+    try:
+        assert ops._wgrad_splits_for(x, dy, dw, (1, 1), (0, 0, 0, 0), 1,
+                                     shape) == default
+        tab.set(autotune.key("wgrad", *shape), default + 3)
+        assert ops._wgrad_splits_for(x, dy, dw, (1, 1), (0, 0, 0, 0), 1,
+                                     shape) == default + 3
+        log = autotune.recorded()
+    finally:
+        autotune.record(False)
+    kind, g = log[autotune.key("wgrad", *shape)]
+    assert kind == "wgrad" and g["x"] == (2, 9, 9, 16)
+    assert g["default"] == default and g["groups"] == 1
+
+
+def test_splitk_lookup(tab, monkeypatch):
+    M, N, K = 256, 512, 4096
+    a = torch.zeros(M, K)
+    b = torch.zeros(N, K)
+    out = torch.zeros(M, N)
+    default = ops.auto_splitk(M, N, K, out)
+    assert default > 1
+    assert ops._splitk_for(a, b, False, True, out, M, N, K, None,
+                           None) == default
+    tab.set(autotune.key("splitk", M, N, K), 0)
+    assert ops._splitk_for(a, b, False, True, out, M, N, K, None, None) == 0
+    tab.set(autotune.key("splitk", M, N, K), 6)
+    assert ops._splitk_for(a, b, False, True, out, M, N, K, None, None) == 6
+    # misaligned rows: never split, whatever the table says
+    out2 = torch.zeros(M, N + 4)[:, :N]
+    assert ops._splitk_for(a, b, False, True, out2, M, N, K, None,
+                           None) == 0 or out2.stride(0) % 8 == 0
+    monkeypatch.setattr(autotune, "_ENABLED", False)
+    assert ops._splitk_for(a, b, False, True, out, M, N, K, None,
+                           None) == default
+
+
+@pytest.mark.gpu
+def test_tune_keeps_numerics(tab):
+    """Record one conv weight gradient and one split-K FC GEMM, tune them,
+    and check the tuned choices give the default's results."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(8, 30, 30, 64, device=dev, generator=g).bfloat16()
+    dy = torch.randn(8, 28, 28, 96, device=dev, generator=g).bfloat16()
+    a = torch.randn(256, 4096, device=dev, generator=g).bfloat16()
+    w = torch.randn(1024, 4096, device=dev, generator=g).bfloat16()
+
+    def run():
+        dw = torch.zeros(96, 3, 3, 64, device=dev)
+        ops.conv_wgrad(x, dy, dw)
+        y = ops.gemm(a, w, trans_b=True)
+        torch.cuda.synchronize()
+        return dw, y
+
+    autotune.record(True)
+    try:
+        dw0, y0 = run()
+        log = autotune.recorded()
+    finally:
+        autotune.record(False)
+    assert {k.split(":")[0] for k in log} == {"wgrad", "splitk"}
+    autotune.tune(log, repeats=2, tab=tab, verbose=False)
+    assert set(tab.entries) == set(log)
+    for e in tab.entries.values():
+        assert e["us"] > 0 and e["us"] <= e["default_us"]
+    dw1, y1 = run()
+    torch.testing.assert_close(dw1, dw0, rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(y1.float(), y0.float(), rtol=2e-2, atol=2e-2)
+    ref = (a.float() @ w.float().t())
+    torch.testing.assert_close(y1.float(), ref, rtol=2e-2, atol=0.5)

@@ -9,8 +9,9 @@ The reference's OpenCL / CUDA / NumPy triple collapses into two devices:
 * ``HipDevice`` - one MI355X (gfx950).  It owns the compute HIP stream on
   which every unit enqueues its kernels, a communication stream for RCCL
   work, a pinned-host staging pool, and the handle to the hand-written kernel
-  library (``veles_amd.ops``).  GEMM tile configs come from a per-device JSON
-  table (``devices/gfx950.json``) the autotuner writes - the MI355X analogue of
+  library (``veles_amd.ops``).  Per-shape kernel choices (split-K counts)
+  come from a per-device JSON table (``devices/gfx950.json``) that the
+  autotuner (``veles_amd/ops/autotune.py``) writes - the MI355X analogue of
   the reference ``devices/device_infos.json``.
 * ``CpuDevice`` - the reference's "numpy" backend: the same ops evaluated by
   PyTorch on the CPU in float32 (the numerics reference for every kernel).
@@ -210,6 +211,11 @@ class HipDevice(Device):
         from veles_amd import ops
         self.ops = ops
         ops.require_library()
+        # per-shape kernel choices measured on this device (ops/autotune.py)
+        from veles_amd.ops import autotune
+        self.tuning = autotune.table()
+        self.debug("tuning table %s: %d entries", self.tuning.path,
+                   len(self.tuning.entries))
 
     def stream(self):
         return self._compute_stream

@@ -264,7 +264,10 @@ class ParameterStore(object):
         segments (adagrad / adadelta / rprop), gradient accumulation and
         ``VELES_AMD_DP_OVERLAP_UPDATE=0``."""
         if self._overlap is None:
-            mode = os.environ.get("VELES_AMD_DP_OVERLAP_UPDATE", "1")
+            from veles_amd.utils.config import root, get
+            mode = os.environ.get(
+                "VELES_AMD_DP_OVERLAP_UPDATE",
+                "1" if get(root.common.engine.dp.overlap, True) else "0")
             gpu = self.master is not None and self.master.is_cuda
             # a host-blocking wait (gloo on GPU tensors) would stall the
             # backward's launches at every bucket: only when forced

@@ -240,7 +240,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         if bias_grad is not None and (trans_b or not accumulate):
             raise ValueError("bias_grad needs accumulate=True, trans_b=False")
         sk = 0 if accumulate or beta != 0.0 else \
-            auto_splitk(M, N, K, out, bias, aux)
+            _splitk_for(a, b, trans_a, trans_b, out, M, N, K, bias, aux)
         if sk > 1:
             # a persistent, self-clearing f32 workspace per size (zeroed once;
             # the finishing pass zeroes what it reads)
@@ -288,6 +288,14 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
 _SPLITK_ENV = os.environ.get("HVK_SPLITK")
 
 
+def _splitk_aligned(N, out, bias, aux):
+    """Operands hvk_gemm_splitk takes (16-B rows for the finishing pass)."""
+    return not (N % 8 or out.stride(0) % 8 or out.data_ptr() % 16 or
+                (bias is not None and bias.data_ptr() % 16) or
+                (aux is not None and (aux.stride(0) % 8 or
+                                      aux.data_ptr() % 16)))
+
+
 def auto_splitk(M, N, K, out, bias=None, aux=None):
     """K splits for a GEMM whose 128 x 128 output tiles cannot fill the
     MI355X's 256 CUs twice over (the FC layers at batch 512): enough splits
@@ -296,14 +304,30 @@ def auto_splitk(M, N, K, out, bias=None, aux=None):
     if _SPLITK_ENV == "0":
         return 0
     tiles = -(-M // 128) * -(-N // 128)
-    if tiles >= 256 or K < 2048 or N % 8:
-        return 0
-    if out.stride(0) % 8 or out.data_ptr() % 16 or \
-            (bias is not None and bias.data_ptr() % 16) or \
-            (aux is not None and (aux.stride(0) % 8 or aux.data_ptr() % 16)):
+    if tiles >= 256 or K < 2048 or not _splitk_aligned(N, out, bias, aux):
         return 0
     sk = min(-(-512 // tiles), K // 1024)
     return sk if sk > 1 else 0
+
+
+# the autotuner's replay forces a split count (ops/autotune.py)
+_splitk_forced = None
+
+
+def _splitk_for(a, b, trans_a, trans_b, out, M, N, K, bias, aux):
+    """auto_splitk, overridden per shape by the device tuning table."""
+    if _splitk_forced is not None:
+        return _splitk_forced if _splitk_aligned(N, out, bias, aux) else 0
+    sk = auto_splitk(M, N, K, out, bias, aux)
+    if _SPLITK_ENV == "0" or -(-M // 128) * -(-N // 128) >= 256 or \
+            K < 1024 or not _splitk_aligned(N, out, bias, aux):
+        return sk
+    from veles_amd.ops import autotune
+    autotune.log_call("splitk", (M, N, K), {
+        "a": tuple(a.shape), "b": tuple(b.shape), "out": tuple(out.shape),
+        "trans_a": trans_a, "trans_b": trans_b, "default": sk})
+    t = autotune.lookup("splitk", M, N, K)
+    return sk if t is None else (t if t > 1 else 0)
 
 
 def _precision_level(level):
@@ -571,8 +595,9 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             # self-clearing workspace: zeroed once, cleared again by the fold
             dw2 = _workspace(("s2dg", dw.data_ptr()), (OC, KH2, KW2, C2),
                              torch.float32, dw.device, zero=True)
-            sp = splits or wgrad_splits(N * OH * OW, OC, KH2 * KW2 * C2 + 1,
-                                        1)
+            sp = splits or _wgrad_splits_for(
+                x, dy, dw, sliding, padding, groups,
+                (N * OH * OW, OC, KH2 * KW2 * C2 + 1, 1))
             _lib_call("hvk_conv_wgrad", _p(x2), _p(dy), _p(dw2), N, H2, W2,
                       C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, int(sp),
                       _p(dbias), _s(x))
@@ -597,14 +622,17 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             return dw
         if needs_im2col(C, groups):
             runp = (KW * C + 7) // 8 * 8
-            sp = splits or wgrad_splits(N * OH * OW, OC, KH * runp + 1, 1)
+            sp = splits or _wgrad_splits_for(
+                x, dy, dw, sliding, padding, groups,
+                (N * OH * OW, OC, KH * runp + 1, 1))
             _lib_call("hvk_conv_wgrad_run", _p(x), _p(dy), _p(dw), _p(dbias),
                       N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW,
                       int(sp), _s(x))
             return dw
         if splits is None:
-            splits = wgrad_splits(N * OH * OW, OC // groups,
-                                  KH * KW * Cg + 1, groups)
+            splits = _wgrad_splits_for(
+                x, dy, dw, sliding, padding, groups,
+                (N * OH * OW, OC // groups, KH * KW * Cg + 1, groups))
         _lib_call("hvk_conv_wgrad", _p(x), _p(dy), _p(dw), N, H, W, C, OC, KH,
                   KW, sy, sx, pt, pl, OH, OW, groups, int(splits), _p(dbias),
                   _s(x))
@@ -621,6 +649,19 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
 # 512 blocks (2 per CU) measured best on AlexNet b512 (72.7k img/s vs 71.6k
 # at 2048 and 69.0k at 4096: fewer splits = fewer f32 atomics)
 _WGRAD_BLOCKS = int(os.environ.get("HVK_WGRAD_BLOCKS", "512"))
+
+
+def _wgrad_splits_for(x, dy, dw, sliding, padding, groups, shape):
+    """wgrad_splits, overridden per shape by the device tuning table (the
+    call's geometry is logged for the autotuner, ops/autotune.py)."""
+    from veles_amd.ops import autotune
+    default = wgrad_splits(*shape)
+    autotune.log_call("wgrad", shape, {
+        "x": tuple(x.shape), "dy": tuple(dy.shape), "dw": tuple(dw.shape),
+        "sliding": tuple(sliding), "padding": tuple(padding),
+        "groups": groups, "default": default})
+    t = autotune.lookup("wgrad", *shape)
+    return default if t is None else max(1, t)
 
 
 def wgrad_splits(P, M, N, groups, target_blocks=None):

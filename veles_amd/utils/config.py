@@ -209,8 +209,10 @@ root.common.update({
             # MB of the last bucket (the layers whose gradients come last):
             # the only all-reduce that cannot overlap the backward pass
             "tail_bucket_mb": 2,
+            # multi-rank: update each bucket on a side stream as soon as its
+            # all-reduce is done (ParameterStore._bucket_update); False keeps
+            # one fused update after the last all-reduce
             "overlap": True,
-            "grad_dtype": "float32",
             "timeout_s": 600,
         },
     },
