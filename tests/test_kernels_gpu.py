@@ -41,6 +41,19 @@ def test_gemm_layouts(ta, tb, M, N, K):
     close(got, ref, 2e-3)
 
 
+def test_gemm_restrides_unaligned_rows():
+    """Operands whose rows miss the 16-B grid (odd pitch, offset views) are
+    re-strided before the LDS-DMA kernel: same result as aligned copies."""
+    big = rnd(300, 1003)
+    a = big[:, 1:1002]          # pointer 2 B off, pitch 1003
+    b = rnd(129, 1001, seed=2)  # pitch 1001
+    ref = ops.gemm(a.contiguous(), b, trans_b=True, out_dtype=torch.float32)
+    got = ops.gemm(big.to(DEV)[:, 1:1002], b.to(DEV), trans_b=True,
+                   out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    close(got, ref, 2e-2)
+
+
 def test_gemm_asymmetric_identity():
     # A = I with an asymmetric B catches a transposed C-write
     n = 128

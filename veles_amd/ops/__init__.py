@@ -234,6 +234,16 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
                 raise ValueError("gemm operands must be row-major")
         if accumulate and out.dtype != torch.float32:
             raise TypeError("accumulate requires a float32 output")
+        # rows off the 16-B grid would drop the whole GEMM to the per-element
+        # loaders (3001^3: 76 vs ~800 TF): re-stride such operands first
+        a, b = _row_aligned(a), _row_aligned(b)
+        res = out
+        if not accumulate and beta == 0.0 and out.dim() == 2 and \
+                (out.stride(0) % 8 or out.data_ptr() % 16):
+            # and a write-only output into an aligned buffer (vector
+            # epilogue stores), copied out after
+            out = torch.empty(M, -(-N // 8) * 8, dtype=out.dtype,
+                              device=dev)[:, :N]
         atomic = 2 if overwrite else (1 if accumulate else 0)
         if splits > 1 and not accumulate:
             raise ValueError("split-K requires accumulate=True")
@@ -252,14 +262,16 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
                       float(alpha), _p(bias), act, _p(aux),
                       0 if aux is None else aux.stride(0), aux_act, sk,
                       _p(ws), 1, _s(a))
-            return out
-        _lib_call("hvk_gemm", int(trans_a), int(trans_b), M, N, K, _p(a),
-                  a.stride(0), _p(b), b.stride(0), _p(out), out.stride(0),
-                  int(out.dtype == torch.float32), atomic, float(alpha),
-                  float(beta), _p(bias), bm, act, _p(aux),
-                  0 if aux is None else aux.stride(0), aux_act, int(splits),
-                  _p(bias_grad), _s(a))
-        return out
+        else:
+            _lib_call("hvk_gemm", int(trans_a), int(trans_b), M, N, K, _p(a),
+                      a.stride(0), _p(b), b.stride(0), _p(out),
+                      out.stride(0), int(out.dtype == torch.float32), atomic,
+                      float(alpha), float(beta), _p(bias), bm, act, _p(aux),
+                      0 if aux is None else aux.stride(0), aux_act,
+                      int(splits), _p(bias_grad), _s(a))
+        if res is not out:
+            res.copy_(out)
+        return res
     A = a.float().t() if trans_a else a.float()
     B = b.float().t() if trans_b else b.float()
     r = alpha * (A @ B)
@@ -283,6 +295,19 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         r = r * act_bwd_ref(aux.float(), aux_act)
     out.copy_(r.to(out.dtype))
     return out
+
+
+def _row_aligned(t):
+    """``t`` itself when its rows start on 16-B boundaries, else a copy in a
+    buffer whose row pitch is padded to a multiple of 8 elements (the view
+    keeps the logical shape; the LDS-DMA loaders never read the pad)."""
+    if t.dim() != 2 or (t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0):
+        return t
+    R, C = t.shape
+    buf = torch.empty(R, -(-C // 8) * 8, dtype=t.dtype, device=t.device)
+    v = buf[:, :C]
+    v.copy_(t)
+    return v
 
 
 _SPLITK_ENV = os.environ.get("HVK_SPLITK")

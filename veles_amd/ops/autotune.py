@@ -288,6 +288,8 @@ def main(argv=None):
     tab = TuningTable(a.out) if a.out else table()
     dev = Device(backend="hip")
     for model in a.model or ["alexnet"]:
+        if model == "none":   # device benchmark only
+            continue
         layers_fn, dataset = MODELS[model]
         record(True)
         wf = StandardWorkflow(
