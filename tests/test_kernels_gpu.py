@@ -54,6 +54,26 @@ def test_gemm_restrides_unaligned_rows():
     close(got, ref, 2e-2)
 
 
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_odd_dims_zero_padded(ta, tb):
+    """A large GEMM with odd M / N / K runs on zero-padded operands (the
+    LDS-DMA loaders) and matches the fp32 reference, bias included."""
+    M, N, K = 331, 257, 1001
+    a = rnd(K, M) if ta else rnd(M, K)
+    b = rnd(N, K, seed=1) if tb else rnd(K, N, seed=1)
+    bias = rnd(N, seed=2, dtype=torch.float32)
+    use_bias = bool(tb)  # an MN-major B pads N: no bias then (not padded)
+    ref = ops.gemm(a, b, trans_a=bool(ta), trans_b=bool(tb),
+                   bias=bias if use_bias else None, act="relu",
+                   out_dtype=torch.float32)
+    got = ops.gemm(a.to(DEV), b.to(DEV), trans_a=bool(ta), trans_b=bool(tb),
+                   bias=bias.to(DEV) if use_bias else None, act="relu",
+                   out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert got.shape == (M, N)
+    close(got, ref, 2e-2)
+
+
 def test_gemm_asymmetric_identity():
     # A = I with an asymmetric B catches a transposed C-write
     n = 128

@@ -234,10 +234,18 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
                 raise ValueError("gemm operands must be row-major")
         if accumulate and out.dtype != torch.float32:
             raise TypeError("accumulate requires a float32 output")
+        res = out
+        pad = None
+        if not accumulate and beta == 0.0 and bias_grad is None:
+            pad = _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux)
+        if pad is not None:
+            # odd M / N / K: zero-padded operands take the LDS-DMA loaders
+            a, b, Mp, Np, Kp = pad
+            out = torch.empty(Mp, Np, dtype=out.dtype, device=dev)
+            M, N, K = Mp, Np, Kp
         # rows off the 16-B grid would drop the whole GEMM to the per-element
         # loaders (3001^3: 76 vs ~800 TF): re-stride such operands first
         a, b = _row_aligned(a), _row_aligned(b)
-        res = out
         if not accumulate and beta == 0.0 and out.dim() == 2 and \
                 (out.stride(0) % 8 or out.data_ptr() % 16):
             # and a write-only output into an aligned buffer (vector
@@ -270,7 +278,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
                       0 if aux is None else aux.stride(0), aux_act,
                       int(splits), _p(bias_grad), _s(a))
         if res is not out:
-            res.copy_(out)
+            res.copy_(out[:res.shape[0], :res.shape[1]])
         return res
     A = a.float().t() if trans_a else a.float()
     B = b.float().t() if trans_b else b.float()
@@ -295,6 +303,38 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         r = r * act_bwd_ref(aux.float(), aux_act)
     out.copy_(r.to(out.dtype))
     return out
+
+
+_DMA_PAD_MIN = 1 << 24   # M*N*K above which padding pays for its copies
+
+
+def _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux):
+    """Zero-padded copies of a large GEMM's operands when an odd dimension
+    keeps them off the LDS-DMA loaders (a K-major operand needs K % 8 == 0,
+    an MN-major one M / N % 8 == 0; csrc/kernels/gemm.hip ``dma_ok``): K
+    pads with zeros (adds nothing), M / N pads are sliced off the output.
+    None when nothing needs padding, the GEMM is small, or a bias / aux
+    operand would have to be padded too."""
+    r8 = lambda v: -(-v // 8) * 8  # noqa: E731
+    ka, kb = not trans_a, bool(trans_b)
+    Kp = r8(K) if (ka or kb) and K % 8 else K
+    Mp = r8(M) if not ka and M % 8 else M
+    Np = r8(N) if not kb and N % 8 else N
+    if (Mp, Np, Kp) == (M, N, K) or M * N * K < _DMA_PAD_MIN:
+        return None
+    if (Np != N and bias is not None) or (aux is not None and
+                                          (Mp, Np) != (M, N)):
+        return None
+
+    def padded(t, rows, cols):
+        if tuple(t.shape) == (rows, cols):
+            return t
+        z = torch.zeros(rows, cols, dtype=t.dtype, device=t.device)
+        z[:t.shape[0], :t.shape[1]].copy_(t)
+        return z
+    a2 = padded(a, M, Kp) if ka else padded(a, Kp, Mp)
+    b2 = padded(b, Np, Kp) if kb else padded(b, Kp, Np)
+    return a2, b2, Mp, Np, Kp
 
 
 def _row_aligned(t):
