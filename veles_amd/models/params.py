@@ -298,7 +298,7 @@ class ParameterStore(object):
             b, e = max(b, lo), min(e, hi)
             if b < e:
                 segs.append((b - lo, e - lo, lr, d, l1, m))
-        if not segs:
+        if not segs and not self.master.is_cuda:
             work.wait()
             return
         zf = True if not self.overwrite else max(0, self.zero_tail - lo)
@@ -320,7 +320,8 @@ class ParameterStore(object):
         # copy cannot race the forward, which finished before that point
         with torch.cuda.stream(self._upd_stream):
             work.wait()
-            ops.sgd_update(*args, **kw)
+            if segs:
+                ops.sgd_update(*args, **kw)
 
     def all_ready(self):
         return len(self._ready) >= len([p for p in self.params
