@@ -466,10 +466,11 @@ def needs_im2col(C, groups):
 # 0.32 ms (+0.05 ms for the pad, shared with the forward), forward 1.41 ->
 # 1.26 ms (tools/bench_c3_pad.py).  HVK_C3_PAD=0 keeps the run kernels.
 _C_PAD8 = os.environ.get("HVK_C3_PAD", "1") != "0"
+_C_PAD_MIN = int(os.environ.get("HVK_C3_PAD_MIN", "3"))
 
 
 def pad8_ok(C, groups):
-    return _C_PAD8 and groups == 1 and 3 <= C < 8
+    return _C_PAD8 and groups == 1 and _C_PAD_MIN <= C < 8
 
 
 class PaddedImage(object):
@@ -509,12 +510,15 @@ class S2DImage(object):
         self.s = s
 
 
+_S2D = os.environ.get("HVK_S2D", "1") != "0"   # A/B knob
+
+
 def s2d_factor(C, groups, sliding, KH, KW):
     """Stride s when a conv is better run as space-to-depth (C -> s*s*C
     channels, stride 1, ceil(K/s) taps): small C, equal strides, s*s*C a
     multiple of 8 (the aligned LDS-DMA loaders), kernel at least s wide."""
     sx, sy = sliding
-    if groups != 1 or C % 8 == 0 or sx != sy or sx < 2:
+    if groups != 1 or C % 8 == 0 or sx != sy or sx < 2 or not _S2D:
         return 0
     if (sx * sx * C) % 8 or KH < sx or KW < sx:
         return 0
