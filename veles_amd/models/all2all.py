@@ -13,6 +13,8 @@ readable by both runtimes.
 """
 from __future__ import annotations
 
+import os
+
 import numpy
 
 from veles_amd.memory import Array
@@ -29,6 +31,7 @@ class All2All(Forward):
     MAPPING = "all2all"
     ACTIVATION = 0
     FP8 = True  # fp8 forward / dgrad under precision_type "float8"
+    FP8_MIN_TILES = int(os.environ.get("VELES_AMD_FP8_FC_MIN_TILES", "128"))
 
     def __init__(self, workflow, **kwargs):
         super().__init__(workflow, **kwargs)
@@ -50,9 +53,17 @@ class All2All(Forward):
             else (n_in, self.neurons_number)
         self.register_params(shape, n_in)
         self.allocate_outputs(self.input.shape[0])
+        # fp8 only where the 128 x 128 output tiles can fill the chip: the
+        # fp8 kernel has no split-K, and a thin layer (VGG-16 fc6 / fc7 at
+        # batch 128: 32 tiles) runs faster on the bf16 split-K GEMM, without
+        # quantizing its weights every step (profiles/c3pad_r2/README.md)
+        tiles = -(-int(self.input.shape[0]) // 128) * \
+            -(-self.neurons_number // 128)
         self.fp8_ = bool(getattr(self.device, "fp8", False)) and \
             self.FP8 and not self.weights_transposed and \
-            n_in % 16 == 0 and self.neurons_number % 16 == 0
+            n_in % 16 == 0 and self.neurons_number % 16 == 0 and \
+            (tiles >= self.FP8_MIN_TILES or
+             not getattr(self.device, "is_gpu", False))
         if self.fp8_ and self.fp8_sx_ is None:
             self.fp8_sx_ = fp8.Scaler(self.torch_device, fp8.E4M3)
             self.fp8_sw_ = fp8.Scaler(self.torch_device, fp8.E4M3)
