@@ -255,6 +255,18 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         atomic = 2 if overwrite else (1 if accumulate else 0)
         if splits > 1 and not accumulate:
             raise ValueError("split-K requires accumulate=True")
+        if accumulate and splits == 1:
+            # a weight gradient with a handful of output tiles and a long K
+            # (CIFAR quick fc2: 10 x 64 over a 4096 batch, ONE workgroup
+            # for 0.27 ms): split K over f32 atomics; an overwrite is then a
+            # zero fill + atomic accumulate
+            sp = _wgrad_gemm_splits(M, N + (bias_grad is not None), K)
+            if sp > 1:
+                if overwrite:
+                    out.zero_()
+                    if bias_grad is not None:
+                        bias_grad.zero_()
+                atomic, splits = 1, sp
         if bias_grad is not None and (trans_b or not accumulate):
             raise ValueError("bias_grad needs accumulate=True, trans_b=False")
         sk = 0 if accumulate or beta != 0.0 else \
@@ -351,6 +363,19 @@ def _row_aligned(t):
 
 
 _SPLITK_ENV = os.environ.get("HVK_SPLITK")
+
+
+def _wgrad_gemm_splits(M, N, K):
+    """K splits for an accumulating GEMM under 64 output tiles with K >= 2048
+    (~256 workgroups, >= 256 of K each); 1 = leave it whole.  The large FC
+    weight gradients (AlexNet fc6: 2304 tiles) keep their single-pass
+    read-modify-write.  HVK_SPLITK=0 disables."""
+    if _SPLITK_ENV == "0" or K < 2048:
+        return 1
+    tiles = -(-M // 128) * -(-N // 128)
+    if tiles >= 64:
+        return 1
+    return max(1, min(-(-256 // tiles), K // 256))
 
 
 def _splitk_aligned(N, out, bias, aux):
