@@ -231,27 +231,43 @@ __global__ void softmax_ce_kernel(const void* logits, int in_dt, int B, int C,
 __global__ void mse_kernel(const void* y, int y_dt, const void* t, int t_dt,
                            int B, int D, float scale, void* err, int err_dt,
                            float* mse_out, float* metrics, int valid_rows) {
-  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  int lane = threadIdx.x & 63;
-  if (row >= B) return;
-  long long base = (long long)row * D;
-  float s = 0.f;
-  bool valid = row < valid_rows;
-  for (int c = lane; c < D; c += 64) {
-    float d = ld_any(y, base + c, y_dt) - ld_any(t, base + c, t_dt);
-    if (!valid) d = 0.f;
-    s += d * d;
-    if (err) st_any(err, base + c, err_dt, d * scale);
-  }
-  s = wave_sum(s);
-  if (lane == 0) {
-    float mse = s / D;
-    if (mse_out) mse_out[row] = mse;
-    if (metrics && valid) {
-      atomicAdd(&metrics[0], mse);
-      atomicAdd(&metrics[1], sqrtf(mse));
-      atomicAdd(&metrics[2], 1.f);
+  // rows grid-strided per wave; one metric atomic per block (softmax_ce)
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < B; row += gridDim.x * 4) {
+    long long base = (long long)row * D;
+    float s = 0.f;
+    bool valid = row < valid_rows;
+    for (int c = lane; c < D; c += 64) {
+      float d = ld_any(y, base + c, y_dt) - ld_any(t, base + c, t_dt);
+      if (!valid) d = 0.f;
+      s += d * d;
+      if (err) st_any(err, base + c, err_dt, d * scale);
     }
+    s = wave_sum(s);
+    if (lane == 0) {
+      float mse = s / D;
+      if (mse_out) mse_out[row] = mse;
+      if (valid) {
+        m0 += mse;
+        m1 += sqrtf(mse);
+        m2 += 1.f;
+      }
+    }
+  }
+  if (!metrics) return;
+  __shared__ float red[3][4];
+  if (lane == 0) {
+    red[0][wave] = m0;
+    red[1][wave] = m1;
+    red[2][wave] = m2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float v = red[threadIdx.x][0] + red[threadIdx.x][1] +
+                    red[threadIdx.x][2] + red[threadIdx.x][3];
+    if (v != 0.f) atomicAdd(&metrics[threadIdx.x], v);
   }
 }
 
@@ -852,7 +868,10 @@ HVK_API int hvk_softmax_ce(const void* logits, int in_dt, int B, int C,
 HVK_API int hvk_mse(const void* y, int y_dt, const void* t, int t_dt, int B,
                     int D, float scale, void* err, int err_dt, float* mse_out,
                     float* metrics, int valid_rows, hipStream_t s) {
-  hipLaunchKernelGGL(mse_kernel, dim3((B + 3) / 4), dim3(256), 0, s, y, y_dt, t,
+  int blocks = (B + 3) / 4;
+  if (blocks > 256) blocks = 256;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(mse_kernel, dim3(blocks), dim3(256), 0, s, y, y_dt, t,
                      t_dt, B, D, scale, err, err_dt, mse_out, metrics,
                      valid_rows);
   return (int)hipGetLastError();
