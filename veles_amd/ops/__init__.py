@@ -495,7 +495,12 @@ _C_PAD_MIN = int(os.environ.get("HVK_C3_PAD_MIN", "3"))
 
 
 def pad8_ok(C, groups):
-    return _C_PAD8 and groups == 1 and _C_PAD_MIN <= C < 8
+    """Channels padded to the next multiple of 8 (3 -> 8, LeNet's 20 -> 24)."""
+    return _C_PAD8 and groups == 1 and C >= _C_PAD_MIN and C % 8 != 0
+
+
+def _cpad(C):
+    return -(-C // 8) * 8
 
 
 class PaddedImage(object):
@@ -508,19 +513,20 @@ class PaddedImage(object):
 
 
 def _pad_channels(x):
-    """x [N,H,W,C] -> [N,H,W,8], channels C..7 zero (a persistent buffer
-    per input tensor: the pad stays zero, only x's channels are copied)."""
+    """x [N,H,W,C] -> [N,H,W,Cp] (Cp = C rounded up to 8), the padding
+    channels zero (a persistent buffer per input tensor: the pad stays zero,
+    only x's channels are copied)."""
     N, H, W, C = x.shape
-    buf = _workspace(("cpad8", x.data_ptr(), N, H, W, C), (N, H, W, 8),
-                     x.dtype, x.device, zero=True)
+    buf = _workspace(("cpad8", x.data_ptr(), N, H, W, C),
+                     (N, H, W, _cpad(C)), x.dtype, x.device, zero=True)
     buf[..., :C].copy_(x)
     return buf
 
 
 def _pad_weights(w, key):
     OC, KH, KW, C = w.shape
-    wp = _workspace((key, id(w)), (OC, KH, KW, 8), w.dtype, w.device,
-                    zero=True)
+    wp = _workspace((key, id(w)), (OC, KH, KW, _cpad(C)), w.dtype,
+                    w.device, zero=True)
     wp[..., :C].copy_(w)
     return wp
 
@@ -639,8 +645,8 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
             xp = _pad_channels(x)
             wp8 = _pad_weights(w, "wpad8")
             _lib_call("hvk_conv_fwd", _p(xp), _p(wp8), _p(bias), _p(out), N,
-                      H, W, 8, OC, KH, KW, sy, sx, pt, pl, OH, OW, 1, act,
-                      _s(x))
+                      H, W, _cpad(C), OC, KH, KW, sy, sx, pt, pl, OH, OW, 1,
+                      act, _s(x))
             if col_out is not None:
                 col_out["col"] = PaddedImage(xp, C)
             return out
@@ -756,12 +762,13 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             xp = col.x if isinstance(col, PaddedImage) and \
                 col.x.shape[:3] == x.shape[:3] else _pad_channels(x)
             # self-clearing padded gradient: zeroed once, cleared after the fold
-            dwp = _workspace(("wgpad8", dw.data_ptr()), (OC, KH, KW, 8),
+            Cp = _cpad(C)
+            dwp = _workspace(("wgpad8", dw.data_ptr()), (OC, KH, KW, Cp),
                              torch.float32, dw.device, zero=True)
             sp = splits or _wgrad_splits_for(
                 xp, dy, dwp, sliding, padding, 1,
-                (N * OH * OW, OC, KH * KW * 8 + 1, 1))
-            _lib_call("hvk_conv_wgrad", _p(xp), _p(dy), _p(dwp), N, H, W, 8,
+                (N * OH * OW, OC, KH * KW * Cp + 1, 1))
+            _lib_call("hvk_conv_wgrad", _p(xp), _p(dy), _p(dwp), N, H, W, Cp,
                       OC, KH, KW, sy, sx, pt, pl, OH, OW, 1, int(sp),
                       _p(dbias), _s(x))
             dw += dwp[..., :C]
