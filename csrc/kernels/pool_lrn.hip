@@ -49,6 +49,7 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
         int off = ((n * H + h) * W + w) * C + cv * VEC;
         uint16_t v[VEC];
         if (VEC == 8) *(uint4*)v = *(const uint4*)(x + off);
+        else if (VEC > 1) __builtin_memcpy(v, x + off, VEC * 2);
         else v[0] = x[off];
 #pragma unroll
         for (int q = 0; q < VEC; ++q) {
@@ -69,6 +70,7 @@ __global__ void pool_fwd_kernel(const uint16_t* x, uint16_t* y, int* argmax,
       o[q] = f2bf(mode == POOL_AVG ? sum[q] / (float)max(cnt, 1) : best[q]);
     int yo = pix * C + cv * VEC;
     if (VEC == 8) *(uint4*)(y + yo) = *(uint4*)o;
+    else if (VEC > 1) __builtin_memcpy(y + yo, o, VEC * 2);
     else y[yo] = o[0];
     if (argmax && mode != POOL_AVG) {
 #pragma unroll
@@ -184,6 +186,7 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
         int yo = ((n * OH + oh) * OW + ow) * C + cv * VEC;
         uint16_t g[VEC];
         if (VEC == 8) *(uint4*)g = *(const uint4*)(dy + yo);
+        else if (VEC > 1) __builtin_memcpy(g, dy + yo, VEC * 2);
         else g[0] = dy[yo];
         if (MODE == POOL_AVG) {
           int hh0 = max(oh * sy - pt, 0), hh1 = min(oh * sy - pt + ky, H);
@@ -201,6 +204,7 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
     if (aux) {
       uint16_t a[VEC];
       if (VEC == 8) *(uint4*)a = *(const uint4*)(aux + xoff);
+      else if (VEC > 1) __builtin_memcpy(a, aux + xoff, VEC * 2);
       else a[0] = aux[xoff];
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[q] *= act_bwd(bf2f(a[q]), aux_act);
@@ -208,6 +212,7 @@ __global__ void pool_bwd_kernel(const uint16_t* dy, const int* argmax,
 #pragma unroll
     for (int q = 0; q < VEC; ++q) o[q] = f2bf(acc[q]);
     if (VEC == 8) *(uint4*)(dx + xoff) = *(uint4*)o;
+    else if (VEC > 1) __builtin_memcpy(dx + xoff, o, VEC * 2);
     else dx[xoff] = o[0];
   }
 }
@@ -1321,10 +1326,17 @@ HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
                        OW, ky, kx, sy, sx, pt, pl, mode, make_fastdiv(C / 8),
                        make_fastdiv(OW), make_fastdiv(OH));
   } else {
-    long long total = (long long)N * OH * OW * C;
-    hipLaunchKernelGGL(pool_fwd_kernel<1>, dim3(grid_for(total)), dim3(256), 0, s,
+    // C off the 8-grid (LeNet's 20 / 50): 4- or 2-channel lanes
+    const int v = (C % 4 == 0 && ((uintptr_t)x & 7) == 0 &&
+                   ((uintptr_t)y & 7) == 0) ? 4
+                  : (C % 2 == 0 && ((uintptr_t)x & 3) == 0 &&
+                     ((uintptr_t)y & 3) == 0) ? 2 : 1;
+    long long total = (long long)N * OH * OW * (C / v);
+    auto k = v == 4 ? pool_fwd_kernel<4> : v == 2 ? pool_fwd_kernel<2>
+                                                  : pool_fwd_kernel<1>;
+    hipLaunchKernelGGL(k, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C, OH,
-                       OW, ky, kx, sy, sx, pt, pl, mode, make_fastdiv(C),
+                       OW, ky, kx, sy, sx, pt, pl, mode, make_fastdiv(C / v),
                        make_fastdiv(OW), make_fastdiv(OH));
   }
   return (int)hipGetLastError();
@@ -1357,13 +1369,20 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
                        aux_act, make_fastdiv(C / 8), make_fastdiv(W),
                        make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
   } else {
-    long long total = (long long)N * H * W * C;
-    auto k1 = mode == POOL_AVG ? pool_bwd_kernel<1, POOL_AVG>
-                               : pool_bwd_kernel<1, POOL_MAX>;
+    const uintptr_t al = (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)aux;
+    const int v = (C % 4 == 0 && (al & 7) == 0) ? 4
+                  : (C % 2 == 0 && (al & 3) == 0) ? 2 : 1;
+    long long total = (long long)N * H * W * (C / v);
+    auto k1 = v == 4 ? (mode == POOL_AVG ? pool_bwd_kernel<4, POOL_AVG>
+                                         : pool_bwd_kernel<4, POOL_MAX>)
+            : v == 2 ? (mode == POOL_AVG ? pool_bwd_kernel<2, POOL_AVG>
+                                         : pool_bwd_kernel<2, POOL_MAX>)
+                     : (mode == POOL_AVG ? pool_bwd_kernel<1, POOL_AVG>
+                                         : pool_bwd_kernel<1, POOL_MAX>);
     hipLaunchKernelGGL(k1, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W, C, OH,
                        OW, ky, kx, sy, sx, pt, pl, mode, (const uint16_t*)aux,
-                       aux_act, make_fastdiv(C), make_fastdiv(W),
+                       aux_act, make_fastdiv(C / v), make_fastdiv(W),
                        make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
   }
   return (int)hipGetLastError();

@@ -225,7 +225,11 @@ def test_conv_wgrad(cfg):
 @pytest.mark.parametrize("shape,k,s", [((2, 55, 55, 96), 3, 2),
                                        ((2, 56, 54, 16), 3, 2),
                                        ((2, 13, 13, 5), 3, 2),
-                                       ((1, 8, 8, 16), 2, 2)])
+                                       ((1, 8, 8, 16), 2, 2),
+                                       # 4- and 2-channel lanes (LeNet)
+                                       ((2, 24, 24, 20), 2, 2),
+                                       ((2, 8, 8, 50), 2, 2),
+                                       ((2, 9, 9, 12), 3, 2)])
 def test_pool(mode, shape, k, s):
     x = rnd(*shape)
     y, am = ops.pool_fwd(x, k, k, (s, s), mode)
