@@ -28,7 +28,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512,
+    # 1024 per GPU: AlexNet's activations at b1024 take ~10 GB of the 288 GB
+    # HBM; b512 -> b1024 lifts 1-GPU throughput 114k -> 126k img/s (longer
+    # GEMMs, half the per-sample update / launch cost) and halves the
+    # all-reduce-to-compute ratio for the multi-GPU points
+    # (profiles/batch_sweep_r2.md)
+    ap.add_argument("--batch", type=int, default=1024,
                     help="per-GPU minibatch (weak scaling)")
     ap.add_argument("--model", default="alexnet")
     ap.add_argument("--precision", default="bfloat16",
