@@ -237,7 +237,8 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         res = out
         pad = None
         if not accumulate and beta == 0.0 and bias_grad is None:
-            pad = _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux)
+            pad = _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux,
+                              bm)
         if pad is not None:
             # odd M / N / K: zero-padded operands take the LDS-DMA loaders
             a, b, Mp, Np, Kp = pad
@@ -320,7 +321,7 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
 _DMA_PAD_MIN = 1 << 24   # M*N*K above which padding pays for its copies
 
 
-def _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux):
+def _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux, bias_mode=1):
     """Zero-padded copies of a large GEMM's operands when an odd dimension
     keeps them off the LDS-DMA loaders (a K-major operand needs K % 8 == 0,
     an MN-major one M / N % 8 == 0; csrc/kernels/gemm.hip ``dma_ok``): K
@@ -334,8 +335,10 @@ def _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux):
     Np = r8(N) if not kb and N % 8 else N
     if (Mp, Np, Kp) == (M, N, K) or M * N * K < _DMA_PAD_MIN:
         return None
-    if (Np != N and bias is not None) or (aux is not None and
-                                          (Mp, Np) != (M, N)):
+    # a per-column (1) / per-row (2) bias would be read past its end
+    if bias is not None and (Np != N if bias_mode == 1 else Mp != M):
+        return None
+    if aux is not None and (Mp, Np) != (M, N):
         return None
 
     def padded(t, rows, cols):
