@@ -1168,6 +1168,36 @@ HVK_API int hvk_join(const void* const* ins, const int* lens, int nin, int dt,
   return (int)hipGetLastError();
 }
 
+// The same image with one 16-B output chunk per lane (chunks of a pixel on
+// consecutive lanes): a wave's stores cover one contiguous 1 KiB span; each
+// lane gathers its 8 elements from <= 2 input rows with 2-B loads.
+template <int S, int C>
+__global__ void space_to_depth_chunk_kernel(const uint16_t* __restrict__ x,
+                                            uint16_t* __restrict__ y, int H,
+                                            int W, int pt, int pl, FastDiv fW2,
+                                            FastDiv fH2, long long chunks) {
+  constexpr int RUN = S * C, PIX = S * RUN, CPP = PIX / 8;
+  static_assert(PIX % 8 == 0, "vector shape");
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       e < chunks; e += (long long)gridDim.x * blockDim.x) {
+    const uint32_t q = (uint32_t)(e / CPP), j = (uint32_t)(e - (long long)q * CPP);
+    uint32_t t, X, n, Y;
+    fdivmod(q, fW2, t, X);
+    fdivmod(t, fH2, n, Y);
+    uint16_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = (int)j * 8 + k;            // element of the pixel vector
+      const int dy = i / RUN, r = i - dy * RUN;
+      const int dx = r / C, c = r - dx * C;
+      const int iy = S * (int)Y + dy - pt, ix = S * (int)X + dx - pl;
+      const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      v[k] = in ? x[(((long long)n * H + iy) * W + ix) * C + c] : (uint16_t)0;
+    }
+    *(uint4*)(y + e * 8) = *(const uint4*)v;
+  }
+}
+
 HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
                                int C, int s, int pt, int pl, int H2, int W2,
                                hipStream_t st) {
@@ -1175,6 +1205,18 @@ HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
   if (C2 % 8) return -1;
   long long runs = (long long)N * H2 * W2 * s;
   if (runs >= (1ll << 32)) return -1;
+  static const bool chunked = [] {
+    const char* e = getenv("HVK_S2D_CHUNK");
+    return !(e && e[0] == '0');
+  }();
+  if (chunked && s == 4 && C == 3 && ((uintptr_t)y & 15) == 0) {
+    const long long chunks = (long long)N * H2 * W2 * 6;
+    hipLaunchKernelGGL((space_to_depth_chunk_kernel<4, 3>),
+                       dim3(grid_for(chunks)), dim3(256), 0, st,
+                       (const uint16_t*)x, (uint16_t*)y, H, W, pt, pl,
+                       make_fastdiv(W2), make_fastdiv(H2), chunks);
+    return (int)hipGetLastError();
+  }
   if (s == 4 && C == 3 && ((uintptr_t)y & 15) == 0) {
     long long pixels = (long long)N * H2 * W2;
     hipLaunchKernelGGL((space_to_depth_px_kernel<4, 3>), dim3(grid_for(pixels)),
