@@ -1185,14 +1185,29 @@ __global__ void space_to_depth_chunk_kernel(const uint16_t* __restrict__ x,
     fdivmod(q, fW2, t, X);
     fdivmod(t, fH2, n, Y);
     uint16_t v[8];
+    const int iy0 = S * (int)Y - pt, ix0 = S * (int)X - pl;
+    if (RUN % 4 == 0 && iy0 >= 0 && iy0 + S <= H && ix0 >= 0 &&
+        ix0 + S <= W) {
+      // interior pixel: each half-chunk (4 elements) lies in one row run,
+      // one unaligned 8-B load (gfx950 unaligned global access)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = (int)j * 8 + k;            // element of the pixel vector
-      const int dy = i / RUN, r = i - dy * RUN;
-      const int dx = r / C, c = r - dx * C;
-      const int iy = S * (int)Y + dy - pt, ix = S * (int)X + dx - pl;
-      const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      v[k] = in ? x[(((long long)n * H + iy) * W + ix) * C + c] : (uint16_t)0;
+      for (int h = 0; h < 2; ++h) {
+        const int i = (int)j * 8 + 4 * h;
+        const int dy = i / RUN, r = i - dy * RUN;
+        __builtin_memcpy(&v[4 * h],
+                         x + (((long long)n * H + iy0 + dy) * W + ix0) * C + r,
+                         8);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = (int)j * 8 + k;          // element of the pixel vector
+        const int dy = i / RUN, r = i - dy * RUN;
+        const int dx = r / C, c = r - dx * C;
+        const int iy = iy0 + dy, ix = ix0 + dx;
+        const bool in = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        v[k] = in ? x[(((long long)n * H + iy) * W + ix) * C + c] : (uint16_t)0;
+      }
     }
     *(uint4*)(y + e * 8) = *(const uint4*)v;
   }
