@@ -434,6 +434,41 @@ __global__ void act_bwd_kernel(const void* dy, int dydt, const void* y, int ydt,
        i += (long long)gridDim.x * blockDim.x)
     st_any(dx, i, dxdt, ld_any(dy, i, dydt) * act_bwd(ld_any(y, i, ydt), act));
 }
+// bf16 -> bf16 activation / its backward, 8 elements per lane, one switch
+// per chunk (standalone activation units: CIFAR quick's ReLU after pooling)
+__global__ void act_fwd_bf16x8_kernel(const uint16_t* __restrict__ x,
+                                      uint16_t* __restrict__ y, long long n8,
+                                      int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint4 a = ((const uint4*)x)[i];
+    const uint16_t* h = (const uint16_t*)&a;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = bf2f(h[q]);
+    act_fwd8(v, act);
+    ((uint4*)y)[i] = pack_bf16x8(v);
+  }
+}
+__global__ void act_bwd_bf16x8_kernel(const uint16_t* __restrict__ dy,
+                                      const uint16_t* __restrict__ y,
+                                      uint16_t* __restrict__ dx, long long n8,
+                                      int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint4 a = ((const uint4*)dy)[i], b = ((const uint4*)y)[i];
+    const uint16_t* ha = (const uint16_t*)&a;
+    const uint16_t* hb = (const uint16_t*)&b;
+    float v[8], yv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      v[q] = bf2f(ha[q]);
+      yv[q] = bf2f(hb[q]);
+    }
+    act_bwd_mul8(v, yv, act);
+    ((uint4*)dx)[i] = pack_bf16x8(v);
+  }
+}
 // bf16 strict-relu backward, 8 elements per lane (the AlexNet hot case)
 __global__ void relu_bwd_bf16x8_kernel(const uint16_t* dy, const uint16_t* y,
                                        uint16_t* dx, long long n8) {
@@ -957,6 +992,13 @@ HVK_API int hvk_row_sum(const void* in, int dt, int R, int C, float* out,
 
 HVK_API int hvk_act_fwd(const void* x, int xdt, void* y, int ydt, long long n,
                         int act, hipStream_t s) {
+  if (xdt == DT_BF16 && ydt == DT_BF16 && n % 8 == 0 &&
+      ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    hipLaunchKernelGGL(act_fwd_bf16x8_kernel, dim3(grid_for(n / 8)),
+                       dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
+                       n / 8, act);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      y, ydt, n, act);
   return (int)hipGetLastError();
@@ -970,6 +1012,12 @@ HVK_API int hvk_act_bwd(const void* dy, int dydt, const void* y, int ydt,
     hipLaunchKernelGGL(relu_bwd_bf16x8_kernel, dim3(grid_for(n / 8)), dim3(256),
                        0, s, (const uint16_t*)dy, (const uint16_t*)y,
                        (uint16_t*)dx, n / 8);
+  } else if (dydt == DT_BF16 && ydt == DT_BF16 && dxdt == DT_BF16 &&
+             n % 8 == 0 && ((uintptr_t)dy & 15) == 0 &&
+             ((uintptr_t)y & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+    hipLaunchKernelGGL(act_bwd_bf16x8_kernel, dim3(grid_for(n / 8)),
+                       dim3(256), 0, s, (const uint16_t*)dy,
+                       (const uint16_t*)y, (uint16_t*)dx, n / 8, act);
   } else {
     hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, dy,
                        dydt, y, ydt, dx, dxdt, n, act);

@@ -83,6 +83,25 @@ def test_gemm_asymmetric_identity():
     assert torch.equal(got.cpu(), b.float())
 
 
+@pytest.mark.parametrize("act", ["linear", "tanh", "relu", "strict_relu",
+                                 "sigmoid"])
+@pytest.mark.parametrize("n", [4096, 1003])
+def test_standalone_activation(act, n):
+    """Activation units: the bf16 x8 kernels (n % 8 == 0) and the scalar
+    kernel (odd n), forward and backward, against the fp32 reference."""
+    x = rnd(n, scale=2.0)
+    err = rnd(n, seed=5)
+    y_ref = ops.act_fwd_ref(x.float(), act)
+    y = ops.act_fwd(x.to(DEV), act)
+    torch.cuda.synchronize()
+    close(y, y_ref, 2e-2)
+    yb = y_ref.to(BF)
+    d_ref = err.float() * ops.act_bwd_ref(yb.float(), act)
+    d = ops.act_bwd(err.to(DEV), yb.to(DEV), act)
+    torch.cuda.synchronize()
+    close(d, d_ref, 2e-2)
+
+
 def test_gemm_epilogue_bias_act_aux():
     M, N, K = 300, 260, 192
     a, w = rnd(M, K), rnd(N, K, seed=2)
