@@ -1374,3 +1374,89 @@ HVK_API int hvk_cast(const void* in, int idt, void* out, int odt, long long n,
   }
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Direct convolution for tiny reductions (C * KH * KW <= 64, OC <= 64: LeNet's
+// conv1, C = 1, 5 x 5 -> 20).  The implicit GEMM spends a whole 128 x 64 tile
+// with ONE 64-deep K step on such a layer (latency bound: 0.37 ms at b4096
+// for 2.4 GFLOP); here a lane computes every output channel of one pixel
+// from the K taps, the weights broadcast from LDS as f32 [k][oc].
+template <int OCMAX>
+__global__ __launch_bounds__(256) void conv_fwd_direct_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+    const float* __restrict__ bias, uint16_t* __restrict__ y, int N, int H,
+    int W, int C, int OC, int KH, int KW, int sy, int sx, int pt, int pl,
+    int OH, int OW, int act, FastDiv fOW, FastDiv fOH) {
+  __shared__ float ws[64 * 64];
+  __shared__ float bs[64];
+  const int K = KH * KW * C;
+  for (int i = threadIdx.x; i < OC * K; i += blockDim.x) {
+    const int oc = i / K, k = i - oc * K;
+    ws[k * OCMAX + oc] = bf2f(w[i]);
+  }
+  for (int i = threadIdx.x; i < OCMAX; i += blockDim.x)
+    bs[i] = (bias && i < OC) ? bias[i] : 0.f;
+  __syncthreads();
+  const uint32_t P = (uint32_t)N * OH * OW;
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < P;
+       p += gridDim.x * blockDim.x) {
+    uint32_t t, ow, n, oh;
+    fdivmod(p, fOW, t, ow);
+    fdivmod(t, fOH, n, oh);
+    float acc[OCMAX];
+#pragma unroll
+    for (int o = 0; o < OCMAX; ++o) acc[o] = bs[o];
+    const int ih0 = (int)oh * sy - pt, iw0 = (int)ow * sx - pl;
+    const uint16_t* img = x + (long long)n * H * W * C;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int ih = ih0 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int iw = iw0 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const uint16_t* px = img + ((long long)ih * W + iw) * C;
+        const float* wk = ws + ((kh * KW + kw) * C) * OCMAX;
+        for (int c = 0; c < C; ++c) {
+          const float xv = bf2f(px[c]);
+#pragma unroll
+          for (int o = 0; o < OCMAX; ++o) acc[o] += xv * wk[c * OCMAX + o];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < OCMAX; o += 8) act_fwd8(acc + o, act);
+    uint16_t* out = y + (long long)p * OC;
+    if ((OC & 1) == 0) {
+#pragma unroll
+      for (int o = 0; o < OCMAX; o += 2)
+        if (o < OC)
+          *(uint32_t*)(out + o) = (uint32_t)f2bf(acc[o]) |
+                                  ((uint32_t)f2bf(acc[o + 1]) << 16);
+    } else {
+#pragma unroll
+      for (int o = 0; o < OCMAX; ++o)
+        if (o < OC) out[o] = f2bf(acc[o]);
+    }
+  }
+}
+
+HVK_API int hvk_conv_fwd_direct(const void* X, const void* Wt,
+                                const float* bias, void* Y, int N, int H,
+                                int W, int C, int OC, int KH, int KW, int sy,
+                                int sx, int pt, int pl, int OH, int OW,
+                                int act, hipStream_t s) {
+  const int K = KH * KW * C;
+  if (K > 64 || OC > 64 || OC < 1 || ((uintptr_t)Y & 3) ||
+      (long long)N * OH * OW >= (1ll << 31))
+    return -1;
+  const long long P = (long long)N * OH * OW;
+  const int grid = grid_for(P);
+  auto k = OC <= 16 ? conv_fwd_direct_kernel<16>
+         : OC <= 32 ? conv_fwd_direct_kernel<32>
+                    : conv_fwd_direct_kernel<64>;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, (const uint16_t*)X,
+                     (const uint16_t*)Wt, bias, (uint16_t*)Y, N, H, W, C, OC,
+                     KH, KW, sy, sx, pt, pl, OH, OW, act, make_fastdiv(OW),
+                     make_fastdiv(OH));
+  return (int)hipGetLastError();
+}

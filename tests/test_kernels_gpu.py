@@ -184,6 +184,9 @@ CONVS = [
     (2, 40, 37, 3, 64, 8, 8, (4, 4), (2, 1, 2, 1), 1),
     (2, 20, 20, 2, 16, 5, 5, (2, 2), (2, 2, 2, 2), 1),
     (2, 31, 29, 3, 32, 7, 7, (2, 2), (3, 3, 3, 3), 1),
+    # direct tiny-reduction forward (LeNet conv1: C = 1, 5 x 5 -> 20; OC 40)
+    (2, 28, 28, 1, 20, 5, 5, (1, 1), (0, 0, 0, 0), 1),
+    (2, 11, 9, 1, 40, 3, 3, (2, 1), (1, 0, 1, 1), 1),
     # channel-padded path: C = 20 -> 24 (LeNet conv2), C = 3 at stride 1
     (2, 12, 12, 20, 50, 5, 5, (1, 1), (0, 0, 0, 0), 1),
     (2, 16, 16, 3, 64, 3, 3, (1, 1), (1, 1, 1, 1), 1),

@@ -494,6 +494,7 @@ def needs_im2col(C, groups):
 # 0.32 ms (+0.05 ms for the pad, shared with the forward), forward 1.41 ->
 # 1.26 ms (tools/bench_c3_pad.py).  HVK_C3_PAD=0 keeps the run kernels.
 _C_PAD8 = os.environ.get("HVK_C3_PAD", "1") != "0"
+_DIRECT = os.environ.get("HVK_CONV_DIRECT", "1") != "0"
 _C_PAD_MIN = int(os.environ.get("HVK_C3_PAD_MIN", "3"))
 
 
@@ -652,6 +653,14 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
                       act, _s(x))
             if col_out is not None:
                 col_out["col"] = PaddedImage(xp, C)
+            return out
+        if _DIRECT and groups == 1 and C < 3 and KH * KW * C <= 64 and \
+                OC <= 64 and out.is_contiguous() and \
+                _lib.lib().hvk_conv_fwd_direct(
+                    _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW,
+                    sy, sx, pt, pl, OH, OW, act, _s(x)) == 0:
+            # a reduction this short (LeNet conv1: 25 taps) is latency bound
+            # on the GEMM tile: direct per-pixel kernel
             return out
         if needs_im2col(C, groups):
             # packed (kw, c) runs: no im2col pass (csrc/kernels/gemm.hip)
