@@ -1460,3 +1460,93 @@ HVK_API int hvk_conv_fwd_direct(const void* X, const void* Wt,
                      make_fastdiv(OH));
   return (int)hipGetLastError();
 }
+
+// Weight gradient of the same tiny convolutions: dW[oc][k] += sum over pixels
+// of dY[p][oc] * X_col[p][k] (and dbias[oc] += sum dY[p][oc]).  A block walks
+// its pixel range in 64-pixel tiles staged in LDS (dY rows and the gathered
+// taps as f32); each lane owns up to 16 of the OC * K outputs and adds its
+// partial sums to dW with one atomic each at the end.
+__global__ __launch_bounds__(256) void conv_wgrad_direct_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+    float* __restrict__ dw, float* __restrict__ dbias, int N, int H, int W,
+    int C, int OC, int KH, int KW, int sy, int sx, int pt, int pl, int OH,
+    int OW, int ppb, FastDiv fOW, FastDiv fOH, FastDiv fK, FastDiv fKWC,
+    FastDiv fC) {
+  constexpr int TP = 64;
+  __shared__ float sdy[TP * 64];
+  __shared__ float sxc[TP * 64];
+  const int K = KH * KW * C, NO = OC * K;
+  const uint32_t P = (uint32_t)N * OH * OW;
+  const uint32_t p0 = (uint32_t)blockIdx.x * ppb;
+  const uint32_t p1 = min(P, p0 + (uint32_t)ppb);
+  float acc[16], bacc = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (uint32_t t0 = p0; t0 < p1; t0 += TP) {
+    const int np = (int)min((uint32_t)TP, p1 - t0);
+    for (int i = threadIdx.x; i < TP * OC; i += blockDim.x) {
+      const int t = i / OC, oc = i - t * OC;
+      sdy[t * 64 + oc] = t < np ? bf2f(dy[(long long)(t0 + t) * OC + oc]) : 0.f;
+    }
+    for (int i = threadIdx.x; i < TP * K; i += blockDim.x) {
+      uint32_t t, k, tap, c, kh, kw;
+      fdivmod((uint32_t)i, fK, t, k);
+      float v = 0.f;
+      if ((int)t < np) {
+        uint32_t q = t0 + t, r, ow, n, oh;
+        fdivmod(q, fOW, r, ow);
+        fdivmod(r, fOH, n, oh);
+        fdivmod(k, fC, tap, c);
+        kh = tap / KW;
+        kw = tap - kh * KW;
+        const int ih = (int)oh * sy - pt + (int)kh;
+        const int iw = (int)ow * sx - pl + (int)kw;
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+          v = bf2f(x[(((long long)n * H + ih) * W + iw) * C + c]);
+      }
+      sxc[t * 64 + k] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = threadIdx.x + r * 256;
+      if (o < NO) {
+        const int oc = o / K, k = o - oc * K;
+        float a = acc[r];
+        for (int t = 0; t < TP; ++t) a += sdy[t * 64 + oc] * sxc[t * 64 + k];
+        acc[r] = a;
+      }
+    }
+    if (dbias && (int)threadIdx.x < OC)
+      for (int t = 0; t < TP; ++t) bacc += sdy[t * 64 + threadIdx.x];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int o = threadIdx.x + r * 256;
+    if (o < NO) atomicAdd(&dw[o], acc[r]);
+  }
+  if (dbias && (int)threadIdx.x < OC) atomicAdd(&dbias[threadIdx.x], bacc);
+}
+
+HVK_API int hvk_conv_wgrad_direct(const void* X, const void* dY, float* dW,
+                                  float* dbias, int N, int H, int W, int C,
+                                  int OC, int KH, int KW, int sy, int sx,
+                                  int pt, int pl, int OH, int OW,
+                                  hipStream_t s) {
+  const int K = KH * KW * C;
+  if (K > 64 || OC > 64 || OC < 1 || (long long)N * OH * OW >= (1ll << 31))
+    return -1;
+  const long long P = (long long)N * OH * OW;
+  if (P == 0) return 0;
+  long long blocks = 512;
+  long long ppb = (P + blocks - 1) / blocks;
+  ppb = (ppb + 63) / 64 * 64;
+  blocks = (P + ppb - 1) / ppb;
+  hipLaunchKernelGGL(conv_wgrad_direct_kernel, dim3((int)blocks), dim3(256),
+                     0, s, (const uint16_t*)X, (const uint16_t*)dY, dW, dbias,
+                     N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, (int)ppb,
+                     make_fastdiv(OW), make_fastdiv(OH), make_fastdiv(K),
+                     make_fastdiv(KW * C), make_fastdiv(C));
+  return (int)hipGetLastError();
+}
