@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--steps-per-epoch", type=int, default=16)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--profile-json", default=None)
+    ap.add_argument("--mark-steps", action="store_true",
+                    help="bracket the timed steps with hvk_trace_marker "
+                         "kernels (step-only rocprofv3 summaries)")
     args = ap.parse_args()
 
     import torch
@@ -61,6 +64,8 @@ def main():
         print("bench.py: --gpus %d but WORLD_SIZE=%d; launch with "
               "torch.distributed.run" % (args.gpus, world), file=sys.stderr)
     backend = "cpu" if args.cpu or not torch.cuda.is_available() else "hip"
+    # exposed all-reduce wait per step (models/params.py comm_report)
+    os.environ.setdefault("VELES_AMD_DP_STATS", "1")
     # VELES_AMD_DP_BACKEND=gloo rehearses the multi-rank path with several
     # ranks on one GPU (RCCL refuses two ranks on one device)
     dp = DataParallel(backend=os.environ.get("VELES_AMD_DP_BACKEND") or
@@ -91,10 +96,19 @@ def main():
 
     wf.run_steps(args.warmup)
     sync()
+    store = getattr(wf, "param_store_", None)
+    if store is not None:
+        store.comm_report()   # drop the warmup steps' events
     dp.barrier()
     sync()
+    mark = args.mark_steps and backend == "hip"
+    if mark:
+        from veles_amd import ops
+        ops.trace_marker(1)
     t0 = time.perf_counter()
     wf.run_steps(args.steps)
+    if mark:
+        ops.trace_marker(2)
     sync()
     dp.barrier()
     sync()
@@ -106,6 +120,7 @@ def main():
         dp.all_reduce_max(t)
     dt = float(t.cpu()[0])
     value = args.steps * global_batch / dt
+    dp_info = dp_report(dp, store, backend)
     if dp.rank == 0:
         base = None
         try:
@@ -130,8 +145,9 @@ def main():
                "config": {"model": args.model, "global_batch": global_batch,
                           "per_gpu_batch": args.batch, "seq_len": None,
                           "parallelism": "dp%d" % dp.world_size,
-                          "image": shape, "grad_allreduce":
-                          "bucketed RCCL, overlapped with backward",
+                          "image": shape,
+                          "grad_allreduce": dp_info.pop("grad_allreduce"),
+                          "dp": dp_info,
                           "hip_graphs": [
                               "%s:%d captured/%d replayed" % (
                                   s.name, s.captures, s.replays)
@@ -144,6 +160,45 @@ def main():
                 json.dump({"result": out, "unit_stats": stats}, f, indent=1)
     dp.barrier()
     dp.shutdown()
+
+
+def dp_report(dp, store, backend):
+    """What the multi-rank step did, for reading an N > 1 result
+    (docs/PARALLEL.md): ranks seen by the process group, RCCL version,
+    gradient bucket layout and wire dtype, and the compute stream's exposed
+    wait for the collectives (max over ranks)."""
+    import torch
+    if not dp.multi:
+        return {"grad_allreduce": "none (one rank: no collectives)"}
+    import torch.distributed as dist
+    info = {"world_size_seen": dist.get_world_size(), "backend": dp.backend,
+            "solo": bool(dp.solo)}
+    if dp.backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            info["rccl_version"] = ".".join(str(x) for x in v) \
+                if isinstance(v, tuple) else str(v)
+        except Exception as e:  # noqa: BLE001
+            info["rccl_version"] = "unknown (%s)" % e
+    rep = None
+    if store is not None:
+        lay = store.bucket_layout()
+        info["buckets_mb"] = [mb for mb, _ in lay]
+        info["grad_dtype"] = store.grad_dtype
+        info["overlapped_update"] = bool(store._overlap_update())
+        rep = store.comm_report()
+    ms = torch.tensor([rep["mean_ms"] if rep else -1.0], dtype=torch.float64)
+    if dp.world_size > 1:
+        if backend == "hip":
+            ms = ms.cuda()
+        dp.all_reduce_max(ms)
+    v = float(ms.cpu()[0])
+    info["exposed_allreduce_ms_per_step"] = round(v, 4) if v >= 0 else None
+    info["grad_allreduce"] = "bucketed %s all-reduce (%s, %d buckets), " \
+        "launched per bucket during backward" % (
+            "RCCL" if dp.backend == "nccl" else dp.backend,
+            info.get("grad_dtype", "float32"), len(info.get("buckets_mb", [])))
+    return info
 
 
 if __name__ == "__main__":

@@ -1168,6 +1168,17 @@ HVK_API int hvk_gather(const void* x, int xdt, const int* idx, void* y,
 }
 
 // seed <- hash(seed + 1): a per-step seed sequence that lives on the device
+// An empty kernel that brackets a region of a kernel trace (bench.py
+// --mark-steps; tools/prof_summary.py --window keeps the dispatches between
+// the two markers: step-only profiles).
+__global__ void hvk_trace_marker_kernel(int tag) {
+  if (tag == -12345 && threadIdx.x == 1024) __builtin_trap();  // never
+}
+HVK_API int hvk_trace_marker(int tag, hipStream_t s) {
+  hipLaunchKernelGGL(hvk_trace_marker_kernel, dim3(1), dim3(64), 0, s, tag);
+  return (int)hipGetLastError();
+}
+
 __global__ void seed_advance_kernel(uint32_t* seed) {
   if (threadIdx.x == 0) seed[0] = hash32(seed[0] + 1u, 0x2545F491u);
 }

@@ -18,8 +18,9 @@ def _free_port():
 
 
 def _train(rank, world, port, out, steps, layers_name, bucket_mb=None,
-           overlap="1", backend="cpu"):
+           overlap="1", backend="cpu", grad_dtype="float32"):
     import torch
+    os.environ["VELES_AMD_DP_GRAD_DTYPE"] = grad_dtype
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world),
                        "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port)})
@@ -57,6 +58,7 @@ def _train(rank, world, port, out, steps, layers_name, bucket_mb=None,
         # small buckets: several per-bucket updates on the overlap path
         assert bucket_mb is None or len(st.buckets) >= 2, len(st.buckets)
         assert st._overlap == (overlap != "0")
+        assert st.grad_dtype == grad_dtype
         dp.shutdown()
 
 
@@ -95,6 +97,40 @@ def test_dp_matches_single_process(tmp_path, layers_name, bucket_mb,
     for k in w0.files:
         numpy.testing.assert_array_equal(w0[k], w1[k])
         numpy.testing.assert_allclose(w0[k], ws[k], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_dp_bf16_gradient_buckets(tmp_path, overlap):
+    """engine.dp.grad_dtype = bfloat16: each bucket goes over the wire as a
+    bf16 shadow and is cast back into the fp32 gradient before the fp32
+    master update.  Both ranks agree bit for bit and stay within bf16
+    rounding of the fp32-wire single-process run."""
+    steps = 6
+    out = str(tmp_path / "w%d.npz")
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_train, args=(r, 2, port, out, steps,
+                                               "lenet", 0.05, overlap,
+                                               "cpu", "bfloat16"))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+    single = str(tmp_path / "s%d.npz")
+    p = ctx.Process(target=_train, args=(0, 1, port, single, steps, "lenet"))
+    p.start()
+    p.join(240)
+    assert p.exitcode == 0
+    w0, w1, ws = (numpy.load(out % 0), numpy.load(out % 1),
+                  numpy.load(single % 0))
+    differs = False
+    for k in w0.files:
+        numpy.testing.assert_array_equal(w0[k], w1[k])
+        numpy.testing.assert_allclose(w0[k], ws[k], rtol=2e-2, atol=2e-3)
+        differs |= not numpy.array_equal(w0[k], ws[k])
+    assert differs, "bf16 wire gave bit-identical weights: not in effect"
 
 
 def _run_ranks(world, out, steps, layers_name, bucket_mb, overlap, backend):

@@ -137,3 +137,42 @@ def test_graphed_stochastic_and_input_derivative_units():
     assert _rel(graphed.param_store_.master, eager.param_store_.master) < 2e-2
     sp = graphed.forwards[1]
     assert sp.seed_dev_ is not None
+
+
+def test_capture_broken_by_a_sync_pins_eager_and_restores_state():
+    """A unit that synchronises (.item()) inside the backward capture: the
+    capture is abandoned, the stream context is restored (the process does
+    not stay on the capture stream), the parameter store's host counters
+    are put back before the eager re-run (one step counts once), the key is
+    pinned to eager mode, and training matches the eager run."""
+    from veles_amd import graphs as G_
+    steps = 8
+    eager = _train(False, steps)
+    seen = {}
+    orig_install = G_.install_step_graphs
+
+    def install(wf, warmup=2):
+        segs = orig_install(wf, warmup)
+        gd = [s for s in segs if s.name == "backward"][0].units[1]
+        cls = type(gd)
+
+        def run(self):
+            seen["n"] = seen.get("n", 0) + 1
+            torch.ones(1, device="cuda").sum().item()  # breaks a capture
+            return cls.run(self)
+        gd.__class__ = type("Sync" + cls.__name__, (cls,), {"run": run})
+        return segs
+
+    G_.install_step_graphs = install
+    try:
+        base = torch.cuda.current_stream()
+        graphed = _train(True, steps)
+    finally:
+        G_.install_step_graphs = orig_install
+    fwd, bwd = graphed.graph_segments_
+    assert bwd.failures >= 1 and bwd.captures == 0 and bwd.eager_keys
+    assert fwd.failures == 0 and fwd.captures >= 1
+    assert torch.cuda.current_stream() == base
+    assert graphed.param_store_.steps == eager.param_store_.steps == steps
+    assert seen["n"] >= steps
+    assert _rel(graphed.param_store_.master, eager.param_store_.master) < 2e-2

@@ -5,8 +5,20 @@ import csv
 import sys
 
 
-def main(trace, out, steps=None, title=""):
+def main(trace, out, steps=None, title="", window=False):
     rows = list(csv.DictReader(open(trace)))
+    if window:
+        # step-only: the dispatches between the two hvk_trace_marker kernels
+        # that bench.py --mark-steps launches around the timed steps
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        idx = [i for i, r in enumerate(rows)
+               if "hvk_trace_marker" in r["Kernel_Name"]]
+        if len(idx) < 2:
+            raise SystemExit("--window: fewer than two trace markers")
+        rows = rows[idx[0] + 1:idx[-1]]
+        if steps:
+            title += " (step-only: %d timed steps between trace markers)" % \
+                steps
     agg = collections.OrderedDict()
     for r in rows:
         n = r["Kernel_Name"].replace("void ", "").replace(
@@ -20,17 +32,30 @@ def main(trace, out, steps=None, title=""):
         a[1] += d
     tot = sum(v[1] for v in agg.values())
     lines = ["# %s" % title, "",
-             "Total kernel time %.3f ms over %d dispatches." %
-             (tot / 1e6, sum(v[0] for v in agg.values())), "",
+             "Total kernel time %.3f ms over %d dispatches%s." %
+             (tot / 1e6, sum(v[0] for v in agg.values()),
+              ("; %.3f ms of kernel time per step" % (tot / 1e6 / steps))
+              if steps else ""), "",
              "| kernel | grid (x,y,z threads) | VGPR | LDS | calls | "
-             "ms/call | total ms | % |", "|---|---|---|---|---|---|---|---|"]
+             "ms/call | total ms | ms/step | % |",
+             "|---|---|---|---|---|---|---|---|---|"]
     for k, (c, d) in sorted(agg.items(), key=lambda x: -x[1][1])[:40]:
-        lines.append("| %s | %s,%s,%s | %s | %s | %d | %.3f | %.3f | %.1f |" %
-                     (k[0], k[1], k[2], k[3], k[4], k[5], c, d / c / 1e6,
-                      d / 1e6, 100.0 * d / tot))
+        lines.append("| %s | %s,%s,%s | %s | %s | %d | %.3f | %.3f | %s | %.1f |"
+                     % (k[0], k[1], k[2], k[3], k[4], k[5], c, d / c / 1e6,
+                        d / 1e6, ("%.3f" % (d / 1e6 / steps)) if steps
+                        else "-", 100.0 * d / tot))
     open(out, "w").write("\n".join(lines) + "\n")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], title=sys.argv[3] if len(sys.argv) > 3
-         else "kernel trace")
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("out")
+    ap.add_argument("title", nargs="?", default="kernel trace")
+    ap.add_argument("--window", action="store_true",
+                    help="keep only dispatches between the trace markers")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps inside the window (per-step column)")
+    a = ap.parse_args()
+    main(a.trace, a.out, steps=a.steps, title=a.title, window=a.window)

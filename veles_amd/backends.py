@@ -203,10 +203,11 @@ class HipDevice(Device):
             "cus": props.multi_processor_count,
             "memory_bytes": props.total_memory,
         }
-        # Dedicated streams: compute (all unit kernels, stream-ordered) and
-        # communication (RCCL all-reduce overlapped with backward).
+        # The compute stream: every unit kernel, stream-ordered.  RCCL runs
+        # the gradient all-reduces on its own internal stream (ordered after
+        # this one at each bucket's launch) and the per-bucket updates go to
+        # the parameter store's side stream (models/params.py).
         self._compute_stream = torch.cuda.Stream(self.index, priority=0)
-        self._comm_stream = torch.cuda.Stream(self.index, priority=-1)
         self._pinned_pool = {}
         from veles_amd import ops
         self.ops = ops
@@ -219,10 +220,6 @@ class HipDevice(Device):
 
     def stream(self):
         return self._compute_stream
-
-    @property
-    def comm_stream(self):
-        return self._comm_stream
 
     @property
     def is_gpu(self):

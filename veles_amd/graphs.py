@@ -36,11 +36,14 @@ A unit class that cannot be captured sets ``graph_safe = False`` (e.g.
 stochastic pooling: a torch.Generator seeded from the host per minibatch);
 any such unit in a segment keeps that segment eager.  A capture that fails
 (an op that synchronises, an unsupported call) re-runs the pass eagerly and
-pins that key to eager mode.  Multi-rank workflows are not captured at
-all (RCCL collectives and the process group's watchdog thread), and
-gradient accumulation keeps the backward eager (``graph_safe`` of the
-parameter store).  Disable with ``root.common.engine.graphs = False`` or
-``VELES_AMD_GRAPHS=0``.
+pins that key to eager mode; host state that the discarded capture
+advanced (the parameter store's step counters, the fp8 history step) is
+restored first (``state_hooks``).  Multi-rank workflows capture the forward
+segment only (it issues no collective), so N = 1 and N > 1 run the same
+forward; their backward stays eager (the bucketed RCCL all-reduces are
+launched from the GD units as gradients become ready), as does any backward
+with gradient accumulation (``graph_safe`` of the parameter store).  Disable
+with ``root.common.engine.graphs = False`` or ``VELES_AMD_GRAPHS=0``.
 """
 from __future__ import annotations
 
@@ -89,6 +92,49 @@ class _Captured(object):
                 arr._state = 0
 
 
+class _HipCapture(object):
+    """Capture context of one HIP graph on a side stream with a private
+    memory pool.  Unlike ``torch.cuda.graph`` it restores the stream context
+    even when ``capture_end`` raises (a capture broken by a synchronising
+    op): the process then continues on the stream it was on."""
+    _stream = None
+
+    def __init__(self, graph):
+        self.graph = graph
+        self.ctx = None
+
+    def __enter__(self):
+        import gc
+        import torch
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.empty_cache()
+        if _HipCapture._stream is None:
+            _HipCapture._stream = torch.cuda.Stream()
+        self.ctx = torch.cuda.stream(_HipCapture._stream)
+        self.ctx.__enter__()
+        try:
+            # thread-local: helper threads (thread pool, a process group's
+            # watchdog) may keep making stream / event calls meanwhile
+            self.graph.capture_begin(capture_error_mode="thread_local")
+        except BaseException:
+            self._leave()
+            raise
+        return self
+
+    def _leave(self):
+        ctx, self.ctx = self.ctx, None
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+
+    def __exit__(self, *exc):
+        try:
+            self.graph.capture_end()
+        finally:
+            self._leave()
+        return False
+
+
 class GraphSegment(object):
     """Capture / replay of ``units`` (run consecutively, head first).
 
@@ -100,7 +146,7 @@ class GraphSegment(object):
     MAX_GRAPHS = 8
 
     def __init__(self, name, units, key_fn, inputs_fn=None, warmup=2,
-                 pre_hooks=(), replay_hooks=()):
+                 pre_hooks=(), replay_hooks=(), state_hooks=()):
         self.name = name
         self.units = list(units)
         self.head = self.units[0]
@@ -110,6 +156,10 @@ class GraphSegment(object):
         self.warmup = warmup
         self.pre_hooks = list(pre_hooks)
         self.replay_hooks = list(replay_hooks)
+        # [(save() -> state, restore(state))]: host state a capture pass
+        # advances, put back before a failed capture's eager re-run
+        self.state_hooks = list(state_hooks)
+        self._saved = None
         self.graphs = {}
         self.seen = {}
         self.eager_keys = set()
@@ -190,6 +240,7 @@ class GraphSegment(object):
         graph, ctx = self.new_graph()
         self.cur = _Captured(graph, key, [(a, a._devmem)
                                           for a in self.inputs_fn()])
+        self._saved = [save() for save, _ in self.state_hooks]
         self.ctx = ctx
         self.ctx.__enter__()
         self.mode = "capture"
@@ -201,10 +252,7 @@ class GraphSegment(object):
         on a side stream with a private memory pool."""
         import torch
         graph = torch.cuda.CUDAGraph()
-        # thread-local: helper threads (thread pool, a process group's
-        # watchdog) may keep making stream / event calls during the capture
-        return graph, torch.cuda.graph(graph,
-                                       capture_error_mode="thread_local")
+        return graph, _HipCapture(graph)
 
     def _end(self):
         if self.mode == "capture":
@@ -214,9 +262,12 @@ class GraphSegment(object):
                 ctx.__exit__(None, None, None)
             except Exception as e:  # noqa: BLE001 - capture_end failed
                 self._pin_eager(cur.key, e)
+                self.failures += 1
                 self.mode = None
+                self._restore_state()
                 self._rerun_eager(len(self.units))
                 return
+            self._saved = None
             self._record(cur)
             self.graphs[cur.key] = cur
             self.captures += 1
@@ -260,9 +311,16 @@ class GraphSegment(object):
         self.failures += 1
         # nothing captured has executed: run this pass for real, eagerly
         self.mode = "eager"
+        self._restore_state()
         self._rerun_eager(self.pos)
         if unit is self.tail:
             self.mode = None
+
+    def _restore_state(self):
+        saved, self._saved = self._saved, None
+        if saved is not None:
+            for (_, restore), st in zip(self.state_hooks, saved):
+                restore(st)
 
     def _pin_eager(self, key, exc):
         self.eager_keys.add(key)
@@ -300,12 +358,11 @@ def install_step_graphs(wf, warmup=2):
     if not graphs_enabled() or dev is None or not getattr(dev, "is_gpu",
                                                           False):
         return []
-    # multi-rank steps stay eager: the collectives and their watchdog are
-    # not captured, and a large-batch data-parallel step is GPU-bound anyway
+    # multi-rank: the forward is captured as at N = 1; the backward stays
+    # eager (its GD units launch the bucketed all-reduces as they go)
     from veles_amd.parallel import find_dp
     dp = find_dp(wf)
-    if dp is not None and getattr(dp, "multi", dp.world_size > 1):
-        return []
+    multi = dp is not None and getattr(dp, "multi", dp.world_size > 1)
     ld = wf.loader
     ev = getattr(wf, "evaluator", None)
     fwd_units = list(wf.forwards) + ([ev] if ev is not None else [])
@@ -328,7 +385,7 @@ def install_step_graphs(wf, warmup=2):
                                  warmup=warmup))
     gds = [g for g in reversed(getattr(wf, "gds", []) or []) if g is not None]
     store = getattr(wf, "param_store_", None)
-    if gds and store is not None and _is_chain(gds):
+    if gds and store is not None and _is_chain(gds) and not multi:
         def bkey():
             if not store.graph_safe():
                 return None
@@ -336,6 +393,7 @@ def install_step_graphs(wf, warmup=2):
         segs.append(GraphSegment(
             "backward", gds, bkey, inputs, warmup=warmup,
             pre_hooks=[store.refresh_table],
-            replay_hooks=[store.replayed_step]))
+            replay_hooks=[store.replayed_step],
+            state_hooks=[(store.host_state, store.restore_host_state)]))
     wf.graph_segments_ = segs
     return segs

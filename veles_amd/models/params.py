@@ -92,6 +92,23 @@ class ParameterStore(object):
         # per CU measured best (profiles/dp_overlap_update_r2.md)
         self._upd_blocks = int(os.environ.get("VELES_AMD_DP_UPDATE_BLOCKS",
                                               "256"))
+        # wire dtype of the gradient all-reduce: float32, or bfloat16 (half
+        # the xGMI bytes; each bucket is cast into a bf16 shadow on the
+        # compute stream, reduced, and cast back into the fp32 gradient
+        # before the fp32 master update)
+        self.grad_dtype = str(get(root.common.engine.dp.grad_dtype,
+                                  os.environ.get("VELES_AMD_DP_GRAD_DTYPE",
+                                                 "float32")))
+        if self.grad_dtype not in ("float32", "bfloat16"):
+            raise ValueError("engine.dp.grad_dtype must be float32 or "
+                             "bfloat16, not %r" % self.grad_dtype)
+        self._shadow = None
+        self._pending = {}   # bucket -> (work, shadow view) to cast back
+        # exposed-communication instrumentation (bench.py at N > 1): a pair
+        # of timing events around the compute stream's wait for the
+        # collectives / per-bucket updates, per step
+        self.comm_stats = os.environ.get("VELES_AMD_DP_STATS", "0") == "1"
+        self._comm_events = []
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -250,10 +267,50 @@ class ParameterStore(object):
 
     def _launch_bucket(self, i):
         self._launched.add(i)
-        work = self.dp.all_reduce_async(self.bucket_view(i))
+        view = self.bucket_view(i)
+        if self.grad_dtype == "bfloat16":
+            import torch
+            if self._shadow is None:
+                self._shadow = torch.empty(self.total, dtype=torch.bfloat16,
+                                           device=self.grad.device)
+            lo = self.buckets[i][0].offset
+            sh = self._shadow[lo:lo + view.numel()]
+            sh.copy_(view)   # compute stream: after the bucket's GD kernels
+            work = self.dp.all_reduce_async(sh)
+            self._pending[i] = (work, sh)
+        else:
+            work = self.dp.all_reduce_async(view)
         self._works.append(work)
         if self._overlap_update():
             self._bucket_update(i, work)
+
+    def _finish_bucket(self, i):
+        """bf16 wire: cast bucket i's reduced shadow back into the fp32
+        gradient (on the current stream, after its collective)."""
+        ent = self._pending.pop(i, None)
+        if ent is not None:
+            ent[0].wait()
+            self.bucket_view(i).copy_(ent[1])
+
+    def bucket_layout(self):
+        """[(MB, parameter count)] per all-reduce bucket, launch order."""
+        return [(round(self.bucket_view(i).numel() * 4 / (1 << 20), 3),
+                 len(b)) for i, b in enumerate(self.buckets)]
+
+    def comm_report(self, reset=True):
+        """Mean exposed all-reduce wait (ms per step) of the compute stream
+        since the last report: the time between the end of this rank's
+        backward enqueue and the point where the collectives (and, when
+        overlapped, the per-bucket updates) are done.  Synchronises."""
+        evs = self._comm_events
+        if reset:
+            self._comm_events = []
+        if not evs:
+            return None
+        evs[-1][1].synchronize()
+        ms = [a.elapsed_time(b) for a, b in evs]
+        return {"steps": len(ms), "mean_ms": sum(ms) / len(ms),
+                "max_ms": max(ms)}
 
     # -- per-bucket update overlapped with the backward (multi-rank) ---------
     def _overlap_update(self):
@@ -300,6 +357,7 @@ class ParameterStore(object):
                 segs.append((b - lo, e - lo, lr, d, l1, m))
         if not segs and not self.master.is_cuda:
             work.wait()
+            self._finish_bucket(i)
             return
         zf = True if not self.overwrite else max(0, self.zero_tail - lo)
         tables = self._bucket_tables
@@ -311,6 +369,7 @@ class ParameterStore(object):
               "max_blocks": self._upd_blocks}
         if not self.master.is_cuda:
             work.wait()
+            self._finish_bucket(i)
             ops.sgd_update(*args, **kw)
             return
         if self._upd_stream is None:
@@ -320,6 +379,7 @@ class ParameterStore(object):
         # copy cannot race the forward, which finished before that point
         with torch.cuda.stream(self._upd_stream):
             work.wait()
+            self._finish_bucket(i)
             if segs:
                 ops.sgd_update(*args, **kw)
 
@@ -367,6 +427,12 @@ class ParameterStore(object):
             return False
         overlapped = False
         if self._multi():
+            ev = None
+            if self.comm_stats and self.master.is_cuda:
+                import torch
+                ev = (torch.cuda.Event(enable_timing=True),
+                      torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             # buckets not launched yet (e.g. params without GD) go now
             for i in range(len(self.buckets)):
                 if i not in self._launched:
@@ -375,12 +441,18 @@ class ParameterStore(object):
             if not overlapped:
                 for w in self._works:
                     w.wait()
+                for i in list(self._pending):
+                    self._finish_bucket(i)
             elif self._upd_stream is not None:
                 # every bucket was updated on the side stream: the next
                 # forward (compute stream) reads the new weights after it
                 import torch
                 torch.cuda.current_stream(self.master.device).wait_stream(
                     self._upd_stream)
+            if ev is not None:
+                ev[1].record()
+                self._comm_events.append(ev)
+                del self._comm_events[:-256]
         segs = [] if overlapped else self._cached_segments()
         if segs and self._seg_table is None:
             self._seg_table = ops.SegmentTable(self.master.device)
@@ -460,6 +532,29 @@ class ParameterStore(object):
         if self.device is not None and getattr(self.device, "fp8", False):
             from veles_amd.ops import fp8
             fp8.registry(self.device.torch_device).step += 1
+
+    def host_state(self):
+        """Host-side step state that ``apply`` advances (saved before a HIP
+        graph capture pass, restored if that capture fails and the pass is
+        re-run eagerly: graphs.py)."""
+        st = {"steps": self.steps, "ready": set(self._ready),
+              "works": list(self._works), "launched": set(self._launched),
+              "accum": self._accum_count, "pending": dict(self._pending)}
+        if self.device is not None and getattr(self.device, "fp8", False):
+            from veles_amd.ops import fp8
+            st["fp8_step"] = fp8.registry(self.device.torch_device).step
+        return st
+
+    def restore_host_state(self, st):
+        self.steps = st["steps"]
+        self._ready = set(st["ready"])
+        self._works = list(st["works"])
+        self._launched = set(st["launched"])
+        self._accum_count = st["accum"]
+        self._pending = dict(st["pending"])
+        if "fp8_step" in st:
+            from veles_amd.ops import fp8
+            fp8.registry(self.device.torch_device).step = st["fp8_step"]
 
     def sync_host(self):
         """Copy master weights back into each Param.host (for snapshots)."""

@@ -1567,6 +1567,14 @@ def seed_advance(seed_dev):
     return seed_dev
 
 
+def trace_marker(tag=0):
+    """Launch the empty marker kernel on the current stream (bench.py
+    --mark-steps: brackets the timed steps in a rocprofv3 kernel trace)."""
+    if torch.cuda.is_available():
+        _lib_call("hvk_trace_marker", int(tag),
+                  torch.cuda.current_stream().cuda_stream)
+
+
 # --------------------------------------------------------------------- RNG
 def xorshift1024star(states, rounds, out=None):
     """states: int64 [n,16] (raw uint64 bits, updated in place); returns int64

@@ -53,6 +53,7 @@ _SIGS = {
     "hvk_dropout": [P, I, P, I, L, U, F, P, P],
     "hvk_dropout_dev": [P, I, P, I, L, P, F, P, P],
     "hvk_seed_advance": [P, P],
+    "hvk_trace_marker": [I, P],
     "hvk_xact": [P, I, P, I, P, I, L, I, F, L, I, P],
     "hvk_gather": [P, I, P, P, I, L, P],
     "hvk_xorshift1024star": [P, I, I, P, P],
