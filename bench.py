@@ -104,11 +104,11 @@ def main():
     mark = args.mark_steps and backend == "hip"
     if mark:
         from veles_amd import ops
-        ops.trace_marker(1)
+        ops.trace_marker(1, device.stream())
     t0 = time.perf_counter()
     wf.run_steps(args.steps)
     if mark:
-        ops.trace_marker(2)
+        ops.trace_marker(2, device.stream())
     sync()
     dp.barrier()
     sync()

@@ -836,6 +836,116 @@ __global__ void space_to_depth_px_kernel(const uint16_t* __restrict__ x,
   }
 }
 
+// Loader gather fused with the space-to-depth transform of the first
+// (strided, small-channel) convolution: uint8 samples [H][W][C] ->
+// normalised bf16 s2d images [H2][W2][S][S][C] (the layout hvk_conv_fwd reads
+// for the stride-1 conv that replaces the strided one), so the bf16 NHWC
+// image is never written and re-read.  mean2 / rdisp2 are the per-feature
+// affine map already laid out in s2d order (0 / 1 where no input pixel is).
+// A thread owns one output pixel (S*S*C elements) of SPT samples: the
+// pixel's affine map is loaded once; each sample reads S runs of S*C
+// contiguous bytes (dword loads + v_alignbyte: the runs are not aligned)
+// and writes S*S*C/8 16-B chunks.
+template <int S, int C, int SPT>
+__global__ void __launch_bounds__(256)
+fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
+                        const int* shuffled, int start, int count, int max_mb,
+                        int H, int W, int pt, int pl, int H2, int W2,
+                        const float* __restrict__ mean2,
+                        const float* __restrict__ rdisp2,
+                        uint16_t* __restrict__ dst, const int* labels,
+                        int* labels_out, int* idx_out) {
+  constexpr int RUN = S * C, PIX = S * RUN, RW = (RUN + 3) / 4;
+  static_assert(PIX % 8 == 0, "16-B output chunks");
+  const int pixels = H2 * W2;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i0 = blockIdx.y * SPT;
+  const long long sample = (long long)H * W * C;
+  if (q < pixels) {
+    const int Y = q / W2, X = q - (q / W2) * W2;
+    float mm[PIX], rr[PIX];
+#pragma unroll
+    for (int j = 0; j < PIX; j += 4) {
+      const float4 a = *(const float4*)(mean2 + (long long)q * PIX + j);
+      const float4 b = *(const float4*)(rdisp2 + (long long)q * PIX + j);
+      mm[j] = a.x; mm[j + 1] = a.y; mm[j + 2] = a.z; mm[j + 3] = a.w;
+      rr[j] = b.x; rr[j + 1] = b.y; rr[j + 2] = b.z; rr[j + 3] = b.w;
+    }
+    const int ix0 = S * X - pl;
+    const bool xin = ix0 >= 0 && ix0 + S <= W;
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int i = i0 + u;
+      if (i >= max_mb) break;
+      const int sid = i < count ? shuffled[start + i] : -1;
+      uint8_t v[PIX];
+#pragma unroll
+      for (int dy = 0; dy < S; ++dy) {
+        const int iy = S * Y + dy - pt;
+        const bool in = sid >= 0 && iy >= 0 && iy < H;
+        const long long o = (long long)sid * sample +
+                            ((long long)(in ? iy : 0) * W + ix0) * C;
+        if (in && xin && (o & ~3ll) + 4 * (RW + 1) <= src_bytes) {
+          const uint32_t* w = (const uint32_t*)(src + (o & ~3ll));
+          const uint32_t sh = (uint32_t)(o & 3);
+          uint32_t d[RW + 1], r[RW];
+#pragma unroll
+          for (int k = 0; k <= RW; ++k) d[k] = w[k];
+#pragma unroll
+          for (int k = 0; k < RW; ++k)
+            r[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+          __builtin_memcpy(&v[dy * RUN], r, RUN);
+        } else {
+#pragma unroll
+          for (int e = 0; e < RUN; ++e) {
+            const int ix = ix0 + e / C;
+            v[dy * RUN + e] = (in && ix >= 0 && ix < W)
+                                  ? src[(long long)sid * sample +
+                                        ((long long)iy * W + ix) * C + e % C]
+                                  : (uint8_t)0;
+          }
+        }
+      }
+      uint16_t o16[PIX];
+#pragma unroll
+      for (int e = 0; e < PIX; ++e)
+        o16[e] = f2bf(((float)v[e] - mm[e]) * rr[e]);
+      uint4* out = (uint4*)(dst + ((long long)i * pixels + q) * PIX);
+#pragma unroll
+      for (int j = 0; j < PIX / 8; ++j) out[j] = ((const uint4*)o16)[j];
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < SPT) {
+    const int i = i0 + threadIdx.x;
+    if (i < max_mb) {
+      const int sid = i < count ? shuffled[start + i] : -1;
+      if (labels_out) labels_out[i] = (sid >= 0 && labels) ? labels[sid] : -1;
+      if (idx_out) idx_out[i] = sid;
+    }
+  }
+}
+
+HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
+                                   const int* shuffled, int start, int count,
+                                   int max_mb, int H, int W, int C, int S,
+                                   int pt, int pl, int H2, int W2,
+                                   const float* mean2, const float* rdisp2,
+                                   void* dst, const int* labels,
+                                   int* labels_out, int* idx_out,
+                                   hipStream_t s) {
+  if (S != 4 || C != 3 || ((uintptr_t)dst & 15) || ((uintptr_t)mean2 & 15) ||
+      ((uintptr_t)rdisp2 & 15) || max_mb > 65535 * 4)
+    return -1;
+  constexpr int SPT = 4;
+  const int pixels = H2 * W2;
+  hipLaunchKernelGGL((fill_s2d_u8_bf16_kernel<4, 3, SPT>),
+                     dim3((pixels + 255) / 256, (max_mb + SPT - 1) / SPT),
+                     dim3(256), 0, s, (const uint8_t*)src, src_bytes, shuffled,
+                     start, count, max_mb, H, W, pt, pl, H2, W2, mean2, rdisp2,
+                     (uint16_t*)dst, labels, labels_out, idx_out);
+  return (int)hipGetLastError();
+}
+
 HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                                int start, int count, int max_mb,
                                long long sample_size, const float* mean,

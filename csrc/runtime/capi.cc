@@ -49,6 +49,29 @@ const char* vr_unit_class(void* h, int i) {
   return s.c_str();
 }
 
+// threads > 0: a thread-pool Engine (independent branches enqueue from
+// several host threads); 0: the serial engine
+int vr_set_engine(void* h, int threads) {
+  VR_TRY({
+    auto* wf = static_cast<veles_rt::Workflow*>(h);
+    wf->SetEngine(threads > 0 ? veles_rt::MakeThreadPoolEngine(threads)
+                              : veles_rt::MakeSerialEngine());
+  });
+}
+
+// 1: capture the GPU pass into a hipGraph (2nd run) and replay it
+int vr_enable_graph(void* h, int on) {
+  VR_TRY(static_cast<veles_rt::Workflow*>(h)->EnableGraph(on != 0));
+}
+
+int vr_graph_active(void* h) {
+  return static_cast<veles_rt::Workflow*>(h)->GraphActive() ? 1 : 0;
+}
+
+int vr_num_streams(void* h) {
+  return static_cast<veles_rt::Workflow*>(h)->NumStreams();
+}
+
 // input_shape: ndim sizes (batch first); gpu: 1 = run through libhvk
 int vr_initialize(void* h, const long long* shape, int ndim, int gpu) {
   VR_TRY({

@@ -150,3 +150,102 @@ def test_native_forward_gpu_matches_cpu(tmp_path):
     numpy.testing.assert_allclose(y, ref, atol=3e-2)
     assert numpy.argmax(y, 1).tolist() == numpy.argmax(ref, 1).tolist() or \
         numpy.mean(numpy.argmax(y, 1) == numpy.argmax(ref, 1)) > 0.9
+
+
+# The reference's own fixtures (libVeles/tests/workflow_files, exported by
+# the reference from its MNIST workflow): the runtime must load both archive
+# formats and compute the forward the packaged arrays define.
+REF_FIX = "/root/reference/libVeles/tests/workflow_files"
+
+
+def _numpy_forward_from_package(pkg, x):
+    """All2AllTanh (1.7159 * tanh(0.6666 v)) -> All2AllSoftmax from the
+    package's own .npy arrays (loaded with allow_pickle=False)."""
+    import io
+    import tarfile
+    if pkg.endswith(".zip"):
+        z = zipfile.ZipFile(pkg)
+        read = z.read
+    else:
+        t = tarfile.open(pkg)
+        read = lambda n: t.extractfile(n).read()  # noqa: E731
+    c = json.loads(read("contents.json"))
+    arrays = {}
+    for u in c["units"]:
+        for k, v in u["data"].items():
+            if isinstance(v, str) and v.startswith("@"):
+                arrays[v] = numpy.load(io.BytesIO(read(v[1:] + ".npy")),
+                                       allow_pickle=False)
+    h = x.reshape(len(x), -1).astype(numpy.float64)
+    for u in c["units"]:
+        w = arrays[u["data"]["weights"]].astype(numpy.float64)
+        b = arrays[u["data"]["bias"]].astype(numpy.float64)
+        v = h @ w.T + b
+        if u["class"]["name"] == "All2AllTanh":
+            h = 1.7159 * numpy.tanh(0.6666 * v)
+        else:
+            e = numpy.exp(v - v.max(1, keepdims=True))
+            h = e / e.sum(1, keepdims=True)
+    return h.astype(numpy.float32)
+
+
+@pytest.mark.skipif(not __import__("os").path.isdir(REF_FIX),
+                    reason="reference fixtures absent")
+@pytest.mark.parametrize("name", ["mnist.zip", "mnist.tar.gz"])
+@pytest.mark.parametrize("threads", [0, 3])
+def test_reference_fixture_packages(tmp_path, name, threads):
+    pkg = REF_FIX + "/" + name
+    x = numpy.random.RandomState(7).uniform(0, 1, (5, 784)).astype(
+        numpy.float32)
+    ref = _numpy_forward_from_package(pkg, x)
+    nw = rt.NativeWorkflow(pkg)
+    assert nw.unit_classes == ["All2AllTanh", "All2AllSoftmax"]
+    nw.set_engine(threads)
+    nw.initialize(x.shape, gpu=False)
+    y = nw.run(x)
+    assert y.shape == (5, 10)
+    numpy.testing.assert_allclose(y, ref, rtol=1e-5, atol=2e-6)
+    # the same through the C++ test binary and the CLI
+    numpy.save(tmp_path / "x.npy", x)
+    numpy.save(tmp_path / "ref.npy", ref)
+    r = subprocess.run([rt.TEST_BIN, pkg, str(tmp_path / "x.npy"),
+                        str(tmp_path / "ref.npy")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    r = subprocess.run([rt.CLI, pkg, str(tmp_path / "x.npy"),
+                        str(tmp_path / "y.npy"), "--threads", "2",
+                        "--repeat", "3"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    numpy.testing.assert_allclose(numpy.load(tmp_path / "y.npy"), ref,
+                                  rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
+def test_native_branch_streams_and_graph_on_gpu():
+    """Branches of a DAG on their own HIP streams joined by events, pooled
+    host enqueue, and a captured + replayed hipGraph of the pass
+    (veles_rt_tests --gpu-branch)."""
+    rt.build_runtime()
+    r = subprocess.run([rt.TEST_BIN, "--gpu-branch"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "OK 0" in r.stdout
+
+
+@pytest.mark.gpu
+def test_native_reference_fixture_gpu_graph(tmp_path):
+    pkg = REF_FIX + "/mnist.zip"
+    if not __import__("os").path.exists(pkg):
+        pytest.skip("reference fixtures absent")
+    x = numpy.random.RandomState(8).uniform(0, 1, (64, 784)).astype(
+        numpy.float32)
+    ref = _numpy_forward_from_package(pkg, x)
+    nw = rt.NativeWorkflow(pkg)
+    nw._gpu = True
+    nw.enable_graph(True)
+    nw.initialize(x.shape, gpu=True)
+    for _ in range(3):
+        y = nw.run(x)
+        numpy.testing.assert_allclose(y, ref, atol=2e-2)
+    assert nw.graph_active

@@ -50,6 +50,10 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         self._dev_mean_ = None
         self._dev_rdisp_ = None
         self._dev_shuffled_ = None
+        # (s, KH, KW, padding) when the first conv asked for its input in
+        # space-to-depth layout (request_s2d_input)
+        self.s2d_layout_ = None
+        self._dev_s2d_affine_ = None
 
     def __getstate__(self):
         st = super().__getstate__()
@@ -79,16 +83,56 @@ class FullBatchLoader(Loader, IFullBatchLoader):
 
     def create_minibatch_data(self):
         import torch
+        from veles_amd import ops
         n = self.local_minibatch_size
         dev = self.device
         shape = (n,) + self.sample_shape
         tdev = dev.torch_device if dev is not None else torch.device("cpu")
+        lay = self.s2d_layout_
+        if lay is not None:
+            s, KH, KW, padding = lay
+            shape = (n,) + ops.s2d_geometry(shape, s, KH, KW, padding)
         t = torch.zeros(shape, dtype=self._torch_dtype_for_minibatch(),
                         device=tdev)
         self.minibatch_data.devmem = t
+        self.minibatch_data.s2d_ = None if lay is None else \
+            (lay[0], (n,) + self.sample_shape)
         for arr in (self.minibatch_labels, self.minibatch_indices):
             if arr.mem is not None:
                 arr.initialize(dev)
+
+    def request_s2d_input(self, s, KH, KW, padding):
+        """The first convolution asks for ``minibatch_data`` in its
+        space-to-depth layout (ops.S2DImage): the gather then writes the
+        normalised s2d image directly (``hvk_fill_minibatch_s2d``) and the
+        bf16 NHWC image is never materialised.  Only for uint8 RGB data on
+        the GPU with the affine map folded into the gather; returns whether
+        the layout is now in effect.  ``minibatch_data.s2d_`` = (s, logical
+        NHWC shape) tells every consumer."""
+        import torch
+        from veles_amd import ops
+        dev = self.device
+        data = self.original_data.devmem
+        if dev is None or not getattr(dev, "is_gpu", False) or \
+                data is None or data.dtype != torch.uint8 or \
+                data.dim() != 4 or data.shape[3] != 3 or s != 4 or \
+                self.export_affine or \
+                self._torch_dtype_for_minibatch() != torch.bfloat16:
+            return False
+        shape = tuple(data.shape[1:])
+        feat = int(numpy.prod(shape))
+        mean = self._affine[0] if self._affine is not None else \
+            numpy.zeros(feat, numpy.float32)
+        rdisp = self._affine[1] if self._affine is not None else \
+            numpy.ones(feat, numpy.float32)
+        pad = tuple(padding)
+        self._dev_s2d_affine_ = tuple(
+            ops.s2d_affine(torch.from_numpy(numpy.ascontiguousarray(v)),
+                           shape, s, KH, KW, pad, f).to(dev.torch_device)
+            for v, f in ((mean, 0.0), (rdisp, 1.0)))
+        self.s2d_layout_ = (s, KH, KW, pad)
+        self.create_minibatch_data()
+        return True
 
     def _apply_validation_ratio(self):
         if not self.validation_ratio:
@@ -191,6 +235,16 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         if self._dev_shuffled_ is None:
             self.on_initialized()
         data = self.original_data.devmem
+        if self.s2d_layout_ is not None:
+            s, KH, KW, padding = self.s2d_layout_
+            ops.fill_minibatch_s2d(
+                data, self._dev_shuffled_, start_offset, count,
+                self.minibatch_data.devmem, s, KH, KW, padding,
+                *self._dev_s2d_affine_, labels=self._dev_labels_,
+                labels_out=self.minibatch_labels.devmem
+                if self.has_labels else None,
+                idx_out=self.minibatch_indices.devmem)
+            return True
         ops.fill_minibatch(
             data, self._dev_shuffled_, start_offset, count,
             self.minibatch_data.devmem, mean=self._dev_mean_,

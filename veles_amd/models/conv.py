@@ -14,7 +14,7 @@ from veles_amd.models.nn_units import Forward
 from veles_amd import ops
 from veles_amd.ops import fp8
 
-__all__ = ["Conv", "ConvTanh", "ConvRELU", "ConvStrictRELU", "ConvSigmoid",
+__all__ = ["Conv", "input_shape", "input_tensor", "ConvTanh", "ConvRELU", "ConvStrictRELU", "ConvSigmoid",
            "norm_padding", "norm_sliding"]
 
 
@@ -37,6 +37,22 @@ def norm_sliding(s):
     return tuple(s)
 
 
+def input_shape(arr):
+    """Logical NHWC shape of a conv input Array (the loader may serve it in
+    space-to-depth layout: ``Array.s2d_``)."""
+    spec = getattr(arr, "s2d_", None)
+    return tuple(spec[1]) if spec is not None else tuple(arr.shape)
+
+
+def input_tensor(arr):
+    """The device tensor of a conv input Array, wrapped as ops.S2DImage when
+    the loader serves it in space-to-depth layout."""
+    spec = getattr(arr, "s2d_", None)
+    if spec is not None:
+        return ops.S2DImage(arr.devmem, spec[0], spec[1])
+    return arr.devmem
+
+
 class Conv(Forward):
     __id__ = "bd4f8f3d-0a43-4a8e-b4d5-5b1b9d3a1c10"
     MAPPING = "conv"
@@ -54,7 +70,8 @@ class Conv(Forward):
 
     def initialize(self, device=None, **kwargs):
         super().initialize(device=device, **kwargs)
-        shape = self.input.shape
+        self._request_s2d_input()
+        shape = input_shape(self.input)
         if len(shape) == 3:
             shape = tuple(shape) + (1,)
         self.in_shape_ = shape
@@ -86,8 +103,50 @@ class Conv(Forward):
         return ops.conv_out_size(H, W, self.ky, self.kx, self.sliding,
                                  self.padding)
 
+    # units besides the forwards that read the loader's minibatch_data as
+    # an NHWC image: with any of them the s2d input layout stays off
+    _IMAGE_READERS = ("avatar", "data_saver", "image_saver",
+                      "immediate_plotter", "meandispnorm")
+
+    def _request_s2d_input(self):
+        """First layer, strided RGB conv (AlexNet conv1): ask the loader to
+        gather straight into this conv's space-to-depth layout, saving the
+        bf16 image's write + read and the separate s2d pass
+        (``root.common.engine.fuse_input_layout``, default on)."""
+        from veles_amd.utils.config import root, get
+        wf = self.workflow
+        ld = getattr(wf, "loader", None)
+        if getattr(self.input, "s2d_", None) is not None:
+            return
+        if ld is None or self.input is not ld.minibatch_data or \
+                not hasattr(ld, "request_s2d_input") or \
+                not get(root.common.engine.fuse_input_layout, True) or \
+                not getattr(self.device, "is_gpu", False) or \
+                getattr(self.device, "fp8", False) or \
+                any(getattr(wf, a, None) is not None
+                    for a in self._IMAGE_READERS):
+            return
+        shape = tuple(self.input.shape)
+        if len(shape) != 4:
+            return
+        s = ops.s2d_factor(shape[3], self.grouping, self.sliding, self.ky,
+                           self.kx)
+        if s and ld.request_s2d_input(s, self.ky, self.kx, self.padding):
+            self.info("input served in space-to-depth layout (s = %d) by "
+                      "the loader's fused gather", s)
+
     def run(self):
-        x = self.input.devmem
+        x = input_tensor(self.input)
+        if isinstance(x, ops.S2DImage):
+            B, H, W, C = x.shape
+            OH, OW = self.output_hw(H, W)
+            y = self.alloc_output((B, OH, OW, self.n_kernels))
+            ws = {}
+            ops.conv_fwd(x, self.weights_lp, self.bias_master, self.sliding,
+                         self.padding, self.grouping, self.activation, out=y,
+                         col_out=ws)
+            self.col_ = ws.get("col")
+            return
         if x.dim() == 3:
             x = x.unsqueeze(-1)
         B, H, W, C = x.shape

@@ -8,6 +8,7 @@ err_input = dgrad(err, W) [* f'(below.output)]  implicit transposed-conv GEMM
 """
 from __future__ import annotations
 
+from veles_amd.models.conv import input_tensor
 from veles_amd.models.nn_units import GradientDescentBase
 from veles_amd import ops
 from veles_amd.ops import fp8
@@ -36,11 +37,12 @@ class GradientDescentConv(GradientDescentBase):
         fwd = self.forward
         fwd.ensure_params()
         err = self.err_output_effective()
-        x = self.input.devmem
-        squeeze = x.dim() == 3
+        x = input_tensor(self.input)
+        s2d = isinstance(x, ops.S2DImage)   # loader-made s2d input
+        squeeze = not s2d and x.dim() == 3
         if squeeze:
             x = x.unsqueeze(-1)
-        if x.dtype != err.dtype:
+        if not s2d and x.dtype != err.dtype:
             x = x.to(err.dtype)
         pw, pb = fwd._pw_, fwd._pb_
         if self.store_.overwrite and not all(

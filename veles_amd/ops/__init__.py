@@ -538,13 +538,16 @@ def _pad_weights(w, key):
 
 
 class S2DImage(object):
-    """The space-to-depth image of a strided small-channel conv input,
-    kept by the forward pass for the weight-gradient GEMM."""
-    __slots__ = ("x", "s")
+    """The space-to-depth image of a strided small-channel conv input: kept
+    by the forward pass for the weight-gradient GEMM, or served directly by
+    the loader's fused gather (``fill_minibatch_s2d``) as the conv input.
+    ``shape`` is the NHWC shape of the image it stands for."""
+    __slots__ = ("x", "s", "shape")
 
-    def __init__(self, x, s):
+    def __init__(self, x, s, shape=None):
         self.x = x
         self.s = s
+        self.shape = tuple(shape) if shape is not None else None
 
 
 _S2D = os.environ.get("HVK_S2D", "1") != "0"   # A/B knob
@@ -566,6 +569,78 @@ def _s2d_geometry(H, W, KH, KW, s, padding):
     OH, OW = conv_out_size(H, W, KH, KW, (s, s), padding)
     KH2, KW2 = -(-KH // s), -(-KW // s)
     return OH, OW, KH2, KW2, OH - 1 + KH2, OW - 1 + KW2
+
+
+def s2d_geometry(shape, s, KH, KW, padding):
+    """(H2, W2, C2) of the space-to-depth image of an NHWC ``shape``."""
+    _, H, W, C = shape
+    _, _, _, _, H2, W2 = _s2d_geometry(H, W, KH, KW, s, padding)
+    return H2, W2, s * s * C
+
+
+def space_to_depth_ref(x, s, KH, KW, padding):
+    """Torch reference of hvk_space_to_depth: x [N,H,W,C] ->
+    [N,H2,W2,s*s*C], y[n,Y,X,dy,dx,c] = x[n, s*Y+dy-pt, s*X+dx-pl, c] (0
+    outside the image)."""
+    N, H, W, C = x.shape
+    _, _, _, _, H2, W2 = _s2d_geometry(H, W, KH, KW, s, padding)
+    pl, pt = padding[0], padding[1]
+    xp = F.pad(x.permute(0, 3, 1, 2), (pl, s * W2 - W - pl, pt,
+                                       s * H2 - H - pt))
+    xp = xp.permute(0, 2, 3, 1)   # [N, s*H2, s*W2, C]
+    return xp.reshape(N, H2, s, W2, s, C).permute(0, 1, 3, 2, 4, 5) \
+        .reshape(N, H2, W2, s * s * C).contiguous()
+
+
+def s2d_affine(vec, sample_shape, s, KH, KW, padding, fill):
+    """A per-feature vector over an [H,W,C] sample laid out in space-to-depth
+    order (``fill`` where the s2d image has no input pixel): the mean /
+    rdisp of ``fill_minibatch_s2d``."""
+    H, W, C = sample_shape
+    v = vec.reshape(1, H, W, C).float()
+    if fill:
+        v = v - fill
+    y = space_to_depth_ref(v, s, KH, KW, padding)
+    if fill:
+        y = y + fill
+    return y.reshape(-1).contiguous()
+
+
+def fill_minibatch_s2d(src, shuffled, start, count, dst, s, KH, KW, padding,
+                       mean2, rdisp2, labels=None, labels_out=None,
+                       idx_out=None):
+    """fill_minibatch fused with the first conv's space-to-depth transform:
+    dst [n,H2,W2,s*s*C] = s2d((src[shuffled[start+i]] - mean) * rdisp),
+    with ``mean2`` / ``rdisp2`` from ``s2d_affine``.  Same labels / indices
+    outputs as fill_minibatch."""
+    N, H, W, C = src.shape
+    max_mb = dst.shape[0]
+    H2, W2, C2 = s2d_geometry(src.shape, s, KH, KW, padding)
+    if _gpu(dst):
+        _lib_call("hvk_fill_minibatch_s2d", _p(src), src.numel(),
+                  _p(shuffled), int(start), int(count), max_mb, H, W, C, s,
+                  padding[1], padding[0], H2, W2, _p(mean2), _p(rdisp2),
+                  _p(dst), _p(labels), _p(labels_out), _p(idx_out), _s(dst))
+        return dst
+    idx = shuffled[start:start + count].long()
+    v = src.reshape(N, -1)[idx].float()
+    v = space_to_depth_ref(v.reshape(-1, H, W, C), s, KH, KW, padding)
+    v = (v.reshape(len(idx), -1) - mean2.reshape(1, -1)) * \
+        rdisp2.reshape(1, -1)
+    # no input pixel: 0 in the normalised image (the conv's zero padding)
+    inb = space_to_depth_ref(torch.ones(1, H, W, C), s, KH, KW,
+                             padding).reshape(1, -1)
+    v = v * inb
+    d = dst.view(max_mb, -1)
+    d[:count] = v.to(dst.dtype)
+    d[count:] = 0
+    if labels_out is not None:
+        labels_out[:count] = labels[idx] if labels is not None else -1
+        labels_out[count:] = -1
+    if idx_out is not None:
+        idx_out[:count] = idx.to(idx_out.dtype)
+        idx_out[count:] = -1
+    return dst
 
 
 def space_to_depth(x, s, KH, KW, padding):
@@ -622,6 +697,7 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
 
     ``col_out``: a dict that receives the im2col matrix when the explicit
     path is used (the weight-gradient GEMM reuses it)."""
+    pre = x if isinstance(x, S2DImage) else None   # loader-made s2d input
     N, H, W, C = x.shape
     OC, KH, KW, Cg = w.shape
     if Cg * groups != C or OC % groups:
@@ -631,6 +707,11 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
     pl, pt, pr, pb = padding
     OH, OW = conv_out_size(H, W, KH, KW, sliding, padding)
     act = act_code(act)
+    if pre is not None:
+        if pre.s != s2d_factor(C, groups, sliding, KH, KW):
+            raise ValueError("conv_fwd: s2d input of factor %d does not fit "
+                             "this conv" % pre.s)
+        x = pre.x
     if out is None:
         out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
     if _gpu(x):
@@ -638,14 +719,15 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
         if s2:
             # strided RGB conv as a stride-1 conv on the space-to-depth image
             _, _, KH2, KW2, H2, W2 = _s2d_geometry(H, W, KH, KW, s2, padding)
-            x2 = space_to_depth(x, s2, KH, KW, padding)
+            x2 = pre.x if pre is not None else \
+                space_to_depth(x, s2, KH, KW, padding)
             w2 = _s2d_weights(w, s2)
             C2 = s2 * s2 * C
             _lib_call("hvk_conv_fwd", _p(x2), _p(w2), _p(bias), _p(out), N,
                       H2, W2, C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, act,
                       _s(x))
             if col_out is not None:
-                col_out["col"] = S2DImage(x2, s2)
+                col_out["col"] = S2DImage(x2, s2, (N, H, W, C))
             return out
         if pad8_ok(C, groups):
             xp = _pad_channels(x)
@@ -740,7 +822,11 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     """dw (float32 [OC,KH,KW,C/g]) += sum over pixels of dy (x) im2col(x);
     ``dbias`` (float32 [OC]) += sum over pixels of dy, fused into the same
     GEMM.  ``col``: an explicit im2col matrix to use instead (optional)."""
-    N, H, W, C = x.shape
+    if isinstance(x, S2DImage):   # loader-made s2d input (conv_fwd)
+        col, x = x, x.x
+        N, H, W, C = col.shape
+    else:
+        N, H, W, C = x.shape
     _, OH, OW, OC = dy.shape
     _, KH, KW, Cg = dw.shape
     sx, sy = sliding
@@ -1567,12 +1653,13 @@ def seed_advance(seed_dev):
     return seed_dev
 
 
-def trace_marker(tag=0):
-    """Launch the empty marker kernel on the current stream (bench.py
-    --mark-steps: brackets the timed steps in a rocprofv3 kernel trace)."""
+def trace_marker(tag=0, stream=None):
+    """Launch the empty marker kernel on ``stream`` (default: the current
+    one; bench.py --mark-steps passes the workflow's compute stream) to
+    bracket the timed steps in a rocprofv3 kernel trace."""
     if torch.cuda.is_available():
-        _lib_call("hvk_trace_marker", int(tag),
-                  torch.cuda.current_stream().cuda_stream)
+        st = stream if stream is not None else torch.cuda.current_stream()
+        _lib_call("hvk_trace_marker", int(tag), st.cuda_stream)
 
 
 # --------------------------------------------------------------------- RNG

@@ -40,6 +40,8 @@ _SIGS = {
     "hvk_conv_wgrad_run": [P, P, P, P] + [I] * 14 + [P],
     "hvk_im2col": [P, P] + [I] * 13 + [P],
     "hvk_fill_minibatch": [P, I, P, I, I, I, L, P, P, P, I, P, P, P, P],
+    "hvk_fill_minibatch_s2d": [P, L, P, I, I, I, I, I, I, I, I, I, I, I, P,
+                               P, P, P, P, P, P],
     "hvk_mean_disp_normalize": [P, I, P, P, P, I, L, L, P],
     "hvk_softmax_ce": [P, I, I, I, P, F, P, I, P, P, P, P, P],
     "hvk_mse": [P, I, P, I, I, I, F, P, I, P, P, I, P],

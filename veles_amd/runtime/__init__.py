@@ -145,6 +145,10 @@ def _load():
         lib.vr_arena_bytes.argtypes = [P]
         lib.vr_arena_bytes.restype = L
         lib.vr_run.argtypes = [P, P, L, P, L]
+        lib.vr_set_engine.argtypes = [P, I]
+        lib.vr_enable_graph.argtypes = [P, I]
+        lib.vr_graph_active.argtypes = [P]
+        lib.vr_num_streams.argtypes = [P]
         lib.vr_optimize_memory.argtypes = [ctypes.POINTER(L), I,
                                            ctypes.POINTER(L)]
         lib.vr_optimize_memory.restype = L
@@ -191,6 +195,23 @@ class NativeWorkflow(object):
         nd = ctypes.c_int()
         _lib.vr_output_shape(self._h, out, ctypes.byref(nd))
         self.output_shape = tuple(out[i] for i in range(nd.value))
+
+    def set_engine(self, threads=0):
+        """threads > 0: run independent branches from a thread pool."""
+        _check(_lib.vr_set_engine(self._h, int(threads)))
+
+    def enable_graph(self, on=True):
+        """GPU: capture the inference pass into a hipGraph on the 2nd run
+        and replay it afterwards."""
+        _check(_lib.vr_enable_graph(self._h, 1 if on else 0))
+
+    @property
+    def graph_active(self):
+        return bool(_lib.vr_graph_active(self._h))
+
+    @property
+    def num_streams(self):
+        return _lib.vr_num_streams(self._h)
 
     @property
     def arena_bytes(self):
