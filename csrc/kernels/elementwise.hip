@@ -841,11 +841,31 @@ __global__ void space_to_depth_px_kernel(const uint16_t* __restrict__ x,
 // normalised bf16 s2d images [H2][W2][S][S][C] (the layout hvk_conv_fwd reads
 // for the stride-1 conv that replaces the strided one), so the bf16 NHWC
 // image is never written and re-read.  mean2 / rdisp2 are the per-feature
-// affine map already laid out in s2d order (0 / 1 where no input pixel is).
-// A thread owns one output pixel (S*S*C elements) of SPT samples: the
-// pixel's affine map is loaded once; each sample reads S runs of S*C
-// contiguous bytes (dword loads + v_alignbyte: the runs are not aligned)
-// and writes S*S*C/8 16-B chunks.
+// affine map already laid out in s2d order (0 / 1 where no input pixel is,
+// so such elements come out 0: the conv's zero padding).
+// A lane owns one 16-B output chunk (8 elements) of SPT samples, so each
+// wave stores 1 KiB contiguous: the chunk's affine map is loaded once; its 8
+// source bytes are one or two pieces of the S*C-byte input row runs, read
+// by aligned dword loads + v_alignbyte (the runs are not dword aligned).
+__device__ __forceinline__ uint64_t load_u8x8(const uint8_t* __restrict__ src,
+                                              long long off, int n,
+                                              long long src_bytes) {
+  // n <= 8 bytes at src + off, little-endian in the low bytes
+  const long long a = off & ~3ll;
+  if (a + 12 <= src_bytes) {
+    const uint32_t* w = (const uint32_t*)(src + a);
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+    const uint32_t sh = (uint32_t)(off & 3);
+    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+    return n >= 8 ? v : (v & ((1ull << (8 * n)) - 1));
+  }
+  uint64_t v = 0;
+  for (int b = 0; b < n; ++b) v |= (uint64_t)src[off + b] << (8 * b);
+  return v;
+}
+
 template <int S, int C, int SPT>
 __global__ void __launch_bounds__(256)
 fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
@@ -855,64 +875,67 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
                         const float* __restrict__ rdisp2,
                         uint16_t* __restrict__ dst, const int* labels,
                         int* labels_out, int* idx_out) {
-  constexpr int RUN = S * C, PIX = S * RUN, RW = (RUN + 3) / 4;
-  static_assert(PIX % 8 == 0, "16-B output chunks");
-  const int pixels = H2 * W2;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int RUN = S * C, PIX = S * RUN, CPP = PIX / 8;
+  static_assert(PIX % 8 == 0 && RUN >= 8, "16-B chunks, <= 2 row pieces");
+  const int chunks = H2 * W2 * CPP;
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   const int i0 = blockIdx.y * SPT;
   const long long sample = (long long)H * W * C;
-  if (q < pixels) {
+  if (ch < chunks) {
+    const int q = ch / CPP, j = ch - (ch / CPP) * CPP;
     const int Y = q / W2, X = q - (q / W2) * W2;
-    float mm[PIX], rr[PIX];
-#pragma unroll
-    for (int j = 0; j < PIX; j += 4) {
-      const float4 a = *(const float4*)(mean2 + (long long)q * PIX + j);
-      const float4 b = *(const float4*)(rdisp2 + (long long)q * PIX + j);
-      mm[j] = a.x; mm[j + 1] = a.y; mm[j + 2] = a.z; mm[j + 3] = a.w;
-      rr[j] = b.x; rr[j + 1] = b.y; rr[j + 2] = b.z; rr[j + 3] = b.w;
+    float mm[8], rr[8];
+    {
+      const float4* m4 = (const float4*)(mean2 + (long long)ch * 8);
+      const float4* r4 = (const float4*)(rdisp2 + (long long)ch * 8);
+      const float4 a = m4[0], b = m4[1], c = r4[0], d = r4[1];
+      mm[0] = a.x; mm[1] = a.y; mm[2] = a.z; mm[3] = a.w;
+      mm[4] = b.x; mm[5] = b.y; mm[6] = b.z; mm[7] = b.w;
+      rr[0] = c.x; rr[1] = c.y; rr[2] = c.z; rr[3] = c.w;
+      rr[4] = d.x; rr[5] = d.y; rr[6] = d.z; rr[7] = d.w;
     }
+    // the chunk's elements 8j .. 8j+7: piece 0 in row dy0 from r0 (n0
+    // bytes), piece 1 (if any) at the start of row dy0 + 1
+    const int e0 = 8 * j, dy0 = e0 / RUN, r0 = e0 - dy0 * RUN;
+    const int n0 = RUN - r0 < 8 ? RUN - r0 : 8;
     const int ix0 = S * X - pl;
     const bool xin = ix0 >= 0 && ix0 + S <= W;
+    const int iy0 = S * Y + dy0 - pt, iy1 = iy0 + 1;
+    const bool y0in = iy0 >= 0 && iy0 < H, y1in = iy1 >= 0 && iy1 < H;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int i = i0 + u;
       if (i >= max_mb) break;
       const int sid = i < count ? shuffled[start + i] : -1;
-      uint8_t v[PIX];
-#pragma unroll
-      for (int dy = 0; dy < S; ++dy) {
-        const int iy = S * Y + dy - pt;
-        const bool in = sid >= 0 && iy >= 0 && iy < H;
-        const long long o = (long long)sid * sample +
-                            ((long long)(in ? iy : 0) * W + ix0) * C;
-        if (in && xin && (o & ~3ll) + 4 * (RW + 1) <= src_bytes) {
-          const uint32_t* w = (const uint32_t*)(src + (o & ~3ll));
-          const uint32_t sh = (uint32_t)(o & 3);
-          uint32_t d[RW + 1], r[RW];
-#pragma unroll
-          for (int k = 0; k <= RW; ++k) d[k] = w[k];
-#pragma unroll
-          for (int k = 0; k < RW; ++k)
-            r[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
-          __builtin_memcpy(&v[dy * RUN], r, RUN);
+      uint4 o = make_uint4(0, 0, 0, 0);
+      if (sid >= 0) {
+        const long long base = (long long)sid * sample;
+        uint64_t v = 0;
+        if (xin) {
+          if (y0in)
+            v = load_u8x8(src, base + ((long long)iy0 * W + ix0) * C + r0, n0,
+                          src_bytes);
+          if (n0 < 8 && y1in)
+            v |= load_u8x8(src, base + ((long long)iy1 * W + ix0) * C,
+                           8 - n0, src_bytes) << (8 * n0);
         } else {
+          // image border: per element, zero outside the image
 #pragma unroll
-          for (int e = 0; e < RUN; ++e) {
-            const int ix = ix0 + e / C;
-            v[dy * RUN + e] = (in && ix >= 0 && ix < W)
-                                  ? src[(long long)sid * sample +
-                                        ((long long)iy * W + ix) * C + e % C]
-                                  : (uint8_t)0;
+          for (int e = 0; e < 8; ++e) {
+            const int ee = e0 + e, dy = ee / RUN, rr2 = ee - dy * RUN;
+            const int iy = S * Y + dy - pt, ix = ix0 + rr2 / C;
+            if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+              v |= (uint64_t)src[base + ((long long)iy * W + ix) * C +
+                                 rr2 % C] << (8 * e);
           }
         }
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          f[e] = ((float)((v >> (8 * e)) & 0xFF) - mm[e]) * rr[e];
+        o = pack_bf16x8(f);
       }
-      uint16_t o16[PIX];
-#pragma unroll
-      for (int e = 0; e < PIX; ++e)
-        o16[e] = f2bf(((float)v[e] - mm[e]) * rr[e]);
-      uint4* out = (uint4*)(dst + ((long long)i * pixels + q) * PIX);
-#pragma unroll
-      for (int j = 0; j < PIX / 8; ++j) out[j] = ((const uint4*)o16)[j];
+      *(uint4*)(dst + (long long)i * chunks * 8 + (long long)ch * 8) = o;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x < SPT) {
@@ -937,9 +960,9 @@ HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
       ((uintptr_t)rdisp2 & 15) || max_mb > 65535 * 4)
     return -1;
   constexpr int SPT = 4;
-  const int pixels = H2 * W2;
+  const int chunks = H2 * W2 * (4 * 4 * 3 / 8);
   hipLaunchKernelGGL((fill_s2d_u8_bf16_kernel<4, 3, SPT>),
-                     dim3((pixels + 255) / 256, (max_mb + SPT - 1) / SPT),
+                     dim3((chunks + 255) / 256, (max_mb + SPT - 1) / SPT),
                      dim3(256), 0, s, (const uint8_t*)src, src_bytes, shuffled,
                      start, count, max_mb, H, W, pt, pl, H2, W2, mean2, rdisp2,
                      (uint16_t*)dst, labels, labels_out, idx_out);

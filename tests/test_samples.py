@@ -30,7 +30,7 @@ def test_sample_trains_one_epoch_cpu(name):
 
 @pytest.mark.parametrize("name", ["alexnet", "vgg16"])
 def test_big_sample_loads_cpu(name):
-    cli("samples/%s.py" % name, "-", "-a", "cpu", "--dry-run", "load")
+    cli("samples/%s.py" % name, "-", "-a", "cpu", "--dry-run", "init")
 
 
 def test_cli_html_help_and_plot_switches():

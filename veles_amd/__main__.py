@@ -53,6 +53,28 @@ def _html_help(parser):
                                 "".join(rows)))
 
 
+def daemonize(log_path=None):
+    """``-b/--background`` (reference __main__.py:372-378): detach from the
+    terminal by a double fork + setsid, BEFORE anything touches the GPU
+    (a process that initialised HIP must never fork).  Returns True in the
+    detached grandchild (which continues the run, stdio on ``log_path`` or
+    /dev/null) and False in the original process (which should exit 0)."""
+    if os.fork() > 0:
+        return False
+    os.setsid()
+    if os.fork() > 0:
+        os._exit(0)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    fd_in = os.open(os.devnull, os.O_RDONLY)
+    fd_out = os.open(log_path, os.O_WRONLY | os.O_CREAT | os.O_APPEND,
+                     0o644) if log_path else os.open(os.devnull, os.O_WRONLY)
+    os.dup2(fd_in, 0)
+    os.dup2(fd_out, 1)
+    os.dup2(fd_out, 2)
+    return True
+
+
 class Main(object):
     def __init__(self, argv=None):
         self.argv = sys.argv[1:] if argv is None else list(argv)
@@ -142,8 +164,14 @@ class Main(object):
         return wf, restored
 
     def _main(self, **kwargs):
+        """The second half of the run(load, main) contract.  ``--dry-run``
+        (reference cmdline.py:172-177, __main__.py:628-656): ``init`` stops
+        before the workflow is initialised, ``exec`` before it runs;
+        ``--visualize`` initialises, writes the workflow graph and renders
+        every plotter once instead of running."""
         args = self.args
-        if args.dry_run == "load":
+        if args.dry_run in ("load", "init"):
+            self.stopped_before = "initialize"
             return
         if args.job_timeout > 0:
             from veles_amd.utils.config import root
@@ -154,7 +182,19 @@ class Main(object):
         self.workflow.initialize(**kwargs)
         if args.workflow_graph:
             self.workflow.generate_graph(args.workflow_graph)
-        if args.dry_run == "init":
+        if args.manhole:
+            from veles_amd.interaction import install_manhole
+            self.manhole_path = install_manhole(self.workflow)
+            logging.getLogger("Main").info(
+                "manhole: kill -USR2 %d, then nc -U %s", os.getpid(),
+                self.manhole_path)
+        if args.dump_unit_attributes != "no":
+            self._dump_unit_attributes(args.dump_unit_attributes == "all")
+        if args.dry_run == "exec":
+            self.stopped_before = "run"
+            return
+        if args.visualize:
+            self.visualized = self._visualize()
             return
         if args.fault_inject_prob > 0:
             from veles_amd.parallel.faults import FaultInjector
@@ -167,10 +207,59 @@ class Main(object):
         if wd is not None:
             wd.stop()
         self.launcher.finish()
-        if args.dump_unit_attributes != "no":
-            for u in self.workflow:
-                print(u.name, {k: v for k, v in u.__dict__.items()
-                               if not k.startswith("_")})
+        if args.pdb_on_finish:
+            self._pdb_on_finish()
+
+    def _dump_unit_attributes(self, arrays):
+        """``--dump-unit-attributes pretty|all`` after initialisation
+        (reference __main__.py:665-685)."""
+        for u in self.workflow:
+            attrs = {}
+            for k, v in sorted(u.__dict__.items()):
+                if k.startswith("_"):
+                    continue
+                if not arrays and hasattr(v, "__len__") and \
+                        not isinstance(v, (str, bytes)):
+                    try:
+                        n = len(v)
+                    except Exception:  # noqa: BLE001
+                        n = 0
+                    if n > 32:
+                        v = "<%s of length %d>" % (type(v).__name__, n)
+                attrs[k] = v
+            print(u.name, attrs)
+
+    def _visualize(self):
+        """``--visualize``: the workflow graph (DOT) and one rendering of
+        every plotter unit, without running the model; returns the files."""
+        from veles_amd.plotter import Plotter
+        files = []
+        dot = self.args.workflow_graph or "%s.dot" % self.workflow.name
+        self.workflow.generate_graph(dot, with_data_links=True)
+        files.append(dot)
+        for u in self.workflow:
+            if isinstance(u, Plotter) and not u.disabled:
+                try:
+                    u.collect()
+                    u.render()
+                    files.extend(u.files)
+                except Exception as e:  # noqa: BLE001 - nothing to draw yet
+                    logging.getLogger("Main").warning(
+                        "--visualize: %s not rendered (%s)", u.name, e)
+        for f in files:
+            print("visualize:", f)
+        return files
+
+    def _pdb_on_finish(self):
+        """``--pdb-on-finish`` (reference launcher.py:688-690): a debugger
+        prompt with the finished workflow in scope (only on a terminal)."""
+        if not sys.stdin.isatty():
+            logging.getLogger("Main").warning(
+                "--pdb-on-finish: stdin is not a terminal, no debugger")
+            return
+        import pdb
+        workflow = self.workflow  # noqa: F841 - in the debugger's scope
+        pdb.set_trace()
 
     def run(self):
         from veles_amd import __version__
@@ -178,6 +267,9 @@ class Main(object):
         from veles_amd.utils.config import root
         args = make_parser().parse_intermixed_args(self.argv)
         self.args = args
+        self.stopped_before = None
+        if args.background and not daemonize(args.log_file or None):
+            return 0   # the original process; the daemon carries on
         if args.version:
             print("veles_amd", __version__)
             return 0
@@ -197,6 +289,9 @@ class Main(object):
         if not args.workflow:
             make_parser().print_help()
             return 1
+        if args.debug_pickle:
+            from veles_amd.utils.pickle2 import setup_pickle_debug
+            setup_pickle_debug()
         self._seed(args.random_seed)
         root.common.engine.backend = "cpu" if args.backend == "numpy" \
             else args.backend
@@ -221,6 +316,10 @@ class Main(object):
         if args.ensemble_train or args.ensemble_test:
             from veles_amd.ensemble.manager import run_ensemble
             return run_ensemble(self, module, args)
+        if args.dry_run == "load":
+            # stop before the workflow is created (module and config only)
+            self.stopped_before = "load"
+            return 0
         from veles_amd.genetics.config import fix_config
         fix_config(root)
         module.run(self._load, self._main)

@@ -32,15 +32,21 @@ def make_parser():
                    choices=["debug", "info", "warning", "error"])
     p.add_argument("--debug", default="",
                    help="comma-separated class names logged at DEBUG")
-    p.add_argument("--debug-pickle", action="store_true")
+    p.add_argument("--debug-pickle", action="store_true",
+                   help="name the attribute that fails to (un)pickle; on a "
+                        "terminal, open the post-mortem debugger there")
     p.add_argument("-r", "--random-seed", default="",
                    help="seed[,seed...] | file:count[:dtype] | -")
     p.add_argument("-w", "--snapshot", default="",
                    help="resume from a snapshot file")
     p.add_argument("--dump-config", action="store_true")
     p.add_argument("--dry-run", default="no",
-                   choices=["load", "init", "exec", "no"])
-    p.add_argument("--visualize", action="store_true")
+                   choices=["load", "init", "exec", "no"],
+                   help="load: stop before creating the workflow; init: "
+                        "before initialising it; exec: before running it")
+    p.add_argument("--visualize", action="store_true",
+                   help="initialise, then write the workflow graph and "
+                        "render every plotter once instead of running")
     p.add_argument("--workflow-graph", default="")
     p.add_argument("--dump-unit-attributes", default="no",
                    choices=["no", "pretty", "all"])
@@ -48,7 +54,9 @@ def make_parser():
                    help="N[:G] genetic hyper-parameter search")
     p.add_argument("--ensemble-train", default="", help="N:ratio")
     p.add_argument("--ensemble-test", default="", help="ensemble file")
-    p.add_argument("-b", "--background", action="store_true")
+    p.add_argument("-b", "--background", action="store_true",
+                   help="run detached as a daemon (forks before any GPU "
+                        "call; output to --log-file)")
     p.add_argument("-t", "--test", action="store_true",
                    help="test (inference) mode")
     p.add_argument("-p", "--matplotlib-backend", default=None,
@@ -57,7 +65,8 @@ def make_parser():
                    help="disable every plotter")
     p.add_argument("--html-help", action="store_true",
                    help="print this help as an HTML page and exit")
-    p.add_argument("--pdb-on-finish", action="store_true")
+    p.add_argument("--pdb-on-finish", action="store_true",
+                   help="open pdb with the finished workflow in scope")
     p.add_argument("-s", "--stealth", action="store_true")
     p.add_argument("-f", "--log-file", default="")
     p.add_argument("--log-file-pid", action="store_true")
@@ -92,7 +101,9 @@ def make_parser():
     p.add_argument("--trace-events", default="",
                    help="write a Chrome-trace JSON of unit events here")
     p.add_argument("--train-ratio", type=float, default=1.0)
-    p.add_argument("--manhole", action="store_true")
+    p.add_argument("--manhole", action="store_true",
+                   help="on SIGUSR2 serve a Python console into the "
+                        "workflow on /tmp/veles_amd_manhole_<pid>.sock")
     for cls in CommandLineArgumentsRegistry.classes:
         try:
             cls.init_parser(p)

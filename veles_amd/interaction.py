@@ -12,6 +12,7 @@ inspected with ``nc -U``.
 from __future__ import annotations
 
 import code
+import contextlib
 import os
 import signal
 import socket
@@ -20,7 +21,55 @@ import threading
 from veles_amd.units import Unit
 from veles_amd.utils.config import get, root
 
-__all__ = ["Shell"]
+__all__ = ["Shell", "serve_console", "install_manhole"]
+
+
+def serve_console(path, namespace):
+    """Serve ONE Python console client on the UNIX socket ``path``."""
+    try:
+        os.remove(path)
+    except OSError:
+        pass
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind(path)
+    srv.listen(1)
+    try:
+        conn, _ = srv.accept()
+        f = conn.makefile("rw")
+        console = code.InteractiveConsole(namespace)
+        console.write = lambda data: (f.write(data), f.flush())
+        f.write(">>> ")
+        f.flush()
+        for line in f:
+            # the client sees what the statement prints (stdout of the
+            # process while it runs: this is a debugging console)
+            with contextlib.redirect_stdout(f):
+                more = console.push(line.rstrip("\n"))
+            f.write("... " if more else ">>> ")
+            f.flush()
+        conn.close()
+    finally:
+        srv.close()
+        try:
+            os.remove(path)
+        except OSError:
+            pass
+
+
+def install_manhole(workflow, path=None):
+    """``--manhole`` (reference thread_pool.py:139-142): on SIGUSR2 the
+    process starts serving a console into ``workflow`` on a UNIX socket
+    (``/tmp/veles_amd_manhole_<pid>.sock`` by default; ``nc -U`` it).
+    Returns the socket path."""
+    path = path or "/tmp/veles_amd_manhole_%d.sock" % os.getpid()
+
+    def handler(signum, frame):
+        ns = {"workflow": workflow, "root": root,
+              "units": {u.name: u for u in workflow}}
+        threading.Thread(target=serve_console, args=(path, ns),
+                         daemon=True, name="manhole").start()
+    signal.signal(signal.SIGUSR2, handler)
+    return path
 
 
 class Shell(Unit):
@@ -55,22 +104,4 @@ class Shell(Unit):
                           local=self.namespace())
 
     def serve_socket(self):
-        path = self.socket_path
-        try:
-            os.remove(path)
-        except OSError:
-            pass
-        srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
-        srv.bind(path)
-        srv.listen(1)
-        conn, _ = srv.accept()
-        f = conn.makefile("rw")
-        console = code.InteractiveConsole(self.namespace())
-        f.write(">>> ")
-        f.flush()
-        for line in f:
-            more = console.push(line.rstrip("\n"))
-            f.write("... " if more else ">>> ")
-            f.flush()
-        conn.close()
-        srv.close()
+        serve_console(self.socket_path, self.namespace())
