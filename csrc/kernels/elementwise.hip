@@ -969,6 +969,140 @@ HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Image minibatch with augmentation (the image loaders' device path): output
+// sample b is built from the uint8 canvas src[idx[b]] ([Hs][Ws][C], NHWC):
+//   crop   a Ho x Wo window at (cy, cx) of the canvas,
+//   mirror it horizontally (mirror != 0),
+//   rotate it by theta about its centre (cv2.getRotationMatrix2D semantics:
+//          the source of output pixel p is c + R(-theta) (p - c), sampled
+//          bilinearly; taps outside the crop window read the background -
+//          bg image [Ho][Wo][C] or the per-channel bgcolor),
+//   sobel  optionally append the gradient magnitude of the grey image
+//          (3x3 Sobel on the final geometry, edges replicated),
+//   normalise (v - mean[f]) * rdisp[f] per output feature f (or 0 / 1),
+// written as bf16 [B][Ho][Wo][C + sobel].  params[b] = {cy, cx, cos, sin,
+// mirror, -}; idx[b] < 0 writes a zero sample.  Replaces the reference's
+// per-image cv2 crop / flip / warpAffine / Sobel on the host
+// (veles/loader/image.py:458-551); the random parameters come from the
+// loader's PRNG on the host, so no device->host sync is needed.
+struct ImgGeom {
+  int Hs, Ws, C, Ho, Wo, Co;
+  long long src_stride;  // bytes per canvas
+};
+
+__device__ __forceinline__ void img_sample(const uint8_t* __restrict__ can,
+                                           const ImgGeom& g, const float* pr,
+                                           const uint8_t* __restrict__ bg,
+                                           const float* __restrict__ bgcolor,
+                                           int oy, int ox, float* v) {
+  const int cy = (int)pr[0], cx = (int)pr[1];
+  const float ct = pr[2], st = pr[3];
+  const bool mir = pr[4] != 0.f;
+  // centre as cv2 uses it: (W // 2, H // 2)
+  const float ccx = (float)(g.Wo / 2), ccy = (float)(g.Ho / 2);
+  const float dx = (float)ox - ccx, dy = (float)oy - ccy;
+  float sx = ccx + ct * dx - st * dy;
+  float sy = ccy + st * dx + ct * dy;
+  if (mir) sx = (float)(g.Wo - 1) - sx;
+  const float fx = floorf(sx), fy = floorf(sy);
+  const int x0 = (int)fx, y0 = (int)fy;
+  const float ax = sx - fx, ay = sy - fy;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int yy = y0 + (t >> 1), xx = x0 + (t & 1);
+    const float w = ((t >> 1) ? ay : 1.f - ay) * ((t & 1) ? ax : 1.f - ax);
+    if (w == 0.f) continue;
+    const bool in = yy >= 0 && yy < g.Ho && xx >= 0 && xx < g.Wo &&
+                    cy + yy < g.Hs && cx + xx < g.Ws;
+    for (int c = 0; c < g.C; ++c) {
+      float s;
+      if (in) {
+        s = (float)can[((long long)(cy + yy) * g.Ws + (cx + xx)) * g.C + c];
+      } else if (bg) {
+        const int by = min(max(yy, 0), g.Ho - 1), bx = min(max(xx, 0), g.Wo - 1);
+        s = (float)bg[((long long)by * g.Wo + bx) * g.C + c];
+      } else {
+        s = bgcolor ? bgcolor[c] : 0.f;
+      }
+      v[c] += w * s;
+    }
+  }
+}
+
+__device__ __forceinline__ float img_gray(const float* v, int C) {
+  return C >= 3 ? 0.299f * v[0] + 0.587f * v[1] + 0.114f * v[2] : v[0];
+}
+
+__global__ void __launch_bounds__(256)
+image_batch_kernel(const uint8_t* __restrict__ src, ImgGeom g,
+                   const int* __restrict__ idx, const float* __restrict__ params,
+                   int B, int sobel, const float* __restrict__ mean,
+                   const float* __restrict__ rdisp,
+                   const uint8_t* __restrict__ bg,
+                   const float* __restrict__ bgcolor,
+                   uint16_t* __restrict__ out) {
+  const long long pix = (long long)g.Ho * g.Wo;
+  const long long total = (long long)B * pix;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+       e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(e / pix);
+    const int q = (int)(e - (long long)b * pix);
+    const int oy = q / g.Wo, ox = q - (q / g.Wo) * g.Wo;
+    uint16_t* o = out + e * g.Co;
+    const int s = idx[b];
+    if (s < 0) {
+      for (int c = 0; c < g.Co; ++c) o[c] = 0;
+      continue;
+    }
+    const uint8_t* can = src + (long long)s * g.src_stride;
+    const float* pr = params + 6 * b;
+    float v[4];
+    img_sample(can, g, pr, bg, bgcolor, oy, ox, v);
+    float sob = 0.f;
+    if (sobel) {
+      float gr[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = min(max(oy + t / 3 - 1, 0), g.Ho - 1);
+        const int xx = min(max(ox + t % 3 - 1, 0), g.Wo - 1);
+        float w[4];
+        img_sample(can, g, pr, bg, bgcolor, yy, xx, w);
+        gr[t] = img_gray(w, g.C);
+      }
+      const float gx = (gr[2] + 2.f * gr[5] + gr[8]) - (gr[0] + 2.f * gr[3] + gr[6]);
+      const float gy = (gr[6] + 2.f * gr[7] + gr[8]) - (gr[0] + 2.f * gr[1] + gr[2]);
+      sob = sqrtf(gx * gx + gy * gy);
+    }
+    const long long f0 = (long long)q * g.Co;
+    for (int c = 0; c < g.Co; ++c) {
+      float x = c < g.C ? v[c] : sob;
+      if (mean) x -= mean[f0 + c];
+      if (rdisp) x *= rdisp[f0 + c];
+      o[c] = f2bf(x);
+    }
+  }
+}
+
+HVK_API int hvk_image_batch(const void* src, long long src_stride, int Hs,
+                            int Ws, int C, const int* idx, const float* params,
+                            int B, int Ho, int Wo, int sobel,
+                            const float* mean, const float* rdisp,
+                            const void* bg, const float* bgcolor, void* out,
+                            hipStream_t s) {
+  if (C < 1 || C > 4 || Ho > Hs || Wo > Ws) return -1;
+  ImgGeom g;
+  g.Hs = Hs; g.Ws = Ws; g.C = C; g.Ho = Ho; g.Wo = Wo; g.Co = C + (sobel ? 1 : 0);
+  g.src_stride = src_stride;
+  const long long total = (long long)B * Ho * Wo;
+  hipLaunchKernelGGL(image_batch_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     s, (const uint8_t*)src, g, idx, params, B, sobel, mean,
+                     rdisp, (const uint8_t*)bg, bgcolor, (uint16_t*)out);
+  return (int)hipGetLastError();
+}
+
 HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                                int start, int count, int max_mb,
                                long long sample_size, const float* mean,

@@ -130,6 +130,11 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
         super().init_unpickled()
         self.pending_minibatches_ = defaultdict(list)
         self._minibatch_serve_timestamp_ = time.time()
+        # sample order before the first shuffle (None: 0..n-1); a validation
+        # split extracted by index (loader/labels.py) rearranges it
+        self.initial_order_ = None
+        self.label_stats = {}
+        self.label_distribution_p = {}
 
     # -- properties ---------------------------------------------------------
     @property
@@ -192,6 +197,8 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
         self.max_minibatch_size = int(kwargs.get("minibatch_size",
                                                  self.max_minibatch_size))
         self._calc_class_end_offsets()
+        if not self.restored_from_snapshot or self.testing:
+            self.setup_label_stats()
         self.info("Samples number: test: %d, validation: %d, train: %d%s",
                   *(self.class_lengths + [
                       "" if self.train_ratio == 1.0 else
@@ -223,6 +230,65 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
     def on_initialized(self, **kwargs):
         """Hook: allocate device buffers after the host state is ready."""
 
+    def initial_order(self):
+        """Sample order before the first shuffle (int array over all
+        samples): the validation split's arrangement or 0..n-1."""
+        if self.initial_order_ is not None and \
+                len(self.initial_order_) == self.total_samples:
+            return numpy.asarray(self.initial_order_, self.INDEX_DTYPE)
+        return numpy.arange(self.total_samples, dtype=self.INDEX_DTYPE)
+
+    def class_labels(self):
+        """[TEST, VALID, TRAIN] lists of the raw labels of the samples of
+        each class, or None when the loader has no per-sample labels to
+        analyse (override)."""
+        return None
+
+    def setup_label_stats(self):
+        """Label mapping, per-class cardinality statistics and the
+        distribution check (loader/labels.py)."""
+        if not self.has_labels:
+            return
+        per = self.class_labels()
+        if per is None:
+            return
+        from veles_amd.loader.labels import label_counts, \
+            setup_labels_mapping
+        setup_labels_mapping(self, [label_counts(c) for c in per],
+                             build=self.BUILDS_LABELS_MAPPING)
+
+    # loaders whose labels are raw values (strings, file-derived) get the
+    # mapping built from the TRAIN labels; index labels keep theirs
+    BUILDS_LABELS_MAPPING = False
+
+    def split_validation(self, labels=None):
+        """Move ``validation_ratio`` of the pooled VALID + TRAIN samples
+        into VALID by index (stratified per label when ``labels`` - one per
+        pooled sample, in sample order - are given; reference
+        fullbatch.py:349-433).  ratio <= 0 merges VALID into TRAIN."""
+        from veles_amd.loader.labels import random_split, stratified_split
+        ratio = getattr(self, "validation_ratio", None)
+        if ratio is None:
+            return
+        if ratio <= 0:
+            self.class_lengths[TRAIN] += self.class_lengths[VALID]
+            self.class_lengths[VALID] = 0
+            return
+        if ratio >= 1:
+            raise ValueError("validation_ratio must be < 1")
+        lo = self.class_lengths[TEST]
+        n = self.class_lengths[VALID] + self.class_lengths[TRAIN]
+        if labels is not None:
+            v, t = stratified_split(labels, ratio, self.prng)
+        else:
+            v, t = random_split(n, ratio, self.prng)
+        order = numpy.arange(lo + n, dtype=self.INDEX_DTYPE)
+        order[lo:] = lo + numpy.concatenate(
+            [numpy.asarray(v, numpy.int64), numpy.asarray(t, numpy.int64)])
+        self.class_lengths[VALID] = len(v)
+        self.class_lengths[TRAIN] = len(t)
+        self.initial_order_ = order
+
     def apply_derived_normalization(self):
         """Hook: a loader without TRAIN data that shares an analysed
         normalizer (``derive_from``) prepares to apply it."""
@@ -235,8 +301,7 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
     # -- serving ------------------------------------------------------------
     def shuffle(self):
         if not self.shuffled_indices:
-            self.shuffled_indices.reset(numpy.arange(self.total_samples,
-                                                     dtype=self.INDEX_DTYPE))
+            self.shuffled_indices.reset(self.initial_order())
         if self.shuffle_limit <= 0 or self.class_lengths[TRAIN] == 0:
             return
         self.shuffle_limit -= 1
@@ -316,8 +381,7 @@ class Loader(Unit, ILoader, metaclass=UserLoaderRegistry):
 
     def analyze_train_data(self):
         if self.shuffled_indices.mem is None:
-            self.shuffled_indices.reset(numpy.arange(self.total_samples,
-                                                     dtype=self.INDEX_DTYPE))
+            self.shuffled_indices.reset(self.initial_order())
         start = self.class_end_offsets[VALID]
         end = self.class_end_offsets[TRAIN]
         step = self.local_minibatch_size
@@ -481,10 +545,12 @@ class LoaderWithValidationRatio(Loader):
         self.validation_ratio = kwargs.get("validation_ratio", None)
 
     def load_data(self):
+        """Subclasses fill class_lengths first, then call this: the
+        validation set is drawn from the pooled VALID + TRAIN samples by
+        index (``split_validation``; stratified when the subclass passes
+        its labels)."""
         if self.validation_ratio is None:
             return
-        if not 0 <= self.validation_ratio < 1:
-            raise ValueError("validation_ratio must be in [0, 1)")
-        n = int(self.class_lengths[TRAIN] * self.validation_ratio)
-        self.class_lengths[VALID] += n
-        self.class_lengths[TRAIN] -= n
+        if not self.validation_ratio < 1:
+            raise ValueError("validation_ratio must be < 1")
+        self.split_validation()

@@ -135,11 +135,36 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         return True
 
     def _apply_validation_ratio(self):
-        if not self.validation_ratio:
+        """``validation_ratio``: VALID = a label-stratified draw from the
+        pooled VALID + TRAIN samples, by index (Loader.split_validation)."""
+        if self.validation_ratio is None:
             return
-        n = int(self.class_lengths[TRAIN] * self.validation_ratio)
-        self.class_lengths[VALID] += n
-        self.class_lengths[TRAIN] -= n
+        labels = None
+        if self.has_labels:
+            lo = self.class_lengths[TEST]
+            labels = numpy.asarray(self.original_labels)[lo:]
+        self.split_validation(labels)
+
+    def class_labels(self):
+        """Per class, the labels of its samples: the raw values of the
+        mapping (``reversed_labels_mapping``) when there is one, else the
+        index labels themselves."""
+        lab = numpy.asarray(self.original_labels)
+        order = self.initial_order()
+        rev = list(self.reversed_labels_mapping or [])
+        out, start = [], 0
+        for n in self.class_lengths:
+            v = lab[order[start:start + n]].tolist()
+            if rev:
+                v = [rev[i] if 0 <= i < len(rev) else i for i in v]
+            out.append(v)
+            start += n
+        return out
+
+    def class_rows(self, cls):
+        """Sample rows of class ``cls`` in the initial order."""
+        start = sum(self.class_lengths[:cls])
+        return self.initial_order()[start:start + self.class_lengths[cls]]
 
     def analyze_dataset(self):
         """Analyse the TRAIN slice on the host, then either keep a
@@ -150,13 +175,13 @@ class FullBatchLoader(Loader, IFullBatchLoader):
             self._affine = None
             return
         data = self.original_data.mem
-        train = data[self.class_end_offsets[VALID]:
-                     self.class_end_offsets[TRAIN]]
+        rows = numpy.sort(self.class_rows(TRAIN))
         step = 4096
-        for i in range(0, len(train), step):
-            self.normalizer.analyze(train[i:i + step].astype(numpy.float32))
+        for i in range(0, len(rows), step):
+            self.normalizer.analyze(
+                data[rows[i:i + step]].astype(numpy.float32))
         if not self.normalizer.is_initialized:
-            self.normalizer.analyze(train[:1].astype(numpy.float32))
+            self.normalizer.analyze(data[rows[:1]].astype(numpy.float32))
         aff = self.normalizer.affine()
         if aff is not None:
             mean, rdisp = aff

@@ -1755,6 +1755,90 @@ def fill_minibatch(src, shuffled, start, count, dst, *, mean=None,
     return dst
 
 
+def image_batch_ref(src, idx, params, Ho, Wo, sobel=False, mean=None,
+                    rdisp=None, bg=None, bgcolor=None):
+    """Torch (f32) reference of hvk_image_batch: crop (cy, cx) -> mirror ->
+    rotate (bilinear, cv2 centre and angle convention) -> optional Sobel
+    magnitude channel -> (v - mean) * rdisp.  src uint8 [N][Hs][Ws][C];
+    params [B][6] = (cy, cx, cos, sin, mirror, -)."""
+    N, Hs, Ws, C = src.shape
+    B = idx.shape[0]
+    dev = src.device
+    p = params.float()
+    oy = torch.arange(Ho, device=dev, dtype=torch.float32).view(1, Ho, 1)
+    ox = torch.arange(Wo, device=dev, dtype=torch.float32).view(1, 1, Wo)
+
+    def sample(yy, xx):
+        cy, cx = p[:, 0].view(B, 1, 1), p[:, 1].view(B, 1, 1)
+        ct, st = p[:, 2].view(B, 1, 1), p[:, 3].view(B, 1, 1)
+        mir = (p[:, 4] != 0).view(B, 1, 1)
+        ccx, ccy = float(Wo // 2), float(Ho // 2)
+        dx, dy = xx - ccx, yy - ccy
+        sx = ccx + ct * dx - st * dy
+        sy = ccy + st * dx + ct * dy
+        sx = torch.where(mir, (Wo - 1) - sx, sx)
+        x0, y0 = torch.floor(sx), torch.floor(sy)
+        axx, ayy = sx - x0, sy - y0
+        v = torch.zeros(B, Ho, Wo, C, device=dev)
+        can = src[idx.clamp_min(0).long()].float()   # [B,Hs,Ws,C]
+        for t in range(4):
+            ty, tx = t >> 1, t & 1
+            w = (ayy if ty else 1 - ayy) * (axx if tx else 1 - axx)
+            yi, xi = (y0 + ty).long(), (x0 + tx).long()
+            inb = (yi >= 0) & (yi < Ho) & (xi >= 0) & (xi < Wo) & \
+                (cy.long() + yi < Hs) & (cx.long() + xi < Ws)
+            gy = (cy.long() + yi).clamp(0, Hs - 1)
+            gx = (cx.long() + xi).clamp(0, Ws - 1)
+            bi = torch.arange(B, device=dev).view(B, 1, 1).expand_as(gy)
+            val = can[bi, gy, gx]                      # [B,Ho,Wo,C]
+            if bg is not None:
+                bgv = bg.float()[yi.clamp(0, Ho - 1), xi.clamp(0, Wo - 1)]
+            elif bgcolor is not None:
+                bgv = bgcolor.float().view(1, 1, 1, C).expand_as(val)
+            else:
+                bgv = torch.zeros_like(val)
+            val = torch.where(inb.unsqueeze(-1), val, bgv)
+            v = v + w.unsqueeze(-1) * val
+        return v
+
+    yy = oy.expand(B, Ho, Wo)
+    xx = ox.expand(B, Ho, Wo)
+    v = sample(yy, xx)
+    if sobel:
+        def gray(a):
+            return (0.299 * a[..., 0] + 0.587 * a[..., 1] + 0.114 * a[..., 2]
+                    if C >= 3 else a[..., 0])
+        g = {}
+        for t in range(9):
+            ry = (yy + (t // 3 - 1)).clamp(0, Ho - 1)
+            rx = (xx + (t % 3 - 1)).clamp(0, Wo - 1)
+            g[t] = gray(sample(ry, rx))
+        gx = (g[2] + 2 * g[5] + g[8]) - (g[0] + 2 * g[3] + g[6])
+        gy = (g[6] + 2 * g[7] + g[8]) - (g[0] + 2 * g[1] + g[2])
+        v = torch.cat([v, torch.sqrt(gx * gx + gy * gy).unsqueeze(-1)], -1)
+    if mean is not None:
+        v = v - mean.float().view(1, Ho, Wo, -1)
+    if rdisp is not None:
+        v = v * rdisp.float().view(1, Ho, Wo, -1)
+    return v * (idx >= 0).float().view(B, 1, 1, 1)
+
+
+def image_batch(src, idx, params, out, sobel=False, mean=None, rdisp=None,
+                bg=None, bgcolor=None):
+    """Augmented, normalised image minibatch from uint8 canvases (the image
+    loaders' device path, hvk_image_batch): out [B][Ho][Wo][C + sobel]."""
+    B, Ho, Wo = out.shape[0], out.shape[1], out.shape[2]
+    N, Hs, Ws, C = src.shape
+    if _gpu(out):
+        _lib_call("hvk_image_batch", _p(src), Hs * Ws * C, Hs, Ws, C,
+                  _p(idx), _p(params), B, Ho, Wo, 1 if sobel else 0,
+                  _p(mean), _p(rdisp), _p(bg), _p(bgcolor), _p(out), _s(out))
+        return out
+    out.copy_(image_batch_ref(src, idx, params, Ho, Wo, sobel, mean, rdisp,
+                              bg, bgcolor).to(out.dtype))
+    return out
+
+
 def mean_disp_normalize(x, mean, rdisp, out=None, out_dtype=None):
     """out = (float(x) - mean) * rdisp, mean/rdisp broadcast per sample."""
     if out is None:

@@ -42,6 +42,7 @@ _SIGS = {
     "hvk_fill_minibatch": [P, I, P, I, I, I, L, P, P, P, I, P, P, P, P],
     "hvk_fill_minibatch_s2d": [P, L, P, I, I, I, I, I, I, I, I, I, I, I, P,
                                P, P, P, P, P, P],
+    "hvk_image_batch": [P, L, I, I, I, P, P, I, I, I, I, P, P, P, P, P, P],
     "hvk_mean_disp_normalize": [P, I, P, P, P, I, L, L, P],
     "hvk_softmax_ce": [P, I, I, I, P, F, P, I, P, P, P, P, P],
     "hvk_mse": [P, I, P, I, I, I, F, P, I, P, P, I, P],
@@ -76,6 +77,7 @@ _SIGS = {
     "hvk_pool2_fwd": [P, P] + [I] * 5 + [P],
     "hvk_stochastic_pool": [P, P, P] + [I] * 12 + [P, P],
     "hvk_pool2_bwd": [P, P, P] + [I] * 5 + [P, I, P],
+    "hvk_set_lrn_pool_tiled": [I],
     "hvk_lrn_pool_fwd_u8": [P, P, P] + [I] * 7 + [F, F, F, P],
     "hvk_lrn_pool_bwd_u8": [P, P, P, P] + [I] * 7 + [F, F, F, P, I, P],
     # exact-precision GEMMs (csrc/kernels/gemm_f32.hip)
