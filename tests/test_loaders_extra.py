@@ -11,7 +11,7 @@ import torch
 from veles_amd.backends import Device
 from veles_amd.dummy import DummyLauncher, DummyWorkflow
 from veles_amd.loader import (
-    EnsembleLoader, FileListImageLoader, FullBatchFileImageLoader,
+    EnsembleLoader, FullBatchFileListImageLoader, FullBatchFileImageLoader,
     FullBatchHDF5Loader, MinibatchesLoader, MinibatchesSaver,
     PicklesImageFullBatchLoader, TRAIN, VALID, TEST)
 from veles_amd.loader.file_loader import FileFilter, scan_files
@@ -61,7 +61,8 @@ def test_full_batch_file_image_loader_trains(tmp_path):
         decision_config={"max_epochs": 6})
     wf.initialize(device=Device(backend="cpu"))
     ld = wf.loader
-    assert ld.class_lengths == [0, 4, 12]
+    # mirror=True serves every canvas plain and flipped (inflation 2)
+    assert ld.class_lengths == [0, 8, 24]
     assert tuple(ld.original_data.shape) == (16, 8, 8, 3)
     assert ld.reversed_labels_mapping == ["cat", "dog"]
     wf.run()
@@ -75,7 +76,7 @@ def test_file_list_loader(tmp_path):
         for c in ("cat", "dog"):
             for i in range(3):
                 f.write("%s/%s_%d.png %s\n" % (c, c, i, c))
-    ld = FileListImageLoader(DummyWorkflow(), train_list=str(lst),
+    ld = FullBatchFileListImageLoader(DummyWorkflow(), train_list=str(lst),
                              size=(6, 6), color_space="GRAY",
                              minibatch_size=2)
     _init(ld)

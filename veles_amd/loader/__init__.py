@@ -8,8 +8,10 @@ from veles_amd.loader.fullbatch import (  # noqa: F401
 from veles_amd.loader.synthetic import (  # noqa: F401
     SyntheticImageLoader, SyntheticMSELoader)
 from veles_amd.loader.image import (  # noqa: F401
-    FullBatchFileImageLoader, FullBatchAutoLabelFileImageLoader,
-    FileListImageLoader, FullBatchImageLoaderMSE)
+    ImageLoader, FileImageLoader, AutoLabelFileImageLoader,
+    FileListImageLoader, FullBatchFileImageLoader,
+    FullBatchAutoLabelFileImageLoader, FullBatchFileListImageLoader,
+    FullBatchImageLoaderMSE)
 from veles_amd.loader.pickles import PicklesImageFullBatchLoader  # noqa
 from veles_amd.loader.ensemble import EnsembleLoader  # noqa: F401
 from veles_amd.loader.loader_hdf5 import FullBatchHDF5Loader  # noqa: F401
