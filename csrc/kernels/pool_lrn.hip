@@ -893,97 +893,6 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8_kernel(
   }
 }
 
-// The same forward, LDS-tiled: a workgroup owns a TOH x TOW tile of pool
-// outputs x a 32-channel slice of one image.  Phase 1 computes the LRN of the
-// tile's (2 TOH + 1) x (2 TOW + 1) input pixels ONCE each (f32 into LDS:
-// the per-thread kernel above recomputes every input pixel in each of the
-// up to 4 windows covering it, 2.25x on average for 3x3 / 2) with
-// consecutive lanes on consecutive 8-channel chunks of one pixel (coalesced
-// 16-B loads, halo from neighbouring chunks through L1); phase 2 max-pools
-// from LDS.  Same LRN arithmetic and window order as the per-thread kernel:
-// bit-identical outputs and argmax.  C % 32 == 0.
-constexpr int LPT_CS = 32, LPT_MAXT = 9;
-constexpr int LPT_MAXP = (2 * LPT_MAXT + 1) * (2 * LPT_MAXT + 1);
-
-template <int half>
-__global__ __launch_bounds__(256) void lrn_pool3s2_fwd_tile_kernel(
-    const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
-    uint8_t* __restrict__ argmax, int H, int W, int C, int OH, int OW,
-    int TOH, int TOW, int tiles_h, int tiles_w, float alpha, float beta,
-    float k) {
-  __shared__ __attribute__((aligned(16))) float lds[LPT_MAXP * LPT_CS];
-  constexpr int QC = LPT_CS / 8;  // 8-channel chunks per slice
-  int b = blockIdx.x;
-  const int ncs = C / LPT_CS;
-  const int cs = b % ncs; b /= ncs;
-  const int tw = b % tiles_w; b /= tiles_w;
-  const int th = b % tiles_h;
-  const int n = b / tiles_h;
-  const int oh0 = th * TOH, ow0 = tw * TOW;
-  const int IH = 2 * TOH + 1, IW = 2 * TOW + 1;
-  const int cb = cs * LPT_CS;
-  const uint16_t* img = x + (long long)n * H * W * C;
-  const int items = IH * IW * QC;
-  for (int it = threadIdx.x; it < items; it += blockDim.x) {
-    const int q = it % QC, p = it / QC;
-    const int pr = p / IW, pc = p - (p / IW) * IW;
-    const int h = 2 * oh0 + pr, w = 2 * ow0 + pc;
-    float o[8];
-    if (h < H && w < W) {
-      float v[24];
-      loadx<half>(img + ((long long)h * W + w) * C, cb + 8 * q, C, v);
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq) {
-        const float sv = lrn_s(v, 8 + qq, half, alpha, k);
-        o[qq] = v[8 + qq] * exp2f(-beta * __log2f(sv));
-      }
-    } else {
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq) o[qq] = -INFINITY;
-    }
-    float4* d = (float4*)(lds + p * LPT_CS + 8 * q);
-    d[0] = make_float4(o[0], o[1], o[2], o[3]);
-    d[1] = make_float4(o[4], o[5], o[6], o[7]);
-  }
-  __syncthreads();
-  const int items2 = TOH * TOW * QC;
-  for (int it = threadIdx.x; it < items2; it += blockDim.x) {
-    const int q = it % QC, oo = it / QC;
-    const int orow = oo / TOW, ocol = oo - (oo / TOW) * TOW;
-    const int oh = oh0 + orow, ow = ow0 + ocol;
-    if (oh >= OH || ow >= OW) continue;
-    float best[8];
-    int bi[8];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int p = (2 * orow + i / 3) * IW + 2 * ocol + i % 3;
-      const float4* s4 = (const float4*)(lds + p * LPT_CS + 8 * q);
-      const float4 a = s4[0], c = s4[1];
-      const float yv[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-#pragma unroll
-      for (int qq = 0; qq < 8; ++qq)
-        if (i == 0 || yv[qq] > best[qq]) { best[qq] = yv[qq]; bi[qq] = i; }
-    }
-    const long long yo = (((long long)n * OH + oh) * OW + ow) * C + cb + 8 * q;
-    *(uint4*)(y + yo) = pack_bf16x8(best);
-    uint2 a;
-    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
-    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
-    *(uint2*)(argmax + yo) = a;
-  }
-}
-
-// output tile edge for an OH-long axis: the largest t <= 9 that leaves the
-// fewest idle rows in the last tile
-inline int lpt_tile(int OH) {
-  int best = LPT_MAXT, waste = 1 << 30;
-  for (int t = LPT_MAXT; t >= 4; --t) {
-    const int w = (OH + t - 1) / t * t - OH;
-    if (w < waste) { waste = w; best = t; }
-  }
-  return best;
-}
-
 template <int half>
 __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_u8_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
@@ -1329,14 +1238,6 @@ HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
 
 // Fused LRN -> 3x3 stride-2 max pooling with a uint8 window-index argmax
 // (see lrn_pool3s2_fwd_u8_kernel).  C % 8 == 0, n / 2 <= 4.
-// 1: the LDS-tiled forward (default); 0: the per-thread kernel (tests
-// compare the two: hvk_set_lrn_pool_tiled)
-int g_lrn_pool_tiled = 1;
-HVK_API int hvk_set_lrn_pool_tiled(int on) {
-  g_lrn_pool_tiled = on;
-  return 0;
-}
-
 HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
                                 int H, int W, int C, int OH, int OW, int n,
                                 float alpha, float beta, float k,
@@ -1345,21 +1246,6 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
       ((uintptr_t)argmax & 7) || (long long)N * H * W * C >= (1ll << 31))
     return -1;
   const int h = n / 2;
-  if (C % LPT_CS == 0 && h >= 1 && g_lrn_pool_tiled) {
-    const int TOH = lpt_tile(OH), TOW = lpt_tile(OW);
-    const int th = (OH + TOH - 1) / TOH, tw = (OW + TOW - 1) / TOW;
-    const long long blocks = (long long)N * th * tw * (C / LPT_CS);
-    if (blocks < (1ll << 31)) {
-      auto kt = h == 1 ? lrn_pool3s2_fwd_tile_kernel<1>
-              : h == 2 ? lrn_pool3s2_fwd_tile_kernel<2>
-              : h == 3 ? lrn_pool3s2_fwd_tile_kernel<3>
-                       : lrn_pool3s2_fwd_tile_kernel<4>;
-      hipLaunchKernelGGL(kt, dim3((unsigned)blocks), dim3(256), 0, s,
-                         (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax,
-                         H, W, C, OH, OW, TOH, TOW, th, tw, alpha, beta, k);
-      return (int)hipGetLastError();
-    }
-  }
   const long long total = (long long)N * OH * OW * (C / 8);
   auto kf = h == 0 ? lrn_pool3s2_fwd_u8_kernel<0>
           : h == 1 ? lrn_pool3s2_fwd_u8_kernel<1>

@@ -513,36 +513,6 @@ def test_lrn_pool_fused(shape, stride, n, aux_mode):
     close(dx, dxr, 2e-2)
 
 
-@pytest.mark.parametrize("shape,n", [
-    ((3, 55, 55, 96), 5), ((2, 27, 27, 256), 5), ((2, 13, 13, 64), 3),
-    ((1, 31, 19, 32), 9), ((2, 41, 41, 96), 5)])
-def test_lrn_pool_tiled_forward_matches_per_thread(shape, n):
-    """The LDS-tiled LRN -> 3x3/2 max-pool forward (LRN once per input
-    pixel) against the per-thread kernel (LRN per covering window): the
-    same arithmetic, so pooled values and u8 argmax are bit-identical,
-    including partial edge tiles and padded tile rows."""
-    from veles_amd.ops import _lib
-    alpha, beta, k = 1e-4 / n, 0.75, 2.0
-    x = rnd(*shape, scale=3.0).to(DEV)
-    outs = []
-    for tiled in (0, 1):
-        _lib.lib().hvk_set_lrn_pool_tiled(tiled)
-        am = torch.zeros((1,), dtype=torch.uint8, device=DEV)
-        N, H, W, C = shape
-        OH, OW = (H - 3) // 2 + 1, (W - 3) // 2 + 1
-        am = torch.full((N, OH, OW, C), 77, dtype=torch.uint8, device=DEV)
-        y = torch.full((N, OH, OW, C), 5.0, dtype=torch.bfloat16,
-                       device=DEV)
-        ops.lrn_pool_fwd(x, n, alpha, beta, k, 3, 3, (2, 2), out=y,
-                         argmax=am)
-        torch.cuda.synchronize()
-        outs.append((y.view(torch.int16).clone(), am.clone()))
-    _lib.lib().hvk_set_lrn_pool_tiled(1)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-    assert int(outs[1][1].max()) <= 8
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["max", "avg", "maxabs"])
 @pytest.mark.parametrize("aux_mode", ["none", "sep", "x"])

@@ -597,12 +597,11 @@ def s2d_affine(vec, sample_shape, s, KH, KW, padding, fill):
     order (``fill`` where the s2d image has no input pixel): the mean /
     rdisp of ``fill_minibatch_s2d``."""
     H, W, C = sample_shape
-    v = vec.reshape(1, H, W, C).float()
-    if fill:
-        v = v - fill
-    y = space_to_depth_ref(v, s, KH, KW, padding)
-    if fill:
-        y = y + fill
+    y = space_to_depth_ref(vec.reshape(1, H, W, C).float(), s, KH, KW,
+                           padding)
+    if fill:   # exact values inside, ``fill`` where no input pixel is
+        inb = space_to_depth_ref(torch.ones(1, H, W, C), s, KH, KW, padding)
+        y = torch.where(inb > 0, y, torch.full_like(y, float(fill)))
     return y.reshape(-1).contiguous()
 
 

@@ -77,7 +77,6 @@ _SIGS = {
     "hvk_pool2_fwd": [P, P] + [I] * 5 + [P],
     "hvk_stochastic_pool": [P, P, P] + [I] * 12 + [P, P],
     "hvk_pool2_bwd": [P, P, P] + [I] * 5 + [P, I, P],
-    "hvk_set_lrn_pool_tiled": [I],
     "hvk_lrn_pool_fwd_u8": [P, P, P] + [I] * 7 + [F, F, F, P],
     "hvk_lrn_pool_bwd_u8": [P, P, P, P] + [I] * 7 + [F, F, F, P, I, P],
     # exact-precision GEMMs (csrc/kernels/gemm_f32.hip)
