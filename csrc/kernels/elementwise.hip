@@ -791,51 +791,6 @@ __global__ void fill_rows_u8_bf16_kernel(const uint8_t* __restrict__ src,
 }
 
 
-// Specialised space-to-depth (compile-time S, C; S*S*C % 8 == 0): a thread
-// builds one output pixel (S*S*C elements) in registers from S unaligned
-// 8-B-chunked row runs and writes it with 16-B stores; a wave reads S
-// contiguous 64-run spans and writes one contiguous span.
-template <int S, int C>
-__global__ void space_to_depth_px_kernel(const uint16_t* __restrict__ x,
-                                         uint16_t* __restrict__ y, int H,
-                                         int W, int pt, int pl, int H2,
-                                         int W2, FastDiv fW2, FastDiv fH2,
-                                         long long pixels) {
-  constexpr int RUN = S * C, PIX = S * RUN;
-  static_assert(RUN % 4 == 0 && PIX % 8 == 0, "vector shape");
-  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-       q < pixels; q += (long long)gridDim.x * blockDim.x) {
-    uint32_t t, X, n, Y;
-    fdivmod((uint32_t)q, fW2, t, X);
-    fdivmod(t, fH2, n, Y);
-    uint16_t v[PIX];
-    const int ix0 = S * (int)X - pl;
-    const bool xin = ix0 >= 0 && ix0 + S <= W;
-#pragma unroll
-    for (int dy = 0; dy < S; ++dy) {
-      const int iy = S * (int)Y + dy - pt;
-      const bool yin = iy >= 0 && iy < H;
-      const uint16_t* row = x + ((long long)n * H + (yin ? iy : 0)) * W * C;
-      if (yin && xin) {
-#pragma unroll
-        for (int e = 0; e < RUN; e += 4)
-          __builtin_memcpy(&v[dy * RUN + e], row + (long long)ix0 * C + e, 8);
-      } else {
-#pragma unroll
-        for (int e = 0; e < RUN; ++e) {
-          const int ix = ix0 + e / C;
-          v[dy * RUN + e] = (yin && ix >= 0 && ix < W)
-                                ? row[(long long)ix * C + e % C]
-                                : (uint16_t)0;
-        }
-      }
-    }
-    uint4* out = (uint4*)(y + q * PIX);
-#pragma unroll
-    for (int j = 0; j < PIX / 8; ++j) out[j] = ((const uint4*)v)[j];
-  }
-}
-
 // Loader gather fused with the space-to-depth transform of the first
 // (strided, small-channel) convolution: uint8 samples [H][W][C] ->
 // normalised bf16 s2d images [H2][W2][S][S][C] (the layout hvk_conv_fwd reads
@@ -1546,24 +1501,12 @@ HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
   if (C2 % 8) return -1;
   long long runs = (long long)N * H2 * W2 * s;
   if (runs >= (1ll << 32)) return -1;
-  static const bool chunked = [] {
-    const char* e = getenv("HVK_S2D_CHUNK");
-    return !(e && e[0] == '0');
-  }();
-  if (chunked && s == 4 && C == 3 && ((uintptr_t)y & 15) == 0) {
+  if (s == 4 && C == 3 && ((uintptr_t)y & 15) == 0) {
     const long long chunks = (long long)N * H2 * W2 * 6;
     hipLaunchKernelGGL((space_to_depth_chunk_kernel<4, 3>),
                        dim3(grid_for(chunks)), dim3(256), 0, st,
                        (const uint16_t*)x, (uint16_t*)y, H, W, pt, pl,
                        make_fastdiv(W2), make_fastdiv(H2), chunks);
-    return (int)hipGetLastError();
-  }
-  if (s == 4 && C == 3 && ((uintptr_t)y & 15) == 0) {
-    long long pixels = (long long)N * H2 * W2;
-    hipLaunchKernelGGL((space_to_depth_px_kernel<4, 3>), dim3(grid_for(pixels)),
-                       dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y, H,
-                       W, pt, pl, H2, W2, make_fastdiv(W2), make_fastdiv(H2),
-                       pixels);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(space_to_depth_kernel, dim3(grid_for(runs)), dim3(256), 0,
@@ -1739,92 +1682,3 @@ HVK_API int hvk_conv_fwd_direct(const void* X, const void* Wt,
   return (int)hipGetLastError();
 }
 
-// Weight gradient of the same tiny convolutions: dW[oc][k] += sum over pixels
-// of dY[p][oc] * X_col[p][k] (and dbias[oc] += sum dY[p][oc]).  A block walks
-// its pixel range in 64-pixel tiles staged in LDS (dY rows and the gathered
-// taps as f32); each lane owns up to 16 of the OC * K outputs and adds its
-// partial sums to dW with one atomic each at the end.
-__global__ __launch_bounds__(256) void conv_wgrad_direct_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-    float* __restrict__ dw, float* __restrict__ dbias, int N, int H, int W,
-    int C, int OC, int KH, int KW, int sy, int sx, int pt, int pl, int OH,
-    int OW, int ppb, FastDiv fOW, FastDiv fOH, FastDiv fK, FastDiv fKWC,
-    FastDiv fC) {
-  constexpr int TP = 64;
-  __shared__ float sdy[TP * 64];
-  __shared__ float sxc[TP * 64];
-  const int K = KH * KW * C, NO = OC * K;
-  const uint32_t P = (uint32_t)N * OH * OW;
-  const uint32_t p0 = (uint32_t)blockIdx.x * ppb;
-  const uint32_t p1 = min(P, p0 + (uint32_t)ppb);
-  float acc[16], bacc = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (uint32_t t0 = p0; t0 < p1; t0 += TP) {
-    const int np = (int)min((uint32_t)TP, p1 - t0);
-    for (int i = threadIdx.x; i < TP * OC; i += blockDim.x) {
-      const int t = i / OC, oc = i - t * OC;
-      sdy[t * 64 + oc] = t < np ? bf2f(dy[(long long)(t0 + t) * OC + oc]) : 0.f;
-    }
-    for (int i = threadIdx.x; i < TP * K; i += blockDim.x) {
-      uint32_t t, k, tap, c, kh, kw;
-      fdivmod((uint32_t)i, fK, t, k);
-      float v = 0.f;
-      if ((int)t < np) {
-        uint32_t q = t0 + t, r, ow, n, oh;
-        fdivmod(q, fOW, r, ow);
-        fdivmod(r, fOH, n, oh);
-        fdivmod(k, fC, tap, c);
-        kh = tap / KW;
-        kw = tap - kh * KW;
-        const int ih = (int)oh * sy - pt + (int)kh;
-        const int iw = (int)ow * sx - pl + (int)kw;
-        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-          v = bf2f(x[(((long long)n * H + ih) * W + iw) * C + c]);
-      }
-      sxc[t * 64 + k] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = threadIdx.x + r * 256;
-      if (o < NO) {
-        const int oc = o / K, k = o - oc * K;
-        float a = acc[r];
-        for (int t = 0; t < TP; ++t) a += sdy[t * 64 + oc] * sxc[t * 64 + k];
-        acc[r] = a;
-      }
-    }
-    if (dbias && (int)threadIdx.x < OC)
-      for (int t = 0; t < TP; ++t) bacc += sdy[t * 64 + threadIdx.x];
-    __syncthreads();
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int o = threadIdx.x + r * 256;
-    if (o < NO) atomicAdd(&dw[o], acc[r]);
-  }
-  if (dbias && (int)threadIdx.x < OC) atomicAdd(&dbias[threadIdx.x], bacc);
-}
-
-HVK_API int hvk_conv_wgrad_direct(const void* X, const void* dY, float* dW,
-                                  float* dbias, int N, int H, int W, int C,
-                                  int OC, int KH, int KW, int sy, int sx,
-                                  int pt, int pl, int OH, int OW,
-                                  hipStream_t s) {
-  const int K = KH * KW * C;
-  if (K > 64 || OC > 64 || OC < 1 || (long long)N * OH * OW >= (1ll << 31))
-    return -1;
-  const long long P = (long long)N * OH * OW;
-  if (P == 0) return 0;
-  long long blocks = 512;
-  long long ppb = (P + blocks - 1) / blocks;
-  ppb = (ppb + 63) / 64 * 64;
-  blocks = (P + ppb - 1) / ppb;
-  hipLaunchKernelGGL(conv_wgrad_direct_kernel, dim3((int)blocks), dim3(256),
-                     0, s, (const uint16_t*)X, (const uint16_t*)dY, dW, dbias,
-                     N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, (int)ppb,
-                     make_fastdiv(OW), make_fastdiv(OH), make_fastdiv(K),
-                     make_fastdiv(KW * C), make_fastdiv(C));
-  return (int)hipGetLastError();
-}

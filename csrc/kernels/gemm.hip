@@ -1122,14 +1122,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 // 128-wide image (the upper half from the zero page), so it saves no fill
 // bandwidth and only adds tiles (AlexNet conv1 wgrad, N = 432: 126 -> 203 TF
 // at 128, step +1.5 %; profiles/gemm_experiments_r1.md §4).
-// HVK_BN_WASTE_DIV overrides both (A/B knob).
-inline int bn_waste_div(bool kmajor) {
-  static int d = [] {
-    const char* e = getenv("HVK_BN_WASTE_DIV");
-    return e ? atoi(e) : 0;
-  }();
-  return d > 0 ? d : (kmajor ? 8 : 2);
-}
+inline int bn_waste_div(bool kmajor) { return kmajor ? 8 : 2; }
 inline int pick_bn(int N, bool allow96) {
   auto waste = [&](int b) { return (N + b - 1) / b * b - N; };
   if (waste(128) * bn_waste_div(allow96) <= N) return 128;
@@ -1139,8 +1132,9 @@ inline int pick_bn(int N, bool allow96) {
   return best;
 }
 
-// GEMM schedule selector (A/B knob, hvk_set_gemm_variant or the
-// HVK_GEMM_VARIANT environment variable): 0 = 4-wave blocks everywhere,
+// GEMM schedule selector (A/B experiments set it explicitly through
+// hvk_set_gemm_variant; nothing is read from the environment): 0 = 4-wave
+// blocks everywhere,
 // default (-1) = 8-wave blocks for the LDS-DMA loaders at BN 64 / 128
 // except conv backward-data.  Measured on
 // the AlexNet / VGG shapes (profiles/gemm_experiments_r2.md §6): 8 waves
@@ -1150,11 +1144,7 @@ int g_gemm_variant = -1;
 
 template <class LA, class LB>
 bool want_w8(const LA& la, const LB& lb, int bn) {
-  static const int env = [] {
-    const char* e = getenv("HVK_GEMM_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
-  const int v = g_gemm_variant >= 0 ? g_gemm_variant : env;
+  const int v = g_gemm_variant;
   if (v == 0 || !(LA::kGlds && LB::kGlds) || (bn != 64 && bn != 128) ||
       !la.dma_ok() || !lb.dma_ok())
     return false;

@@ -410,26 +410,13 @@ hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
   const int tiles = tiles_m * tiles_n;
   dim3 grid((unsigned)((long long)tiles * groups));
-  // 8-wave blocks unless HVK_FP8_W8=0 (A/B knob)
-  static const bool w8 = [] {
-    const char* v = getenv("HVK_FP8_W8");
-    return !(v && v[0] == '0');
-  }();
-  if (w8) {
-    if (n64)
-      hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB, true>), grid,
-                         dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
-    else
-      hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB, true>), grid,
-                         dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
-    return hipGetLastError();
-  }
+  // 8-wave blocks (profiles/gemm_experiments_r2.md section 8)
   if (n64)
-    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB, false>), grid,
-                       dim3(NTHR), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
+    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 64, FA, FB, true>), grid,
+                       dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
   else
-    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB, false>), grid,
-                       dim3(NTHR), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
+    hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB, true>), grid,
+                       dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
   return hipGetLastError();
 }
 

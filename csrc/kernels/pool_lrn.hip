@@ -1271,11 +1271,7 @@ HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
   const int h = n / 2;
   const int BH = (H + 1) / 2, BW = (W + 1) / 2;
   const long long tb = (long long)N * BH * BW * (C / 8);
-  static const bool dpp_on = [] {
-    const char* e = getenv("HVK_LRN_DPP");
-    return !(e && e[0] == '0');
-  }();
-  if (dpp_on && C / 8 <= 64 && h >= 1 && h <= 4) {
+  if (C / 8 <= 64 && h >= 1 && h <= 4) {
     // whole 2 x 2 blocks per wave, their chunks on consecutive lanes
     const int CV = C / 8, bpw = 64 / CV;
     const long long nblk = (long long)N * BH * BW;

@@ -167,3 +167,35 @@ def test_hdf5_loader_reports_missing_h5py():
 
 
 _ = torch
+
+
+REF_WINE = "/root/reference/veles/tests/res/wine_ensemble.json"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_WINE),
+                    reason="reference fixture absent")
+def test_ensemble_loader_on_reference_wine_results():
+    """The reference's own --ensemble-train result file (3 wine models,
+    178 test outputs each; veles/tests/res/wine_ensemble.json): test mode
+    stacks the members' outputs per sample; with labels (the members'
+    consensus here: the reference file holds no ground truth) it trains an
+    ensemble-of-outputs classifier input."""
+    import json as _json
+    ens = _json.load(open(REF_WINE))
+    t = EnsembleLoader(DummyWorkflow(), file=REF_WINE, testing=True,
+                       minibatch_size=32)
+    _init(t)
+    assert t.class_lengths[TEST] == 178
+    d = t.original_data.mem
+    assert d.shape == (178, 3, 3)
+    for i, m in enumerate(ens["models"]):
+        numpy.testing.assert_allclose(d[:, i], numpy.asarray(m["Output"]),
+                                      rtol=1e-6)
+    vote = numpy.asarray([m["Output"] for m in ens["models"]]).mean(0)
+    labels = vote.argmax(1).tolist()
+    tr = EnsembleLoader(DummyWorkflow(), file=REF_WINE, labels=labels,
+                        minibatch_size=32)
+    _init(tr)
+    assert tr.class_lengths[TRAIN] == 178
+    assert tr.reversed_labels_mapping == [0, 1, 2]
+    assert list(tr.original_labels) == labels

@@ -495,8 +495,6 @@ def needs_im2col(C, groups):
 # 1.26 ms (tools/bench_c3_pad.py).  HVK_C3_PAD=0 keeps the run kernels.
 _C_PAD8 = os.environ.get("HVK_C3_PAD", "1") != "0"
 _DIRECT = os.environ.get("HVK_CONV_DIRECT", "1") != "0"
-# the matching weight-gradient kernel (hvk_conv_wgrad_direct)
-_DIRECT_WGRAD = os.environ.get("HVK_CONV_DIRECT_WGRAD", "0") == "1"
 _C_PAD_MIN = int(os.environ.get("HVK_C3_PAD_MIN", "3"))
 
 
@@ -872,12 +870,6 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
                       _p(dbias), _s(x))
             dw += dwp[..., :C]
             dwp.zero_()
-            return dw
-        if _DIRECT_WGRAD and groups == 1 and C < 3 and \
-                KH * KW * Cg <= 64 and OC <= 64 and dw.is_contiguous() and \
-                _lib.lib().hvk_conv_wgrad_direct(
-                    _p(x), _p(dy), _p(dw), _p(dbias), N, H, W, C, OC, KH, KW,
-                    sy, sx, pt, pl, OH, OW, _s(x)) == 0:
             return dw
         if isinstance(col, (S2DImage, PaddedImage)):
             col = None

@@ -36,7 +36,6 @@ _SIGS = {
     "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P, P],
     "hvk_conv_fwd_run": [P, P, P, P] + [I] * 14 + [P],
     "hvk_conv_fwd_direct": [P, P, P, P] + [I] * 14 + [P],
-    "hvk_conv_wgrad_direct": [P, P, P, P] + [I] * 13 + [P],
     "hvk_conv_wgrad_run": [P, P, P, P] + [I] * 14 + [P],
     "hvk_im2col": [P, P] + [I] * 13 + [P],
     "hvk_fill_minibatch": [P, I, P, I, I, I, L, P, P, P, I, P, P, P, P],
