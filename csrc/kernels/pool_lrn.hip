@@ -893,77 +893,85 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8_kernel(
   }
 }
 
-// The same forward with a 2 x 2 block of pool outputs per thread: the 5 x 5
-// input pixels under the four overlapping 3 x 3 / stride-2 windows are
-// normalised once each (25 LRN pixel evaluations for 4 outputs instead of
-// 36) and fed to every window that contains them, in row-major order - the
-// order of the one-output kernel, so the maxima, their tie-breaking and the
-// window-local argmax are bit-identical to it.
+// The same forward (half <= 2) with every window pixel's 16 channels
+// loaded before any arithmetic: the 9 x 32-B loads of a thread are all in
+// flight at once (clamped in-range addresses, out-of-window taps masked
+// afterwards) instead of one pixel's loads per LRN evaluation - the kernel
+// is bound by memory latency, not by its transcendental work (a 2 x 2
+// outputs-per-thread variant that evaluated 31 % fewer LRN pixels ran at the
+// same speed: profiles/r3_experiments.md).  Same arithmetic and window order:
+// bit-identical to lrn_pool3s2_fwd_u8_kernel.
 template <int half>
-__global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8x4_kernel(
+__global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8p_kernel(
     const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
     uint8_t* __restrict__ argmax, int N, int H, int W, int C, int OH, int OW,
-    float alpha, float beta, float k, FastDiv fCV, FastDiv fPW, FastDiv fPH) {
+    float alpha, float beta, float k, FastDiv fCV, FastDiv fOW, FastDiv fOH) {
+  static_assert(half <= 2, "16-channel halo");
   const int CV = C >> 3;
-  const int PH = (OH + 1) >> 1, PW = (OW + 1) >> 1;
-  const int total = N * PH * PW * CV;
+  const int total = N * OH * OW * CV;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
-    uint32_t blk, cvu, t, pwu, nu, phu;
-    fdivmod((uint32_t)e, fCV, blk, cvu);
-    fdivmod(blk, fPW, t, pwu);
-    fdivmod(t, fPH, nu, phu);
+    uint32_t pix, cvu, t, owu, nu, ohu;
+    fdivmod((uint32_t)e, fCV, pix, cvu);
+    fdivmod(pix, fOW, t, owu);
+    fdivmod(t, fOH, nu, ohu);
     const int c0 = (int)cvu * 8;
-    const int oh0 = (int)phu * 2, ow0 = (int)pwu * 2;
-    const int h0 = oh0 * 2, w0 = ow0 * 2;
+    const int h0 = (int)ohu * 2, w0 = (int)owu * 2;
     const uint16_t* img = x + (long long)nu * H * W * C;
-    float best[4][8];
-    uint32_t bi[4][2];
+    const int clo = c0 >= 8 ? c0 - 4 : c0;        // in-range halo addresses
+    const int chi = c0 + 8 < C ? c0 + 8 : c0 + 4;
+    uint2 lo[9], hi[9];
+    uint4 mid[9];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      bi[o][0] = bi[o][1] = 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) best[o][q] = -INFINITY;
+    for (int i = 0; i < 9; ++i) {
+      const int h = min(h0 + i / 3, H - 1), w = min(w0 + i % 3, W - 1);
+      const uint16_t* row = img + ((long long)h * W + w) * C;
+      lo[i] = *(const uint2*)(row + clo);
+      mid[i] = *(const uint4*)(row + c0);
+      hi[i] = *(const uint2*)(row + chi);
     }
+    float best[8];
+    int bi[8];
 #pragma unroll
-    for (int r = 0; r < 5; ++r) {
+    for (int i = 0; i < 9; ++i) {
+      const bool in = h0 + i / 3 < H && w0 + i % 3 < W;
+      float v[24];
 #pragma unroll
-      for (int c = 0; c < 5; ++c) {
-        const int h = h0 + r, w = w0 + c;
-        if (h >= H || w >= W) continue;
-        float v[24];
-        loadx<half>(img + ((long long)h * W + w) * C, c0, C, v);
-        float yv[8];
+      for (int q = 0; q < 24; ++q) v[q] = 0.f;
+      if (c0 >= 8) {
+        v[4] = __uint_as_float(lo[i].x << 16);
+        v[5] = __uint_as_float(lo[i].x & 0xffff0000u);
+        v[6] = __uint_as_float(lo[i].y << 16);
+        v[7] = __uint_as_float(lo[i].y & 0xffff0000u);
+      }
+      const uint32_t m[4] = {mid[i].x, mid[i].y, mid[i].z, mid[i].w};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float sv = lrn_s(v, 8 + q, half, alpha, k);
-          yv[q] = v[8 + q] * exp2f(-beta * __log2f(sv));
-        }
+      for (int q = 0; q < 4; ++q) {
+        v[8 + 2 * q] = __uint_as_float(m[q] << 16);
+        v[9 + 2 * q] = __uint_as_float(m[q] & 0xffff0000u);
+      }
+      if (c0 + 8 < C) {
+        v[16] = __uint_as_float(hi[i].x << 16);
+        v[17] = __uint_as_float(hi[i].x & 0xffff0000u);
+        v[18] = __uint_as_float(hi[i].y << 16);
+        v[19] = __uint_as_float(hi[i].y & 0xffff0000u);
+      }
 #pragma unroll
-        for (int o = 0; o < 4; ++o) {
-          const int a = o >> 1, b = o & 1;
-          const int rr = r - 2 * a, cc = c - 2 * b;
-          if (rr < 0 || rr > 2 || cc < 0 || cc > 2) continue;
-          const uint32_t i = (uint32_t)(rr * 3 + cc);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            if (i == 0 || yv[q] > best[o][q]) {
-              best[o][q] = yv[q];
-              const int sh = 8 * (q & 3);
-              bi[o][q >> 2] = (bi[o][q >> 2] & ~(0xFFu << sh)) | (i << sh);
-            }
-          }
-        }
+      for (int q = 0; q < 8; ++q) {
+        const float sv = lrn_s(v, 8 + q, half, alpha, k);
+        const float yv = v[8 + q] * exp2f(-beta * __log2f(sv));
+        if (i == 0 || (in && yv > best[q])) { best[q] = yv; bi[q] = i; }
       }
     }
+    uint16_t o[8];
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      const int oh = oh0 + (o >> 1), ow = ow0 + (o & 1);
-      if (oh >= OH || ow >= OW) continue;
-      const long long yo = (((long long)nu * OH + oh) * OW + ow) * C + c0;
-      *(uint4*)(y + yo) = pack_bf16x8(best[o]);
-      *(uint2*)(argmax + yo) = make_uint2(bi[o][0], bi[o][1]);
-    }
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(best[q]);
+    const long long yo = (long long)pix * C + c0;
+    *(uint4*)(y + yo) = *(const uint4*)o;
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+    *(uint2*)(argmax + yo) = a;
   }
 }
 
@@ -1320,21 +1328,16 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
       ((uintptr_t)argmax & 7) || (long long)N * H * W * C >= (1ll << 31))
     return -1;
   const int h = n / 2;
-  if (h >= 1) {
-    // 2 x 2 pool outputs per thread (LRN of each input pixel once per block)
-    const int PH = (OH + 1) / 2, PW = (OW + 1) / 2;
-    const long long tot4 = (long long)N * PH * PW * (C / 8);
-    auto k4 = h == 1 ? lrn_pool3s2_fwd_u8x4_kernel<1>
-            : h == 2 ? lrn_pool3s2_fwd_u8x4_kernel<2>
-            : h == 3 ? lrn_pool3s2_fwd_u8x4_kernel<3>
-                     : lrn_pool3s2_fwd_u8x4_kernel<4>;
-    hipLaunchKernelGGL(k4, dim3(grid_for(tot4)), dim3(256), 0, s,
+  const long long total = (long long)N * OH * OW * (C / 8);
+  if (h >= 1 && h <= 2) {
+    auto kp = h == 1 ? lrn_pool3s2_fwd_u8p_kernel<1>
+                     : lrn_pool3s2_fwd_u8p_kernel<2>;
+    hipLaunchKernelGGL(kp, dim3(grid_for(total)), dim3(256), 0, s,
                        (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N,
                        H, W, C, OH, OW, alpha, beta, k, make_fastdiv(C / 8),
-                       make_fastdiv(PW), make_fastdiv(PH));
+                       make_fastdiv(OW), make_fastdiv(OH));
     return (int)hipGetLastError();
   }
-  const long long total = (long long)N * OH * OW * (C / 8);
   auto kf = h == 0 ? lrn_pool3s2_fwd_u8_kernel<0>
           : h == 1 ? lrn_pool3s2_fwd_u8_kernel<1>
           : h == 2 ? lrn_pool3s2_fwd_u8_kernel<2>

@@ -8,7 +8,7 @@ compared layer by layer.  The HIP path computes in bf16 (activations,
 weights' compute copy, GEMM operands) with f32 accumulation and f32 master
 weights; the stated tolerance is therefore on the accumulated UPDATE of
 every parameter tensor: ||dW_hip - dW_cpu|| / ||dW_cpu|| <= 0.15, plus the
-loss of the last step within 5 %.  Dropout is left out (the device and host
+accumulated training loss of the 5 steps within 5 %.  Dropout is left out (the device and host
 draw different mask streams); LRN, grouped convolutions, max pooling, the
 fused space-to-depth gather of conv1 and the split-K FC GEMMs are in.
 """
@@ -83,13 +83,14 @@ def _run(layers, dataset, backend, steps, batch, n_classes=None):
 def _compare(cpu, hip, tol=0.15):
     (c0, c1, cm), (h0, h1, hm) = cpu, hip
     assert len(c0) == len(h0)
-    worst = 0.0
+    rels = []
     for a0, a1, b0, b1 in zip(c0, c1, h0, h1):
         assert torch.equal(a0, b0), "runs did not start from the same weights"
         dc, dh = a1 - a0, b1 - b0
-        rel = float((dh - dc).norm() / (dc.norm() + 1e-12))
-        worst = max(worst, rel)
-        assert rel <= tol, "update differs by %.3f (> %.2f)" % (rel, tol)
+        rels.append(float((dh - dc).norm() / (dc.norm() + 1e-12)))
+    worst = max(rels)
+    assert worst <= tol, "per-layer update differences %s (> %.2f)" % (
+        ["%.3f" % r for r in rels], tol)
     assert torch.isfinite(hm).all()
     # accumulated TRAIN loss over the 5 steps (metrics[class][1])
     lc, lh = float(cm[2][1]), float(hm[2][1])

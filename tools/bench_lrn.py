@@ -1,0 +1,56 @@
+"""HIP-event timing of the fused LRN -> 3x3/2 max-pool forward / backward on
+the AlexNet b1024 shapes (conv1: 55x55x96, conv2: 27x27x256), with the
+bytes each moves and the resulting HBM rate."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(
+    __file__))))
+
+import torch  # noqa: E402
+
+from veles_amd import ops  # noqa: E402
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(True), torch.cuda.Event(True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    res = {}
+    for name, (H, C) in {"conv1": (55, 96), "conv2": (27, 256)}.items():
+        x = torch.relu(torch.randn(B, H, H, C, device="cuda")).to(
+            torch.bfloat16)
+        OH = (H - 3) // 2 + 1
+        y = torch.empty(B, OH, OH, C, device="cuda", dtype=torch.bfloat16)
+        am = torch.empty(B, OH, OH, C, device="cuda", dtype=torch.uint8)
+        dp = torch.randn(B, OH, OH, C, device="cuda").to(torch.bfloat16)
+        dx = torch.empty_like(x)
+        kw = dict(n=5, alpha=2e-5, beta=0.75, k=1.0)
+        f = lambda: ops.lrn_pool_fwd(x, kw["n"], kw["alpha"], kw["beta"],  # noqa
+                                     kw["k"], 3, 3, (2, 2), out=y, argmax=am)
+        g = lambda: ops.lrn_pool_bwd(x, dp, am, kw["n"], kw["alpha"],  # noqa
+                                     kw["beta"], kw["k"], 3, 3, (2, 2),
+                                     aux=x, aux_act=3, out=dx)
+        tf, tb = timeit(f), timeit(g)
+        bf = x.numel() * 2 + y.numel() * 3
+        bb = x.numel() * 4 + dp.numel() * 3
+        res[name] = {"fwd_us": round(tf, 1), "fwd_TBps": round(bf / tf / 1e6, 2),
+                     "bwd_us": round(tb, 1), "bwd_TBps": round(bb / tb / 1e6, 2)}
+        print(name, res[name], flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
