@@ -6,9 +6,15 @@ Both runs start from the same weights (host PRNG) and the same synthetic
 data (generated on the host), train 5 steps with momentum SGD, and are
 compared layer by layer.  The HIP path computes in bf16 (activations,
 weights' compute copy, GEMM operands) with f32 accumulation and f32 master
-weights; the stated tolerance is therefore on the accumulated UPDATE of
-every parameter tensor: ||dW_hip - dW_cpu|| / ||dW_cpu|| <= 0.15, plus the
-accumulated training loss of the 5 steps within 5 %.  Dropout is left out (the device and host
+weights; the tolerance is therefore on the accumulated UPDATE of every
+parameter tensor, r = ||dW_hip - dW_cpu|| / ||dW_cpu||, measured against
+the bf16 NOISE FLOOR of the same workflow: a third run on the float32 CPU
+path that rounds every activation and every back-propagated error to bf16
+as the HIP path stores them (nothing else changes).  The HIP run must stay
+within 1.25 x that floor + 0.03 for every layer (the first layers of a deep
+net sit at r ~ 0.2 from the activation rounding alone: the weight gradient
+of conv1 is a sum over 16 x 55 x 55 positions with heavy cancellation), and
+the accumulated training loss of the 5 steps within 5 %.  Dropout is left out (the device and host
 draw different mask streams); LRN, grouped convolutions, max pooling, the
 fused space-to-depth gather of conv1 and the split-K FC GEMMs are in.
 """
@@ -18,7 +24,6 @@ import torch
 
 from veles_amd.utils.config import root
 
-pytestmark = pytest.mark.gpu
 
 
 def _small_alexnet():
@@ -50,7 +55,27 @@ def _small_alexnet():
                     "weights_stddev": 0.05}, "<-": dict(g)}]
 
 
-def _run(layers, dataset, backend, steps, batch, n_classes=None):
+def _round_bf16(arr):
+    import numpy as _np
+    t = getattr(arr, "mem", None) if arr is not None else None
+    if isinstance(t, _np.ndarray) and t.dtype == _np.float32:
+        tt = torch.from_numpy(t)
+        tt.copy_(tt.bfloat16().float())
+
+
+def _emulate_bf16_storage(wf):
+    """Round each unit's output / err_input to bf16 after it runs."""
+    for u in list(wf.forwards) + list(getattr(wf, "gds", [])):
+        def run(inner=u.do_run, u=u):
+            r = inner()
+            _round_bf16(getattr(u, "output", None))
+            _round_bf16(getattr(u, "err_input", None))
+            return r
+        u.__dict__["do_run"] = run
+
+
+def _run(layers, dataset, backend, steps, batch, n_classes=None,
+         bf16_storage=False):
     from veles_amd.backends import Device
     from veles_amd.dummy import DummyLauncher
     from veles_amd.models import StandardWorkflow
@@ -59,7 +84,9 @@ def _run(layers, dataset, backend, steps, batch, n_classes=None):
     random_generator.get().seed(77)
     numpy.random.seed(77)
     torch.manual_seed(77)
-    cfg = {"dataset": dataset, "class_lengths": (0, 0, batch * steps),
+    # one minibatch more than run: the epoch (and its metrics reset) does
+    # not end inside the compared steps
+    cfg = {"dataset": dataset, "class_lengths": (0, 0, batch * (steps + 1)),
            "minibatch_size": batch, "normalization_type": "mean_disp",
            "seed": 9, "generate_on_device": False}
     if n_classes:
@@ -69,6 +96,8 @@ def _run(layers, dataset, backend, steps, batch, n_classes=None):
         layers=layers, decision_config={"max_epochs": None,
                                         "fail_iterations": None})
     wf.initialize(device=Device(backend=backend))
+    if bf16_storage:
+        _emulate_bf16_storage(wf)
     w0 = [f.weights_master.detach().float().cpu().clone()
           for f in wf.forwards if getattr(f, "_pw_", None) is not None]
     wf.run_steps(steps)
@@ -80,44 +109,75 @@ def _run(layers, dataset, backend, steps, batch, n_classes=None):
     return w0, w1, m
 
 
-def _compare(cpu, hip, tol=0.15):
-    (c0, c1, cm), (h0, h1, hm) = cpu, hip
+def _rel_updates(ref, other):
+    (c0, c1, _), (h0, h1, _) = ref, other
     assert len(c0) == len(h0)
     rels = []
     for a0, a1, b0, b1 in zip(c0, c1, h0, h1):
         assert torch.equal(a0, b0), "runs did not start from the same weights"
         dc, dh = a1 - a0, b1 - b0
         rels.append(float((dh - dc).norm() / (dc.norm() + 1e-12)))
-    worst = max(rels)
-    assert worst <= tol, "per-layer update differences %s (> %.2f)" % (
-        ["%.3f" % r for r in rels], tol)
+    return rels
+
+
+def _compare(cpu, floor_run, hip):
+    rels = _rel_updates(cpu, hip)
+    floor = _rel_updates(cpu, floor_run)
+    bad = [(i, r, f) for i, (r, f) in enumerate(zip(rels, floor))
+           if r > 1.25 * f + 0.03]
+    assert not bad, "update differences %s vs bf16 floor %s" % (
+        ["%.3f" % r for r in rels], ["%.3f" % f for f in floor])
+    hm, cm = hip[2], cpu[2]
     assert torch.isfinite(hm).all()
-    # accumulated TRAIN loss over the 5 steps (metrics[class][1])
+    # accumulated TRAIN loss over the compared steps (metrics[class][1])
     lc, lh = float(cm[2][1]), float(hm[2][1])
+    assert lc > 0
     assert abs(lh - lc) <= 0.05 * abs(lc), (lh, lc)
-    return worst
+    return max(rels), max(floor)
 
 
+@pytest.mark.gpu
 def test_lenet_5_steps_hip_matches_fp32_cpu():
     from veles_amd.models.zoo import lenet
     old = root.common.engine.precision_type
     root.common.engine.precision_type = "bfloat16"
     try:
         cpu = _run(lenet(0.01), "mnist", "cpu", 5, 64)
+        flo = _run(lenet(0.01), "mnist", "cpu", 5, 64, bf16_storage=True)
         hip = _run(lenet(0.01), "mnist", "hip", 5, 64)
     finally:
         root.common.engine.precision_type = old
-    worst = _compare(cpu, hip)
-    print("LeNet: worst relative update difference %.4f" % worst)
+    worst, floor = _compare(cpu, flo, hip)
+    print("LeNet: worst relative update difference %.4f (bf16 floor %.4f)"
+          % (worst, floor))
 
 
+@pytest.mark.gpu
 def test_reduced_alexnet_5_steps_hip_matches_fp32_cpu():
     old = root.common.engine.precision_type
     root.common.engine.precision_type = "bfloat16"
     try:
         cpu = _run(_small_alexnet(), "imagenet", "cpu", 5, 16, n_classes=16)
+        flo = _run(_small_alexnet(), "imagenet", "cpu", 5, 16, n_classes=16,
+                   bf16_storage=True)
         hip = _run(_small_alexnet(), "imagenet", "hip", 5, 16, n_classes=16)
     finally:
         root.common.engine.precision_type = old
-    worst = _compare(cpu, hip)
-    print("reduced AlexNet: worst relative update difference %.4f" % worst)
+    worst, floor = _compare(cpu, flo, hip)
+    print("reduced AlexNet: worst relative update difference %.4f "
+          "(bf16 floor %.4f)" % (worst, floor))
+
+
+def test_bf16_floor_emulation_changes_cpu_updates():
+    """CPU check of the floor run itself: it differs from float32, and by
+    more in the first layer than in the classifier."""
+    old = root.common.engine.precision_type
+    root.common.engine.precision_type = "bfloat16"
+    try:
+        cpu = _run(_small_alexnet(), "imagenet", "cpu", 1, 8, n_classes=16)
+        flo = _run(_small_alexnet(), "imagenet", "cpu", 1, 8, n_classes=16,
+                   bf16_storage=True)
+    finally:
+        root.common.engine.precision_type = old
+    floor = _rel_updates(cpu, flo)
+    assert 0 < floor[-1] < floor[0], floor

@@ -12,6 +12,22 @@ DEV = "cuda"
 BF = torch.bfloat16
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _gemm_variant():
+    """HVK_TEST_GEMM_VARIANT=v runs this module's GEMM / conv kernels on the
+    library's A/B schedule v (hvk_set_gemm_variant), default schedule
+    otherwise."""
+    import os
+    v = os.environ.get("HVK_TEST_GEMM_VARIANT")
+    if v is None:
+        yield
+        return
+    fn = ops._lib.lib().hvk_set_gemm_variant
+    fn(int(v))
+    yield
+    fn(-1)
+
+
 def rnd(*shape, scale=1.0, dtype=BF, seed=0):
     g = torch.Generator().manual_seed(seed + sum(shape))
     return (torch.randn(*shape, generator=g) * scale).to(dtype)
@@ -29,7 +45,9 @@ def close(gpu, ref, tol):
 @pytest.mark.parametrize("M,N,K", [(17, 1999, 231), (7, 9, 8), (9, 7, 800),
                                    (1, 1, 1), (256, 384, 512),
                                    (1000, 100, 784), (640, 512, 1000),
-                                   (384, 640, 64), (200, 136, 96)])
+                                   (384, 640, 64), (200, 136, 96),
+                                   # 96-row tile variant (65..96 rows)
+                                   (80, 300, 512), (96, 1024, 256)])
 def test_gemm_layouts(ta, tb, M, N, K):
     a = rnd(K, M) if ta else rnd(M, K)
     b = rnd(N, K, seed=1) if tb else rnd(K, N, seed=1)
