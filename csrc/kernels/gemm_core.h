@@ -766,12 +766,8 @@ __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2
 //      zero rows 96..127 of the 128-row tile;
 //   2  48 columns of a 64-wide tile (4 waves stacked along M, each 32 x 48):
 //      a 48-wide output (AlexNet conv2 backward-data, 48 channels per group).
-// MF32: v_mfma_f32_32x32x16_bf16 on 32 x 32 wave sub-tiles instead of
-// 16x16x32 on 16 x 16 ones (same wave tile, same LDS images and reads per
-// K tile; a quarter of the MFMA issues, each blocking issue for 8 of 32
-// cycles instead of 8 of 16).
 template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF, bool W8,
-          int VAR = 0, bool MF32 = false>
+          int VAR = 0>
 __global__ void __launch_bounds__(W8 ? 512 : NTHR, 2)
 gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
             int tiles_n, int tiles, int splits) {
@@ -784,9 +780,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   constexpr int NC = VAR == 2 ? 48 : BN_;      // columns computed per block
   constexpr int NB = NC / (16 * WNC);          // MFMA n-tiles per wave
   static_assert(BMC <= BM && NC <= BN_ && NB * 16 * WNC == NC, "layout");
-  constexpr int MT2 = WMR / 32, NB2 = NC / WNC / 32;  // 32 x 32 sub-tiles
-  static_assert(!MF32 || (VAR == 0 && MT2 * 32 == WMR &&
-                          NB2 * 32 * WNC == NC), "MF32 layout");
   static_assert(!W8 || BN_ % 64 == 0, "W8 needs BN 64 / 128");
   constexpr int CPR = BN_ / 8;          // MN-major B: chunks per k-row
   constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
@@ -820,21 +813,11 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 
   const int fr = lane & 15, fq = lane >> 4;
   const int trq = fr >> 2, trp = fr & 3;
-  f32x4 acc[MF32 ? 1 : MT][MF32 ? 1 : NB];  // 16x16 sub-tiles
-  f32x16 acc2[MF32 ? MT2 : 1][MF32 ? NB2 : 1];
-  if constexpr (MF32) {
+  f32x4 acc[MT][NB];
 #pragma unroll
-    for (int i = 0; i < MT2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NB2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc2[i][j][r] = 0.f;
-  } else {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto frag_k = [&](const uint16_t* s, int rowbase, int ks) -> bf16x8 {
     int row = rowbase + fr;
@@ -852,51 +835,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, v);
   };
-  // 32x32x16 operands: lane l holds row / column (l & 31), k = 8 (l >> 5)
-  // + 0..7 of the 16-deep slice kk
-  auto frag_k32 = [&](const uint16_t* s, int rowbase, int kk) -> bf16x8 {
-    int row = rowbase + (lane & 31);
-    int c = kk * 2 + (lane >> 5);
-    return *(const bf16x8*)(s + row * 64 + ((c ^ (row & 7)) << 3));
-  };
-  auto frag_mn32 = [&](const uint16_t* s, int colbase, int kk) -> bf16x8 {
-    // per 16-lane group g: the 16 columns 16 (g & 1) .. of the 32, k rows
-    // 8 (g >> 1) + trq and + 4
-    const int g = lane >> 4;
-    int k = kk * 16 + (g >> 1) * 8 + trq;
-    int b = (colbase >> 4) + (g & 1);
-    const uint16_t* p0 = s + k * 128 + ((b ^ hk(k)) << 4) + trp * 4;
-    const uint16_t* p1 = s + (k + 4) * 128 + ((b ^ hk(k + 4)) << 4) + trp * 4;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-    typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, v);
-  };
   auto compute = [&](const uint16_t* sA, const uint16_t* sB) {
-    if constexpr (MF32) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        bf16x8 af[MT2], bfv[NB2];
-#pragma unroll
-        for (int i = 0; i < MT2; ++i) {
-          if constexpr (AK) af[i] = frag_k32(sA, wm * WMR + i * 32, kk);
-          else af[i] = frag_mn32(sA, wm * WMR + i * 32, kk);
-        }
-#pragma unroll
-        for (int j = 0; j < NB2; ++j) {
-          if constexpr (BKM) bfv[j] = frag_k32(sB, wn * (NC / WNC) + j * 32, kk);
-          else bfv[j] = frag_mn32(sB, wn * (NC / WNC) + j * 32, kk);
-        }
-#pragma unroll
-        for (int i = 0; i < MT2; ++i)
-#pragma unroll
-          for (int j = 0; j < NB2; ++j)
-            acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                af[i], bfv[j], acc2[i][j], 0, 0, 0);
-      }
-      return;
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[MT], bfv[NB];
@@ -1150,23 +1089,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
   }  // register-staged path
 
-  // 32x32 accumulator element r: row (r & 3) + 8 (r >> 2) + 4 (lane >> 5),
-  // column lane & 31
-  if constexpr (MF32) {
-    if (epi.atomic) {
-#pragma unroll
-      for (int i = 0; i < MT2; ++i)
-#pragma unroll
-        for (int j = 0; j < NB2; ++j) {
-          int mb = m0 + wm * WMR + i * 32 + 4 * (lane >> 5);
-          int n = n0 + wn * (NC / WNC) + j * 32 + (lane & 31);
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            epi.store(gi, mb + (r & 3) + 8 * (r >> 2), n, acc2[i][j][r]);
-        }
-      return;
-    }
-  } else if (epi.atomic) {
+  if (epi.atomic) {
     // split-K partial sums: f32 atomics straight from the accumulators
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -1182,18 +1105,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   // stage the f32 tile through LDS, then row-contiguous 16-B stores
   constexpr int LDC = BN_ + 4;
   float* sC = (float*)smem;
-  if constexpr (MF32) {
-#pragma unroll
-    for (int i = 0; i < MT2; ++i)
-#pragma unroll
-      for (int j = 0; j < NB2; ++j) {
-        int rb = wm * WMR + i * 32 + 4 * (lane >> 5);
-        int cc = wn * (NC / WNC) + j * 32 + (lane & 31);
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          sC[(rb + (r & 3) + 8 * (r >> 2)) * LDC + cc] = acc2[i][j][r];
-      }
-  } else {
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -1203,7 +1114,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + cc] = acc[i][j][rr];
     }
-  }
   __syncthreads();
   constexpr int CH = NC / 8;
   const bool fast = epi.fast_ok();
@@ -1261,26 +1171,15 @@ bool want_w8(const LA& la, const LB& lb, int bn) {
   return v == 1 || !std::is_base_of<ConvDgradA, LA>::value;
 }
 
-// one kernel instantiation; hvk_gemm_variant 2 (A/B only) runs the
-// 32x32x16 MFMA form where the wave tile allows it
+// one kernel instantiation
 template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF, bool W8,
           int VAR = 0>
 hipError_t go(const LA& la, const LB& lb, const Epi& epi, int M, int N, int K,
               int k_split, int tiles_n, int tiles, int splits, dim3 grid,
               hipStream_t s) {
-  constexpr bool can32 = VAR == 0 && (W8 ? BN_ == 128 : BN_ % 64 == 0);
-  const dim3 blk(W8 ? 512 : NTHR);
-  if constexpr (can32) {
-    if (hvk_gemm_variant == 2) {
-      hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, 0, true>),
-                         grid, blk, 0, s, la, lb, epi, M, N, K, k_split,
-                         tiles_n, tiles, splits);
-      return hipGetLastError();
-    }
-  }
   hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, VAR>), grid,
-                     blk, 0, s, la, lb, epi, M, N, K, k_split, tiles_n, tiles,
-                     splits);
+                     dim3(W8 ? 512 : NTHR), 0, s, la, lb, epi, M, N, K,
+                     k_split, tiles_n, tiles, splits);
   return hipGetLastError();
 }
 

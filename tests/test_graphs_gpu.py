@@ -26,15 +26,19 @@ LAYERS = [
     {"type": "softmax", "->": {"output_sample_shape": 10}, "<-": dict(G)}]
 
 
-def _train(graphs, steps, precision="bfloat16", layers=LAYERS):
+def _train(graphs, steps, precision="bfloat16", layers=LAYERS,
+           overlap=True, bucket_mb=32):
     from veles_amd.backends import Device
     from veles_amd.dummy import DummyLauncher
     from veles_amd.models import StandardWorkflow
     from veles_amd.prng import random_generator
     import veles_amd.loader  # noqa: F401
-    old = (root.common.engine.graphs, root.common.engine.precision_type)
+    old = (root.common.engine.graphs, root.common.engine.precision_type,
+           root.common.engine.overlap_update, root.common.engine.dp.bucket_mb)
     root.common.engine.graphs = graphs
     root.common.engine.precision_type = precision
+    root.common.engine.overlap_update = overlap
+    root.common.engine.dp.bucket_mb = bucket_mb
     try:
         random_generator.get().seed(1234)
         numpy.random.seed(1234)
@@ -51,7 +55,9 @@ def _train(graphs, steps, precision="bfloat16", layers=LAYERS):
         torch.cuda.synchronize()
         return wf
     finally:
-        root.common.engine.graphs, root.common.engine.precision_type = old
+        (root.common.engine.graphs, root.common.engine.precision_type,
+         root.common.engine.overlap_update,
+         root.common.engine.dp.bucket_mb) = old
 
 
 def _rel(a, b):
@@ -176,3 +182,23 @@ def test_capture_broken_by_a_sync_pins_eager_and_restores_state():
     assert graphed.param_store_.steps == eager.param_store_.steps == steps
     assert seen["n"] >= steps
     assert _rel(graphed.param_store_.master, eager.param_store_.master) < 2e-2
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_single_rank_overlapped_update_matches_serial(graphs):
+    """One rank, several buckets: each bucket's SGD runs on the side stream
+    as soon as its layers' backward is enqueued (ParameterStore
+    ._single_overlap), eagerly and inside the captured backward.  Same
+    trajectory as the one fused update at the end of the step."""
+    steps = 12
+    ser = _train(graphs, steps, overlap=False, bucket_mb=0.05)
+    ovl = _train(graphs, steps, overlap=True, bucket_mb=0.05)
+    st = ovl.param_store_
+    assert len(st.buckets) > 2 and st._single is True
+    assert ser.param_store_._single is False
+    if graphs:
+        assert ovl.graph_segments_[1].failures == 0
+        assert ovl.graph_segments_[1].replays > 0
+    assert st.steps == ser.param_store_.steps == steps
+    assert _rel(st.master, ser.param_store_.master) < 2e-2
+    assert torch.equal(st.lp, st.master.to(st.lp.dtype))

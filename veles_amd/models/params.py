@@ -86,6 +86,7 @@ class ParameterStore(object):
         self.zero_tail = 0
         # multi-rank: per-bucket updates on a side stream (_overlap_update)
         self._overlap = None
+        self._single = None   # single-rank overlapped update (decided once)
         self._upd_stream = None
         self._bucket_tables = {}
         # workgroups of a side-stream bucket update (0: the full grid); one
@@ -256,6 +257,12 @@ class ParameterStore(object):
         for p in params:
             self._ready.add(id(p))
         if not self._multi():
+            if self._single_overlap():
+                for i, b in enumerate(self.buckets):
+                    if i not in self._launched and \
+                            all(id(p) in self._ready for p in b):
+                        self._launched.add(i)
+                        self._bucket_update(i, None)
             return
         if self._accum_count + 1 < self.accumulate:
             return
@@ -337,6 +344,28 @@ class ParameterStore(object):
         self._cached_segments()
         return self._solver_segs is None
 
+    def _single_overlap(self):
+        """One rank on a GPU, plain SGD, no accumulation: each bucket's
+        update runs on the side stream as soon as its GD units are enqueued
+        (after their backward-data GEMMs, the last readers of the bf16
+        weights in this step), while the lower layers are still in backward.
+        AlexNet: the 58 M classifier parameters (0.2 ms of HBM-bound update)
+        run under the convolutions' backward.  Off with
+        ``root.common.engine.overlap_update = False`` or
+        ``VELES_AMD_OVERLAP_UPDATE=0``."""
+        if self._single is None:
+            from veles_amd.utils.config import root, get
+            on = os.environ.get(
+                "VELES_AMD_OVERLAP_UPDATE",
+                "1" if get(root.common.engine.overlap_update, True) else "0")
+            gpu = self.master is not None and self.master.is_cuda
+            self._single = (on != "0" and gpu and not self._multi() and
+                            self.accumulate == 1 and len(self.buckets) > 1)
+            if self._single:
+                self._cached_segments()
+                self._single = self._solver_segs is None
+        return self._single
+
     def _bucket_span(self, i):
         """[lo, hi) of bucket i's update: from its first parameter to the
         next bucket's (the last bucket to ``total``), so the spans tile the
@@ -346,15 +375,21 @@ class ParameterStore(object):
             else self.total
         return lo, hi
 
-    def _bucket_update(self, i, work):
-        import torch
-        from veles_amd import ops
+    def _bucket_segs(self, i):
+        """The update segments inside bucket i's span, span-relative."""
         lo, hi = self._bucket_span(i)
         segs = []
         for b, e, lr, d, l1, m in self._cached_segments():
             b, e = max(b, lo), min(e, hi)
             if b < e:
                 segs.append((b - lo, e - lo, lr, d, l1, m))
+        return segs
+
+    def _bucket_update(self, i, work):
+        import torch
+        from veles_amd import ops
+        lo, hi = self._bucket_span(i)
+        segs = self._bucket_segs(i)
         if not segs and not self.master.is_cuda:
             work.wait()
             self._finish_bucket(i)
@@ -374,12 +409,18 @@ class ParameterStore(object):
             return
         if self._upd_stream is None:
             self._upd_stream = torch.cuda.Stream(device=self.master.device)
+        if work is None:
+            # one rank: the side stream waits for the compute stream (the
+            # bucket's GD kernels); joined back in apply()
+            self._upd_stream.wait_stream(
+                torch.cuda.current_stream(self.master.device))
         # the side stream waits for this bucket's collective (which itself
         # waited for the compute stream at launch); its writes to the bf16
         # copy cannot race the forward, which finished before that point
         with torch.cuda.stream(self._upd_stream):
-            work.wait()
-            self._finish_bucket(i)
+            if work is not None:
+                work.wait()
+                self._finish_bucket(i)
             if segs:
                 ops.sgd_update(*args, **kw)
 
@@ -426,7 +467,17 @@ class ParameterStore(object):
             self._ready.clear()
             return False
         overlapped = False
-        if self._multi():
+        if not self._multi() and self._single_overlap():
+            for i in range(len(self.buckets)):
+                if i not in self._launched:
+                    self._launched.add(i)
+                    self._bucket_update(i, None)
+            overlapped = True
+            if self._upd_stream is not None:
+                import torch
+                torch.cuda.current_stream(self.master.device).wait_stream(
+                    self._upd_stream)
+        elif self._multi():
             ev = None
             if self.comm_stats and self.master.is_cuda:
                 import torch
@@ -521,6 +572,9 @@ class ParameterStore(object):
             self._seg_table.update(ops._pack_solver_segs(self._solver_segs))
         else:
             self._seg_table.update(ops._pack_sgd_segs(segs))
+            # per-bucket tables of the overlapped updates
+            for i, tab in self._bucket_tables.items():
+                tab.update(ops._pack_sgd_segs(self._bucket_segs(i)))
 
     def replayed_step(self):
         """Host bookkeeping of one update whose kernels ran in a graph."""
