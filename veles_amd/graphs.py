@@ -119,6 +119,7 @@ class _HipCapture(object):
             self.graph.capture_begin(capture_error_mode="thread_local")
         except BaseException:
             self._leave()
+            self.retire_stream()
             raise
         return self
 
@@ -128,11 +129,23 @@ class _HipCapture(object):
             ctx.__exit__(None, None, None)
 
     def __exit__(self, *exc):
+        ok = False
         try:
             self.graph.capture_end()
+            ok = True
         finally:
             self._leave()
+            if not ok:
+                self.retire_stream()
         return False
+
+    @staticmethod
+    def retire_stream():
+        """A capture that ended in an error can leave its stream in the
+        invalidated capture state on HIP (the next ``capture_begin`` on it
+        fails with hipStreamCaptureStatusInvalidated): later captures get a
+        fresh stream."""
+        _HipCapture._stream = None
 
 
 class GraphSegment(object):

@@ -349,15 +349,17 @@ class ParameterStore(object):
         update runs on the side stream as soon as its GD units are enqueued
         (after their backward-data GEMMs, the last readers of the bf16
         weights in this step), while the lower layers are still in backward.
-        AlexNet: the 58 M classifier parameters (0.2 ms of HBM-bound update)
-        run under the convolutions' backward.  Off with
-        ``root.common.engine.overlap_update = False`` or
-        ``VELES_AMD_OVERLAP_UPDATE=0``."""
+        Off by default (``root.common.engine.overlap_update = True`` or
+        ``VELES_AMD_OVERLAP_UPDATE=1`` turn it on): on AlexNet b1024 the
+        side-stream update of the 58 M classifier parameters slowed the
+        concurrent weight-gradient GEMMs by more than the 0.22 ms it took
+        off the critical path (132.2k -> 129.1k img/s,
+        profiles/r3_experiments.md §7)."""
         if self._single is None:
             from veles_amd.utils.config import root, get
             on = os.environ.get(
                 "VELES_AMD_OVERLAP_UPDATE",
-                "1" if get(root.common.engine.overlap_update, True) else "0")
+                "1" if get(root.common.engine.overlap_update, False) else "0")
             gpu = self.master is not None and self.master.is_cuda
             self._single = (on != "0" and gpu and not self._multi() and
                             self.accumulate == 1 and len(self.buckets) > 1)
