@@ -975,6 +975,166 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8p_kernel(
   }
 }
 
+// The same forward as a vertical walk: a thread owns one output column
+// (x 8 channels) over a strip of R output rows.  Consecutive windows share
+// an input row (window oh covers rows 2oh .. 2oh+2), so after the strip's
+// first window each output row evaluates the LRN of 6 window pixels instead
+// of 9, and the column max of the shared row (value and column index) is
+// carried into the next window.  The LRN runs on PAIRS of pixels (row
+// 2oh+1 and row 2oh+2 of one column) in float2 lanes, so its squares, window
+// sums, scale and product are v_pk_* instructions.  Per channel the
+// arithmetic, its order and the window scan order are those of
+// lrn_pool3s2_fwd_u8_kernel (first maximum in row-major window order): the
+// outputs and argmax bytes are bit-identical.  half <= 2: the halo is the
+// dword on each side of the thread's 8 channels.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+struct LrnPx {   // one pixel's channels c0-2 .. c0+9 (bf16 pairs)
+  uint32_t lo, hi;
+  uint4 mid;
+};
+
+__device__ __forceinline__ LrnPx lrn_ldpx(const uint16_t* px, int c0,
+                                          bool has_lo, bool has_hi) {
+  LrnPx r;
+  // in-range addresses always (c0 for an absent halo), zeroed after
+  const uint32_t lo = *(const uint32_t*)(px + (has_lo ? c0 - 2 : c0));
+  const uint32_t hi = *(const uint32_t*)(px + (has_hi ? c0 + 8 : c0));
+  r.mid = *(const uint4*)(px + c0);
+  r.lo = has_lo ? lo : 0u;
+  r.hi = has_hi ? hi : 0u;
+  return r;
+}
+
+// y[q] = x * (k + alpha * sum of the window's squares)^-beta for channels
+// c0 + q of pixel a (.x) and pixel b (.y)
+template <int half>
+__device__ __forceinline__ void lrn_pair(const LrnPx& a, const LrnPx& b,
+                                         float alpha, float beta, float k,
+                                         f32x2v* y) {
+  f32x2v v[12];
+  auto up = [](uint32_t ua, uint32_t ub, f32x2v& l, f32x2v& h) {
+    l = f32x2v{__uint_as_float(ua << 16), __uint_as_float(ub << 16)};
+    h = f32x2v{__uint_as_float(ua & 0xffff0000u),
+               __uint_as_float(ub & 0xffff0000u)};
+  };
+  up(a.lo, b.lo, v[0], v[1]);
+  up(a.mid.x, b.mid.x, v[2], v[3]);
+  up(a.mid.y, b.mid.y, v[4], v[5]);
+  up(a.mid.z, b.mid.z, v[6], v[7]);
+  up(a.mid.w, b.mid.w, v[8], v[9]);
+  up(a.hi, b.hi, v[10], v[11]);
+  f32x2v e[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) e[j] = v[j] * v[j];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    // ascending channel order from 0, as lrn_s
+    f32x2v w = e[q + 2 - half];
+#pragma unroll
+    for (int d = 1 - half; d <= half; ++d) w = w + e[q + 2 + d];
+    const f32x2v sv = k + alpha * w;
+    f32x2v l2 = f32x2v{__log2f(sv.x), __log2f(sv.y)};
+    l2 = -beta * l2;
+    y[q] = v[q + 2] * f32x2v{exp2f(l2.x), exp2f(l2.y)};
+  }
+}
+
+template <int half, bool PF>
+__global__ __launch_bounds__(256) void lrn_pool3s2_fwd_walk_kernel(
+    const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+    uint8_t* __restrict__ argmax, int N, int H, int W, int C, int OH, int OW,
+    int R, int S, float alpha, float beta, float k, FastDiv fCV, FastDiv fOW,
+    FastDiv fS) {
+  static_assert(half >= 1 && half <= 2, "dword halo");
+  const int CV = C >> 3;
+  const int total = N * S * OW * CV;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t t1, cvu, t2, owu, nu, su;
+    fdivmod((uint32_t)e, fCV, t1, cvu);
+    fdivmod(t1, fOW, t2, owu);
+    fdivmod(t2, fS, nu, su);
+    const int c0 = (int)cvu * 8, w0 = (int)owu * 2;
+    const int oh0 = (int)su * R, oh1 = min(OH, oh0 + R);
+    const bool has_lo = c0 >= 8, has_hi = c0 + 8 < C;
+    const uint16_t* img = x + (long long)nu * H * W * C;
+    const bool c1v = w0 + 1 < W, c2v = w0 + 2 < W;
+    const int wc1 = c1v ? w0 + 1 : W - 1, wc2 = c2v ? w0 + 2 : W - 1;
+    auto px = [&](int h, int w) { return img + ((long long)h * W + w) * C; };
+    // column max of a row: value and column (first maximum)
+    auto rowmax = [&](float y0, float y1v, float y2v, float& b, int& bi) {
+      b = y0;
+      bi = 0;
+      if (c1v && y1v > b) { b = y1v; bi = 1; }
+      if (c2v && y2v > b) { b = y2v; bi = 2; }
+    };
+    float cb[8];
+    int ci[8];
+    {   // the strip's first window row
+      const int h = 2 * oh0;
+      const LrnPx p0 = lrn_ldpx(px(h, w0), c0, has_lo, has_hi);
+      const LrnPx p1 = lrn_ldpx(px(h, wc1), c0, has_lo, has_hi);
+      const LrnPx p2 = lrn_ldpx(px(h, wc2), c0, has_lo, has_hi);
+      f32x2v ya[8], yb[8];
+      lrn_pair<half>(p0, p1, alpha, beta, k, ya);
+      lrn_pair<half>(p2, p2, alpha, beta, k, yb);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) rowmax(ya[q].x, ya[q].y, yb[q].x, cb[q], ci[q]);
+    }
+    // rows 2oh+1 / 2oh+2 of the three window columns; the next output
+    // row's six pixels are loaded before this row's arithmetic (clamped
+    // row indexes: always in range, masked by r1v / r2v when used)
+    LrnPx a[3], b[3];
+    auto load_rows = [&](int oh, LrnPx* ra, LrnPx* rb) {
+      const int hc1 = min(2 * oh + 1, H - 1), hc2 = min(2 * oh + 2, H - 1);
+      ra[0] = lrn_ldpx(px(hc1, w0), c0, has_lo, has_hi);
+      ra[1] = lrn_ldpx(px(hc1, wc1), c0, has_lo, has_hi);
+      ra[2] = lrn_ldpx(px(hc1, wc2), c0, has_lo, has_hi);
+      rb[0] = lrn_ldpx(px(hc2, w0), c0, has_lo, has_hi);
+      rb[1] = lrn_ldpx(px(hc2, wc1), c0, has_lo, has_hi);
+      rb[2] = lrn_ldpx(px(hc2, wc2), c0, has_lo, has_hi);
+    };
+    load_rows(oh0, a, b);
+    for (int oh = oh0; oh < oh1; ++oh) {
+      const bool r1v = 2 * oh + 1 < H, r2v = 2 * oh + 2 < H;
+      LrnPx na[3], nb[3];
+      if constexpr (PF) load_rows(min(oh + 1, oh1 - 1), na, nb);
+      else if (oh > oh0) load_rows(oh, a, b);
+      f32x2v yc[3][8];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) lrn_pair<half>(a[c], b[c], alpha, beta, k, yc[c]);
+      uint16_t o[8];
+      uint8_t ai[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float b1, b2;
+        int i1, i2;
+        rowmax(yc[0][q].x, yc[1][q].x, yc[2][q].x, b1, i1);
+        rowmax(yc[0][q].y, yc[1][q].y, yc[2][q].y, b2, i2);
+        float best = cb[q];
+        int bi = ci[q];
+        if (r1v && b1 > best) { best = b1; bi = 3 + i1; }
+        if (r2v && b2 > best) { best = b2; bi = 6 + i2; }
+        o[q] = f2bf(best);
+        ai[q] = (uint8_t)bi;
+        cb[q] = b2;   // this window's last row starts the next one
+        ci[q] = i2;
+      }
+      const long long yo = (((long long)nu * OH + oh) * OW + owu) * C + c0;
+      *(uint4*)(y + yo) = *(const uint4*)o;
+      *(uint2*)(argmax + yo) = *(const uint2*)ai;
+      if constexpr (PF) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          a[c] = na[c];
+          b[c] = nb[c];
+        }
+      }
+    }
+  }
+}
+
 template <int half>
 __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_u8_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
@@ -1318,6 +1478,12 @@ HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
   return (int)hipGetLastError();
 }
 
+// forward kernel selector for A/B runs (hvk_set_lrn_fwd_variant): 0 the
+// vertical walk with the next row prefetched, 1 the per-output preloading
+// kernel, 2 the walk without the prefetch
+static int g_lrn_fwd_variant = 0;
+HVK_API void hvk_set_lrn_fwd_variant(int v) { g_lrn_fwd_variant = v; }
+
 // Fused LRN -> 3x3 stride-2 max pooling with a uint8 window-index argmax
 // (see lrn_pool3s2_fwd_u8_kernel).  C % 8 == 0, n / 2 <= 4.
 HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
@@ -1329,6 +1495,22 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
     return -1;
   const int h = n / 2;
   const long long total = (long long)N * OH * OW * (C / 8);
+  if (h >= 1 && h <= 2 && g_lrn_fwd_variant != 1) {
+    // vertical walk over strips of about 9 output rows (enough threads to
+    // fill the chip at batch >= 64)
+    const int S = (OH + 8) / 9, R = (OH + S - 1) / S;
+    const long long tw = (long long)N * S * OW * (C / 8);
+    const bool pf = g_lrn_fwd_variant == 0;
+    auto kw = h == 1 ? (pf ? lrn_pool3s2_fwd_walk_kernel<1, true>
+                           : lrn_pool3s2_fwd_walk_kernel<1, false>)
+                     : (pf ? lrn_pool3s2_fwd_walk_kernel<2, true>
+                           : lrn_pool3s2_fwd_walk_kernel<2, false>);
+    hipLaunchKernelGGL(kw, dim3(grid_for(tw)), dim3(256), 0, s,
+                       (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N,
+                       H, W, C, OH, OW, R, S, alpha, beta, k,
+                       make_fastdiv(C / 8), make_fastdiv(OW), make_fastdiv(S));
+    return (int)hipGetLastError();
+  }
   if (h >= 1 && h <= 2) {
     auto kp = h == 1 ? lrn_pool3s2_fwd_u8p_kernel<1>
                      : lrn_pool3s2_fwd_u8p_kernel<2>;

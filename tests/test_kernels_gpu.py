@@ -477,6 +477,33 @@ def test_solver_kernel(mode):
 
 
 
+@pytest.mark.parametrize("shape,n", [
+    ((2, 55, 55, 96), 5), ((3, 13, 13, 16), 5), ((2, 14, 12, 8), 3),
+    ((1, 16, 17, 24), 3), ((2, 27, 27, 256), 5), ((1, 40, 9, 32), 5),
+    ((1, 41, 8, 8), 5)])
+def test_lrn_pool_fwd_walk_matches_per_output(shape, n):
+    """The vertical-walk forward (strips of output rows, the shared input
+    row's column max carried, pixel pairs in packed lanes) against the
+    per-output kernel: bit-identical outputs and window indices, including
+    strips that do not divide OH and windows clipped at the image edge."""
+    lib = ops._lib.lib()
+    x = rnd(*shape, scale=3.0).to(DEV)
+    res = []
+    for v in (1, 0, 2):
+        lib.hvk_set_lrn_fwd_variant(v)
+        N, H, W, C = shape
+        OH, OW = ops.pool_out_size(H, W, 3, 3, 2, 2)
+        am8 = torch.zeros(N, OH, OW, C, dtype=torch.uint8, device=DEV)
+        y8, _ = ops.lrn_pool_fwd(x, n, 1e-4 / n, 0.75, 1.0, 3, 3, (2, 2),
+                                 argmax=am8)
+        torch.cuda.synchronize()
+        res.append((y8.cpu(), am8.cpu()))
+    lib.hvk_set_lrn_fwd_variant(0)
+    for r in res[1:]:
+        assert torch.equal(res[0][0], r[0])
+        assert torch.equal(res[0][1], r[1])
+
+
 @pytest.mark.parametrize("shape,stride,n,aux_mode", [
     ((2, 27, 27, 96), 2, 5, "sep"), ((3, 13, 13, 16), 2, 5, "sep"),
     ((2, 55, 55, 96), 2, 5, "sep"), ((2, 55, 55, 96), 2, 5, "x"),

@@ -43,7 +43,33 @@ def main():
         g = lambda: ops.lrn_pool_bwd(x, dp, am, kw["n"], kw["alpha"],  # noqa
                                      kw["beta"], kw["k"], 3, 3, (2, 2),
                                      aux=x, aux_act=3, out=dx)
-        tf, tb = timeit(f), timeit(g)
+        setv = getattr(ops._lib.lib(), "hvk_set_lrn_fwd_variant", None)
+        tf = None
+        if setv is not None:
+            # forward A/B (interleaved, median of 5): 0 walk + prefetch,
+            # 1 per-output, 2 walk; and they must agree bit for bit
+            outs, ts = {}, {0: [], 1: [], 2: []}
+            for v in (0, 1, 2):
+                setv(v)
+                f()
+                torch.cuda.synchronize()
+                outs[v] = (y.clone(), am.clone())
+            for _ in range(5):
+                for v in (0, 1, 2):
+                    setv(v)
+                    ts[v].append(timeit(f))
+            setv(0)
+            same = all(torch.equal(outs[0][0], outs[v][0]) and
+                       torch.equal(outs[0][1], outs[v][1]) for v in (1, 2))
+            med = {v: sorted(t)[2] for v, t in ts.items()}
+            res.setdefault("fwd_ab", {})[name] = {
+                "walk_pf_us": round(med[0], 1), "perout_us": round(med[1], 1),
+                "walk_us": round(med[2], 1), "bit_identical": same}
+            print(name, "fwd walk+prefetch %.1f us, per-output %.1f us, "
+                  "walk %.1f us, identical %s"
+                  % (med[0], med[1], med[2], same), flush=True)
+            tf = med[0]
+        tf, tb = tf or timeit(f), timeit(g)
         bf = x.numel() * 2 + y.numel() * 3
         bb = x.numel() * 4 + dp.numel() * 3
         res[name] = {"fwd_us": round(tf, 1), "fwd_TBps": round(bf / tf / 1e6, 2),
