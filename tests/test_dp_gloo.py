@@ -385,6 +385,20 @@ def test_multi_node_respawn_needs_shared_snapshot_dir(tmp_path, monkeypatch):
     for t in ts:
         t.join(20)
     assert ok == [True, True]
+    # what that job left under the tag proves nothing to the next launch:
+    # node 1 alone (node 0 not started) must still time out, and so must
+    # node 0 alone
+    for r in (1, 0):
+        with pytest.raises(ValueError, match="shared"):
+            check_shared_dir(shared, 2, r, "job", timeout=0.6)
+    # and a fresh pair under the same tag passes again
+    ok = [None, None]
+    ts = [threading.Thread(target=node, args=(r,)) for r in (1, 0)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(20)
+    assert ok == [True, True]
 
 
 def _digest_rank(rank, port, path, q):

@@ -24,6 +24,7 @@ import socket
 import subprocess
 import sys
 import time
+import uuid
 
 from veles_amd.backends import parse_device_spec
 
@@ -58,32 +59,78 @@ def snapshot_digest(path):
     return os.path.getsize(path), h.hexdigest()
 
 
+def _write_atomic(path, text):
+    tmp = "%s.%s.tmp" % (path, uuid.uuid4().hex)
+    with open(tmp, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
 def check_shared_dir(directory, nnodes, node_rank, tag, timeout=120.0,
                      poll=0.2):
     """Multi-node respawn resumes every node from ``directory``'s newest
     ``*_current`` snapshot, which only global rank 0 writes: unless the
     directory is shared by all nodes, nodes != 0 would resume from a stale
-    or no snapshot and diverge (momentum, epoch, loader position).  Each
-    node's launcher drops a marker named after the job ``tag`` and waits
-    until it sees the markers of all ``nnodes`` nodes; raises ValueError
-    when they do not all appear within ``timeout`` seconds."""
+    or no snapshot and diverge (momentum, epoch, loader position).
+
+    A challenge-response through files under ``.veles_nodes/<tag>``, with
+    fresh nonces on both sides, so that files an earlier job left under the
+    same tag prove nothing: node 0 publishes a random challenge; every other
+    node answers it with its own random nonce; node 0 accepts once every
+    node echoed THIS challenge and then publishes the accepted nonces; a
+    node accepts once its own nonce is listed.  Raises ValueError when this
+    does not complete within ``timeout`` seconds."""
     d = os.path.join(directory, ".veles_nodes", tag)
     os.makedirs(d, exist_ok=True)
-    with open(os.path.join(d, "node%d" % node_rank), "w") as f:
-        f.write(socket.gethostname())
-    want = ["node%d" % i for i in range(nnodes)]
+    chal_p, done_p = os.path.join(d, "challenge"), os.path.join(d, "done")
     deadline = time.time() + timeout
+
+    def fail(what):
+        raise ValueError(
+            "multi-node --respawn needs a snapshot directory shared by "
+            "every node: %s shows no %s after %.0f s (mount it on all nodes "
+            "or drop --respawn)" % (directory, what, timeout))
+
+    if node_rank == 0:
+        chal = uuid.uuid4().hex
+        _write_atomic(chal_p, chal)
+        while True:
+            got = {}
+            for i in range(1, nnodes):
+                r = (_read(os.path.join(d, "resp%d" % i)) or "").split()
+                if len(r) == 2 and r[0] == chal:
+                    got[i] = r[1]
+            if len(got) == nnodes - 1:
+                _write_atomic(done_p, "\n".join(
+                    [chal] + ["%d %s" % kv for kv in sorted(got.items())]))
+                return True
+            if time.time() >= deadline:
+                fail("answer to this launch's challenge from node(s) %s" % (
+                    ", ".join(str(i) for i in range(1, nnodes)
+                              if i not in got)))
+            time.sleep(poll)
+    mine = uuid.uuid4().hex
+    seen = None
     while True:
-        have = set(os.listdir(d))
-        if all(w in have for w in want):
+        chal = _read(chal_p)
+        if chal and chal != seen:
+            _write_atomic(os.path.join(d, "resp%d" % node_rank),
+                          "%s %s" % (chal, mine))
+            seen = chal
+        done = (_read(done_p) or "").split("\n")
+        if seen and done[0] == seen and \
+                "%d %s" % (node_rank, mine) in done[1:]:
             return True
         if time.time() >= deadline:
-            missing = [w for w in want if w not in have]
-            raise ValueError(
-                "multi-node --respawn needs a snapshot directory shared by "
-                "every node: %s does not show %s after %.0f s (mount it on "
-                "all nodes or drop --respawn)" % (directory,
-                                                  ", ".join(missing), timeout))
+            fail("acceptance of node %d by node 0" % node_rank)
         time.sleep(poll)
 
 
