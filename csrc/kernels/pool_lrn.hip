@@ -1247,7 +1247,7 @@ __device__ __forceinline__ float lane_from_above(float v) {  // lane + 1
       0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
 }
 
-template <int half>
+template <int half, bool PRE>
 __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
     const uint8_t* __restrict__ argmax, uint16_t* __restrict__ dx, int N,
@@ -1275,14 +1275,48 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
     for (int p = 0; p < 4; ++p)
 #pragma unroll
       for (int q = 0; q < 8; ++q) g[p][q] = 0.f;
+    // PRE: every load of the iteration (4 windows' gradient + argmax, 4
+    // pixels of x) issued before any arithmetic, at clamped in-range
+    // addresses - one memory round trip per iteration instead of one per
+    // window and pixel
+    uint4 gvv[4], xr[4];
+    uint2 avv[4];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int wi = 0; wi < 4; ++wi) {
+        const int a = wi >> 1, b = wi & 1;
+        const int oh = (int)bhu - 1 + a, ow = (int)bwu - 1 + b;
+        const bool wv_ok = ok && oh >= 0 && ow >= 0 && oh < OH && ow < OW;
+        const long long yo = (((long long)nu * OH + min(max(oh, 0), OH - 1)) *
+                                  OW + min(max(ow, 0), OW - 1)) * C + c0;
+        gvv[wi] = *(const uint4*)(dp + yo);
+        const uint2 av = *(const uint2*)(argmax + yo);
+        // an absent window matches no pixel (index 0xff)
+        avv[wi] = wv_ok ? av : make_uint2(0xffffffffu, 0xffffffffu);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int hp = min((int)bhu * 2 + (p >> 1), H - 1);
+        const int wp = min((int)bwu * 2 + (p & 1), W - 1);
+        xr[p] = *(const uint4*)(x + (((long long)nu * H + hp) * W + wp) * C +
+                                c0);
+      }
+    }
 #pragma unroll
     for (int wi = 0; wi < 4; ++wi) {
       const int a = wi >> 1, b = wi & 1;
-      const int oh = (int)bhu - 1 + a, ow = (int)bwu - 1 + b;
-      if (!ok || oh < 0 || ow < 0 || oh >= OH || ow >= OW) continue;
-      const long long yo = (((long long)nu * OH + oh) * OW + ow) * C + c0;
-      const uint4 gv = *(const uint4*)(dp + yo);
-      const uint2 av = *(const uint2*)(argmax + yo);
+      uint4 gv;
+      uint2 av;
+      if constexpr (PRE) {
+        gv = gvv[wi];
+        av = avv[wi];
+      } else {
+        const int oh = (int)bhu - 1 + a, ow = (int)bwu - 1 + b;
+        if (!ok || oh < 0 || ow < 0 || oh >= OH || ow >= OW) continue;
+        const long long yo = (((long long)nu * OH + oh) * OW + ow) * C + c0;
+        gv = *(const uint4*)(dp + yo);
+        av = *(const uint2*)(argmax + yo);
+      }
       const uint16_t* gh = (const uint16_t*)&gv;
       const uint8_t* ah = (const uint8_t*)&av;
 #pragma unroll
@@ -1300,7 +1334,11 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
       const bool pv = ok && hp < H && wp < W;
       const long long po = (((long long)nu * H + hp) * W + wp) * C + c0;
       float xv[8];
-      if (pv) {
+      if constexpr (PRE) {
+        const uint16_t* h8 = (const uint16_t*)&xr[p];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xv[q] = pv ? bf2f(h8[q]) : 0.f;
+      } else if (pv) {
         load8(x + po, xv);
       } else {
 #pragma unroll
@@ -1483,6 +1521,10 @@ HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
 // kernel, 2 the walk without the prefetch
 static int g_lrn_fwd_variant = 0;
 HVK_API void hvk_set_lrn_fwd_variant(int v) { g_lrn_fwd_variant = v; }
+// backward selector (hvk_set_lrn_bwd_variant): 0 every load of an
+// iteration issued first, 1 loads next to their use
+static int g_lrn_bwd_variant = 0;
+HVK_API void hvk_set_lrn_bwd_variant(int v) { g_lrn_bwd_variant = v; }
 
 // Fused LRN -> 3x3 stride-2 max pooling with a uint8 window-index argmax
 // (see lrn_pool3s2_fwd_u8_kernel).  C % 8 == 0, n / 2 <= 4.
@@ -1550,10 +1592,15 @@ HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
     const long long nblk = (long long)N * BH * BW;
     const long long waves = (nblk + bpw - 1) / bpw;
     const long long blocks = std::min<long long>((waves + 3) / 4, 1 << 16);
-    auto kd = h == 1 ? lrn_pool3s2_bwd_dpp_kernel<1>
-            : h == 2 ? lrn_pool3s2_bwd_dpp_kernel<2>
-            : h == 3 ? lrn_pool3s2_bwd_dpp_kernel<3>
-                     : lrn_pool3s2_bwd_dpp_kernel<4>;
+    const bool pre = g_lrn_bwd_variant == 0;
+    auto kd = h == 1 ? (pre ? lrn_pool3s2_bwd_dpp_kernel<1, true>
+                            : lrn_pool3s2_bwd_dpp_kernel<1, false>)
+            : h == 2 ? (pre ? lrn_pool3s2_bwd_dpp_kernel<2, true>
+                            : lrn_pool3s2_bwd_dpp_kernel<2, false>)
+            : h == 3 ? (pre ? lrn_pool3s2_bwd_dpp_kernel<3, true>
+                            : lrn_pool3s2_bwd_dpp_kernel<3, false>)
+                     : (pre ? lrn_pool3s2_bwd_dpp_kernel<4, true>
+                            : lrn_pool3s2_bwd_dpp_kernel<4, false>);
     hipLaunchKernelGGL(kd, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const uint16_t*)x, (const uint16_t*)dp,
                        (const uint8_t*)argmax, (uint16_t*)dx, N, H, W, C, OH,

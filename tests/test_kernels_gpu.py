@@ -245,6 +245,42 @@ def test_conv_dgrad(cfg):
     close(got, ref, 1e-2)
 
 
+HALO_CONVS = [c for c in CONVS if c[7] == (1, 1)] + [
+    # AlexNet conv2 / conv1-after-space-to-depth / conv4 shapes (small batch)
+    (2, 27, 27, 96, 256, 5, 5, (1, 1), (2, 2, 2, 2), 2),
+    (2, 57, 57, 48, 96, 3, 3, (1, 1), (0, 0, 0, 0), 1),
+    (2, 13, 13, 384, 384, 3, 3, (1, 1), (1, 1, 1, 1), 2),
+    (3, 20, 23, 64, 40, 3, 3, (1, 1), (1, 1, 1, 1), 1)]
+
+
+@pytest.mark.parametrize("cfg", HALO_CONVS)
+def test_conv_halo_matches_implicit_gemm(cfg):
+    """Stride-1 forward / backward-data with the input tile in LDS
+    (conv_halo.hip) against the implicit-GEMM kernels: the same products in
+    the same MFMA order, so bit-identical outputs (where the halo path does
+    not apply it falls back, trivially identical)."""
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    x = rnd(N, H, W, C).to(DEV)
+    w = rnd(OC, KH, KW, C // g, seed=1, scale=0.1).to(DEV)
+    b = torch.randn(OC).to(DEV)
+    OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
+    dy = rnd(N, OH, OW, OC, seed=2).to(DEV)
+    aux = rnd(N, H, W, C, seed=3).to(DEV)
+    res = {}
+    for halo in (False, True):
+        ops.set_conv_halo(halo, dgrad=halo)
+        try:
+            y = ops.conv_fwd(x, w, b, sl, pad, g, 3)
+            dx = ops.conv_dgrad(dy, w, (N, H, W, C), sl, pad, g, aux=aux,
+                                aux_act=3)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_conv_halo(True, dgrad=False)
+        res[halo] = (y.cpu(), dx.cpu())
+    assert torch.equal(res[False][0], res[True][0])
+    assert torch.equal(res[False][1], res[True][1])
+
+
 @pytest.mark.parametrize("cfg", CONVS)
 def test_conv_wgrad(cfg):
     N, H, W, C, OC, KH, KW, sl, pad, g = cfg
@@ -502,6 +538,37 @@ def test_lrn_pool_fwd_walk_matches_per_output(shape, n):
     for r in res[1:]:
         assert torch.equal(res[0][0], r[0])
         assert torch.equal(res[0][1], r[1])
+
+
+@pytest.mark.parametrize("shape,n,aux_mode", [
+    ((2, 55, 55, 96), 5, "x"), ((2, 27, 27, 256), 5, "sep"),
+    ((2, 14, 12, 8), 3, "none"), ((1, 15, 17, 24), 9, "x"),
+    ((1, 9, 9, 512), 5, "sep")])
+def test_lrn_pool_bwd_preload_matches_inline(shape, n, aux_mode):
+    """The backward with every load of an iteration issued first (clamped
+    addresses, absent windows masked) against loads beside their use:
+    the same arithmetic, bit-identical gradients."""
+    lib = ops._lib.lib()
+    alpha, beta, k = 1e-4 / n, 0.75, 1.0
+    x = rnd(*shape, scale=3.0)
+    if aux_mode == "x":
+        x = x.clamp_min(0.0)
+    xg = x.to(DEV)
+    N, H, W, C = shape
+    OH, OW = ops.pool_out_size(H, W, 3, 3, 2, 2)
+    am8 = torch.zeros(N, OH, OW, C, dtype=torch.uint8, device=DEV)
+    y, _ = ops.lrn_pool_fwd(xg, n, alpha, beta, k, 3, 3, (2, 2), argmax=am8)
+    dp = rnd(*y.shape, seed=5).to(DEV)
+    aux = {"x": xg, "sep": rnd(*shape, seed=6).to(DEV), "none": None}[aux_mode]
+    outs = []
+    for v in (1, 0):
+        lib.hvk_set_lrn_bwd_variant(v)
+        outs.append(ops.lrn_pool_bwd(xg, dp, am8, n, alpha, beta, k, 3, 3,
+                                     (2, 2), aux=aux,
+                                     aux_act=3 if aux is not None else 0))
+        torch.cuda.synchronize()
+    lib.hvk_set_lrn_bwd_variant(0)
+    assert torch.equal(outs[0].cpu(), outs[1].cpu())
 
 
 @pytest.mark.parametrize("shape,stride,n,aux_mode", [

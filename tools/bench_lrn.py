@@ -69,7 +69,30 @@ def main():
                   "walk %.1f us, identical %s"
                   % (med[0], med[1], med[2], same), flush=True)
             tf = med[0]
-        tf, tb = tf or timeit(f), timeit(g)
+        setb = getattr(ops._lib.lib(), "hvk_set_lrn_bwd_variant", None)
+        tb = None
+        if setb is not None:
+            # backward A/B: 0 all loads first, 1 loads beside their use
+            outs, ts = {}, {0: [], 1: []}
+            for v in (0, 1):
+                setb(v)
+                g()
+                torch.cuda.synchronize()
+                outs[v] = dx.clone()
+            for _ in range(5):
+                for v in (0, 1):
+                    setb(v)
+                    ts[v].append(timeit(g))
+            setb(0)
+            same = bool(torch.equal(outs[0], outs[1]))
+            med = {v: sorted(t)[2] for v, t in ts.items()}
+            res.setdefault("bwd_ab", {})[name] = {
+                "preload_us": round(med[0], 1), "inline_us": round(med[1], 1),
+                "bit_identical": same}
+            print(name, "bwd preload %.1f us, inline %.1f us, identical %s"
+                  % (med[0], med[1], same), flush=True)
+            tb = med[0]
+        tf, tb = tf or timeit(f), tb or timeit(g)
         bf = x.numel() * 2 + y.numel() * 3
         bb = x.numel() * 4 + dp.numel() * 3
         res[name] = {"fwd_us": round(tf, 1), "fwd_TBps": round(bf / tf / 1e6, 2),

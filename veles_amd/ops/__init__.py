@@ -688,6 +688,38 @@ def im2col(x, KH, KW, sliding, padding, out=None):
     return out
 
 
+# stride-1 convolutions with the input tile held in LDS
+# (csrc/kernels/conv_halo.hip); False runs every conv on the implicit GEMM
+_HALO = True
+# the backward-data halo kernel measured slower than the implicit GEMM on
+# every AlexNet shape (profiles/r3_experiments.md §9): off unless asked for
+_HALO_DGRAD = False
+
+
+def set_conv_halo(on, dgrad=None):
+    """Enable / disable the LDS-halo stride-1 conv kernels (A/B runs);
+    ``dgrad`` sets the backward-data kernel separately (default: same as
+    ``on`` when given, else unchanged)."""
+    global _HALO, _HALO_DGRAD
+    _HALO = bool(on)
+    if dgrad is not None:
+        _HALO_DGRAD = bool(dgrad)
+
+
+def _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
+                   OH, OW, groups, act, stream):
+    if _HALO and sy == 1 and sx == 1 and out.is_contiguous():
+        rc = _lib.lib().hvk_conv_fwd_halo(
+            _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
+            OH, OW, groups, act, stream)
+        if rc == 0:
+            return
+        if rc != -2:
+            _lib.check(rc, "hvk_conv_fwd_halo")
+    _lib_call("hvk_conv_fwd", _p(x), _p(w), _p(bias), _p(out), N, H, W, C,
+              OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, act, stream)
+
+
 def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
              groups=1, act=0, out=None, col_out=None):
     """x [N,H,W,C], w [OC,KH,KW,C/g] -> y [N,OH,OW,OC].
@@ -720,18 +752,16 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
                 space_to_depth(x, s2, KH, KW, padding)
             w2 = _s2d_weights(w, s2)
             C2 = s2 * s2 * C
-            _lib_call("hvk_conv_fwd", _p(x2), _p(w2), _p(bias), _p(out), N,
-                      H2, W2, C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, act,
-                      _s(x))
+            _conv_fwd_call(x2, w2, bias, out, N, H2, W2, C2, OC, KH2, KW2,
+                           1, 1, 0, 0, OH, OW, 1, act, _s(x))
             if col_out is not None:
                 col_out["col"] = S2DImage(x2, s2, (N, H, W, C))
             return out
         if pad8_ok(C, groups):
             xp = _pad_channels(x)
             wp8 = _pad_weights(w, "wpad8")
-            _lib_call("hvk_conv_fwd", _p(xp), _p(wp8), _p(bias), _p(out), N,
-                      H, W, _cpad(C), OC, KH, KW, sy, sx, pt, pl, OH, OW, 1,
-                      act, _s(x))
+            _conv_fwd_call(xp, wp8, bias, out, N, H, W, _cpad(C), OC, KH,
+                           KW, sy, sx, pt, pl, OH, OW, 1, act, _s(x))
             if col_out is not None:
                 col_out["col"] = PaddedImage(xp, C)
             return out
@@ -756,8 +786,8 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
                       N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, act,
                       _s(x))
             return out
-        _lib_call("hvk_conv_fwd", _p(x), _p(w), _p(bias), _p(out), N, H, W, C,
-                  OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, act, _s(x))
+        _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt,
+                       pl, OH, OW, groups, act, _s(x))
         return out
     xp = F.pad(_nchw(x), (pl, pr, pt, pb))
     y = F.conv2d(xp, w.permute(0, 3, 1, 2).float(),
@@ -799,6 +829,14 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
             wt = _workspace(("dgrad_wt", id(w)), (groups, Cg, KH, KW, OCg),
                             w.dtype, w.device)
             wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1))
+        if _HALO_DGRAD and sx == 1 and sy == 1 and out.is_contiguous():
+            rc = _lib.lib().hvk_conv_dgrad_halo(
+                _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH,
+                OW, groups, _p(aux), aux_act, _s(dy))
+            if rc == 0:
+                return out
+            if rc != -2:
+                _lib.check(rc, "hvk_conv_dgrad_halo")
         _lib_call("hvk_conv_dgrad_t", _p(dy), _p(wt), _p(out), N, H, W, C,
                   OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, _p(aux),
                   aux_act, _s(dy))

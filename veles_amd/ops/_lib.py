@@ -33,6 +33,11 @@ _SIGS = {
                         I, P, I, P],
     "hvk_conv_fwd": [P, P, P, P] + [I] * 15 + [P],
     "hvk_conv_dgrad_t": [P, P, P] + [I] * 14 + [P, I, P],
+    # (X, Wt, bias, Y, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, act, s)
+    "hvk_conv_fwd_halo": [P, P, P, P] + [I] * 13 + [P],
+    # (dY, Wt, dX, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, aux,
+    #  aux_act, s)
+    "hvk_conv_dgrad_halo": [P, P, P] + [I] * 12 + [P, I, P],
     "hvk_conv_wgrad": [P, P, P] + [I] * 15 + [P, P],
     "hvk_conv_fwd_run": [P, P, P, P] + [I] * 14 + [P],
     "hvk_conv_fwd_direct": [P, P, P, P] + [I] * 14 + [P],
