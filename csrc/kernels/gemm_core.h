@@ -766,8 +766,11 @@ __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2
 //      zero rows 96..127 of the 128-row tile;
 //   2  48 columns of a 64-wide tile (4 waves stacked along M, each 32 x 48):
 //      a 48-wide output (AlexNet conv2 backward-data, 48 channels per group).
+// ABL (diagnostic builds only, selected by hvk_set_gemm_variant 11..13 in
+// A/B runs; wrong results by design): 1 half the MFMAs (ks = 0 only), 2 no
+// LDS-DMA after the first K tile, 3 neither DMA nor barriers after it.
 template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF, bool W8,
-          int VAR = 0>
+          int VAR = 0, int ABL = 0>
 __global__ void __launch_bounds__(W8 ? 512 : NTHR, 2)
 gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
             int tiles_n, int tiles, int splits) {
@@ -837,7 +840,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   };
   auto compute = [&](const uint16_t* sA, const uint16_t* sB) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < (ABL == 1 ? 1 : 2); ++ks) {
       bf16x8 af[MT], bfv[NB];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -1005,7 +1008,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
       issue(kbeg, smem, smem + 2 * SA);
       for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) {
+        if (kt + 1 < nk && ABL < 2) {
           issue(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * SA,
                 smem + 2 * SA + (cur ^ 1) * SB);
           // leave exactly the next tile's DMAs (NIA + NIB) in flight
@@ -1013,11 +1016,11 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __builtin_amdgcn_s_barrier();
+        if (ABL < 3 || kt == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         compute(smem + cur * SA, smem + 2 * SA + cur * SB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if (ABL < 3) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
       done = true;
@@ -1177,6 +1180,20 @@ template <class LA, bool AK, class LB, bool BKM, int BN_, bool BUF, bool W8,
 hipError_t go(const LA& la, const LB& lb, const Epi& epi, int M, int N, int K,
               int k_split, int tiles_n, int tiles, int splits, dim3 grid,
               hipStream_t s) {
+  if constexpr (W8 && BN_ == 128 && VAR == 0 && BUF && AK && BKM &&
+                std::is_same<LB, DenseK>::value &&
+                (std::is_same<LA, DenseK>::value ||
+                 std::is_same<LA, ConvFwdA>::value)) {
+    const int v = hvk_gemm_variant;
+    if (v >= 11 && v <= 13) {
+      auto k = v == 11 ? gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, 0, 1>
+             : v == 12 ? gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, 0, 2>
+                       : gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, 0, 3>;
+      hipLaunchKernelGGL(k, grid, dim3(512), 0, s, la, lb, epi, M, N, K,
+                         k_split, tiles_n, tiles, splits);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, VAR>), grid,
                      dim3(W8 ? 512 : NTHR), 0, s, la, lb, epi, M, N, K,
                      k_split, tiles_n, tiles, splits);
