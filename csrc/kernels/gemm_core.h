@@ -1152,184 +1152,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
 }
 
-// ---------------------------------------------------------------------------
-// 256 x 128 block tile for K-major A and B with buffer LDS-DMA (dense NT
-// GEMM, conv forward, stride-1 conv backward-data): 8 waves as 4 (M) x 2
-// (N), each 64 x 64 = 4 x 4 MFMA 16x16 tiles.  Per K tile the block moves
-// 48 KiB for 2 x 128 x 128 x 64 MACs: 0.75x the L2 -> LDS bytes per FLOP of
-// the 128 x 128 tile, which the main-loop ablation showed is what binds it
-// (profiles/r3_experiments.md §10).  One workgroup per CU (3-stage ring of
-// 48 KiB stages = 144 KiB): tile kt+2 is DMA'd while tile kt is computed, one
-// barrier per K tile (the stage a DMA overwrites was last read two tiles
-// ago, before that barrier).  The f32 C tile is staged in two 128-row
-// halves.
-constexpr int BM2 = 256, BN2 = 128, NST = 3;
-constexpr int SA2 = BM2 * BK, SB2 = BN2 * BK, SST = SA2 + SB2;
-
-template <class LA, class LB>
-__global__ void __launch_bounds__(512, 1)
-gemm256_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
-               int tiles_n, int tiles, int splits, int gm) {
-  constexpr int NW = 8, NT = 512;
-  constexpr int NIA = BM2 / (8 * NW), NIB = BN2 / (8 * NW);  // 4, 2
-  constexpr int NP = NIA + NIB;
-  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
-  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile = wgid % tiles;
-  const int gs = wgid / tiles;
-  const int gi = gs / splits;
-  int tm, tn;
-  if (gm > 1) {
-    const int tiles_m = tiles / tiles_n;
-    const int g = tile / (gm * tiles_n);
-    const int m0g = g * gm;
-    const int gh = min(tiles_m - m0g, gm);
-    const int r = tile - g * gm * tiles_n;
-    tm = m0g + r % gh;
-    tn = r / gh;
-  } else {
-    tm = tile / tiles_n;
-    tn = tile - tm * tiles_n;
-  }
-  const int kbeg = (gs - gi * splits) * k_split;
-  const int kend = min(K, kbeg + k_split);
-  if (kbeg >= kend) return;
-  la.group(gi);
-  lb.group(gi);
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int w = __builtin_amdgcn_readfirstlane(wid);
-  const int wm = wid >> 1, wn = wid & 1;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  // DMA slots: A piece I covers rows 8I .. 8I+7, B piece likewise; the
-  // lane's 16-B chunk along K is the same in every slot (XOR swizzle)
-  const int kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
-  const __amdgpu_buffer_rsrc_t ra = dma_rsrc(la.dbase());
-  const __amdgpu_buffer_rsrc_t rb = dma_rsrc(lb.dbase());
-  DRow fa[NIA];
-  uint32_t va[NIA], vb[NIB];
-#pragma unroll
-  for (int i = 0; i < NIA; ++i) {
-    const int row = m0 + 8 * (w * NIA + i) + (lane >> 3);
-    if constexpr (LA::kFast) fa[i] = la.drow(row);
-    else va[i] = la.row_voff(row);
-  }
-#pragma unroll
-  for (int i = 0; i < NIB; ++i)
-    vb[i] = lb.row_voff(n0 + 8 * (w * NIB + i) + (lane >> 3));
-  auto issue = [&](int k0, uint16_t* st) {
-    const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
-    if constexpr (LA::kFast) {
-      const DTap tp = la.dtap(k0 + kc);
-#pragma unroll
-      for (int i = 0; i < NIA; ++i)
-        dma16(ra, st + (w * NIA + i) * 512, la.dvoff(fa[i], tp));
-    } else {
-      const bool kin = k0 + kc < la.K;
-#pragma unroll
-      for (int i = 0; i < NIA; ++i)
-        dma16(ra, st + (w * NIA + i) * 512, kin ? va[i] + kbyte : kBufOOB);
-    }
-    const bool kinb = k0 + kc < lb.K;
-#pragma unroll
-    for (int i = 0; i < NIB; ++i)
-      dma16(rb, st + SA2 + (w * NIB + i) * 512, kinb ? vb[i] + kbyte : kBufOOB);
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto frag = [&](const uint16_t* sm, int rowbase, int ks) -> bf16x8 {
-    const int row = rowbase + fr;
-    const int c = ks * 4 + fq;
-    return *(const bf16x8*)(sm + row * 64 + ((c ^ (row & 7)) << 3));
-  };
-  auto compute = [&](const uint16_t* st) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(st, wm * 64 + i * 16, ks);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfv[j] = frag(st + SA2, wn * 64 + j * 16, ks);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
-                                                              acc[i][j], 0, 0, 0);
-    }
-  };
-
-  const int nk = (kend - kbeg + BK - 1) / BK;
-  issue(kbeg, dsm);
-  if (nk > 1) issue(kbeg + BK, dsm + SST);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (tile kt+1's pieces may stay in flight)
-    if (kt + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (kt + 2 < nk) issue(kbeg + (kt + 2) * BK, dsm + ((kt + 2) % NST) * SST);
-    compute(dsm + (kt % NST) * SST);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-
-  if (epi.atomic) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int mb = m0 + wm * 64 + i * 16 + fq * 4;
-        const int n = n0 + wn * 64 + j * 16 + fr;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) epi.store(gi, mb + rr, n, acc[i][j][rr]);
-      }
-    return;
-  }
-  // two 128-row halves through LDS, then row-contiguous 16-B stores
-  constexpr int LDC = BN2 + 4, CH = BN2 / 8;
-  float* sC = (float*)dsm;
-  const bool fast = epi.fast_ok();
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    __syncthreads();
-    if ((wm >> 1) == half) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int rb2 = (wm & 1) * 64 + i * 16 + fq * 4;
-          const int cc = wn * 64 + j * 16 + fr;
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-            sC[(rb2 + rr) * LDC + cc] = acc[i][j][rr];
-        }
-    }
-    __syncthreads();
-    const int mh = m0 + half * 128;
-    for (int q = t; q < 128 * CH; q += NT) {
-      const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
-      if (mh + row >= M) continue;
-      const float4* src = (const float4*)(sC + row * LDC + c8);
-      float v[8];
-      const float4 lo = src[0], hi = src[1];
-      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-      if (fast && n0 + c8 + 8 <= epi.N &&
-          (epi.ones_col < 0 || n0 + c8 + 8 <= epi.ones_col))
-        epi.store8_fast(gi, mh + row, n0 + c8, v);
-      else
-        epi.store8(gi, mh + row, n0 + c8, v);
-    }
-  }
-}
-
 // Tile width: 128 unless it wastes more than 1/8 of the columns; then 64,
 // or 96 for a single 96-wide column tile (K-major B only: AlexNet conv1,
 // N = 96, +16 % over 128).  N = 192 measured faster as 3 x 64 than as
@@ -1493,63 +1315,11 @@ hipError_t launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                                      tiles, splits, groups, bn, grid, s);
 }
 
-// the 256 x 128 tile applies: K-major A and B through buffer DMA (dense or
-// the fast stride-1 conv loaders), a 128-wide column tile, and enough
-// 256-row tiles to fill the chip; hvk_gemm_variant 30 turns it off (A/B)
-template <class LA, bool AK, class LB, bool BKM>
-bool use256(const LA& la, const LB& lb, int M, int bn, int tiles_n, int splits,
-            int groups) {
-  if constexpr (AK && BKM && LA::kBuf && LB::kBuf &&
-                std::is_same<LB, DenseK>::value &&
-                (std::is_same<LA, DenseK>::value ||
-                 std::is_same<LA, ConvFwdA>::value ||
-                 std::is_same<LA, ConvDgradA>::value)) {
-    if (hvk_gemm_variant == 30 || bn != 128) return false;
-    if (!la.dma_ok() || !lb.dma_ok() || !la.buf_ok(groups) ||
-        !lb.buf_ok(groups))
-      return false;
-    const long long blocks =
-        (long long)((M + BM2 - 1) / BM2) * tiles_n * splits * groups;
-    return blocks >= 512;
-  }
-  return false;
-}
-
-template <class LA, class LB>
-hipError_t launch256(const LA& la, const LB& lb, const Epi& epi, int M, int N,
-                     int K, int k_split, int tiles_n, int splits, int groups,
-                     hipStream_t s) {
-  static bool attr = false;  // once, before any capture
-  if (!attr) {
-    hipError_t err = hipFuncSetAttribute(
-        (const void*)gemm256_kernel<LA, LB>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, NST * SST * 2);
-    if (err != hipSuccess) return err;
-    attr = true;
-  }
-  const int tiles_m = (M + BM2 - 1) / BM2;
-  const int tiles = tiles_m * tiles_n;
-  const int gm = (tiles_n >= 4 && hvk_gemm_variant != 20) ? 8 : 1;
-  const dim3 grid((unsigned)((long long)tiles * splits * groups));
-  hipLaunchKernelGGL((gemm256_kernel<LA, LB>), grid, dim3(512),
-                     NST * SST * 2, s, la, lb, epi, M, N, K, k_split, tiles_n,
-                     tiles, splits, gm);
-  return hipGetLastError();
-}
-
 template <class LA, bool AK, class LB, bool BKM>
 hipError_t launch_sel(const LA& la, const LB& lb, const Epi& epi, int M,
                       int N, int K, int k_split, int tiles_n, int tiles,
                       int splits, int groups, int bn, dim3 grid,
                       hipStream_t s) {
-  if constexpr (AK && BKM && std::is_same<LB, DenseK>::value &&
-                (std::is_same<LA, DenseK>::value ||
-                 std::is_same<LA, ConvFwdA>::value ||
-                 std::is_same<LA, ConvDgradA>::value)) {
-    if (use256<LA, AK, LB, BKM>(la, lb, M, bn, tiles_n, splits, groups))
-      return launch256<LA, LB>(la, lb, epi, M, N, K, k_split, tiles_n, splits,
-                               groups, s);
-  }
   if constexpr (LA::kBuf || LB::kBuf) {
     if ((!LA::kBuf || la.buf_ok(groups)) && (!LB::kBuf || lb.buf_ok(groups)))
       return launch_bn<LA, AK, LB, BKM, true>(la, lb, epi, M, N, K, k_split,

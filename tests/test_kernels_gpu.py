@@ -59,58 +59,6 @@ def test_gemm_layouts(ta, tb, M, N, K):
     close(got, ref, 2e-3)
 
 
-def _with_variant(v, fn):
-    lib = ops._lib.lib()
-    lib.hvk_set_gemm_variant(v)
-    try:
-        out = fn()
-        torch.cuda.synchronize()
-        return out
-    finally:
-        lib.hvk_set_gemm_variant(-1)
-
-
-@pytest.mark.parametrize("M,N,K,bias,act", [(16384, 1024, 320, True, 3),
-                                            (20000, 1152, 200, False, 0)])
-def test_gemm_256_row_tile(M, N, K, bias, act):
-    """The 256 x 128 tile (3-stage ring, one workgroup per CU) on a dense NT
-    GEMM large enough to select it: against an fp32 reference, and
-    bit-identical to the 128-row kernel (same MFMA chain per element)."""
-    a = rnd(M, K).to(DEV)
-    b = rnd(N, K, seed=1).to(DEV)
-    bs = torch.randn(N, device=DEV) if bias else None
-    run = lambda: ops.gemm(a, b, trans_b=True, bias=bs, act=act)  # noqa
-    big = _with_variant(-1, run)
-    small = _with_variant(30, run)
-    assert torch.equal(big, small)
-    ref = a.float() @ b.float().t()
-    if bias:
-        ref = ref + bs
-    if act == 3:
-        ref = torch.relu(ref)
-    close(big, ref, 2e-2)
-
-
-def test_conv_256_row_tile_matches_128():
-    """Conv forward and stride-1 backward-data on the 256-row tile (AlexNet
-    conv2 geometry at a batch that selects it) equal the 128-row kernels."""
-    N, H, W, C, OC, k, p, g = 96, 27, 27, 96, 256, 5, 2, 2
-    x = rnd(N, H, W, C).to(DEV)
-    w = rnd(OC, k, k, C // g, seed=1, scale=0.1).to(DEV)
-    b = torch.randn(OC).to(DEV)
-    dy = rnd(N, H, W, OC, seed=2).to(DEV)
-    run = lambda: (ops.conv_fwd(x, w, b, (1, 1), (p, p, p, p), g, 3),  # noqa
-                   ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1), (p, p, p, p),
-                                  g))
-    y1, d1 = _with_variant(-1, run)
-    y0, d0 = _with_variant(30, run)
-    assert torch.equal(y1, y0)
-    assert torch.equal(d1, d0)
-    ref = ops.conv_fwd(x[:4].cpu(), w.cpu(), b.cpu(), (1, 1), (p, p, p, p),
-                       g, 3)
-    close(y1[:4], ref, 1e-2)
-
-
 def test_gemm_restrides_unaligned_rows():
     """Operands whose rows miss the 16-B grid (odd pitch, offset views) are
     re-strided before the LDS-DMA kernel: same result as aligned copies."""
