@@ -175,10 +175,24 @@ struct Epi8 {
   const float* sb;
   int hist;
   float fa, fb;          // effective fp8 maxima of A and B
+  // fused quantisation for the NEXT fp8 op (optional): q8 (same indexing as
+  // c) = sat(bf16(out) * scale(q8_st)) in format q8_fmt, and amax|bf16(out)|
+  // into one of 32 shards of q8_shard (one atomicMax per workgroup; the
+  // registry's roll folds the shards into the current amax)
+  uint8_t* q8;
+  const float* q8_st;
+  float* q8_shard;
+  float q8_fmax;
+  int q8_fmt;
 };
 
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c,
+                                              float d, int fmt);
+__device__ __forceinline__ float sat(float v, float lim);
+
 __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
-                                       int m, int n, const float* v) {
+                                       int m, int n, const float* v,
+                                       float qs = 1.f, float* amax = nullptr) {
   if (m >= e.M || n >= e.N) return;
   const int gn = n + gi * e.gcol;
   const long long idx = (long long)m * e.ldc + gn;
@@ -225,11 +239,44 @@ __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
     for (int q = 0; q < 8; ++q) o[q] *= a[q];
   }
   if (vec) {
-    *(uint4*)(e.c + idx) = pack_bf16x8(o);
+    const uint4 ob = pack_bf16x8(o);
+    *(uint4*)(e.c + idx) = ob;
+    if (e.q8) {
+      // quantise what the consumer would read: the bf16-rounded output
+      const uint32_t w4[4] = {ob.x, ob.y, ob.z, ob.w};
+      float r[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        r[2 * q] = __uint_as_float(w4[q] << 16);
+        r[2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
+      }
+      const float lim = e.q8_fmt == 0 ? 448.f : 57344.f;
+      float mx = *amax;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) mx = fmaxf(mx, fabsf(r[q]));
+      *amax = mx;
+      uint2 qv;
+      qv.x = pack4_fp8(sat(r[0] * qs, lim), sat(r[1] * qs, lim),
+                       sat(r[2] * qs, lim), sat(r[3] * qs, lim), e.q8_fmt);
+      qv.y = pack4_fp8(sat(r[4] * qs, lim), sat(r[5] * qs, lim),
+                       sat(r[6] * qs, lim), sat(r[7] * qs, lim), e.q8_fmt);
+      *(uint2*)(e.q8 + idx) = qv;
+    }
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       if (n + q < e.N) e.c[idx + q] = f2bf(o[q]);
+    if (e.q8) {
+      const float lim = e.q8_fmt == 0 ? 448.f : 57344.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (n + q < e.N) {
+          const float r = bf2f(f2bf(o[q]));
+          *amax = fmaxf(*amax, fabsf(r));
+          e.q8[idx + q] = (uint8_t)(pack4_fp8(sat(r * qs, lim), 0.f, 0.f, 0.f,
+                                              e.q8_fmt) & 0xFF);
+        }
+    }
   }
 }
 
@@ -384,6 +431,8 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
     }
   __syncthreads();
   constexpr int CH = BN_ / 8;
+  const float qs = epi.q8 ? fp8_scale(epi.q8_st, epi.hist, epi.q8_fmax) : 1.f;
+  float amax = 0.f;
   for (int q = t; q < BM * CH; q += NT) {
     const int row = q / CH, c8 = (q - row * CH) * 8;
     if (m0 + row >= M) continue;
@@ -392,7 +441,23 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
     float4 lo = src[0], hi = src[1];
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    store8(epi, alpha, gi, m0 + row, n0 + c8, v);
+    store8(epi, alpha, gi, m0 + row, n0 + c8, v, qs, &amax);
+  }
+  if (epi.q8) {
+    // one atomicMax per workgroup, spread over 32 shards (128-B apart) so
+    // that tens of thousands of workgroups do not serialise on one address
+    amax = wave_max(amax);
+    __syncthreads();   // sC reads done: reuse its first words
+    float* red = (float*)smem;
+    if (lane == 0) red[wid] = amax;
+    __syncthreads();
+    if (t == 0) {
+      float mx = 0.f;
+      for (int i = 0; i < NW; ++i) mx = fmaxf(mx, red[i]);
+      if (mx > 0.f)
+        atomicMax((unsigned int*)(epi.q8_shard + (blockIdx.x & 31) * 32),
+                  __float_as_uint(mx));
+    }
   }
 }
 
@@ -439,6 +504,8 @@ Epi8 make_epi8(void* c, int ldc, int M, int N, const float* bias, int act,
   e.grow_unused = 0; e.gcol = 0; e.bias = bias; e.act = act;
   e.aux = (const uint16_t*)aux; e.ld_aux = ld_aux; e.aux_act = aux_act;
   e.sa = sa; e.sb = sb; e.hist = hist; e.fa = fa; e.fb = fb;
+  e.q8 = nullptr; e.q8_st = nullptr; e.q8_shard = nullptr; e.q8_fmax = 1.f;
+  e.q8_fmt = 0;
   return e;
 }
 
@@ -560,12 +627,19 @@ __global__ void fp8_amax_kernel(const void* x, long long n, float* st,
 // step (optional): the history slot is step % hist read from device memory
 // (graph-safe roll; the registry advances the counter after the launch)
 __global__ void fp8_roll_kernel(float* states, int count, int hist, int idx,
-                                int fill, const int* step) {
+                                int fill, const int* step, float* shards) {
   if (step) idx = __builtin_amdgcn_readfirstlane(step[0]) % hist;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= count) return;
   float* st = states + (long long)s * (hist + 1);
-  const float cur = st[hist];
+  float cur = st[hist];
+  if (shards) {   // amaxes recorded by fused-quantising epilogues
+    float* sh = shards + (long long)s * 1024;
+    for (int i = 0; i < 32; ++i) {
+      cur = fmaxf(cur, sh[i * 32]);
+      sh[i * 32] = 0.f;
+    }
+  }
   if (fill) {
     for (int i = 0; i < hist; ++i) st[i] = cur;
   } else if (cur > 0.f) {
@@ -614,20 +688,34 @@ HVK_API int hvk_fp8_amax(const void* x, int x_f32, long long n, float* st,
   return (int)hipGetLastError();
 }
 
+// shards (optional): [count][1024] f32, 32 amax shards per scaler 32 floats
+// apart, folded into the current amax and cleared
 HVK_API int hvk_fp8_roll(float* states, int count, int hist, int idx,
-                         int fill, hipStream_t s) {
+                         int fill, float* shards, hipStream_t s) {
   if (count <= 0) return 0;
   hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
-                     states, count, hist, idx, fill, (const int*)nullptr);
+                     states, count, hist, idx, fill, (const int*)nullptr,
+                     shards);
   return (int)hipGetLastError();
 }
 
 HVK_API int hvk_fp8_roll_dev(float* states, int count, int hist,
-                             const void* step, hipStream_t s) {
+                             const void* step, float* shards, hipStream_t s) {
   if (count <= 0) return 0;
   hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
-                     states, count, hist, 0, 0, (const int*)step);
+                     states, count, hist, 0, 0, (const int*)step, shards);
   return (int)hipGetLastError();
+}
+
+// the fused quantisation of an fp8 conv's output (Epi8::q8); q8 == nullptr
+// leaves it off
+inline void set_q8(Epi8& e, void* q8, const float* st, float* shard,
+                   float fmax, int fmt) {
+  e.q8 = (uint8_t*)q8;
+  e.q8_st = st;
+  e.q8_shard = shard;
+  e.q8_fmax = fmax;
+  e.q8_fmt = fmt;
 }
 
 // C[M][N] (bf16) = act(A[M][K] . B[N][K]^T / (sA sB) + bias) * f'(aux)
@@ -652,8 +740,9 @@ HVK_API int hvk_conv_fwd_fp8(const void* X, const void* Wt, const float* bias,
                              int KH, int KW, int sy, int sx, int pt, int pl,
                              int OH, int OW, int groups, int act, int fx,
                              int fw, const float* sxs, const float* sws,
-                             int hist, float fmax_x, float fmax_w,
-                             hipStream_t s) {
+                             int hist, float fmax_x, float fmax_w, void* q8,
+                             const float* q8_st, float* q8_shard,
+                             float q8_fmax, int q8_fmt, hipStream_t s) {
   ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
   const int M = N * OH * OW, K = KH * KW * g.Cg;
   if ((g.Cg & 15) || (C & 15) || !al16(X) || !al16(Wt) || KH > 32 ||
@@ -664,6 +753,8 @@ HVK_API int hvk_conv_fwd_fp8(const void* X, const void* Wt, const float* bias,
   Epi8 e = make_epi8(Y, OC, M, g.OCg, bias, act, nullptr, 0, 0, sxs, sws,
                      hist, fmax_x, fmax_w);
   e.gcol = g.OCg;
+  if (q8 && (((uintptr_t)q8) & 7)) return -3;
+  set_q8(e, q8, q8_st, q8_shard, q8_fmax, q8_fmt);
   return (int)dispatch8(fx, fw, la, lb, e, M, g.OCg, K, groups, s);
 }
 
@@ -675,7 +766,9 @@ HVK_API int hvk_conv_dgrad_fp8(const void* dY, const void* Wt, void* dX,
                                int OW, int groups, const void* aux,
                                int aux_act, int fdy, int fw, const float* sds,
                                const float* sws, int hist, float fmax_dy,
-                               float fmax_w, hipStream_t s) {
+                               float fmax_w, void* q8, const float* q8_st,
+                               float* q8_shard, float q8_fmax, int q8_fmt,
+                               hipStream_t s) {
   ConvGeom g = make_geom(N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups);
   const int M = N * H * W, K = KH * KW * g.OCg;
   if ((g.OCg & 15) || (OC & 15) || !al16(dY) || !al16(Wt)) return -3;
@@ -684,6 +777,8 @@ HVK_API int hvk_conv_dgrad_fp8(const void* dY, const void* Wt, void* dX,
   Epi8 e = make_epi8(dX, C, M, g.Cg, nullptr, 0, aux, C, aux_act, sds, sws,
                      hist, fmax_dy, fmax_w);
   e.gcol = g.Cg;
+  if (q8 && (((uintptr_t)q8) & 7)) return -3;
+  set_q8(e, q8, q8_st, q8_shard, q8_fmax, q8_fmt);
   if (sy != 1 || sx != 1 || KH > 32 || KW > 32) {
     ConvDgradA8Str ls;
     static_cast<ConvDgradA8&>(ls) = la;

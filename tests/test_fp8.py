@@ -3,6 +3,7 @@ scaling semantics and a float8 training run on the CPU reference; on the
 MI355X every fp8 kernel against the CPU reference fed with the SAME
 quantized operands (so only accumulation order differs), plus quantizer
 bit-exactness against PyTorch's float8 casts."""
+import numpy
 import pytest
 import torch
 
@@ -96,6 +97,63 @@ def test_float8_workflow_trains_cpu():
         assert f[1].fp8_sx_.registry.step - step0 == wf.param_store_.steps
     finally:
         root.common.engine.precision_type = old
+
+
+def _fp8_two_conv_run(fuse, steps=4, backend="cpu"):
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    from veles_amd.prng import random_generator
+    import veles_amd.loader  # noqa: F401
+    g = {"learning_rate": 0.05, "gradient_moment": 0.9}
+    layers = [
+        {"type": "conv_str", "->": {"n_kernels": 16, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(g)},
+        {"type": "conv_str", "->": {"n_kernels": 32, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(g)},
+        {"type": "conv_str", "->": {"n_kernels": 32, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(g)},
+        {"type": "max_pooling", "->": {"kx": 2, "ky": 2, "sliding": 2}},
+        {"type": "softmax", "->": {"output_sample_shape": 10}, "<-": dict(g)}]
+    old = (root.common.engine.precision_type,
+           root.common.engine.fp8_fuse_quant)
+    root.common.engine.precision_type = "float8"
+    root.common.engine.fp8_fuse_quant = fuse
+    try:
+        random_generator.get().seed(5)
+        numpy.random.seed(5)
+        torch.manual_seed(0)
+        wf = StandardWorkflow(
+            DummyLauncher(), loader_name="synthetic_images",
+            loader_config={"dataset": "mnist", "class_lengths": (0, 0, 400),
+                           "minibatch_size": 50, "normalization_type":
+                           "mean_disp", "seed": 7, "noise": 110.0,
+                           "generate_on_device": False},
+            layers=layers, decision_config={"max_epochs": None,
+                                            "fail_iterations": None})
+        wf.initialize(device=Device(backend=backend))
+        wf.run_steps(steps)
+        if backend == "hip":
+            torch.cuda.synchronize()
+        return wf
+    finally:
+        (root.common.engine.precision_type,
+         root.common.engine.fp8_fuse_quant) = old
+
+
+def test_fused_fp8_quantisation_matches_separate_pass_cpu():
+    """conv -> fp8 conv -> fp8 conv: from step 1 on the middle conv's
+    epilogue writes the last conv's e4m3 input copy and the last GD's
+    epilogue the middle GD's e5m2 gradient copy (no quantize pass for
+    them); training is identical to the separate-pass run."""
+    a = _fp8_two_conv_run(False)
+    b = _fp8_two_conv_run(True)
+    f = b.forwards
+    assert f[1].fp8_ and f[2].fp8_
+    assert f[1].fp8_input_consumer() is f[2]
+    gd = {id(u.forward): u for u in b.gds}
+    assert gd[id(f[2])].fp8_grad_consumer() is gd[id(f[1])]
+    assert torch.equal(a.param_store_.master, b.param_store_.master)
 
 
 # ------------------------------------------------------------------ GPU
@@ -210,3 +268,39 @@ def test_fp8_roll_kernel():
     assert st[fp8.HIST].item() == 0
     assert st[step % fp8.HIST].item() == 8.0
     assert abs(s.scale() - 448.0 / 8.0) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dgrad", [False, True])
+def test_fused_quantisation_epilogue(dgrad):
+    """The fp8 conv epilogue's fused copy for the next layer equals a
+    separate quantize pass of the bf16 output at the consumer scaler's
+    scale, and its amax reaches the history at the roll."""
+    N, H, W, C, OC = 4, 14, 14, 32, 48
+    nxt = fp8.Scaler(DEV, fp8.E5M2 if dgrad else fp8.E4M3)
+    nxt.prime(torch.full((16,), 3.0, device=DEV))
+    w8, sw, _, _ = _pair(rnd(OC, 3, 3, C, seed=1, scale=0.1))
+    if not dgrad:
+        x8, sx, _, _ = _pair(rnd(N, H, W, C))
+        q8 = torch.empty(N, H, W, OC, dtype=fp8.TORCH_DT[nxt.fmt],
+                         device=DEV)
+        y = fp8.conv_fwd(x8, sx, w8, sw, None, (1, 1), (1, 1, 1, 1), 1, 3,
+                         q8=q8, q8_scaler=nxt)
+    else:
+        d8, sd, _, _ = _pair(rnd(N, H, W, OC, seed=2, scale=1e-2), fp8.E5M2)
+        q8 = torch.empty(N, H, W, C, dtype=fp8.TORCH_DT[nxt.fmt], device=DEV)
+        aux = rnd(N, H, W, C, seed=3).to(torch.bfloat16).to(DEV)
+        y = fp8.conv_dgrad(d8, sd, w8, sw, (N, H, W, C), (1, 1),
+                           (1, 1, 1, 1), 1, aux=aux, aux_act=3, q8=q8,
+                           q8_scaler=nxt)
+    torch.cuda.synchronize()
+    ref = fp8.quantize(y, nxt, record=False)
+    torch.cuda.synchronize()
+    assert torch.equal(q8.view(torch.uint8), ref.view(torch.uint8))
+    r = nxt.registry
+    step = r.step
+    r.roll()
+    torch.cuda.synchronize()
+    amax = y.float().abs().max().item()
+    assert nxt.state[step % fp8.HIST].item() == amax
+    assert nxt.shard.abs().max().item() == 0.0

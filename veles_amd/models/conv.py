@@ -98,6 +98,35 @@ class Conv(Forward):
         self.fp8_ = False
         self.fp8_sx_ = self.fp8_sw_ = None
         self.x8_ = self.w8_ = None
+        # fused input quantisation: the producing conv wrote x8_ this pass
+        self.x8_fresh_ = False
+        self.q8_consumer_ = None
+
+    def fp8_input_consumer(self):
+        """The fp8 conv that reads this conv's output as its input (direct
+        link, no unit in between), or None: this conv's epilogue then also
+        writes that conv's e4m3 input copy (``fp8.conv_fwd(q8=...)``)."""
+        if self.q8_consumer_ is None:
+            self.q8_consumer_ = False
+            for u in getattr(self, "links_to", ()):
+                if isinstance(u, Conv) and u.fp8_ and \
+                        getattr(u, "input", None) is self.output:
+                    self.q8_consumer_ = u
+                    break
+        return self.q8_consumer_ or None
+
+    def _q8_target(self, y):
+        """(x8 buffer, scaler) of the consumer when its scaler is primed and
+        its buffer matches this output, else (None, None)."""
+        from veles_amd.utils.config import root, get
+        if not get(root.common.engine.fp8_fuse_quant, True):
+            return None, None
+        c = self.fp8_input_consumer()
+        if c is None or not c.fp8_sx_.primed or c.x8_ is None or \
+                tuple(c.x8_.shape) != tuple(y.shape) or \
+                c.x8_.device != y.device:
+            return None, None
+        return c.x8_, c.fp8_sx_
 
     def output_hw(self, H, W):
         return ops.conv_out_size(H, W, self.ky, self.kx, self.sliding,
@@ -153,13 +182,22 @@ class Conv(Forward):
         OH, OW = self.output_hw(H, W)
         y = self.alloc_output((B, OH, OW, self.n_kernels))
         if self.fp8_:
-            # e4m3 input and weights, delayed per-tensor scaling (ops/fp8.py)
-            self.x8_ = fp8.quantize(x, self.fp8_sx_, out=self.x8_)
+            # e4m3 input and weights, delayed per-tensor scaling (ops/fp8.py);
+            # the input copy comes from the producing conv's epilogue when
+            # that conv wrote it this pass (x8_fresh_)
+            if not self.x8_fresh_ or self.x8_ is None or \
+                    tuple(self.x8_.shape) != tuple(x.shape):
+                self.x8_ = fp8.quantize(x, self.fp8_sx_, out=self.x8_)
+            self.x8_fresh_ = False
             self.w8_ = fp8.quantize(self.weights_lp, self.fp8_sw_,
                                     out=self.w8_)
+            q8, qs = self._q8_target(y)
             fp8.conv_fwd(self.x8_, self.fp8_sx_, self.w8_, self.fp8_sw_,
                          self.bias_master, self.sliding, self.padding,
-                         self.grouping, self.activation, out=y)
+                         self.grouping, self.activation, out=y, q8=q8,
+                         q8_scaler=qs)
+            if q8 is not None:
+                self.fp8_input_consumer().x8_fresh_ = True
             return
         if x.dtype != self.weights_lp.dtype:
             x = x.to(self.weights_lp.dtype)

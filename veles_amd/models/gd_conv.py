@@ -32,6 +32,38 @@ class GradientDescentConv(GradientDescentBase):
         super().init_unpickled()
         self.fp8_sdy_ = None
         self.dy8_ = None
+        # fused gradient quantisation: the GD that produces err_output wrote
+        # dy8_ this pass
+        self.dy8_fresh_ = False
+        self.q8_consumer_ = None
+
+    def fp8_grad_consumer(self):
+        """The conv GD whose err_output is this unit's err_input, running
+        fp8 backward-data on it unmodified (its activation derivative fused
+        into this unit's epilogue), or None."""
+        if self.q8_consumer_ is None:
+            self.q8_consumer_ = False
+            for u in getattr(self, "links_to", ()):
+                if isinstance(u, GradientDescentConv) and \
+                        getattr(u, "err_output", None) is self.err_input and \
+                        u.need_err_input and \
+                        getattr(u.forward, "fp8_", False):
+                    act = getattr(u.forward, "activation", 0)
+                    if not (u.own_derivative and act):
+                        self.q8_consumer_ = u
+                    break
+        return self.q8_consumer_ or None
+
+    def _q8_target(self, ei):
+        from veles_amd.utils.config import root, get
+        if not get(root.common.engine.fp8_fuse_quant, True):
+            return None, None
+        c = self.fp8_grad_consumer()
+        if c is None or c.fp8_sdy_ is None or not c.fp8_sdy_.primed or \
+                c.dy8_ is None or tuple(c.dy8_.shape) != tuple(ei.shape) or \
+                c.dy8_.device != ei.device:
+            return None, None
+        return c.dy8_, c.fp8_sdy_
 
     def run(self):
         fwd = self.forward
@@ -64,13 +96,23 @@ class GradientDescentConv(GradientDescentBase):
                 # e5m2 gradient x e4m3 weights on the fp8 MFMA kernel
                 if self.fp8_sdy_ is None:
                     self.fp8_sdy_ = fp8.Scaler(self.torch_device, fp8.E5M2)
-                self.dy8_ = fp8.quantize(err, self.fp8_sdy_, out=self.dy8_)
+                # the e5m2 copy comes from the epilogue of the GD that
+                # produced err_output when it wrote it this pass
+                if not self.dy8_fresh_ or self.dy8_ is None or \
+                        tuple(self.dy8_.shape) != tuple(err.shape):
+                    self.dy8_ = fp8.quantize(err, self.fp8_sdy_,
+                                             out=self.dy8_)
+                self.dy8_fresh_ = False
                 wt8 = fp8.permute_for_dgrad(fwd.w8_, fwd.grouping) \
                     if err.is_cuda else None
+                q8, qs = self._q8_target(ei)
                 fp8.conv_dgrad(self.dy8_, self.fp8_sdy_, fwd.w8_,
                                fwd.fp8_sw_, tuple(x.shape), fwd.sliding,
                                fwd.padding, fwd.grouping, aux=aux,
-                               aux_act=aux_act, out=ei, wt8=wt8)
+                               aux_act=aux_act, out=ei, wt8=wt8, q8=q8,
+                               q8_scaler=qs)
+                if q8 is not None:
+                    self.fp8_grad_consumer().dy8_fresh_ = True
             else:
                 ops.conv_dgrad(err, fwd.weights_lp, tuple(x.shape),
                                fwd.sliding, fwd.padding, fwd.grouping,

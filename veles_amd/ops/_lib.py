@@ -89,13 +89,14 @@ _SIGS = {
     # fp8 (csrc/kernels/gemm_fp8.hip)
     "hvk_fp8_quant": [P, I, L, P, I, P, I, F, I, P],
     "hvk_fp8_amax": [P, I, L, P, I, P],
-    "hvk_fp8_roll": [P, I, I, I, I, P],
-    "hvk_fp8_roll_dev": [P, I, I, P, P],
+    "hvk_fp8_roll": [P, I, I, I, I, P, P],
+    "hvk_fp8_roll_dev": [P, I, I, P, P, P],
     "hvk_gemm_fp8": [I, I, I, P, I, I, P, I, I, P, I, P, I, P, I, I, P, P, I,
                      F, F, P],
-    "hvk_conv_fwd_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F, P],
+    "hvk_conv_fwd_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F,
+                                                  P, P, P, F, I, P],
     "hvk_conv_dgrad_fp8": [P, P, P] + [I] * 14 + [P, I, I, I, P, P, I, F, F,
-                                                  P],
+                           P, P, P, F, I, P],
 }
 _OPTIONAL = {}
 

@@ -38,6 +38,7 @@ HIST = 16
 FMAX = {E4M3: 448.0, E5M2: 57344.0}
 TORCH_DT = {E4M3: torch.float8_e4m3fn, E5M2: torch.float8_e5m2}
 _CHUNK = 256
+SHARDS = 32
 
 
 def _s(t):
@@ -54,18 +55,27 @@ class _Registry(object):
     def __init__(self, device):
         self.device = device
         self.blocks = []
+        # per scaler: 32 amax shards, 32 floats (128 B) apart, that the
+        # fused-quantising fp8 epilogues atomicMax into (one per workgroup);
+        # the roll folds them into the current amax
+        self.shard_blocks = []
         self.used = 0
         self.step = 0
         self.step_dev = None  # device mirror of ``step`` (GPU roll)
 
     def allocate(self):
+        """(state row [HIST + 1], shard row [1024]) of a new scaler."""
         i = self.used
         if i // _CHUNK >= len(self.blocks):
             self.blocks.append(torch.zeros(_CHUNK, HIST + 1,
                                            dtype=torch.float32,
                                            device=self.device))
+            self.shard_blocks.append(torch.zeros(_CHUNK, SHARDS * 32,
+                                                 dtype=torch.float32,
+                                                 device=self.device))
         self.used += 1
-        return self.blocks[i // _CHUNK][i % _CHUNK]
+        return (self.blocks[i // _CHUNK][i % _CHUNK],
+                self.shard_blocks[i // _CHUNK][i % _CHUNK])
 
     def roll(self):
         """End of step: current amax -> history slot; current = 0.  On the
@@ -86,8 +96,13 @@ class _Registry(object):
                             device=blk.device)
                     gpu_step = self.step_dev
                 _call("hvk_fp8_roll_dev", blk.data_ptr(), count, HIST,
-                      gpu_step.data_ptr(), _s(blk))
+                      gpu_step.data_ptr(),
+                      self.shard_blocks[bi].data_ptr(), _s(blk))
             else:
+                sh = self.shard_blocks[bi][:count].view(count, SHARDS, 32)
+                blk[:count, HIST] = torch.maximum(blk[:count, HIST],
+                                                  sh[:, :, 0].max(1).values)
+                sh.zero_()
                 cur = blk[:count, HIST]
                 keep = cur > 0
                 blk[:count, idx] = torch.where(keep, cur, blk[:count, idx])
@@ -116,7 +131,7 @@ class Scaler(object):
         self.fmt = fmt
         self.margin = margin
         self.registry = registry(device)
-        self.state = self.registry.allocate()
+        self.state, self.shard = self.registry.allocate()
         self.primed = False
 
     @property
@@ -143,7 +158,7 @@ class Scaler(object):
             _call("hvk_fp8_amax", xf.data_ptr(),
                   int(xf.dtype == torch.float32), xf.numel(), st.data_ptr(),
                   HIST, _s(xf))
-            _call("hvk_fp8_roll", st.data_ptr(), 1, HIST, 0, 1, _s(xf))
+            _call("hvk_fp8_roll", st.data_ptr(), 1, HIST, 0, 1, None, _s(xf))
         else:
             st[:HIST] = x.float().abs().max()
             st[HIST] = 0
@@ -224,8 +239,33 @@ def fp8_conv_ok(C, OC, groups, KH=1, KW=1):
         (OC // groups) % 16 == 0 and KH <= 32 and KW <= 32
 
 
+def _q8_args(q8, qs):
+    """Kernel arguments of a fused output quantisation (or none)."""
+    if q8 is None:
+        return [None, None, None, 1.0, 0]
+    return [q8.data_ptr(), qs.state.data_ptr(), qs.shard.data_ptr(),
+            float(qs.fmax_eff), qs.fmt]
+
+
+def _q8_ref(y, q8, qs):
+    """CPU model of the fused quantisation: q8 = quantize(y) - y as stored,
+    exactly what the consumer would quantize (the GPU epilogue quantizes the
+    bf16-rounded output it stores) - with the amax recorded in the scaler's
+    first shard."""
+    if q8 is None:
+        return
+    yb = y.float()
+    lim = FMAX[qs.fmt]
+    q8.copy_((yb * qs._scale_t()).clamp(-lim, lim).to(q8.dtype))
+    qs.shard[0] = torch.maximum(qs.shard[0], yb.abs().max())
+
+
 def conv_fwd(x8, sx, w8, sw, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
-             groups=1, act=0, out=None):
+             groups=1, act=0, out=None, q8=None, q8_scaler=None):
+    """y (bf16 on GPU) = act(conv(deq(x8), deq(w8)) + bias).  ``q8`` /
+    ``q8_scaler``: also write the fp8 copy of y the NEXT fp8 layer reads
+    (its input scaler; the amax is recorded for the scaler's roll) from the
+    same epilogue - no separate quantize pass."""
     from veles_amd import ops
     N, H, W, C = x8.shape
     OC, KH, KW, Cg = w8.shape
@@ -240,15 +280,18 @@ def conv_fwd(x8, sx, w8, sw, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
               out.data_ptr(), N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH,
               OW, groups, ops.act_code(act), sx.fmt, sw.fmt,
               sx.state.data_ptr(), sw.state.data_ptr(), HIST,
-              float(sx.fmax_eff), float(sw.fmax_eff), _s(x8))
+              float(sx.fmax_eff), float(sw.fmax_eff),
+              *_q8_args(q8, q8_scaler), _s(x8))
         return out
-    return ops.conv_fwd(dequantize(x8, sx), dequantize(w8, sw), bias, sliding,
-                        padding, groups, act, out=out)
+    y = ops.conv_fwd(dequantize(x8, sx), dequantize(w8, sw), bias, sliding,
+                     padding, groups, act, out=out)
+    _q8_ref(y, q8, q8_scaler)
+    return y
 
 
 def conv_dgrad(dy8, sdy, w8, sw, x_shape, sliding=(1, 1),
                padding=(0, 0, 0, 0), groups=1, aux=None, aux_act=0, out=None,
-               wt8=None):
+               wt8=None, q8=None, q8_scaler=None):
     """dx = conv^T(deq(dy8), deq(w8)) [* f'(aux)]; ``wt8`` is the
     ``permute_for_dgrad`` image of w8 (computed here when not given)."""
     from veles_amd import ops
@@ -267,8 +310,11 @@ def conv_dgrad(dy8, sdy, w8, sw, x_shape, sliding=(1, 1),
               out.data_ptr(), N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH,
               OW, groups, ops._p(aux), ops.act_code(aux_act), sdy.fmt,
               sw.fmt, sdy.state.data_ptr(), sw.state.data_ptr(), HIST,
-              float(sdy.fmax_eff), float(sw.fmax_eff), _s(dy8))
+              float(sdy.fmax_eff), float(sw.fmax_eff),
+              *_q8_args(q8, q8_scaler), _s(dy8))
         return out
-    return ops.conv_dgrad(dequantize(dy8, sdy), dequantize(w8, sw), x_shape,
-                          sliding, padding, groups, aux=aux, aux_act=aux_act,
-                          out=out)
+    dx = ops.conv_dgrad(dequantize(dy8, sdy), dequantize(w8, sw), x_shape,
+                        sliding, padding, groups, aux=aux, aux_act=aux_act,
+                        out=out)
+    _q8_ref(dx, q8, q8_scaler)
+    return dx
