@@ -26,6 +26,7 @@
 // the fully-connected forward.  Weight gradients and the fully-connected
 // dgrad (whose fp8 B operand would be W^T) stay on the bf16 kernels
 // (docs/OPS.md §FP8).
+#include "fp8_common.h"
 #include "conv_geom.h"
 
 using namespace hvk;
@@ -38,16 +39,7 @@ constexpr int BM = 128, BK = 128, NTHR = 256;
 
 __device__ __attribute__((aligned(16))) const uint8_t g_zero16[16] = {0};
 
-// ------------------------------------------------------------------ scales
-// A scaler state is float st[hist + 1]: amax history, then the running amax
-// of the current step.  scale = fmax_eff / max(history) (1 when empty); the
-// quantizer multiplies by it and the GEMM epilogue divides by sA * sB.
-__device__ __forceinline__ float fp8_scale(const float* st, int hist,
-                                           float fmax_eff) {
-  float m = 0.f;
-  for (int i = 0; i < hist; ++i) m = fmaxf(m, st[i]);
-  return m > 0.f ? fmax_eff / m : 1.f;
-}
+// scales, packs, the fused-quantisation output: fp8_common.h
 
 // ----------------------------------------------------------------- loaders
 struct Dense8 {
@@ -185,10 +177,6 @@ struct Epi8 {
   float q8_fmax;
   int q8_fmt;
 };
-
-__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c,
-                                              float d, int fmt);
-__device__ __forceinline__ float sat(float v, float lim);
 
 __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
                                        int m, int n, const float* v,
@@ -510,22 +498,6 @@ Epi8 make_epi8(void* c, int ldc, int M, int N, const float* bias, int act,
 }
 
 // -------------------------------------------------------------- quantizers
-__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c,
-                                              float d, int fmt) {
-  int v;
-  if (fmt == 0) {
-    v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
-  } else {
-    v = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    v = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, v, true);
-  }
-  return (uint32_t)v;
-}
-
-__device__ __forceinline__ float sat(float v, float lim) {
-  return fminf(fmaxf(v, -lim), lim);
-}
 
 // Units of 8 elements (one 16-B bf16 load or two float4 loads -> one 8-B
 // fp8 store), lanes on consecutive units so every load is fully coalesced;

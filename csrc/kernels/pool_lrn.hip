@@ -7,6 +7,7 @@
 // LRN waves own one pixel and stage its channels in LDS.  Pooling backward is
 // a deterministic GATHER (each input element sums the windows that chose it)
 // instead of atomics.
+#include "fp8_common.h"
 #include "hvk_common.h"
 
 using namespace hvk;
@@ -749,12 +750,16 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_kernel(
 // four input pixels of the window: it reads x + dy instead of dy + an int32
 // argmax as large as x / 2, and the forward writes no argmax at all.  Even H
 // and W only (every input pixel belongs to exactly one window).
+// q8.q (optional): also the fp8 copy of y for the next fp8 layer (fused
+// quantisation, fp8_common.h)
 template <int MODE>
 __global__ __launch_bounds__(256) void pool2_fwd_kernel(
     const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int N, int H,
-    int W, int C, FastDiv fCV, FastDiv fOW, FastDiv fOH) {
+    int W, int C, FastDiv fCV, FastDiv fOW, FastDiv fOH, Q8 q8) {
   const int CV = C >> 3, OH = H >> 1, OW = W >> 1;
   const int total = N * OH * OW * CV;
+  const float qs = q8.q ? fp8_scale(q8.st, q8.hist, q8.fmax) : 1.f;
+  float amax = 0.f;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
     uint32_t pix, cvu, t, owu, nu, ohu;
@@ -781,7 +786,13 @@ __global__ __launch_bounds__(256) void pool2_fwd_kernel(
       }
       o[q] = f2bf(MODE == POOL_AVG ? 0.25f * sum : best);
     }
-    *(uint4*)(y + (long long)pix * C + cvu * 8) = *(const uint4*)o;
+    const long long yo = (long long)pix * C + cvu * 8;
+    *(uint4*)(y + yo) = *(const uint4*)o;
+    if (q8.q) q8_store8(q8, yo, *(const uint4*)o, qs, amax);
+  }
+  if (q8.q) {
+    __shared__ float red[4];
+    q8_block_amax(q8, amax, red);
   }
 }
 
@@ -790,9 +801,11 @@ __global__ __launch_bounds__(256) void pool2_bwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
     uint16_t* __restrict__ dx, int N, int H, int W, int C,
     const uint16_t* aux, int aux_act, FastDiv fCV, FastDiv fOW,
-    FastDiv fOH) {
+    FastDiv fOH, Q8 q8) {
   const int CV = C >> 3, OH = H >> 1, OW = W >> 1;
   const int total = N * OH * OW * CV;
+  const float qs = q8.q ? fp8_scale(q8.st, q8.hist, q8.fmax) : 1.f;
+  float amax = 0.f;
   const bool aux_x = aux == x;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
@@ -836,7 +849,14 @@ __global__ __launch_bounds__(256) void pool2_bwd_kernel(
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(uint4*)(dx + off[i]) = *(const uint4*)o[i];
+    for (int i = 0; i < 4; ++i) {
+      *(uint4*)(dx + off[i]) = *(const uint4*)o[i];
+      if (q8.q) q8_store8(q8, off[i], *(const uint4*)o[i], qs, amax);
+    }
+  }
+  if (q8.q) {
+    __shared__ float red[4];
+    q8_block_amax(q8, amax, red);
   }
 }
 
@@ -1479,11 +1499,17 @@ HVK_API int hvk_stochastic_pool(const void* x, void* y, int* argmax, int N,
 
 // 2 x 2 / stride-2 pooling without argmax (pool2_fwd_kernel): C % 8 == 0,
 // even H and W, 16-B aligned tensors; mode 0 max, 1 avg, 2 maxabs.
-HVK_API int hvk_pool2_fwd(const void* x, void* y, int N, int H, int W, int C,
-                          int mode, hipStream_t s) {
+// q8 / q8_st / q8_shard / q8_fmax / q8_fmt / hist (q8 may be null): the
+// fused fp8 copy of the result for the next fp8 layer (fp8_common.h Q8)
+HVK_API int hvk_pool2_fwd_q8(const void* x, void* y, int N, int H, int W,
+                             int C, int mode, void* q8, const float* q8_st,
+                             float* q8_shard, float q8_fmax, int q8_fmt,
+                             int hist, hipStream_t s) {
   if (C % 8 || (H & 1) || (W & 1) || ((uintptr_t)x & 15) ||
-      ((uintptr_t)y & 15) || (long long)N * H * W * C >= (1ll << 31))
+      ((uintptr_t)y & 15) || ((uintptr_t)q8 & 7) ||
+      (long long)N * H * W * C >= (1ll << 31))
     return -1;
+  const Q8 q{(uint8_t*)q8, q8_st, q8_shard, q8_fmax, q8_fmt, hist};
   const long long total = (long long)N * (H / 2) * (W / 2) * (C / 8);
   auto k = mode == POOL_AVG ? pool2_fwd_kernel<POOL_AVG>
            : mode == POOL_MAXABS ? pool2_fwd_kernel<POOL_MAXABS>
@@ -1491,19 +1517,28 @@ HVK_API int hvk_pool2_fwd(const void* x, void* y, int N, int H, int W, int C,
   hipLaunchKernelGGL(k, dim3(grid_for(total)), dim3(256), 0, s,
                      (const uint16_t*)x, (uint16_t*)y, N, H, W, C,
                      make_fastdiv(C / 8), make_fastdiv(W / 2),
-                     make_fastdiv(H / 2));
+                     make_fastdiv(H / 2), q);
   return (int)hipGetLastError();
+}
+
+HVK_API int hvk_pool2_fwd(const void* x, void* y, int N, int H, int W, int C,
+                          int mode, hipStream_t s) {
+  return hvk_pool2_fwd_q8(x, y, N, H, W, C, mode, nullptr, nullptr, nullptr,
+                          1.f, 0, 0, s);
 }
 
 // dx of a 2 x 2 / stride-2 pooling, the choice recomputed from x (the
 // forward input); aux multiplies by act_bwd(aux) (aux may be x itself)
-HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
-                          int H, int W, int C, int mode, const void* aux,
-                          int aux_act, hipStream_t s) {
+HVK_API int hvk_pool2_bwd_q8(const void* x, const void* dy, void* dx, int N,
+                             int H, int W, int C, int mode, const void* aux,
+                             int aux_act, void* q8, const float* q8_st,
+                             float* q8_shard, float q8_fmax, int q8_fmt,
+                             int hist, hipStream_t s) {
   if (C % 8 || (H & 1) || (W & 1) || ((uintptr_t)x & 15) ||
       ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15) || ((uintptr_t)aux & 15) ||
-      (long long)N * H * W * C >= (1ll << 31))
+      ((uintptr_t)q8 & 7) || (long long)N * H * W * C >= (1ll << 31))
     return -1;
+  const Q8 q{(uint8_t*)q8, q8_st, q8_shard, q8_fmax, q8_fmt, hist};
   const long long total = (long long)N * (H / 2) * (W / 2) * (C / 8);
   auto k = mode == POOL_AVG ? pool2_bwd_kernel<POOL_AVG>
            : mode == POOL_MAXABS ? pool2_bwd_kernel<POOL_MAXABS>
@@ -1512,8 +1547,15 @@ HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
                      (const uint16_t*)x, (const uint16_t*)dy, (uint16_t*)dx,
                      N, H, W, C, (const uint16_t*)aux, aux_act,
                      make_fastdiv(C / 8), make_fastdiv(W / 2),
-                     make_fastdiv(H / 2));
+                     make_fastdiv(H / 2), q);
   return (int)hipGetLastError();
+}
+
+HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
+                          int H, int W, int C, int mode, const void* aux,
+                          int aux_act, hipStream_t s) {
+  return hvk_pool2_bwd_q8(x, dy, dx, N, H, W, C, mode, aux, aux_act, nullptr,
+                          nullptr, nullptr, 1.f, 0, 0, s);
 }
 
 // forward kernel selector for A/B runs (hvk_set_lrn_fwd_variant): 0 the

@@ -114,6 +114,9 @@ def _fp8_two_conv_run(fuse, steps=4, backend="cpu"):
         {"type": "conv_str", "->": {"n_kernels": 32, "kx": 3, "ky": 3,
                                     "padding": 1}, "<-": dict(g)},
         {"type": "max_pooling", "->": {"kx": 2, "ky": 2, "sliding": 2}},
+        {"type": "conv_str", "->": {"n_kernels": 32, "kx": 3, "ky": 3,
+                                    "padding": 1}, "<-": dict(g)},
+        {"type": "max_pooling", "->": {"kx": 2, "ky": 2, "sliding": 2}},
         {"type": "softmax", "->": {"output_sample_shape": 10}, "<-": dict(g)}]
     old = (root.common.engine.precision_type,
            root.common.engine.fp8_fuse_quant)
@@ -142,17 +145,22 @@ def _fp8_two_conv_run(fuse, steps=4, backend="cpu"):
 
 
 def test_fused_fp8_quantisation_matches_separate_pass_cpu():
-    """conv -> fp8 conv -> fp8 conv: from step 1 on the middle conv's
-    epilogue writes the last conv's e4m3 input copy and the last GD's
-    epilogue the middle GD's e5m2 gradient copy (no quantize pass for
+    """conv -> fp8 conv -> fp8 conv -> 2x2 pool -> fp8 conv: from step 1 on
+    the producing conv's epilogue / the pooling kernel writes the next fp8
+    conv's e4m3 input copy, and in the backward the GD / pooling-GD kernel
+    the e5m2 gradient copy of the fp8 conv GD below it (no quantize pass for
     them); training is identical to the separate-pass run."""
     a = _fp8_two_conv_run(False)
     b = _fp8_two_conv_run(True)
     f = b.forwards
-    assert f[1].fp8_ and f[2].fp8_
+    assert f[1].fp8_ and f[2].fp8_ and f[4].fp8_
     assert f[1].fp8_input_consumer() is f[2]
+    from veles_amd.models.conv import fp8_input_consumer
+    from veles_amd.models.gd_conv import fp8_grad_consumer
+    assert fp8_input_consumer(f[3]) is f[4]        # pool -> fp8 conv
     gd = {id(u.forward): u for u in b.gds}
     assert gd[id(f[2])].fp8_grad_consumer() is gd[id(f[1])]
+    assert fp8_grad_consumer(gd[id(f[3])]) is gd[id(f[2])]  # pool GD
     assert torch.equal(a.param_store_.master, b.param_store_.master)
 
 
@@ -304,3 +312,33 @@ def test_fused_quantisation_epilogue(dgrad):
     amax = y.float().abs().max().item()
     assert nxt.state[step % fp8.HIST].item() == amax
     assert nxt.shard.abs().max().item() == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bwd", [False, True])
+def test_fused_quantisation_pool2(bwd):
+    """The 2 x 2 pooling kernels' fused fp8 copy of their result equals a
+    separate quantize pass at the consumer scaler's scale; the amax reaches
+    the history at the roll."""
+    N, H, W, C = 3, 16, 14, 32
+    nxt = fp8.Scaler(DEV, fp8.E5M2 if bwd else fp8.E4M3)
+    nxt.prime(torch.full((16,), 2.0, device=DEV))
+    x = rnd(N, H, W, C).to(torch.bfloat16).to(DEV)
+    if not bwd:
+        q8 = torch.empty(N, H // 2, W // 2, C, dtype=fp8.TORCH_DT[nxt.fmt],
+                         device=DEV)
+        y = ops.pool2_fwd(x, "max", q8=q8, q8_scaler=nxt)
+    else:
+        dy = rnd(N, H // 2, W // 2, C, seed=4).to(torch.bfloat16).to(DEV)
+        q8 = torch.empty(N, H, W, C, dtype=fp8.TORCH_DT[nxt.fmt], device=DEV)
+        y = ops.pool2_bwd(x, dy, "max", aux=x, aux_act=3, q8=q8,
+                          q8_scaler=nxt)
+    torch.cuda.synchronize()
+    ref = fp8.quantize(y, nxt, record=False)
+    torch.cuda.synchronize()
+    assert torch.equal(q8.view(torch.uint8), ref.view(torch.uint8))
+    r = nxt.registry
+    step = r.step
+    r.roll()
+    torch.cuda.synchronize()
+    assert nxt.state[step % fp8.HIST].item() == y.float().abs().max().item()

@@ -103,30 +103,10 @@ class Conv(Forward):
         self.q8_consumer_ = None
 
     def fp8_input_consumer(self):
-        """The fp8 conv that reads this conv's output as its input (direct
-        link, no unit in between), or None: this conv's epilogue then also
-        writes that conv's e4m3 input copy (``fp8.conv_fwd(q8=...)``)."""
-        if self.q8_consumer_ is None:
-            self.q8_consumer_ = False
-            for u in getattr(self, "links_to", ()):
-                if isinstance(u, Conv) and u.fp8_ and \
-                        getattr(u, "input", None) is self.output:
-                    self.q8_consumer_ = u
-                    break
-        return self.q8_consumer_ or None
+        return fp8_input_consumer(self)
 
     def _q8_target(self, y):
-        """(x8 buffer, scaler) of the consumer when its scaler is primed and
-        its buffer matches this output, else (None, None)."""
-        from veles_amd.utils.config import root, get
-        if not get(root.common.engine.fp8_fuse_quant, True):
-            return None, None
-        c = self.fp8_input_consumer()
-        if c is None or not c.fp8_sx_.primed or c.x8_ is None or \
-                tuple(c.x8_.shape) != tuple(y.shape) or \
-                c.x8_.device != y.device:
-            return None, None
-        return c.x8_, c.fp8_sx_
+        return fp8_input_target(self, y)
 
     def output_hw(self, H, W):
         return ops.conv_out_size(H, W, self.ky, self.kx, self.sliding,
@@ -233,3 +213,36 @@ class ConvStrictRELU(Conv):
 class ConvSigmoid(Conv):
     MAPPING = "conv_sigmoid"
     ACTIVATION = 4
+
+
+def fp8_input_consumer(unit):
+    """The fp8 conv that reads ``unit``'s output as its input (direct link,
+    no unit in between), or None: ``unit`` then also writes that conv's e4m3
+    input copy from the kernel producing its output (fused quantisation:
+    ``fp8.conv_fwd(q8=...)``, ``ops.pool2_fwd(q8=...)``)."""
+    c = getattr(unit, "q8_consumer_", None)
+    if c is None:
+        c = False
+        for u in getattr(unit, "links_to", ()):
+            if isinstance(u, Conv) and u.fp8_ and \
+                    getattr(u, "input", None) is unit.output:
+                c = u
+                break
+        unit.q8_consumer_ = c
+    return c or None
+
+
+def fp8_input_target(unit, y):
+    """(x8 buffer, scaler) for ``unit``'s fused output quantisation when the
+    consumer's scaler is primed (its first pass quantized and primed it) and
+    its buffer matches ``y``; (None, None) otherwise or with
+    ``root.common.engine.fp8_fuse_quant = False``.  The caller sets the
+    consumer's ``x8_fresh_`` once the producing kernel is enqueued."""
+    from veles_amd.utils.config import root, get
+    if not get(root.common.engine.fp8_fuse_quant, True):
+        return None, None
+    c = fp8_input_consumer(unit)
+    if c is None or not c.fp8_sx_.primed or c.x8_ is None or \
+            tuple(c.x8_.shape) != tuple(y.shape) or c.x8_.device != y.device:
+        return None, None
+    return c.x8_, c.fp8_sx_

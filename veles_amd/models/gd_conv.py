@@ -38,32 +38,10 @@ class GradientDescentConv(GradientDescentBase):
         self.q8_consumer_ = None
 
     def fp8_grad_consumer(self):
-        """The conv GD whose err_output is this unit's err_input, running
-        fp8 backward-data on it unmodified (its activation derivative fused
-        into this unit's epilogue), or None."""
-        if self.q8_consumer_ is None:
-            self.q8_consumer_ = False
-            for u in getattr(self, "links_to", ()):
-                if isinstance(u, GradientDescentConv) and \
-                        getattr(u, "err_output", None) is self.err_input and \
-                        u.need_err_input and \
-                        getattr(u.forward, "fp8_", False):
-                    act = getattr(u.forward, "activation", 0)
-                    if not (u.own_derivative and act):
-                        self.q8_consumer_ = u
-                    break
-        return self.q8_consumer_ or None
+        return fp8_grad_consumer(self)
 
     def _q8_target(self, ei):
-        from veles_amd.utils.config import root, get
-        if not get(root.common.engine.fp8_fuse_quant, True):
-            return None, None
-        c = self.fp8_grad_consumer()
-        if c is None or c.fp8_sdy_ is None or not c.fp8_sdy_.primed or \
-                c.dy8_ is None or tuple(c.dy8_.shape) != tuple(ei.shape) or \
-                c.dy8_.device != ei.device:
-            return None, None
-        return c.dy8_, c.fp8_sdy_
+        return fp8_grad_target(self, ei)
 
     def run(self):
         fwd = self.forward
@@ -136,3 +114,38 @@ class GDStrictRELUConv(GradientDescentConv):
 
 class GDSigmoidConv(GradientDescentConv):
     MAPPING = "conv_sigmoid"
+
+
+def fp8_grad_consumer(unit):
+    """The conv GD whose err_output is ``unit``'s err_input and which runs
+    fp8 backward-data on it unmodified (its activation derivative already
+    fused into ``unit``'s kernel), or None: ``unit`` then also writes that
+    GD's e5m2 gradient copy (fused quantisation)."""
+    c = getattr(unit, "q8_consumer_", None)
+    if c is None:
+        c = False
+        for u in getattr(unit, "links_to", ()):
+            if isinstance(u, GradientDescentConv) and \
+                    getattr(u, "err_output", None) is unit.err_input and \
+                    u.need_err_input and getattr(u.forward, "fp8_", False):
+                if not (u.own_derivative and
+                        getattr(u.forward, "activation", 0)):
+                    c = u
+                break
+        unit.q8_consumer_ = c
+    return c or None
+
+
+def fp8_grad_target(unit, ei):
+    """(dy8 buffer, scaler) for ``unit``'s fused gradient quantisation, or
+    (None, None) (see conv.fp8_input_target); the caller sets the
+    consumer's ``dy8_fresh_``."""
+    from veles_amd.utils.config import root, get
+    if not get(root.common.engine.fp8_fuse_quant, True):
+        return None, None
+    c = fp8_grad_consumer(unit)
+    if c is None or c.fp8_sdy_ is None or not c.fp8_sdy_.primed or \
+            c.dy8_ is None or tuple(c.dy8_.shape) != tuple(ei.shape) or \
+            c.dy8_.device != ei.device:
+        return None, None
+    return c.dy8_, c.fp8_sdy_

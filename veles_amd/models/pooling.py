@@ -106,7 +106,14 @@ class Pooling(AcceleratedUnit):
             return
         x = self._in()
         if self.argmax_free_:
-            ops.pool2_fwd(x, self.MODE, out=self.output.devmem)
+            from veles_amd.models.conv import (fp8_input_consumer,
+                                               fp8_input_target)
+            y = self.output.devmem
+            q8, qs = fp8_input_target(self, y) if y is not None and \
+                y.is_cuda else (None, None)
+            ops.pool2_fwd(x, self.MODE, out=y, q8=q8, q8_scaler=qs)
+            if q8 is not None:
+                fp8_input_consumer(self).x8_fresh_ = True
             return
         B, H, W, C = x.shape
         OH, OW = ops.pool_out_size(H, W, self.ky, self.kx, self.sliding[1],
@@ -336,7 +343,13 @@ class GDPooling(GradientDescentBase):
         ei = self.alloc_err_input(shape)
         aux, aux_act = self.aux_tensor()
         if fwd is not None and getattr(fwd, "argmax_free_", False):
-            ops.pool2_bwd(x, err, self.MODE, aux=aux, aux_act=aux_act, out=ei)
+            from veles_amd.models.gd_conv import (fp8_grad_consumer,
+                                                  fp8_grad_target)
+            q8, qs = fp8_grad_target(self, ei) if ei.is_cuda else (None, None)
+            ops.pool2_bwd(x, err, self.MODE, aux=aux, aux_act=aux_act, out=ei,
+                          q8=q8, q8_scaler=qs)
+            if q8 is not None:
+                fp8_grad_consumer(self).dy8_fresh_ = True
             return
         if aux is not None and aux.dim() == 3:
             aux = aux.unsqueeze(-1)

@@ -1193,31 +1193,50 @@ def pool2_ok(x_shape, ky, kx, sliding):
         C % 8 == 0 and H % 2 == 0 and W % 2 == 0
 
 
-def pool2_fwd(x, mode="max", out=None):
+def _q8_pool_args(q8, qs):
+    from veles_amd.ops import fp8 as _f8
+    if q8 is None:
+        return [None, None, None, 1.0, 0, _f8.HIST]
+    return [q8.data_ptr(), qs.state.data_ptr(), qs.shard.data_ptr(),
+            float(qs.fmax_eff), qs.fmt, _f8.HIST]
+
+
+def pool2_fwd(x, mode="max", out=None, q8=None, q8_scaler=None):
     """2 x 2 / stride-2 NHWC pooling that writes no argmax: ``pool2_bwd``
-    recomputes the window's choice from x."""
+    recomputes the window's choice from x.  ``q8`` / ``q8_scaler``: also the
+    fp8 copy of the result for the next fp8 layer (fused quantisation)."""
     N, H, W, C = x.shape
     m = POOL[mode]
     if out is None:
         out = torch.empty(N, H // 2, W // 2, C, dtype=x.dtype,
                           device=x.device)
     if _gpu(x):
-        _lib_call("hvk_pool2_fwd", _p(x), _p(out), N, H, W, C, m, _s(x))
+        _lib_call("hvk_pool2_fwd_q8", _p(x), _p(out), N, H, W, C, m,
+                  *_q8_pool_args(q8, q8_scaler), _s(x))
         return out
     y, _ = pool_fwd(x, 2, 2, (2, 2), mode, out=out)
+    if q8 is not None:
+        from veles_amd.ops import fp8 as _f8
+        _f8._q8_ref(y, q8, q8_scaler)
     return y
 
 
-def pool2_bwd(x, dy, mode="max", aux=None, aux_act=0, out=None):
+def pool2_bwd(x, dy, mode="max", aux=None, aux_act=0, out=None, q8=None,
+              q8_scaler=None):
     N, H, W, C = x.shape
     m = POOL[mode]
     aux_act = act_code(aux_act)
     if out is None:
         out = torch.empty_like(x, dtype=dy.dtype)
     if _gpu(x):
-        _lib_call("hvk_pool2_bwd", _p(x), _p(dy), _p(out), N, H, W, C, m,
-                  _p(aux), aux_act, _s(x))
+        _lib_call("hvk_pool2_bwd_q8", _p(x), _p(dy), _p(out), N, H, W, C, m,
+                  _p(aux), aux_act, *_q8_pool_args(q8, q8_scaler), _s(x))
         return out
+    if q8 is not None:
+        dx = pool2_bwd(x, dy, mode, aux=aux, aux_act=aux_act, out=out)
+        from veles_amd.ops import fp8 as _f8
+        _f8._q8_ref(dx, q8, q8_scaler)
+        return dx
     am = None
     if m != 1:
         _, am = pool_fwd(x, 2, 2, (2, 2), mode)

@@ -79,8 +79,11 @@ _SIGS = {
     "hvk_lrn_pool_fwd": [P, P, P] + [I] * 9 + [F, F, F, P],
     "hvk_lrn_pool_bwd": [P, P, P, P] + [I] * 9 + [F, F, F, P, I, P],
     "hvk_pool2_fwd": [P, P] + [I] * 5 + [P],
+    # + (q8, q8_st, q8_shard, q8_fmax, q8_fmt, hist): fused fp8 copy
+    "hvk_pool2_fwd_q8": [P, P] + [I] * 5 + [P, P, P, F, I, I, P],
     "hvk_stochastic_pool": [P, P, P] + [I] * 12 + [P, P],
     "hvk_pool2_bwd": [P, P, P] + [I] * 5 + [P, I, P],
+    "hvk_pool2_bwd_q8": [P, P, P] + [I] * 5 + [P, I, P, P, P, F, I, I, P],
     "hvk_lrn_pool_fwd_u8": [P, P, P] + [I] * 7 + [F, F, F, P],
     "hvk_lrn_pool_bwd_u8": [P, P, P, P] + [I] * 7 + [F, F, F, P, I, P],
     # exact-precision GEMMs (csrc/kernels/gemm_f32.hip)
