@@ -1152,6 +1152,8 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   }
 }
 
+#include "gemm_pp.h"
+
 // Tile width: 128 unless it wastes more than 1/8 of the columns; then 64,
 // or 96 for a single 96-wide column tile (K-major B only: AlexNet conv1,
 // N = 96, +16 % over 128).  N = 192 measured faster as 3 x 64 than as
@@ -1223,6 +1225,24 @@ template <class LA, bool AK, class LB, bool BKM, bool BUF>
 hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles_n, int tiles, int splits,
                      int bn, dim3 grid, hipStream_t s) {
+  // large dense NT / NN GEMMs: the ping-pong 256 x 128 loop (gemm_pp.h)
+  if constexpr (BUF && pp_loader_ok<LA, AK, true>() &&
+                pp_loader_ok<LB, BKM, false>()) {
+    const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+    // a split-K accumulation (f32 atomics) is re-split so that the 256 x 128
+    // tiles launch as many workgroups as the 128 x bn tiles would have
+    int sp = splits, ks = k_split;
+    if (epi.atomic == 1 && splits > 1) {
+      const long long pt = (long long)((M + PP_BM - 1) / PP_BM) *
+                           ((N + PP_BN - 1) / PP_BN);
+      const long long want = ((long long)tiles * splits + pt - 1) / pt;
+      ks = (int)((K + want - 1) / want);
+      ks = (ks + BK - 1) / BK * BK;
+      sp = (K + ks - 1) / ks;
+    }
+    if (want_pp<LA, AK, LB, BKM>(la, lb, M, N, bn, sp, groups))
+      return go_pp<LA, AK, LB, BKM>(la, lb, epi, M, N, K, ks, sp, groups, s);
+  }
 #define HVK_GO(BNV, W8V, VARV)                                              \
   return go<LA, AK, LB, BKM, BNV, BUF, W8V, VARV>(la, lb, epi, M, N, K,     \
                                                   k_split, tiles_n, tiles,  \

@@ -1,0 +1,360 @@
+// gemm_pp.h - ping-pong main loop for large bf16 GEMM / implicit-GEMM
+// convolution tiles (LDS-DMA operands).  Included by gemm_core.h inside its
+// anonymous namespace, after the loaders and Epi.
+//
+// Why a second main loop: the 128 x BN / 2-barriers-per-K-tile loop of
+// gemm_kernel is bound by moving its operands (profiles/r3_experiments.md §10:
+// with the LDS-DMA removed after the first K tile the 8192^3 GEMM runs 2x
+// faster; halving its MFMAs takes 2 % off).  This loop moves 0.75x the bytes
+// per FLOP (256 x 128 tile) and keeps the DMA off the MFMA critical path:
+//
+//   * 8 waves = two groups of 4 (one wave of each group per SIMD).  Group g
+//     owns tile rows g*128 .. +128 of the 256-row tile; inside a group the
+//     waves are 2 x 2, each 64 x 64 (4 x 4 MFMA 16x16x32 accumulators).
+//   * a K tile (BK = 64) is two phases; a phase = MEM slot (ds_read the
+//     fragments for this phase, issue this phase's LDS-DMA pieces, counted
+//     waits) then MFMA slot (16 MFMAs), each slot closed by s_barrier.
+//   * group 1 runs one barrier behind group 0, so on every SIMD one wave is
+//     in its MFMA slot while the other is in its MEM slot (ping-pong): LDS
+//     read latency and DMA issue hide under the other group's MFMAs.
+//   * 3-stage LDS ring (3 x 48 KiB): during K tile t the waves DMA tile t+2
+//     (the 256-row operand in phase 0, the 128-row one in phase 1); tile t+1
+//     is waited for with vmcnt(6) in phase 1 (tile t+2's six pieces stay in
+//     flight), so every piece has 4-6 slots to land.  One workgroup per CU.
+//
+// Hazards, by barrier-delimited slot number (group g, phase P = 2t + ph: MEM
+// slot 2P + g, MFMA slot 2P + g + 1):
+//   RAW  tile t+1 is waited for in slots 4t+2 (g0) / 4t+3 (g1), both before
+//        the barrier that ends them; its first reads are in slots 4t+4 / 4t+5.
+//   WAR  stage (t+2)%3 held tile t-1, last read in slot 4t-1 (g1, phase 1,
+//        lgkmcnt(0) before that slot's barrier); its first DMA is issued in
+//        slot 4t (g0).
+//
+// Operands: the LDS images and DMA addressing of gemm_kernel - K-major
+// [rows][64 k] (16-B chunk c of row r at c ^ (r & 7), ds_read_b128
+// fragments) or MN-major [64 k][128 cols] images (32-B block b of k-row k at
+// b ^ hk(k), ds_read_b64_tr_b16 fragments), written lane-linear by the DMA
+// from pre-permuted source offsets.  Every loader keeps its own addressing.
+//
+// Measured against gemm_kernel (tools/bench_gemm_ab.py, profiles/
+// r3_experiments.md §12): +8..14 % on the large dense NT / NN GEMMs; slower on
+// the implicit-GEMM convolutions and short-K / TN weight gradients, which keep
+// gemm_kernel (one workgroup per CU cannot overlap one tile's prologue and
+// epilogue with another's main loop).
+
+constexpr int PP_BM = 256, PP_BN = 128, PP_NST = 3;
+constexpr int PP_SA = PP_BM * BK, PP_SB = PP_BN * BK, PP_SST = PP_SA + PP_SB;
+constexpr int PP_LDC = PP_BN + 4;      // staged epilogue row pitch (floats)
+constexpr int PP_SMEM_BYTES = PP_NST * PP_SST * 2;
+static_assert(PP_BM * PP_LDC * 4 <= PP_SMEM_BYTES,
+              "epilogue staging fits the ring");
+
+// the operands the ping-pong loop takes (measured, profiles/r3_experiments.md
+// §12): dense K-major A (DenseK) against dense K-major or MN-major B (NT / NN
+// GEMMs).  The implicit-GEMM convolutions and the MN-major-A (TN) weight
+// gradients ran 2-50 % slower on it than on gemm_kernel's two workgroups per
+// CU and stay there.
+template <class L, bool KM, bool ISP>
+constexpr bool pp_loader_ok() {
+  if constexpr (ISP) return KM && std::is_same<L, DenseK>::value;
+  else return std::is_same<L, DenseK>::value || std::is_same<L, DenseMN>::value;
+}
+
+// One operand's DMA slots.  ROWS (256 / 128) x 64 k of bf16 = ROWS / 64
+// pieces of 1 KiB per wave.  K-major slot I: rows 8I .. 8I+7, all 8 chunks;
+// MN-major slot I: image I / 16 (128 columns each), k-rows 4 (I % 16) .. +3.
+template <class L, bool KM, int ROWS>
+struct PPOp {
+  static constexpr int NS = ROWS / 64;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t v[NS];
+  int kr[NS];
+  int kc;
+  __device__ __forceinline__ void init(const L& l, int r0, int w, int lane) {
+    rs = dma_rsrc(l.dbase());
+    kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int I = w * NS + i;
+      if constexpr (KM) {
+        v[i] = l.row_voff(r0 + 8 * I + (lane >> 3));
+      } else {
+        const int Ii = I & 15, h = I >> 4;
+        const int hkv = ((lane >> 4) & 3) | (((Ii >> 1) & 1) << 2);
+        const int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
+        kr[i] = 4 * Ii + (lane >> 4);
+        v[i] = l.col_voff(r0 + h * 128 + 8 * c, kr[i]);
+      }
+    }
+  }
+  __device__ __forceinline__ static uint16_t* dst(uint16_t* s, int I) {
+    if constexpr (KM) return s + I * 512;
+    else return s + (I >> 4) * (64 * 128) + (I & 15) * 512;
+  }
+  __device__ __forceinline__ void issue(const L& l, int k0, uint16_t* s, int w) {
+    if constexpr (KM) {
+      const bool kin = k0 + kc < l.K;
+      const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        dma16(rs, dst(s, w * NS + i), kin ? v[i] + kbyte : kBufOOB);
+    } else {
+      const uint32_t kadv = (uint32_t)k0 * (uint32_t)l.ld * 2u;
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        dma16(rs, dst(s, w * NS + i), k0 + kr[i] < l.K ? v[i] + kadv : kBufOOB);
+    }
+  }
+};
+
+// fragment of a 16-row MFMA tile at `row` (16-row aligned), 32-deep half ks
+template <bool KM>
+__device__ __forceinline__ bf16x8 pp_frag(const uint16_t* s, int row, int ks,
+                                          int fr, int fq) {
+  if constexpr (KM) {
+    const int r = row + fr;
+    const int c = ks * 4 + fq;
+    return *(const bf16x8*)(s + r * 64 + ((c ^ (r & 7)) << 3));
+  } else {
+    const uint16_t* im = s + (row >> 7) * (64 * 128);
+    const int b = (row & 127) >> 4;
+    const int trq = fr >> 2, trp = fr & 3;
+    const int k = ks * 32 + fq * 8 + trq;
+    const uint16_t* p0 = im + k * 128 + ((b ^ hk(k)) << 4) + trp * 4;
+    const uint16_t* p1 = im + (k + 4) * 128 + ((b ^ hk(k + 4)) << 4) + trp * 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// LP / PK: the 256-row operand (rows P) and whether it is K-major; LQ / QK
+// the 128-row one (rows Q): P x Q = M x N.
+// ABL (diagnostic builds, hvk_gemm_variant 31; wrong results by design): 1 =
+// no DMA after the prologue (the loop's MFMA / LDS / barrier cost alone)
+template <class LP, bool PK, class LQ, bool QK, int ABL = 0>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
+               int tiles_q, int tiles, int splits, int gm) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[PP_SMEM_BYTES / 2];
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  const int gs = wgid / tiles;
+  const int gi = gs / splits;
+  int tp, tq;
+  if (gm > 1) {  // grouped tile order, as in gemm_kernel
+    const int tiles_p = tiles / tiles_q;
+    const int g = tile / (gm * tiles_q);
+    const int p0g = g * gm;
+    const int gh = min(tiles_p - p0g, gm);
+    const int r = tile - g * gm * tiles_q;
+    tp = p0g + r % gh;
+    tq = r / gh;
+  } else {
+    tp = tile / tiles_q;
+    tq = tile - tp * tiles_q;
+  }
+  const int kbeg = (gs - gi * splits) * k_split;
+  const int kend = min(K, kbeg + k_split);
+  if (kbeg >= kend) return;
+  lp.group(gi);
+  lq.group(gi);
+  const int p0 = tp * PP_BM, q0 = tq * PP_BN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = w >> 2;
+  const int prow = grp * 128 + ((w >> 1) & 1) * 64;  // wave's first P row
+  const int qrow = (w & 1) * 64;                     // wave's first Q row
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PPOp<LP, PK, PP_BM> op;
+  PPOp<LQ, QK, PP_BN> oq;
+  op.init(lp, p0, w, lane);
+  oq.init(lq, q0, w, lane);
+  constexpr int NIP = PPOp<LP, PK, PP_BM>::NS;
+  constexpr int NIQ = PPOp<LQ, QK, PP_BN>::NS;
+  static_assert(NIP + NIQ == 6, "vmcnt counts below assume 6 pieces per tile");
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  // prologue: tiles 0 and 1 in flight, wait for tile 0
+  op.issue(lp, kbeg, smem, w);
+  oq.issue(lq, kbeg, smem + PP_SA, w);
+  if (nk > 1) {
+    op.issue(lp, kbeg + BK, smem + PP_SST, w);
+    oq.issue(lq, kbeg + BK, smem + PP_SST + PP_SA, w);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one slot
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[2][2], bfv[4][2];
+  int scur = 0, spre = 2;  // stage of tile t, of tile t + 2
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* sP = smem + scur * PP_SST;
+    const uint16_t* sQ = sP + PP_SA;
+    uint16_t* dP = smem + spre * PP_SST;
+    const bool pre = kt + 2 < nk;
+    const int kpre = kbeg + (kt + 2) * BK;
+    // ---- phase 0, MEM: P rows 0..31 of the wave, all of its Q rows
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfv[j][ks] = pp_frag<QK>(sQ, qrow + j * 16, ks, fr, fq);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i][ks] = pp_frag<PK>(sP, prow + i * 16, ks, fr, fq);
+    }
+    if (pre && ABL != 1) op.issue(lp, kpre, dP, w);
+    // no wait here: the fragment reads retire across the barrier (the MFMA
+    // slot waits for them); tile t's stage is not restaged before tile t+1's
+    // phase 0, and its last reads (phase 1) are retired before a barrier
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 0, MFMA
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i][ks], bfv[j][ks], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 1, MEM: P rows 32..63; tile t + 2's Q; wait for tile t + 1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i][ks] = pp_frag<PK>(sP, prow + 32 + i * 16, ks, fr, fq);
+    if (pre && ABL != 1) {
+      oq.issue(lq, kpre, dP + PP_SA, w);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase 1, MFMA
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[2 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i][ks], bfv[j][ks], acc[2 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    scur = scur == 2 ? 0 : scur + 1;
+    spre = spre == 2 ? 0 : spre + 1;
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // group 1's last slot
+  asm volatile("" ::: "memory");
+
+  // accumulator (i, j)[rr] is tile element (P row prow + 16i + 4fq + rr,
+  // Q row qrow + 16j + fr)
+  // stage the f32 tile through LDS (the ring is drained: every DMA waited
+  // for, every fragment read retired before the last barrier), then
+  // row-contiguous 16-B stores
+  float* sC = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pb = prow + i * 16 + fq * 4;
+      const int qc = qrow + j * 16 + fr;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        sC[(pb + rr) * PP_LDC + qc] = acc[i][j][rr];
+      }
+    }
+  __syncthreads();
+  constexpr int ROWS = PP_BM, LD = PP_LDC;
+  const int m0 = p0, n0 = q0;
+  if (epi.atomic) {
+    // split-K partial sums: f32 atomics, a wave adding 64 consecutive
+    // columns of one row per instruction (256 contiguous bytes: the full
+    // atomic rate; 16 x 4 accumulator fragments straight from registers hit
+    // 16 rows per instruction)
+    constexpr int COLS = PP_BN;
+    constexpr int RSTEP = 512 / COLS;
+    const int c = t % COLS;
+    for (int row = t / COLS; row < ROWS; row += RSTEP)
+      epi.store(gi, m0 + row, n0 + c, sC[row * LD + c]);
+    return;
+  }
+  constexpr int CH = PP_BN / 8;
+  const bool fast = epi.fast_ok();
+  for (int q = t; q < ROWS * CH; q += 512) {
+    const int row = q / CH, c8 = (q % CH) * 8;
+    if (m0 + row >= epi.M) continue;
+    const float4* src = (const float4*)(sC + row * LD + c8);
+    float v[8];
+    const float4 lo = src[0], hi = src[1];
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    if (fast && n0 + c8 + 8 <= epi.N &&
+        (epi.ones_col < 0 || n0 + c8 + 8 <= epi.ones_col))
+      epi.store8_fast(gi, m0 + row, n0 + c8, v);
+    else
+      epi.store8(gi, m0 + row, n0 + c8, v);
+  }
+}
+
+// The ping-pong loop takes a dense NT / NN GEMM (buffer-DMA operands) with
+// a 128-wide column tile and at least one 256 x 128 tile per CU (one
+// workgroup per CU).  hvk_gemm_variant 30 (or 0) disables it, 31 runs
+// its no-DMA ablation (A/B runs).
+template <class LA, bool AK, class LB, bool BKM>
+bool want_pp(const LA& la, const LB& lb, int M, int N, int bn, int splits,
+             int groups) {
+  if constexpr (!pp_loader_ok<LA, AK, true>() ||
+                !pp_loader_ok<LB, BKM, false>()) {
+    return false;
+  } else {
+    if (hvk_gemm_variant == 30 || hvk_gemm_variant == 0) return false;
+    if (bn != 128 || !la.dma_ok() || !lb.dma_ok()) return false;
+    return (long long)((M + PP_BM - 1) / PP_BM) * ((N + PP_BN - 1) / PP_BN) *
+               splits * groups >= 256;
+  }
+}
+
+template <class LP, bool PK, class LQ, bool QK>
+hipError_t go_pp(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
+                 int K, int k_split, int splits, int groups, hipStream_t s) {
+  const int tiles_p = (P + PP_BM - 1) / PP_BM;
+  const int tiles_q = (Q + PP_BN - 1) / PP_BN;
+  const int tiles = tiles_p * tiles_q;
+  const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
+  dim3 grid((unsigned)((long long)tiles * splits * groups));
+  if constexpr (QK) {
+    if (hvk_gemm_variant == 31) {
+      hipLaunchKernelGGL((gemm_pp_kernel<LP, PK, LQ, QK, 1>), grid, dim3(512),
+                         0, s, lp, lq, epi, P, Q, K, k_split, tiles_q, tiles,
+                         splits, gm);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((gemm_pp_kernel<LP, PK, LQ, QK>), grid, dim3(512), 0, s,
+                     lp, lq, epi, P, Q, K, k_split, tiles_q, tiles, splits, gm);
+  return hipGetLastError();
+}
