@@ -263,6 +263,62 @@ def test_conv_dgrad_fp8(cfg):
     close(got, ref, 1e-2)
 
 
+WGRAD8 = CONVS8 + [
+    # several K tiles / splits, OC and KK off the 128 grid, 7 x 7 images
+    (4, 28, 28, 64, 128, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (8, 14, 14, 256, 160, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (16, 7, 7, 48, 32, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", WGRAD8)
+def test_conv_wgrad_fp8(cfg):
+    """e5m2 gradient x e4m3 input weight gradient (wgrad_fp8.hip, transposed
+    LDS reads) against the float32 weight gradient of the same dequantized
+    operands; accumulates into the gradient, any pixel split"""
+    N, H, W, C, OC, KH, KW, sl, pad, g = cfg
+    OH, OW = ops.conv_out_size(H, W, KH, KW, sl, pad)
+    x8, sx, x8c, sxc = _pair(rnd(N, H, W, C))
+    d8, sd, d8c, sdc = _pair(rnd(N, OH, OW, OC, seed=2, scale=1e-2),
+                             fp8.E5M2)
+    ref = torch.zeros(OC, KH, KW, C // g)
+    refb = torch.zeros(OC)
+    fp8.conv_wgrad(x8c, sxc, d8c, sdc, ref, sl, pad, g, dbias=refb)
+    for splits in (1, 3, None):
+        got = torch.ones(OC, KH, KW, C // g, device=DEV)
+        gotb = torch.ones(OC, device=DEV)
+        fp8.conv_wgrad(x8, sx, d8, sd, got, sl, pad, g, splits=splits,
+                       dbias=gotb)
+        torch.cuda.synchronize()
+        close(got - 1.0, ref, 2e-3)
+        close(gotb - 1.0, refb, 2e-3)
+
+
+@pytest.mark.gpu
+def test_fp8_workflow_wgrad_fp8_vs_bf16():
+    """the same fp8 conv stack trained a few steps with the weight
+    gradients on the fp8 kernel and on the bf16 kernel: the fp8 wgrad path
+    is taken, and the trajectories agree to the fp8 gradient rounding"""
+    old = root.common.engine.fp8_wgrad
+    try:
+        root.common.engine.fp8_wgrad = False
+        a = _fp8_two_conv_run(True, steps=3, backend="hip")
+        root.common.engine.fp8_wgrad = True
+        b = _fp8_two_conv_run(True, steps=3, backend="hip")
+    finally:
+        root.common.engine.fp8_wgrad = old
+    gd = [u for u in b.gds if getattr(u.forward, "fp8_", False)]
+    assert gd and all(u._fp8_wgrad_ok(u.forward, u.forward.x8_) for u in gd)
+    w0 = _fp8_two_conv_run(True, steps=0, backend="hip").param_store_ \
+        .master.float().cpu()
+    da = a.param_store_.master.float().cpu() - w0
+    db = b.param_store_.master.float().cpu() - w0
+    assert torch.isfinite(db).all() and db.norm() > 0
+    rel = ((da - db).norm() / da.norm()).item()
+    assert 0 < rel < 0.3, rel
+
+
 @pytest.mark.gpu
 def test_fp8_roll_kernel():
     r = fp8.registry(DEV)

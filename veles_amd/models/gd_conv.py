@@ -3,8 +3,12 @@
 grad_W += wgrad(x, err)   implicit-GEMM MFMA, split over pixels, f32 atomics
 grad_b += colsum(err)
 err_input = dgrad(err, W) [* f'(below.output)]  implicit transposed-conv GEMM
-            (fp8: e5m2 err x e4m3 W on the fp8 MFMA kernel when the forward
-            layer runs in fp8; the weight gradient stays bf16)
+
+When the forward layer runs in fp8 both GEMMs take the e5m2 copy of err:
+backward-data against the e4m3 weights, the weight gradient against the
+layer's e4m3 input copy (fp8 MFMA kernels; the bias gradient from the same
+launch, as the pixel sums of the e5m2 err).  ``root.common.engine.fp8_wgrad = False``
+keeps the weight gradient on the bf16 kernel.
 """
 from __future__ import annotations
 
@@ -61,26 +65,32 @@ class GradientDescentConv(GradientDescentBase):
             # the split-K atomics of this layer start from its own zeroed
             # span (normally the update already cleared it: zero_tail)
             self.store_.zero_grads((pw, pb))
-        # weight AND bias gradients from one implicit-GEMM launch
-        ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,
-                       fwd.grouping, col=getattr(fwd, "col_", None),
-                       dbias=None if pb is None else pb.grad)
+        use8 = getattr(fwd, "fp8_", False)
+        if use8:
+            if self.fp8_sdy_ is None:
+                self.fp8_sdy_ = fp8.Scaler(self.torch_device, fp8.E5M2)
+            # the e5m2 copy comes from the epilogue of the GD that produced
+            # err_output when it wrote it this pass
+            if not self.dy8_fresh_ or self.dy8_ is None or \
+                    tuple(self.dy8_.shape) != tuple(err.shape):
+                self.dy8_ = fp8.quantize(err, self.fp8_sdy_, out=self.dy8_)
+            self.dy8_fresh_ = False
+        if use8 and self._fp8_wgrad_ok(fwd, x):
+            fp8.conv_wgrad(fwd.x8_, fwd.fp8_sx_, self.dy8_, self.fp8_sdy_,
+                           pw.grad, fwd.sliding, fwd.padding, fwd.grouping,
+                           dbias=None if pb is None else pb.grad)
+        else:
+            # weight AND bias gradients from one implicit-GEMM launch
+            ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,
+                           fwd.grouping, col=getattr(fwd, "col_", None),
+                           dbias=None if pb is None else pb.grad)
         if self.need_err_input:
             ei = self.alloc_err_input(tuple(x.shape))
             aux, aux_act = self.aux_tensor()
             if aux is not None and aux.dim() == 3:
                 aux = aux.unsqueeze(-1)
-            if getattr(fwd, "fp8_", False):
+            if use8:
                 # e5m2 gradient x e4m3 weights on the fp8 MFMA kernel
-                if self.fp8_sdy_ is None:
-                    self.fp8_sdy_ = fp8.Scaler(self.torch_device, fp8.E5M2)
-                # the e5m2 copy comes from the epilogue of the GD that
-                # produced err_output when it wrote it this pass
-                if not self.dy8_fresh_ or self.dy8_ is None or \
-                        tuple(self.dy8_.shape) != tuple(err.shape):
-                    self.dy8_ = fp8.quantize(err, self.fp8_sdy_,
-                                             out=self.dy8_)
-                self.dy8_fresh_ = False
                 wt8 = fp8.permute_for_dgrad(fwd.w8_, fwd.grouping) \
                     if err.is_cuda else None
                 q8, qs = self._q8_target(ei)
@@ -98,6 +108,17 @@ class GradientDescentConv(GradientDescentBase):
             if squeeze:
                 self.err_input.devmem = ei.squeeze(-1)
         self.report_gradients()
+
+
+    @staticmethod
+    def _fp8_wgrad_ok(fwd, x):
+        """the fp8 weight gradient needs the forward's e4m3 input copy of
+        this very input (not the s2d / im2col paths)"""
+        from veles_amd.utils.config import root, get
+        x8 = getattr(fwd, "x8_", None)
+        return get(root.common.engine.fp8_wgrad, True) and x8 is not None \
+            and not isinstance(x, ops.S2DImage) and \
+            tuple(x8.shape) == tuple(x.shape) and x8.device == x.device
 
 
 class GDTanhConv(GradientDescentConv):

@@ -30,8 +30,8 @@ import torch
 from veles_amd.ops import _lib
 
 __all__ = ["E4M3", "E5M2", "Scaler", "registry", "quantize", "gemm",
-           "conv_fwd", "conv_dgrad", "permute_for_dgrad", "transpose",
-           "dequantize", "HIST"]
+           "conv_fwd", "conv_dgrad", "conv_wgrad", "permute_for_dgrad",
+           "transpose", "dequantize", "HIST"]
 
 E4M3, E5M2 = 0, 1
 HIST = 16
@@ -318,3 +318,37 @@ def conv_dgrad(dy8, sdy, w8, sw, x_shape, sliding=(1, 1),
                         out=out)
     _q8_ref(dx, q8, q8_scaler)
     return dx
+
+
+def conv_wgrad(x8, sx, dy8, sdy, dw, sliding=(1, 1), padding=(0, 0, 0, 0),
+               groups=1, splits=None, dbias=None):
+    """dw (float32 [OC][KH][KW][C/g]) += conv weight gradient of deq(x8)
+    (the layer's input copy) and deq(dy8) (its output-gradient copy), and
+    ``dbias`` (float32 [OC]) += the pixel sums of deq(dy8): the e5m2 x e4m3
+    MFMA kernel on the GPU (the bias from MFMAs against an all-ones operand),
+    split over pixels with f32 atomics; the float32 op on dequantized
+    operands on the CPU."""
+    from veles_amd import ops
+    N, H, W, C = x8.shape
+    _, OH, OW, OC = dy8.shape
+    _, KH, KW, Cg = dw.shape
+    sxx, syy = sliding
+    pl, pt, pr, pb = padding
+    if x8.is_cuda:
+        if splits is None:
+            splits = ops.wgrad_splits(N * OH * OW, OC // groups, KH * KW * Cg,
+                                      groups)
+        _call("hvk_conv_wgrad_fp8", x8.data_ptr(), dy8.data_ptr(),
+              dw.data_ptr(), None if dbias is None else dbias.data_ptr(),
+              N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH, OW,
+              groups, int(splits), sx.fmt, sdy.fmt, sx.state.data_ptr(),
+              sdy.state.data_ptr(), HIST, float(sx.fmax_eff),
+              float(sdy.fmax_eff), _s(x8))
+        return dw
+    acc = torch.zeros_like(dw)
+    dq = dequantize(dy8, sdy)
+    ops.conv_wgrad(dequantize(x8, sx), dq, acc, sliding, padding, groups)
+    dw += acc
+    if dbias is not None:
+        dbias += dq.reshape(-1, OC).sum(0)
+    return dw
