@@ -765,7 +765,11 @@ __device__ __forceinline__ int hk(int k) { return (k & 3) | (((k >> 3) & 1) << 2
 //      rows (AlexNet conv1 weight gradient, OC = 96) wastes no MFMAs on the
 //      zero rows 96..127 of the 128-row tile;
 //   2  48 columns of a 64-wide tile (4 waves stacked along M, each 32 x 48):
-//      a 48-wide output (AlexNet conv2 backward-data, 48 channels per group).
+//      a 48-wide output (AlexNet conv2 backward-data, 48 channels per group);
+//   3  a 256-row tile (twice the A stage), 8 waves stacked along M, each
+//      32 x BN (BN 64): narrow outputs move 0.83x the L2 -> LDS bytes per
+//      FLOP of the 128 x 64 tile and still fit two blocks per CU (80 KiB);
+//   4  as 3, computing 48 of the 64 columns.
 // ABL (diagnostic builds only, selected by hvk_set_gemm_variant 11..13 in
 // A/B runs; wrong results by design): 1 half the MFMAs (ks = 0 only), 2 no
 // LDS-DMA after the first K tile, 3 neither DMA nor barriers after it.
@@ -776,14 +780,17 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
             int tiles_n, int tiles, int splits, int gm) {
   constexpr int NW = W8 ? 8 : 4;        // waves per block
   constexpr int NT = NW * 64;           // threads per block
-  constexpr int WNC = VAR == 2 ? 1 : NW / 2;   // waves along N
-  constexpr int MT = VAR == 1 ? 3 : (VAR == 2 ? 2 : 4);  // m-tiles per wave
+  constexpr int BMT = VAR >= 3 ? 256 : BM;     // rows loaded per block
+  constexpr int WNC = VAR >= 2 ? 1 : NW / 2;   // waves along N
+  constexpr int MT = VAR == 1 ? 3 : (VAR >= 2 ? 2 : 4);  // m-tiles per wave
   constexpr int WMR = 16 * MT;                 // rows per wave
   constexpr int BMC = (NW / WNC) * WMR;        // rows computed per block
-  constexpr int NC = VAR == 2 ? 48 : BN_;      // columns computed per block
+  constexpr int NC = (VAR == 2 || VAR == 4) ? 48 : BN_;  // columns computed
   constexpr int NB = NC / (16 * WNC);          // MFMA n-tiles per wave
-  static_assert(BMC <= BM && NC <= BN_ && NB * 16 * WNC == NC, "layout");
+  static_assert(BMC <= BMT && NC <= BN_ && NB * 16 * WNC == NC, "layout");
   static_assert(!W8 || BN_ % 64 == 0, "W8 needs BN 64 / 128");
+  static_assert(VAR < 3 || (W8 && AK && BKM && BN_ == 64 && BMC == 256),
+                "256-row tiles: 8 waves, K-major operands, BN 64");
   constexpr int CPR = BN_ / 8;          // MN-major B: chunks per k-row
   constexpr int RPS = NTHR / CPR;       // MN-major B: k-rows per sweep
   // operand double buffers (64 KiB); reused as the f32 C tile (with a
@@ -791,10 +798,10 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   // A stages (BM x BK) then B stages (BN x BK K-major, or the 128-wide
   // MN-major image); a 64-wide K-major B halves its stage, so such kernels
   // fit 3 blocks per CU (48 KiB) instead of 2
-  constexpr int SA = BM * BK;
+  constexpr int SA = BMT * BK;
   constexpr int SB = (BKM ? BN_ : 128) * BK;
-  constexpr int SMEM_BYTES = (2 * (SA + SB) * 2 > 128 * (BN_ + 4) * 4)
-                                 ? 2 * (SA + SB) * 2 : 128 * (BN_ + 4) * 4;
+  constexpr int SMEM_BYTES = (2 * (SA + SB) * 2 > BMT * (BN_ + 4) * 4)
+                                 ? 2 * (SA + SB) * 2 : BMT * (BN_ + 4) * 4;
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM_BYTES / 2];
   // 1-D grid over (group, split, tile), tile fastest.  Bijective XCD remap
   // (cdna_hip_programming.md T1): each XCD gets a contiguous wgid range, so
@@ -884,7 +891,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     if (la.dma_ok() && lb.dma_ok()) {
       // ---- LDS-DMA pipeline (global_load_lds_dwordx4): the next tile's
       // loads stay in flight across the barrier; one counted vmcnt per tile.
-      constexpr int NIA = 16 / NW;         // DMA instructions / wave (A)
+      constexpr int NIA = BMT / 8 / NW;    // DMA instructions / wave (A)
       constexpr int NIB = BKM ? BN_ / (8 * NW) : 16 / NW;
       const int w = __builtin_amdgcn_readfirstlane(wid);
       typename LA::Ctx da[NIA];
@@ -1247,6 +1254,24 @@ hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
   return go<LA, AK, LB, BKM, BNV, BUF, W8V, VARV>(la, lb, epi, M, N, K,     \
                                                   k_split, tiles_n, tiles,  \
                                                   splits, grid, s)
+  // narrow K-major GEMMs (64-wide column tiles: conv backward-data with 48 /
+  // 192 channels per group, forward with 192 outputs per group) over many
+  // rows: the 256-row tile (VAR 3 / 4); hvk_gemm_variant 40 turns it off
+  if constexpr (AK && BKM && LA::kGlds && LB::kGlds) {
+    if (bn == 64 && hvk_gemm_variant != 40 && hvk_gemm_variant != 0 &&
+        la.dma_ok() && lb.dma_ok()) {
+      const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+      const int t256 = (M + 255) / 256 * tiles_n;
+      if ((long long)t256 * splits * groups >= 512) {
+        const dim3 g256((unsigned)((long long)t256 * splits * groups));
+        if (N > 32 && N <= 48)
+          return go<LA, AK, LB, BKM, 64, BUF, true, 4>(
+              la, lb, epi, M, N, K, k_split, tiles_n, t256, splits, g256, s);
+        return go<LA, AK, LB, BKM, 64, BUF, true, 3>(
+            la, lb, epi, M, N, K, k_split, tiles_n, t256, splits, g256, s);
+      }
+    }
+  }
   // (backward-data never runs 8-wave: not instantiated, half the compile)
   if constexpr (LA::kGlds && LB::kGlds &&
                 !std::is_base_of<ConvDgradA, LA>::value) {

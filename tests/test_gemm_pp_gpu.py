@@ -85,3 +85,41 @@ def test_pp_splitk_accumulate():
     ref = a.float() @ b.float().t() + 0.5
     close(old, ref, 1e-3)
     close(new, ref, 1e-3)
+
+
+def _conv_case(N, H, W, C, OC, k, p, g):
+    x = rnd(N, H, W, C, seed=3)
+    w = rnd(OC, k, k, C // g, seed=4, scale=0.05)
+    return x, w
+
+
+@pytest.mark.parametrize("cfg", [
+    # AlexNet conv2 backward-data (48 channels per group: VAR 4), conv4 /
+    # conv5 backward-data and conv4 forward (192 per group -> 3 x 64: VAR 3)
+    (128, 27, 27, 96, 256, 5, 2, 2),
+    (256, 13, 13, 384, 384, 3, 1, 2),
+    (256, 13, 13, 384, 256, 3, 1, 2)])
+def test_256_row_narrow_tiles(cfg):
+    """the 256-row x 64 tile of gemm_kernel (VAR 3 / 4) against the 128-row
+    tile (hvk_set_gemm_variant 40): bit-identical, and against fp32"""
+    import torch.nn.functional as F
+    N, H, W, C, OC, k, p, g = cfg
+    x, w = _conv_case(*cfg)
+    pad = (p, p, p, p)
+    dy = rnd(N, H, W, OC, seed=5)
+    old, new = run_variants(lambda: ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1),
+                                                   pad, g), (40, -1))
+    assert torch.equal(old, new)
+    ref = torch.nn.grad.conv2d_input(
+        (N, C, H, W), w.float().permute(0, 3, 1, 2),
+        dy.float().permute(0, 3, 1, 2), padding=p,
+        groups=g).permute(0, 2, 3, 1)
+    close(new, ref, 1e-2)
+    b = torch.randn(OC, device=DEV)
+    old, new = run_variants(lambda: ops.conv_fwd(x, w, b, (1, 1), pad, g, 3),
+                            (40, -1))
+    assert torch.equal(old, new)
+    ref = F.relu(F.conv2d(x.float().permute(0, 3, 1, 2),
+                          w.float().permute(0, 3, 1, 2), b, padding=p,
+                          groups=g)).permute(0, 2, 3, 1)
+    close(new, ref, 1e-2)
