@@ -202,6 +202,9 @@ conv_halo_kernel(HaloGeom hg, const uint16_t* __restrict__ src, DenseK lb,
   constexpr int CH = NC / 8;
   const bool fast = epi.fast_ok();
   const int rows = hg.TH * hg.TW;
+  const float qs = epi.q8.q ? fp8_scale(epi.q8.st, epi.q8.hist, epi.q8.fmax)
+                            : 1.f;
+  float amax = 0.f;
   for (int q = t; q < rows * CH; q += NT) {
     const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
     uint32_t py, px;
@@ -215,9 +218,13 @@ conv_halo_kernel(HaloGeom hg, const uint16_t* __restrict__ src, DenseK lb,
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
     if (fast && n0 + c8 + 8 <= epi.N)
-      epi.store8_fast((int)gi, P, n0 + c8, v);
+      epi.store8_fast((int)gi, P, n0 + c8, v, qs, &amax);
     else
       epi.store8((int)gi, P, n0 + c8, v);
+  }
+  if (epi.q8.q) {  // block-uniform
+    __syncthreads();
+    q8_block_amax(epi.q8, amax, sC);
   }
 }
 
@@ -322,10 +329,10 @@ hipError_t run_halo(const HaloGeom& g, const uint16_t* src, const DenseK& lb,
 // conv forward, stride 1 (the s2d conv1 and AlexNet conv2..5 / VGG shapes):
 // -2 when the halo path does not apply (the caller falls back to
 // hvk_conv_fwd)
-HVK_API int hvk_conv_fwd_halo(const void* X, const void* Wt, const float* bias,
-                              void* Y, int N, int H, int W, int C, int OC,
-                              int KH, int KW, int pt, int pl, int OH, int OW,
-                              int groups, int act, hipStream_t s) {
+static int conv_fwd_halo(const void* X, const void* Wt, const float* bias,
+                         void* Y, int N, int H, int W, int C, int OC, int KH,
+                         int KW, int pt, int pl, int OH, int OW, int groups,
+                         int act, const Q8* q8, hipStream_t s) {
   const int Cg = C / groups, OCg = OC / groups;
   HaloGeom g = make_halo(N, H, W, C, Cg, OH, OW, KH, KW, -pt, -pl, 0);
   const int K = KH * KW * Cg;
@@ -337,7 +344,33 @@ HVK_API int hvk_conv_fwd_halo(const void* X, const void* Wt, const float* bias,
   Epi e = make_epi(Y, OC, N * OH * OW, OCg, 0, 0, 1.f, 0.f, bias, 1, act,
                    nullptr, 0, 0);
   e.gcol = OCg;
+  if (q8) {
+    if (!e.fast_ok() || OCg % 8 || (((uintptr_t)q8->q) & 7)) return -3;
+    e.q8 = *q8;
+  }
   return (int)run_halo(g, (const uint16_t*)X, lb, e, K, OCg, groups, s);
+}
+
+HVK_API int hvk_conv_fwd_halo(const void* X, const void* Wt, const float* bias,
+                              void* Y, int N, int H, int W, int C, int OC,
+                              int KH, int KW, int pt, int pl, int OH, int OW,
+                              int groups, int act, hipStream_t s) {
+  return conv_fwd_halo(X, Wt, bias, Y, N, H, W, C, OC, KH, KW, pt, pl, OH,
+                       OW, groups, act, nullptr, s);
+}
+
+// as hvk_conv_fwd_halo, and the fp8 copy of Y for the fp8 layer reading it
+// (q8: [N][OH][OW][OC] bytes; fmt 0 e4m3 / 1 e5m2; amax into the shards)
+HVK_API int hvk_conv_fwd_halo_q8(const void* X, const void* Wt,
+                                 const float* bias, void* Y, int N, int H,
+                                 int W, int C, int OC, int KH, int KW, int pt,
+                                 int pl, int OH, int OW, int groups, int act,
+                                 void* q8, const float* q8_st, float* q8_shard,
+                                 float q8_fmax, int q8_fmt, int hist,
+                                 hipStream_t s) {
+  const Q8 z{(uint8_t*)q8, q8_st, q8_shard, q8_fmax, q8_fmt, hist};
+  return conv_fwd_halo(X, Wt, bias, Y, N, H, W, C, OC, KH, KW, pt, pl, OH,
+                       OW, groups, act, &z, s);
 }
 
 // conv backward-data, stride 1, weights pre-permuted to Wt[g][c][kh][kw][oc]

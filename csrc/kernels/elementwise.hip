@@ -821,6 +821,11 @@ __device__ __forceinline__ uint64_t load_u8x8(const uint8_t* __restrict__ src,
   return v;
 }
 
+// Per thread: the SPT sample ids first, then every source load of the SPT
+// samples (both row pieces, three aligned dwords each, at clamped in-range
+// addresses - absent pieces are masked afterwards), then the arithmetic and
+// the stores: one memory round trip per thread instead of one per sample and
+// piece (the branchy per-sample form waited on each load in turn).
 template <int S, int C, int SPT>
 __global__ void __launch_bounds__(256)
 fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
@@ -839,6 +844,77 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
   if (ch < chunks) {
     const int q = ch / CPP, j = ch - (ch / CPP) * CPP;
     const int Y = q / W2, X = q - (q / W2) * W2;
+    // the chunk's elements 8j .. 8j+7: piece 0 in row dy0 from r0 (n0
+    // bytes), piece 1 (if any) at the start of row dy0 + 1
+    const int e0 = 8 * j, dy0 = e0 / RUN, r0 = e0 - dy0 * RUN;
+    const int n0 = RUN - r0 < 8 ? RUN - r0 : 8;
+    const int ix0 = S * X - pl;
+    const bool xin = ix0 >= 0 && ix0 + S <= W;
+    const int iy0 = S * Y + dy0 - pt, iy1 = iy0 + 1;
+    const bool y0in = iy0 >= 0 && iy0 < H, y1in = iy1 >= 0 && iy1 < H;
+    int sid[SPT];
+#pragma unroll
+    for (int u = 0; u < SPT; ++u) {
+      const int i = i0 + u;
+      sid[u] = (i < max_mb && i < count) ? shuffled[start + i] : -1;
+    }
+    uint64_t v[SPT];
+    if (xin) {
+      // in-row offsets of the two pieces (the 4-byte aligned starts and
+      // the byte shifts) - the same for every sample
+      const long long o0 = ((long long)iy0 * W + ix0) * C + r0;
+      const long long o1 = ((long long)iy1 * W + ix0) * C;
+      const uint32_t sh0 = (uint32_t)(o0 & 3), sh1 = (uint32_t)(o1 & 3);
+      uint32_t d[SPT][6];
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const long long base = (long long)(sid[u] < 0 ? 0 : sid[u]) * sample;
+        long long a0 = (base + o0) & ~3ll, a1 = (base + o1) & ~3ll;
+        // clamp into the buffer (out-of-image rows, the last image's tail):
+        // such words are masked or re-read exactly below
+        a0 = min(max(a0, 0ll), src_bytes - 12);
+        a1 = min(max(a1, 0ll), src_bytes - 12);
+        const uint32_t* w0 = (const uint32_t*)(src + a0);
+        const uint32_t* w1 = (const uint32_t*)(src + a1);
+        d[u][0] = w0[0]; d[u][1] = w0[1]; d[u][2] = w0[2];
+        d[u][3] = w1[0]; d[u][4] = w1[1]; d[u][5] = w1[2];
+      }
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        const long long base = (long long)(sid[u] < 0 ? 0 : sid[u]) * sample;
+        uint64_t p0 = ((uint64_t)__builtin_amdgcn_alignbyte(d[u][2], d[u][1], sh0)
+                       << 32) |
+                      __builtin_amdgcn_alignbyte(d[u][1], d[u][0], sh0);
+        uint64_t p1 = ((uint64_t)__builtin_amdgcn_alignbyte(d[u][5], d[u][4], sh1)
+                       << 32) |
+                      __builtin_amdgcn_alignbyte(d[u][4], d[u][3], sh1);
+        // the rare clamped tail: exact byte reads
+        if (((base + o0) & ~3ll) + 12 > src_bytes && y0in)
+          p0 = load_u8x8(src, base + o0, n0, src_bytes);
+        if (n0 < 8 && ((base + o1) & ~3ll) + 12 > src_bytes && y1in)
+          p1 = load_u8x8(src, base + o1, 8 - n0, src_bytes);
+        if (n0 < 8) p0 &= (1ull << (8 * n0)) - 1;
+        uint64_t r = y0in ? p0 : 0;
+        if (n0 < 8 && y1in) r |= p1 << (8 * n0);
+        v[u] = sid[u] >= 0 ? r : 0;
+      }
+    } else {
+      // image border: per element, zero outside the image
+#pragma unroll
+      for (int u = 0; u < SPT; ++u) {
+        v[u] = 0;
+        if (sid[u] < 0) continue;
+        const long long base = (long long)sid[u] * sample;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int ee = e0 + e, dy = ee / RUN, rr2 = ee - dy * RUN;
+          const int iy = S * Y + dy - pt, ix = ix0 + rr2 / C;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+            v[u] |= (uint64_t)src[base + ((long long)iy * W + ix) * C +
+                                  rr2 % C] << (8 * e);
+        }
+      }
+    }
     float mm[8], rr[8];
     {
       const float4* m4 = (const float4*)(mean2 + (long long)ch * 8);
@@ -849,45 +925,16 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
       rr[0] = c.x; rr[1] = c.y; rr[2] = c.z; rr[3] = c.w;
       rr[4] = d.x; rr[5] = d.y; rr[6] = d.z; rr[7] = d.w;
     }
-    // the chunk's elements 8j .. 8j+7: piece 0 in row dy0 from r0 (n0
-    // bytes), piece 1 (if any) at the start of row dy0 + 1
-    const int e0 = 8 * j, dy0 = e0 / RUN, r0 = e0 - dy0 * RUN;
-    const int n0 = RUN - r0 < 8 ? RUN - r0 : 8;
-    const int ix0 = S * X - pl;
-    const bool xin = ix0 >= 0 && ix0 + S <= W;
-    const int iy0 = S * Y + dy0 - pt, iy1 = iy0 + 1;
-    const bool y0in = iy0 >= 0 && iy0 < H, y1in = iy1 >= 0 && iy1 < H;
 #pragma unroll
     for (int u = 0; u < SPT; ++u) {
       const int i = i0 + u;
       if (i >= max_mb) break;
-      const int sid = i < count ? shuffled[start + i] : -1;
       uint4 o = make_uint4(0, 0, 0, 0);
-      if (sid >= 0) {
-        const long long base = (long long)sid * sample;
-        uint64_t v = 0;
-        if (xin) {
-          if (y0in)
-            v = load_u8x8(src, base + ((long long)iy0 * W + ix0) * C + r0, n0,
-                          src_bytes);
-          if (n0 < 8 && y1in)
-            v |= load_u8x8(src, base + ((long long)iy1 * W + ix0) * C,
-                           8 - n0, src_bytes) << (8 * n0);
-        } else {
-          // image border: per element, zero outside the image
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int ee = e0 + e, dy = ee / RUN, rr2 = ee - dy * RUN;
-            const int iy = S * Y + dy - pt, ix = ix0 + rr2 / C;
-            if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-              v |= (uint64_t)src[base + ((long long)iy * W + ix) * C +
-                                 rr2 % C] << (8 * e);
-          }
-        }
+      if (sid[u] >= 0) {
         float f[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          f[e] = ((float)((v >> (8 * e)) & 0xFF) - mm[e]) * rr[e];
+          f[e] = ((float)((v[u] >> (8 * e)) & 0xFF) - mm[e]) * rr[e];
         o = pack_bf16x8(f);
       }
       *(uint4*)(dst + (long long)i * chunks * 8 + (long long)ch * 8) = o;

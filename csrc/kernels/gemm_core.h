@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "conv_geom.h"
+#include "fp8_common.h"
 
 using namespace hvk;
 
@@ -609,6 +610,9 @@ struct Epi {
   float* bias_grad;
   int bias_store;  // 1: the bias-gradient column is stored, not added
   int run_in, run_out;  // column remap n = kh*run_in + j -> kh*run_out + j
+  // fused fp8 copy of the (bf16) output for the fp8 layer reading it
+  // (store8_fast only; q8.q == nullptr: off)
+  Q8 q8;
   __device__ __forceinline__ void store(int gi, int m, int n, float v) const {
     if (m >= M || n >= N) return;
     if (n == ones_col) {
@@ -654,7 +658,8 @@ struct Epi {
   // fast_ok() and n + 8 <= N: one switch per chunk, vector bias / aux loads,
   // packed bf16 conversion (v is scratch)
   __device__ __forceinline__ void store8_fast(int gi, int m, int n,
-                                              float* v) const {
+                                              float* v, float qs = 1.f,
+                                              float* amax = nullptr) const {
     const int gm = m + gi * grow, gn = n + gi * gcol;
     const long long idx = (long long)gm * ldc + gn;
     if (alpha != 1.f) {
@@ -697,7 +702,9 @@ struct Epi {
       d[0] = make_float4(v[0], v[1], v[2], v[3]);
       d[1] = make_float4(v[4], v[5], v[6], v[7]);
     } else {
-      *(uint4*)((uint16_t*)c + idx) = pack_bf16x8(v);
+      const uint4 ob = pack_bf16x8(v);
+      *(uint4*)((uint16_t*)c + idx) = ob;
+      if (amax && q8.q) q8_store8(q8, idx, ob, qs, *amax);
     }
   }
   // 8 consecutive columns of one row: 16-B vector stores when possible
@@ -1143,6 +1150,9 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   __syncthreads();
   constexpr int CH = NC / 8;
   const bool fast = epi.fast_ok();
+  const float qs = epi.q8.q ? fp8_scale(epi.q8.st, epi.q8.hist, epi.q8.fmax)
+                            : 1.f;
+  float amax = 0.f;
   for (int q = t; q < BMC * CH; q += NT) {
     int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
     if (m0 + row >= M) continue;
@@ -1153,9 +1163,13 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
     if (fast && n0 + c8 + 8 <= epi.N &&
         (epi.ones_col < 0 || n0 + c8 + 8 <= epi.ones_col))
-      epi.store8_fast(gi, m0 + row, n0 + c8, v);
+      epi.store8_fast(gi, m0 + row, n0 + c8, v, qs, &amax);
     else
       epi.store8(gi, m0 + row, n0 + c8, v);
+  }
+  if (epi.q8.q) {  // block-uniform
+    __syncthreads();   // sC reads done: its first words hold the reduction
+    q8_block_amax(epi.q8, amax, sC);
   }
 }
 
@@ -1388,6 +1402,12 @@ Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
   e.grow = 0; e.gcol = 0; e.preact = nullptr;
   e.ones_col = -1; e.bias_grad = nullptr; e.run_in = 0; e.run_out = 0;
   e.bias_store = 0;
+  e.q8.q = nullptr;
+  e.q8.st = nullptr;
+  e.q8.shard = nullptr;
+  e.q8.fmax = 1.f;
+  e.q8.fmt = 0;
+  e.q8.hist = 0;
   return e;
 }
 

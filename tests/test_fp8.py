@@ -371,6 +371,40 @@ def test_fused_quantisation_epilogue(dgrad):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [
+    # VGG conv1_1 (C = 3 -> channel-padded, halo kernel), a strided conv
+    # (implicit GEMM), a grouped conv with 24 outputs per group
+    (2, 24, 24, 3, 64, 3, (1, 1), 1, 1),
+    (2, 17, 17, 32, 48, 3, (2, 2), 1, 1),
+    (2, 12, 12, 48, 48, 3, (1, 1), 1, 2)])
+def test_fused_quantisation_bf16_conv(cfg):
+    """A bf16 conv feeding an fp8 conv writes that conv's e4m3 input copy
+    from its epilogue: equal to a separate quantize pass of its bf16
+    output, amax in the shards; the bf16 output is unchanged"""
+    N, H, W, C, OC, k, sl, p, g = cfg
+    x = rnd(N, H, W, C).to(torch.bfloat16).to(DEV)
+    w = rnd(OC, k, k, C // g, seed=1, scale=0.1).to(torch.bfloat16).to(DEV)
+    b = torch.randn(OC, device=DEV)
+    nxt = fp8.Scaler(DEV, fp8.E4M3)
+    nxt.prime(torch.full((16,), 3.0, device=DEV))
+    pad = (p, p, p, p)
+    plain = ops.conv_fwd(x, w, b, sl, pad, g, 3)
+    OH, OW = ops.conv_out_size(H, W, k, k, sl, pad)
+    q8 = torch.empty(N, OH, OW, OC, dtype=fp8.TORCH_DT[nxt.fmt], device=DEV)
+    y = ops.conv_fwd(x, w, b, sl, pad, g, 3, q8=q8, q8_scaler=nxt)
+    torch.cuda.synchronize()
+    assert torch.equal(y, plain)
+    ref = fp8.quantize(y, nxt, record=False)
+    torch.cuda.synchronize()
+    assert torch.equal(q8.view(torch.uint8), ref.view(torch.uint8))
+    r = nxt.registry
+    step = r.step
+    r.roll()
+    torch.cuda.synchronize()
+    assert nxt.state[step % fp8.HIST].item() == y.float().abs().max().item()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bwd", [False, True])
 def test_fused_quantisation_pool2(bwd):
     """The 2 x 2 pooling kernels' fused fp8 copy of their result equals a

@@ -182,9 +182,14 @@ class Conv(Forward):
         if x.dtype != self.weights_lp.dtype:
             x = x.to(self.weights_lp.dtype)
         ws = {}
+        # a bf16 conv feeding an fp8 conv (VGG conv1_1, C = 3) writes that
+        # conv's e4m3 input copy from its epilogue too
+        q8, qs = self._q8_target(y)
         ops.conv_fwd(x, self.weights_lp, self.bias_master, self.sliding,
                      self.padding, self.grouping, self.activation, out=y,
-                     col_out=ws)
+                     col_out=ws, q8=q8, q8_scaler=qs)
+        if q8 is not None:
+            self.fp8_input_consumer().x8_fresh_ = True
         self.col_ = ws.get("col")
 
     def package_export(self):

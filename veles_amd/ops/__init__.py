@@ -707,25 +707,67 @@ def set_conv_halo(on, dgrad=None):
 
 
 def _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
-                   OH, OW, groups, act, stream):
+                   OH, OW, groups, act, stream, q8=None):
+    """``q8``: the kernel arguments of a fused fp8 copy of ``out``
+    (``fp8._q8_args`` + history length) or None.  Returns whether the fp8
+    copy was written (the fused epilogue needs aligned rows and bias)."""
+    sfx = "" if q8 is None else "_q8"
+    extra = [] if q8 is None else list(q8)
     if _HALO and sy == 1 and sx == 1 and out.is_contiguous():
-        rc = _lib.lib().hvk_conv_fwd_halo(
+        rc = getattr(_lib.lib(), "hvk_conv_fwd_halo" + sfx)(
             _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
-            OH, OW, groups, act, stream)
+            OH, OW, groups, act, *extra, stream)
         if rc == 0:
-            return
+            return True
+        if rc == -3 and q8 is not None:
+            # the fused output needs the vector epilogue (aligned rows,
+            # bias): unfused call, the caller quantizes separately
+            return _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW,
+                                  sy, sx, pt, pl, OH, OW, groups, act, stream)
         if rc != -2:
-            _lib.check(rc, "hvk_conv_fwd_halo")
-    _lib_call("hvk_conv_fwd", _p(x), _p(w), _p(bias), _p(out), N, H, W, C,
-              OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, act, stream)
+            _lib.check(rc, "hvk_conv_fwd_halo" + sfx)
+    rc = getattr(_lib.lib(), "hvk_conv_fwd" + sfx)(
+        _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, sy, sx, pt,
+        pl, OH, OW, groups, act, *extra, stream)
+    if rc == -3 and q8 is not None:
+        _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt,
+                       pl, OH, OW, groups, act, stream)
+        return False
+    _lib.check(rc, "hvk_conv_fwd" + sfx)
+    return q8 is not None
 
 
 def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
-             groups=1, act=0, out=None, col_out=None):
+             groups=1, act=0, out=None, col_out=None, q8=None,
+             q8_scaler=None):
     """x [N,H,W,C], w [OC,KH,KW,C/g] -> y [N,OH,OW,OC].
 
     ``col_out``: a dict that receives the im2col matrix when the explicit
-    path is used (the weight-gradient GEMM reuses it)."""
+    path is used (the weight-gradient GEMM reuses it).  ``q8`` /
+    ``q8_scaler``: also write the fp8 copy of y that the fp8 layer reading
+    it takes (``ops.fp8.conv_fwd`` semantics) - from the GEMM / halo
+    epilogue where the kernel path has one, else by a separate quantize
+    pass."""
+    if q8 is None:
+        return _conv_fwd(x, w, bias, sliding, padding, groups, act, out,
+                         col_out, None)
+    from veles_amd.ops import fp8
+    if not _gpu(x):
+        y = _conv_fwd(x, w, bias, sliding, padding, groups, act, out,
+                      col_out, None)
+        fp8._q8_ref(y, q8, q8_scaler)
+        return y
+    fq = [fp8._q8_args(q8, q8_scaler) + [fp8.HIST], False]
+    y = _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out,
+                  fq)
+    if not fq[1]:   # a kernel path without the fused output: separate pass
+        fp8.quantize(y, q8_scaler, out=q8)
+    return y
+
+
+def _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out, fq):
+    """conv_fwd; ``fq`` = [q8 kernel arguments, fused flag] or None: the
+    fused-epilogue calls pass the arguments and set the flag."""
     pre = x if isinstance(x, S2DImage) else None   # loader-made s2d input
     N, H, W, C = x.shape
     OC, KH, KW, Cg = w.shape
@@ -744,6 +786,14 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
     if out is None:
         out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
     if _gpu(x):
+        def call(*a):
+            q = None
+            if fq is not None and out.dtype == torch.bfloat16 and \
+                    out.is_contiguous() and (OC // groups) % 8 == 0:
+                q = fq[0]
+            fused = _conv_fwd_call(*a, q8=q)
+            if q is not None:
+                fq[1] = fused
         s2 = s2d_factor(C, groups, sliding, KH, KW)
         if s2:
             # strided RGB conv as a stride-1 conv on the space-to-depth image
@@ -752,16 +802,16 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
                 space_to_depth(x, s2, KH, KW, padding)
             w2 = _s2d_weights(w, s2)
             C2 = s2 * s2 * C
-            _conv_fwd_call(x2, w2, bias, out, N, H2, W2, C2, OC, KH2, KW2,
-                           1, 1, 0, 0, OH, OW, 1, act, _s(x))
+            call(x2, w2, bias, out, N, H2, W2, C2, OC, KH2, KW2, 1, 1, 0, 0,
+                 OH, OW, 1, act, _s(x))
             if col_out is not None:
                 col_out["col"] = S2DImage(x2, s2, (N, H, W, C))
             return out
         if pad8_ok(C, groups):
             xp = _pad_channels(x)
             wp8 = _pad_weights(w, "wpad8")
-            _conv_fwd_call(xp, wp8, bias, out, N, H, W, _cpad(C), OC, KH,
-                           KW, sy, sx, pt, pl, OH, OW, 1, act, _s(x))
+            call(xp, wp8, bias, out, N, H, W, _cpad(C), OC, KH, KW, sy, sx,
+                 pt, pl, OH, OW, 1, act, _s(x))
             if col_out is not None:
                 col_out["col"] = PaddedImage(xp, C)
             return out
@@ -786,8 +836,8 @@ def conv_fwd(x, w, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
                       N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW, act,
                       _s(x))
             return out
-        _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt,
-                       pl, OH, OW, groups, act, _s(x))
+        call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW,
+             groups, act, _s(x))
         return out
     xp = F.pad(_nchw(x), (pl, pr, pt, pb))
     y = F.conv2d(xp, w.permute(0, 3, 1, 2).float(),

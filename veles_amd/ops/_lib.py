@@ -35,6 +35,8 @@ _SIGS = {
     "hvk_conv_dgrad_t": [P, P, P] + [I] * 14 + [P, I, P],
     # (X, Wt, bias, Y, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, act, s)
     "hvk_conv_fwd_halo": [P, P, P, P] + [I] * 13 + [P],
+    "hvk_conv_fwd_halo_q8": [P, P, P, P] + [I] * 13 + [P, P, P, F, I, I, P],
+    "hvk_conv_fwd_q8": [P, P, P, P] + [I] * 15 + [P, P, P, F, I, I, P],
     # (dY, Wt, dX, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, aux,
     #  aux_act, s)
     "hvk_conv_dgrad_halo": [P, P, P] + [I] * 12 + [P, I, P],
