@@ -860,11 +860,10 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
     }
     uint64_t v[SPT];
     if (xin) {
-      // in-row offsets of the two pieces (the 4-byte aligned starts and
-      // the byte shifts) - the same for every sample
+      // in-image offsets of the two pieces (the byte shift within the
+      // aligned dwords depends on the sample base too: H*W*C may be odd)
       const long long o0 = ((long long)iy0 * W + ix0) * C + r0;
       const long long o1 = ((long long)iy1 * W + ix0) * C;
-      const uint32_t sh0 = (uint32_t)(o0 & 3), sh1 = (uint32_t)(o1 & 3);
       uint32_t d[SPT][6];
 #pragma unroll
       for (int u = 0; u < SPT; ++u) {
@@ -882,6 +881,8 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
 #pragma unroll
       for (int u = 0; u < SPT; ++u) {
         const long long base = (long long)(sid[u] < 0 ? 0 : sid[u]) * sample;
+        const uint32_t sh0 = (uint32_t)((base + o0) & 3);
+        const uint32_t sh1 = (uint32_t)((base + o1) & 3);
         uint64_t p0 = ((uint64_t)__builtin_amdgcn_alignbyte(d[u][2], d[u][1], sh0)
                        << 32) |
                       __builtin_amdgcn_alignbyte(d[u][1], d[u][0], sh0);
