@@ -84,12 +84,40 @@ def build(force=False, jobs=None, verbose=True):
     return LIB
 
 
+BENCH_SRC = os.path.join(REPO, "csrc", "bench", "allreduce_bench.cpp")
+BENCH_BIN = os.path.join(REPO, "build", "bin", "allreduce_bench")
+
+
+def build_allreduce_bench(verbose=True):
+    """The RCCL all-reduce micro-benchmark (csrc/bench/allreduce_bench.cpp):
+    ``build/bin/allreduce_bench [ngpus] [min_mb] [max_mb] [iters] [f32|bf16]``
+    (docs/PARALLEL.md).  Rebuilt when the source changes."""
+    os.makedirs(os.path.dirname(BENCH_BIN), exist_ok=True)
+    stamp = BENCH_BIN + ".stamp"
+    h = _hash(BENCH_SRC, ["-lrccl"])
+    if os.path.exists(BENCH_BIN) and os.path.exists(stamp) and \
+            open(stamp).read() == h:
+        return BENCH_BIN
+    cmd = [HIPCC, "-O2", "-std=c++17", "--offload-arch=" + ARCH, BENCH_SRC,
+           "-o", BENCH_BIN + ".tmp", "-L/opt/rocm/lib", "-lrccl"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("allreduce_bench build failed:\n%s" % r.stderr)
+    os.replace(BENCH_BIN + ".tmp", BENCH_BIN)
+    with open(stamp, "w") as f:
+        f.write(h)
+    if verbose:
+        print("built %s" % BENCH_BIN)
+    return BENCH_BIN
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
     a = ap.parse_args(argv)
     build(a.force, a.j)
+    build_allreduce_bench()
 
 
 if __name__ == "__main__":
