@@ -66,12 +66,16 @@ int main(int argc, char** argv) {
   std::vector<ncclComm_t> comms(n);
   NCCLCHECK(ncclCommInitAll(comms.data(), n, devs.data()));
   std::vector<hipStream_t> streams(n);
-  std::vector<void*> buf(n);
+  // out-of-place (send != recv), as the trainer's bucket reduce is not: with
+  // one GPU RCCL then still moves the bytes (a device copy) instead of
+  // returning at once, so the 1-GPU line is the copy floor
+  std::vector<void*> buf(n), rbuf(n);
   std::vector<hipEvent_t> e0(n), e1(n);
   for (int i = 0; i < n; ++i) {
     HIPCHECK(hipSetDevice(i));
     HIPCHECK(hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking));
     HIPCHECK(hipMalloc(&buf[i], max_bytes));
+    HIPCHECK(hipMalloc(&rbuf[i], max_bytes));
     HIPCHECK(hipMemset(buf[i], 0, max_bytes));
     HIPCHECK(hipEventCreate(&e0[i]));
     HIPCHECK(hipEventCreate(&e1[i]));
@@ -86,7 +90,7 @@ int main(int argc, char** argv) {
   auto run = [&](size_t count) {
     NCCLCHECK(ncclGroupStart());
     for (int i = 0; i < n; ++i)
-      NCCLCHECK(ncclAllReduce(buf[i], buf[i], count, dt, ncclSum, comms[i],
+      NCCLCHECK(ncclAllReduce(buf[i], rbuf[i], count, dt, ncclSum, comms[i],
                               streams[i]));
     NCCLCHECK(ncclGroupEnd());
   };
@@ -131,6 +135,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < n; ++i) {
     HIPCHECK(hipSetDevice(i));
     HIPCHECK(hipFree(buf[i]));
+    HIPCHECK(hipFree(rbuf[i]));
     HIPCHECK(hipStreamDestroy(streams[i]));
     HIPCHECK(hipEventDestroy(e0[i]));
     HIPCHECK(hipEventDestroy(e1[i]));

@@ -65,6 +65,13 @@ __global__ void splitk_finish_kernel(float* __restrict__ ws, int M, int N,
 
 HVK_API void hvk_set_gemm_variant(int v) { hvk_gemm_variant = v; }
 
+// Returns and clears this thread's pending HIP error.  The entry points
+// report hipGetLastError() after their launches, so an error left pending by
+// an earlier runtime call (a graph capture that was invalidated and then
+// abandoned: hipErrorStreamCaptureInvalidated) would otherwise be charged to
+// the next kernel launched; graphs.py drains it after a failed capture.
+HVK_API int hvk_take_last_error() { return (int)hipGetLastError(); }
+
 // col[M][Kp] = im2col(X) for a single-group conv (Kp = round_up(KH*KW*C, 8))
 HVK_API int hvk_im2col(const void* X, void* col, int N, int H, int W, int C,
                        int KH, int KW, int sy, int sx, int pt, int pl, int OH,

@@ -144,8 +144,16 @@ class _HipCapture(object):
         """A capture that ended in an error can leave its stream in the
         invalidated capture state on HIP (the next ``capture_begin`` on it
         fails with hipStreamCaptureStatusInvalidated): later captures get a
-        fresh stream."""
+        fresh stream.  The thread's pending HIP error from the broken
+        capture is drained too, so that the next kernel library launch
+        (which reports hipGetLastError) is not charged with it."""
         _HipCapture._stream = None
+        try:
+            from veles_amd.ops import _lib
+            if _lib.available():
+                _lib.lib().hvk_take_last_error()
+        except Exception:  # noqa: BLE001 - best effort on an error path
+            pass
 
 
 class GraphSegment(object):

@@ -103,6 +103,7 @@ _SIGS = {
     "hvk_conv_dgrad_fp8": [P, P, P] + [I] * 14 + [P, I, I, I, P, P, I, F, F,
                            P, P, P, F, I, P],
     "hvk_conv_wgrad_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F, P],
+    "hvk_take_last_error": [],
 }
 _OPTIONAL = {}
 
