@@ -293,7 +293,7 @@ hipError_t launch_halo(const HaloGeom& g, const uint16_t* src, const DenseK& lb,
   const long long grid = (long long)tiles_n * g.tiles_sp * groups;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(W8 ? 512 : NTHR), lds, s,
                      g, src, lb, e, K, tiles_n);
-  return hipGetLastError();
+  return launch_status(s);
 }
 
 // the halo path applies: stride 1, 16-B channel chunks, a halo that fits LDS

@@ -969,7 +969,7 @@ HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
                      dim3(256), 0, s, (const uint8_t*)src, src_bytes, shuffled,
                      start, count, max_mb, H, W, pt, pl, H2, W2, mean2, rdisp2,
                      (uint16_t*)dst, labels, labels_out, idx_out);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1103,7 +1103,7 @@ HVK_API int hvk_image_batch(const void* src, long long src_stride, int Hs,
   hipLaunchKernelGGL(image_batch_kernel, dim3(grid_for(total)), dim3(256), 0,
                      s, (const uint8_t*)src, g, idx, params, B, sobel, mean,
                      rdisp, (const uint8_t*)bg, bgcolor, (uint16_t*)out);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
@@ -1145,7 +1145,7 @@ HVK_API int hvk_fill_minibatch(const void* src, int src_dt, const int* shuffled,
                        sample_size, mean, rdisp, dst, dst_dt, labels, labels_out,
                        idx_out);
   }
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_mean_disp_normalize(const void* in, int in_dt, const float* mean,
@@ -1154,7 +1154,7 @@ HVK_API int hvk_mean_disp_normalize(const void* in, int in_dt, const float* mean
                                     hipStream_t s) {
   hipLaunchKernelGGL(mean_disp_kernel, dim3(grid_for(total)), dim3(256), 0, s,
                      in, in_dt, mean, rdisp, out, out_dt, total, sample);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_softmax_ce(const void* logits, int in_dt, int B, int C,
@@ -1167,7 +1167,7 @@ HVK_API int hvk_softmax_ce(const void* logits, int in_dt, int B, int C,
   hipLaunchKernelGGL(softmax_ce_kernel, dim3(blocks), dim3(256), 0, s,
                      logits, in_dt, B, C, labels, scale, err, err_dt, probs,
                      max_idx, metrics, confusion);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_mse(const void* y, int y_dt, const void* t, int t_dt, int B,
@@ -1179,7 +1179,7 @@ HVK_API int hvk_mse(const void* y, int y_dt, const void* t, int t_dt, int B,
   hipLaunchKernelGGL(mse_kernel, dim3(blocks), dim3(256), 0, s, y, y_dt, t,
                      t_dt, B, D, scale, err, err_dt, mse_out, metrics,
                      valid_rows);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_sgd4(float* w, float* grad, float* mom, void* w_lp,
@@ -1191,7 +1191,7 @@ HVK_API int hvk_sgd4(float* w, float* grad, float* mom, void* w_lp,
   hipLaunchKernelGGL(sgd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0, s,
                      (float4*)w, (float4*)grad, (float4*)mom, (uint2*)w_lp,
                      (const SgdSeg*)segs, nseg, total / 4, gscale, zero_from);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // The same update on at most `max_blocks` workgroups (grid-stride): a
@@ -1209,7 +1209,7 @@ HVK_API int hvk_sgd4_grid(float* w, float* grad, float* mom, void* w_lp,
   hipLaunchKernelGGL(sgd4_kernel, dim3(g), dim3(256), 0, s, (float4*)w,
                      (float4*)grad, (float4*)mom, (uint2*)w_lp,
                      (const SgdSeg*)segs, nseg, total / 4, gscale, zero_from);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_solver(float* w, float* grad, float* s1, float* s2,
@@ -1219,7 +1219,7 @@ HVK_API int hvk_solver(float* w, float* grad, float* s1, float* s2,
   hipLaunchKernelGGL(solver_kernel, dim3(grid_for(total)), dim3(256), 0, s, w,
                      grad, s1, s2, (uint16_t*)w_lp, (const SolverSeg*)segs,
                      nseg, total, gscale, zero_from);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
@@ -1228,7 +1228,7 @@ HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(total)), dim3(256), 0, s, w,
                      grad, mom, (uint16_t*)w_lp, (const SgdSeg*)segs, nseg,
                      total, gscale);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
@@ -1241,7 +1241,7 @@ HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
     int blocks = (R + rpb - 1) / rpb;
     hipLaunchKernelGGL(col_sum_bf16x8_kernel, dim3(blocks), dim3(256), 0, s,
                        (const uint16_t*)in, R, C, out, rpb, scale);
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   int rpb = 256;
   // aim for >= 1024 blocks in total
@@ -1250,14 +1250,14 @@ HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
   while (rb * cb < 1024 && rpb > 16) { rpb >>= 1; rb = (R + rpb - 1) / rpb; }
   hipLaunchKernelGGL(col_sum_kernel, dim3(cb, rb), dim3(256), 0, s, in, dt, R, C,
                      out, rpb, scale);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_row_sum(const void* in, int dt, int R, int C, float* out,
                         float scale, hipStream_t s) {
   hipLaunchKernelGGL(row_sum_kernel, dim3((R + 3) / 4), dim3(256), 0, s, in, dt,
                      R, C, out, scale);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_act_fwd(const void* x, int xdt, void* y, int ydt, long long n,
@@ -1267,11 +1267,11 @@ HVK_API int hvk_act_fwd(const void* x, int xdt, void* y, int ydt, long long n,
     hipLaunchKernelGGL(act_fwd_bf16x8_kernel, dim3(grid_for(n / 8)),
                        dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
                        n / 8, act);
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   hipLaunchKernelGGL(act_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      y, ydt, n, act);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_act_bwd(const void* dy, int dydt, const void* y, int ydt,
@@ -1292,7 +1292,7 @@ HVK_API int hvk_act_bwd(const void* dy, int dydt, const void* y, int ydt,
     hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, dy,
                        dydt, y, ydt, dx, dxdt, n, act);
   }
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_dropout(const void* x, int xdt, void* y, int ydt, long long n,
@@ -1302,7 +1302,7 @@ HVK_API int hvk_dropout(const void* x, int xdt, void* y, int ydt, long long n,
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      y, ydt, n, seed, thresh, scale, (uint8_t*)mask_out,
                      (const uint32_t*)nullptr);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // dropout with the seed in device memory (graph-safe: the forward unit
@@ -1315,7 +1315,7 @@ HVK_API int hvk_dropout_dev(const void* x, int xdt, void* y, int ydt,
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      y, ydt, n, 0u, thresh, scale, (uint8_t*)mask_out,
                      (const uint32_t*)seed_dev);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // ------------------------------------------------ input-derivative activations
@@ -1417,7 +1417,7 @@ HVK_API int hvk_xact(const void* x, int xdt, const void* err, int edt,
   hipLaunchKernelGGL(xact_kernel, dim3(grid_for(vec ? n / 8 : n)), dim3(256),
                      0, s, x, xdt, err, edt, y, ydt, n, kind, p, rowlen, bwd,
                      vec);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // ------------------------------------------------------------- gather
@@ -1434,7 +1434,7 @@ HVK_API int hvk_gather(const void* x, int xdt, const int* idx, void* y,
                        int ydt, long long n, hipStream_t s) {
   hipLaunchKernelGGL(gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      idx, y, ydt, n);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // seed <- hash(seed + 1): a per-step seed sequence that lives on the device
@@ -1446,7 +1446,7 @@ __global__ void hvk_trace_marker_kernel(int tag) {
 }
 HVK_API int hvk_trace_marker(int tag, hipStream_t s) {
   hipLaunchKernelGGL(hvk_trace_marker_kernel, dim3(1), dim3(64), 0, s, tag);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 __global__ void seed_advance_kernel(uint32_t* seed) {
@@ -1455,7 +1455,7 @@ __global__ void seed_advance_kernel(uint32_t* seed) {
 HVK_API int hvk_seed_advance(void* seed, hipStream_t s) {
   hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, s,
                      (uint32_t*)seed);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_xorshift1024star(void* states, int n_states, int rounds,
@@ -1464,20 +1464,20 @@ HVK_API int hvk_xorshift1024star(void* states, int n_states, int rounds,
   hipLaunchKernelGGL(xorshift1024_kernel, dim3((n_states + bs - 1) / bs),
                      dim3(bs), 0, s, (uint64_t*)states, n_states, rounds,
                      (uint64_t*)out);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_xorshift128plus(void* states, int n, void* out, hipStream_t s) {
   hipLaunchKernelGGL(xorshift128p_kernel, dim3((n + 255) / 256), dim3(256), 0, s,
                      (uint64_t*)states, n, (uint64_t*)out);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_u64_to_uniform(const void* in, float* out, long long n, float lo,
                                float hi, hipStream_t s) {
   hipLaunchKernelGGL(u64_to_uniform_kernel, dim3(grid_for(n)), dim3(256), 0, s,
                      (const uint64_t*)in, out, n, lo, hi);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_join(const void* const* ins, const int* lens, int nin, int dt,
@@ -1494,7 +1494,7 @@ HVK_API int hvk_join(const void* const* ins, const int* lens, int nin, int dt,
   long long total = (long long)B * off;
   hipLaunchKernelGGL(join_kernel, dim3(grid_for(total)), dim3(256), 0, s, a, nin,
                      dt, out, B, off);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // The same image with one 16-B output chunk per lane (chunks of a pixel on
@@ -1555,13 +1555,13 @@ HVK_API int hvk_space_to_depth(const void* x, void* y, int N, int H, int W,
                        dim3(grid_for(chunks)), dim3(256), 0, st,
                        (const uint16_t*)x, (uint16_t*)y, H, W, pt, pl,
                        make_fastdiv(W2), make_fastdiv(H2), chunks);
-    return (int)hipGetLastError();
+    return (int)launch_status(st);
   }
   hipLaunchKernelGGL(space_to_depth_kernel, dim3(grid_for(runs)), dim3(256), 0,
                      st, (const uint16_t*)x, (uint16_t*)y, H, W, C, s, pt, pl,
                      H2, W2, make_fastdiv(s), make_fastdiv(W2),
                      make_fastdiv(H2), runs);
-  return (int)hipGetLastError();
+  return (int)launch_status(st);
 }
 
 // Space-to-depth weights: w [OC][KH][KW][C] -> w2 [OC][KH2][KW2][s][s][C],
@@ -1619,7 +1619,7 @@ HVK_API int hvk_s2d_weights(const void* w, void* w2, int OC, int KH, int KW,
   hipLaunchKernelGGL(s2d_weights_kernel, dim3(grid_for(total)), dim3(256), 0,
                      st, (const uint16_t*)w, (uint16_t*)w2, OC, KH, KW, C, s,
                      KH2, KW2);
-  return (int)hipGetLastError();
+  return (int)launch_status(st);
 }
 
 HVK_API int hvk_s2d_grad_fold(float* dw2, float* dw, int OC, int KH, int KW,
@@ -1628,7 +1628,7 @@ HVK_API int hvk_s2d_grad_fold(float* dw2, float* dw, int OC, int KH, int KW,
   const long long total = (long long)OC * KH2 * KW2 * s * s * C;
   hipLaunchKernelGGL(s2d_grad_fold_kernel, dim3(grid_for(total)), dim3(256), 0,
                      st, dw2, dw, OC, KH, KW, C, s, KH2, KW2, clear);
-  return (int)hipGetLastError();
+  return (int)launch_status(st);
 }
 
 HVK_API int hvk_cast(const void* in, int idt, void* out, int odt, long long n,
@@ -1641,7 +1641,7 @@ HVK_API int hvk_cast(const void* in, int idt, void* out, int odt, long long n,
     hipLaunchKernelGGL(cast_kernel, dim3(grid_for(n)), dim3(256), 0, s, in, idt,
                        out, odt, n, scale);
   }
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1727,6 +1727,6 @@ HVK_API int hvk_conv_fwd_direct(const void* X, const void* Wt,
                      (const uint16_t*)Wt, bias, (uint16_t*)Y, N, H, W, C, OC,
                      KH, KW, sy, sx, pt, pl, OH, OW, act, make_fastdiv(OW),
                      make_fastdiv(OH));
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 

@@ -66,11 +66,37 @@ __global__ void splitk_finish_kernel(float* __restrict__ ws, int M, int N,
 HVK_API void hvk_set_gemm_variant(int v) { hvk_gemm_variant = v; }
 
 // Returns and clears this thread's pending HIP error.  The entry points
-// report hipGetLastError() after their launches, so an error left pending by
+// report launch_status(s) after their launches, so an error left pending by
 // an earlier runtime call (a graph capture that was invalidated and then
 // abandoned: hipErrorStreamCaptureInvalidated) would otherwise be charged to
 // the next kernel launched; graphs.py drains it after a failed capture.
 HVK_API int hvk_take_last_error() { return (int)hipGetLastError(); }
+
+// A non-blocking stream of the library's own (graphs.py captures on it, via
+// torch.cuda.ExternalStream): a capture stream broken by a failed capture
+// is dropped for good instead of going back to torch's stream pool.
+HVK_API void* hvk_stream_create() {
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+    return nullptr;
+  return (void*)s;
+}
+
+// Ends a stream capture that failed (its graph is discarded): a capture
+// whose capture_end raised can leave the stream in the capture state, and
+// torch hands pooled streams out again - a later "new" stream that is still
+// capturing fails every launch with hipErrorStreamCaptureInvalidated.
+// Returns 1 if a capture was ended, 0 if none was in progress.
+HVK_API int hvk_end_stream_capture(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess) (void)hipGetLastError();
+  if (st == hipStreamCaptureStatusNone) return 0;
+  hipGraph_t g = nullptr;
+  (void)hipStreamEndCapture(s, &g);
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  return 1;
+}
 
 // col[M][Kp] = im2col(X) for a single-group conv (Kp = round_up(KH*KW*C, 8))
 HVK_API int hvk_im2col(const void* X, void* col, int N, int H, int W, int C,
@@ -83,7 +109,7 @@ HVK_API int hvk_im2col(const void* X, void* col, int N, int H, int W, int C,
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(im2col_kernel, dim3((int)blocks), dim3(256), 0, s,
                      (const uint16_t*)X, (uint16_t*)col, g, M, K, Kp);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // C[M][N] = alpha*op(A)*op(B) + beta*C (+bias, act, aux-derivative mask)
@@ -161,6 +187,6 @@ HVK_API int hvk_gemm_splitk(int transA, int transB, int M, int N, int K,
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(splitk_finish_kernel, dim3((int)blocks), dim3(256), 0, s,
                      ws, M, N, e, ws_zero);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 

@@ -1233,13 +1233,13 @@ hipError_t go(const LA& la, const LB& lb, const Epi& epi, int M, int N, int K,
                        : gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, 0, 3>;
       hipLaunchKernelGGL(k, grid, dim3(512), 0, s, la, lb, epi, M, N, K,
                          k_split, tiles_n, tiles, splits, gm);
-      return hipGetLastError();
+      return launch_status(s);
     }
   }
   hipLaunchKernelGGL((gemm_kernel<LA, AK, LB, BKM, BN_, BUF, W8, VAR>), grid,
                      dim3(W8 ? 512 : NTHR), 0, s, la, lb, epi, M, N, K,
                      k_split, tiles_n, tiles, splits, gm);
-  return hipGetLastError();
+  return launch_status(s);
 }
 
 template <class LA, bool AK, class LB, bool BKM, bool BUF>

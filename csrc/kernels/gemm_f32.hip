@@ -270,7 +270,7 @@ int launch_fx(int ta, int tb, int M, int N, int K, const T* A, int lda,
   else
     hipLaunchKernelGGL((gemm_fx_kernel<T, 2>), grid, dim3(NTHR), 0, s, oa, ob,
                        C, ldc, M, N, K, alpha, beta, tiles_n, va, vb);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 }  // namespace

@@ -470,7 +470,7 @@ hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
   else
     hipLaunchKernelGGL((gemm_fp8_kernel<LA, LB, 128, FA, FB, true>), grid,
                        dim3(512), 0, s, la, lb, e, M, N, K, tiles_n, tiles);
-  return hipGetLastError();
+  return launch_status(s);
 }
 
 // fmt: 0 = e4m3 (fp8), 1 = e5m2 (bf8) -> the f8f6f4 cbsz/blgp codes.  B is
@@ -644,7 +644,7 @@ HVK_API int hvk_fp8_quant(const void* x, int x_f32, long long n, void* out,
   else
     hipLaunchKernelGGL(fp8_quant_kernel<false>, grid, dim3(256), 0, s, x, n,
                        (uint8_t*)out, fmt, st, hist, fmax_eff, lim, record);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_fp8_amax(const void* x, int x_f32, long long n, float* st,
@@ -657,7 +657,7 @@ HVK_API int hvk_fp8_amax(const void* x, int x_f32, long long n, float* st,
   else
     hipLaunchKernelGGL(fp8_amax_kernel<false>, grid, dim3(256), 0, s, x, n,
                        st, hist);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // shards (optional): [count][1024] f32, 32 amax shards per scaler 32 floats
@@ -668,7 +668,7 @@ HVK_API int hvk_fp8_roll(float* states, int count, int hist, int idx,
   hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
                      states, count, hist, idx, fill, (const int*)nullptr,
                      shards);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_fp8_roll_dev(float* states, int count, int hist,
@@ -676,7 +676,7 @@ HVK_API int hvk_fp8_roll_dev(float* states, int count, int hist,
   if (count <= 0) return 0;
   hipLaunchKernelGGL(fp8_roll_kernel, dim3((count + 63) / 64), dim3(64), 0, s,
                      states, count, hist, 0, 0, (const int*)step, shards);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // the fused quantisation of an fp8 conv's output (Epi8::q8); q8 == nullptr

@@ -351,10 +351,10 @@ hipError_t go_pp(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
       hipLaunchKernelGGL((gemm_pp_kernel<LP, PK, LQ, QK, 1>), grid, dim3(512),
                          0, s, lp, lq, epi, P, Q, K, k_split, tiles_q, tiles,
                          splits, gm);
-      return hipGetLastError();
+      return launch_status(s);
     }
   }
   hipLaunchKernelGGL((gemm_pp_kernel<LP, PK, LQ, QK>), grid, dim3(512), 0, s,
                      lp, lq, epi, P, Q, K, k_split, tiles_q, tiles, splits, gm);
-  return hipGetLastError();
+  return launch_status(s);
 }

@@ -6,6 +6,25 @@
 
 #define HVK_API extern "C" __attribute__((visibility("default")))
 
+// Status of the launch just enqueued on stream s.  hipGetLastError() also
+// returns an error left pending on this thread by an earlier, abandoned
+// graph capture (hipErrorStreamCaptureInvalidated after a capture broken by
+// a synchronising op); a launch on a stream that is NOT capturing did not
+// cause it, so it is not reported as this launch's failure (the entry
+// points would otherwise fail the next kernel of an eager pass).
+inline hipError_t launch_status(hipStream_t s) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipErrorStreamCaptureInvalidated ||
+      e == hipErrorStreamCaptureUnsupported ||
+      e == hipErrorStreamCaptureImplicit) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusActive;
+    if (hipStreamIsCapturing(s, &st) == hipSuccess &&
+        st == hipStreamCaptureStatusNone)
+      return hipSuccess;
+  }
+  return e;
+}
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;

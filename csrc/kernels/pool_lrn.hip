@@ -1494,7 +1494,7 @@ HVK_API int hvk_stochastic_pool(const void* x, void* y, int* argmax, int N,
                      C, OH, OW, ky, kx, sy, sx, use_abs, train,
                      (const uint32_t*)seed_dev, make_fastdiv(C),
                      make_fastdiv(OW), make_fastdiv(OH));
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // 2 x 2 / stride-2 pooling without argmax (pool2_fwd_kernel): C % 8 == 0,
@@ -1518,7 +1518,7 @@ HVK_API int hvk_pool2_fwd_q8(const void* x, void* y, int N, int H, int W,
                      (const uint16_t*)x, (uint16_t*)y, N, H, W, C,
                      make_fastdiv(C / 8), make_fastdiv(W / 2),
                      make_fastdiv(H / 2), q);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_pool2_fwd(const void* x, void* y, int N, int H, int W, int C,
@@ -1548,7 +1548,7 @@ HVK_API int hvk_pool2_bwd_q8(const void* x, const void* dy, void* dx, int N,
                      N, H, W, C, (const uint16_t*)aux, aux_act,
                      make_fastdiv(C / 8), make_fastdiv(W / 2),
                      make_fastdiv(H / 2), q);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
@@ -1593,7 +1593,7 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
                        (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N,
                        H, W, C, OH, OW, R, S, alpha, beta, k,
                        make_fastdiv(C / 8), make_fastdiv(OW), make_fastdiv(S));
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   if (h >= 1 && h <= 2) {
     auto kp = h == 1 ? lrn_pool3s2_fwd_u8p_kernel<1>
@@ -1602,7 +1602,7 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
                        (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N,
                        H, W, C, OH, OW, alpha, beta, k, make_fastdiv(C / 8),
                        make_fastdiv(OW), make_fastdiv(OH));
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   auto kf = h == 0 ? lrn_pool3s2_fwd_u8_kernel<0>
           : h == 1 ? lrn_pool3s2_fwd_u8_kernel<1>
@@ -1613,7 +1613,7 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
                      (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N, H,
                      W, C, OH, OW, alpha, beta, k, make_fastdiv(C / 8),
                      make_fastdiv(OW), make_fastdiv(OH));
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
@@ -1648,7 +1648,7 @@ HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
                        (const uint8_t*)argmax, (uint16_t*)dx, N, H, W, C, OH,
                        OW, alpha, beta, k, (const uint16_t*)aux, aux_act, bpw,
                        (int)nblk, make_fastdiv(BW), make_fastdiv(BH));
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   auto k2 = h == 0 ? lrn_pool3s2_bwd_u8_kernel<0>
           : h == 1 ? lrn_pool3s2_bwd_u8_kernel<1>
@@ -1660,7 +1660,7 @@ HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
                      (const uint8_t*)argmax, (uint16_t*)dx, N, H, W, C, OH, OW,
                      alpha, beta, k, (const uint16_t*)aux, aux_act,
                      make_fastdiv(C / 8), make_fastdiv(BW), make_fastdiv(BH));
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
@@ -1697,7 +1697,7 @@ HVK_API int hvk_pool_fwd(const void* x, void* y, int* argmax, int N, int H,
                        OW, ky, kx, sy, sx, pt, pl, mode, make_fastdiv(C / v),
                        make_fastdiv(OW), make_fastdiv(OH));
   }
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
@@ -1717,7 +1717,7 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
                          C, OH, OW, sy, sx, pt, pl, (const uint16_t*)aux,
                          aux_act, make_fastdiv(C / 8), make_fastdiv(W),
                          make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
-      return (int)hipGetLastError();
+      return (int)launch_status(s);
     }
     auto k8 = mode == POOL_AVG ? pool_bwd_kernel<8, POOL_AVG>
                                : pool_bwd_kernel<8, POOL_MAX>;
@@ -1743,7 +1743,7 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
                        aux_act, make_fastdiv(C / v), make_fastdiv(W),
                        make_fastdiv(H), make_fastdiv(sy), make_fastdiv(sx));
   }
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_lrn_fwd(const void* x, void* y, long long P, int C, int n,
@@ -1757,12 +1757,12 @@ HVK_API int hvk_lrn_fwd(const void* x, void* y, long long P, int C, int n,
     hipLaunchKernelGGL(kf, dim3(grid_for(total)), dim3(256), 0,
                        s, (const uint16_t*)x, (uint16_t*)y, (int)P, C,
                        alpha, beta, k, make_fastdiv(C / 8));
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   if (C > 1024) return -1;
   hipLaunchKernelGGL(lrn_fwd_kernel, dim3(grid_for(P, 4)), dim3(256), 0, s,
                      (const uint16_t*)x, (uint16_t*)y, P, C, n, alpha, beta, k);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 HVK_API int hvk_lrn_bwd(const void* x, const void* dy, void* dx, long long P,
@@ -1779,13 +1779,13 @@ HVK_API int hvk_lrn_bwd(const void* x, const void* dy, void* dx, long long P,
                        s, (const uint16_t*)x, (const uint16_t*)dy,
                        (uint16_t*)dx, (int)P, C, alpha, beta, k,
                        (const uint16_t*)aux, aux_act, make_fastdiv(C / 8));
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   if (C > 1024) return -1;
   hipLaunchKernelGGL(lrn_bwd_kernel, dim3(grid_for(P, 4)), dim3(256), 0, s,
                      (const uint16_t*)x, (const uint16_t*)dy, (uint16_t*)dx, P,
                      C, n, alpha, beta, k, (const uint16_t*)aux, aux_act);
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // Fused LRN (across channels) -> 3x3 max pooling (no padding, stride >= 2),
@@ -1807,7 +1807,7 @@ HVK_API int hvk_lrn_pool_fwd(const void* x, void* y, int* argmax, int N,
                      (const uint16_t*)x, (uint16_t*)y, argmax, N, H, W, C, OH,
                      OW, sy, sx, alpha, beta, k, make_fastdiv(C / 8),
                      make_fastdiv(OW), make_fastdiv(OH));
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }
 
 // dx = lrn_bwd(x, pool_bwd(dp, argmax)) [* f'(aux)] in one pass
@@ -1834,7 +1834,7 @@ HVK_API int hvk_lrn_pool_bwd(const void* x, const void* dp, const int* argmax,
                        (uint16_t*)dx, N, H, W, C, OH, OW, alpha, beta, k,
                        (const uint16_t*)aux, aux_act, make_fastdiv(C / 8),
                        make_fastdiv(BW), make_fastdiv(BH));
-    return (int)hipGetLastError();
+    return (int)launch_status(s);
   }
   const long long total = (long long)N * H * W * (C / 8);
   auto kb = h == 0 ? lrn_pool3_bwd_kernel<0> : h == 1 ? lrn_pool3_bwd_kernel<1>
@@ -1846,5 +1846,5 @@ HVK_API int hvk_lrn_pool_bwd(const void* x, const void* dp, const int* argmax,
                      (const uint16_t*)aux, aux_act, make_fastdiv(C / 8),
                      make_fastdiv(W), make_fastdiv(H), make_fastdiv(sy),
                      make_fastdiv(sx));
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }

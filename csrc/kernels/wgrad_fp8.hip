@@ -270,5 +270,5 @@ HVK_API int hvk_conv_wgrad_fp8(const void* X8, const void* dY8, float* dW,
   else if (fdy == 1 && fx == 1) HVK_WG8(1, 1);
   else HVK_WG8(0, 1);
 #undef HVK_WG8
-  return (int)hipGetLastError();
+  return (int)launch_status(s);
 }

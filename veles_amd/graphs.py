@@ -54,6 +54,21 @@ __all__ = ["GraphSegment", "graphs_enabled", "install_step_graphs"]
 
 _log = logging.getLogger("graphs")
 
+# the GraphSegment whose capture is in progress (at most one: segments run
+# on the main thread, one after the other).  A unit outside it that runs
+# while it is open (Unit.do_run -> interrupt_open_capture) would enqueue its
+# kernels into the graph - the capture is abandoned instead.
+_open_segment = None
+
+
+def interrupt_open_capture(unit):
+    """Called for every unit that is not in a graph segment: abandon an
+    open capture (the key runs eagerly from then on, the units captured so
+    far re-run eagerly) so that the unit's work is not recorded into it."""
+    seg = _open_segment
+    if seg is not None and seg.mode == "capture":
+        seg.interrupt(unit)
+
 
 def graphs_enabled():
     from veles_amd.utils.config import root, get
@@ -92,12 +107,27 @@ class _Captured(object):
                 arr._state = 0
 
 
+def _capture_stream():
+    """A capture stream of the kernel library's own (not from torch's
+    round-robin stream pool: a stream that a failed capture leaves in the
+    invalidated capture state would otherwise come back later as some
+    other "new" stream, e.g. a device's compute stream)."""
+    import torch
+    from veles_amd.ops import _lib
+    if _lib.available():
+        ptr = _lib.lib().hvk_stream_create()
+        if ptr:
+            return torch.cuda.ExternalStream(ptr)
+    return torch.cuda.Stream()
+
+
 class _HipCapture(object):
     """Capture context of one HIP graph on a side stream with a private
     memory pool.  Unlike ``torch.cuda.graph`` it restores the stream context
     even when ``capture_end`` raises (a capture broken by a synchronising
     op): the process then continues on the stream it was on."""
     _stream = None
+    _retired = []
 
     def __init__(self, graph):
         self.graph = graph
@@ -110,7 +140,7 @@ class _HipCapture(object):
         gc.collect()
         torch.cuda.empty_cache()
         if _HipCapture._stream is None:
-            _HipCapture._stream = torch.cuda.Stream()
+            _HipCapture._stream = _capture_stream()
         self.ctx = torch.cuda.stream(_HipCapture._stream)
         self.ctx.__enter__()
         try:
@@ -142,15 +172,22 @@ class _HipCapture(object):
     @staticmethod
     def retire_stream():
         """A capture that ended in an error can leave its stream in the
-        invalidated capture state on HIP (the next ``capture_begin`` on it
-        fails with hipStreamCaptureStatusInvalidated): later captures get a
-        fresh stream.  The thread's pending HIP error from the broken
-        capture is drained too, so that the next kernel library launch
-        (which reports hipGetLastError) is not charged with it."""
-        _HipCapture._stream = None
+        (invalidated) capture state on HIP: the capture is ended on it and
+        later captures get a fresh stream - torch pools its streams, so this
+        one is handed out again later, e.g. as a Device compute stream, and
+        must not still be capturing then.  The thread's pending HIP error is
+        drained too, so that the next kernel library launch (which reports
+        hipGetLastError) is not charged with it."""
+        st, _HipCapture._stream = _HipCapture._stream, None
+        if st is not None:
+            _HipCapture._retired.append(st)   # never handed out again
         try:
             from veles_amd.ops import _lib
             if _lib.available():
+                if st is not None:
+                    ended = _lib.lib().hvk_end_stream_capture(st.cuda_stream)
+                    _log.info("retired capture stream %#x (capture ended "
+                              "here: %d)", st.cuda_stream, ended)
                 _lib.lib().hvk_take_last_error()
         except Exception:  # noqa: BLE001 - best effort on an error path
             pass
@@ -265,6 +302,8 @@ class GraphSegment(object):
         self.ctx = ctx
         self.ctx.__enter__()
         self.mode = "capture"
+        global _open_segment
+        _open_segment = self
 
     @staticmethod
     def new_graph():
@@ -275,8 +314,21 @@ class GraphSegment(object):
         graph = torch.cuda.CUDAGraph()
         return graph, _HipCapture(graph)
 
+    def _closed(self):
+        global _open_segment
+        if _open_segment is self:
+            _open_segment = None
+
+    def interrupt(self, unit):
+        """a unit outside this segment runs while its capture is open"""
+        _log.warning("%s: %s ran while the capture was open; this key runs "
+                     "eagerly", self.name, unit)
+        self._capture_failed(None, RuntimeError(
+            "capture interrupted by %s" % unit))
+
     def _end(self):
         if self.mode == "capture":
+            self._closed()
             cur, ctx = self.cur, self.ctx
             self.cur = self.ctx = None
             try:
@@ -314,6 +366,7 @@ class GraphSegment(object):
         cur.keep.extend(ops._SEG_CACHE.values())
 
     def _abort_capture(self):
+        self._closed()
         ctx, cur = self.ctx, self.cur
         self.ctx = self.cur = None
         if ctx is not None:

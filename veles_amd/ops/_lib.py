@@ -104,6 +104,8 @@ _SIGS = {
                            P, P, P, F, I, P],
     "hvk_conv_wgrad_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F, P],
     "hvk_take_last_error": [],
+    "hvk_end_stream_capture": [P],
+    "hvk_stream_create": [],
 }
 _OPTIONAL = {}
 
@@ -124,6 +126,7 @@ def _load():
                                            (LIB_PATH, name))
             fn.argtypes = sig
             fn.restype = ctypes.c_int
+        lib.hvk_stream_create.restype = ctypes.c_void_p
         _lib = lib
         return lib
 
@@ -147,4 +150,24 @@ def lib():
 
 def check(rc, name):
     if rc != 0:
-        raise RuntimeError("%s failed with HIP error %d" % (name, rc))
+        raise RuntimeError("%s failed with HIP error %d%s" % (
+            name, rc, _capture_context() if 900 <= rc < 910 else ""))
+
+
+def _capture_context():
+    """stream-capture errors: which stream the launch went to and whether
+    a capture is in progress on it (diagnostics for the error message)"""
+    try:
+        import torch
+        from veles_amd import graphs
+        st = torch.cuda.current_stream()
+        side = graphs._HipCapture._stream
+        return (" (current stream %#x%s, capturing %s, open graph segment %s,"
+                " capture side stream %s)" % (
+                    st.cuda_stream,
+                    " = default" if st == torch.cuda.default_stream() else "",
+                    torch.cuda.is_current_stream_capturing(),
+                    getattr(graphs._open_segment, "name", None),
+                    None if side is None else "%#x" % side.cuda_stream))
+    except Exception as e:  # noqa: BLE001 - diagnostics only
+        return " (%s)" % e

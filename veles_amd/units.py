@@ -113,6 +113,19 @@ class _Scheduler(object):
 _ROCTX = [None, False]
 
 
+_GRAPHS = None
+
+
+def _graphs_mod():
+    """veles_amd.graphs, imported on first use (it imports nothing of the
+    unit layer at module level, but keeps this module import-light)"""
+    global _GRAPHS
+    if _GRAPHS is None:
+        from veles_amd import graphs
+        _GRAPHS = graphs
+    return _GRAPHS
+
+
 def _roctx():
     """torch.cuda.nvtx (roctx on ROCm builds) when unit ranges are enabled
     by ``root.common.trace.roctx`` or ``VELES_AMD_ROCTX=1``: each unit run
@@ -532,6 +545,8 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
         # a unit inside a captured HIP-graph segment (veles_amd/graphs.py)
         # is dispatched by the segment: eager, captured or replayed
         seg = self.__dict__.get("graph_segment_")
+        if seg is None and _graphs_mod()._open_segment is not None:
+            _graphs_mod().interrupt_open_capture(self)
         body = type(self).run if seg is None else seg.run_unit
         if rng is not None:
             rng.range_push(self.name)
