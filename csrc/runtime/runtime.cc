@@ -341,15 +341,23 @@ std::vector<float> Workflow::Run(const std::vector<float>& input) {
   } else if (ctx_.gpu && use_graph_ && graph_runs_ >= 1) {
     // capture this pass (every branch stream joins through the events)
     ReleaseGraph();
+    // the captured pass is enqueued by ONE host thread: appending to one
+    // capture graph from several pool threads at once is not safe in the
+    // HIP runtime (a rare crash in the --gpu-branch test); the branch
+    // streams and their events keep the parallelism inside the graph
+    std::unique_ptr<Engine> pool = std::move(engine_);
+    engine_ = MakeSerialEngine();
     HIPCHECK(hipStreamBeginCapture(ctx_.stream, hipStreamCaptureModeRelaxed));
     hipGraph_t g = nullptr;
     try {
       RunPass(in);
     } catch (...) {
+      engine_ = std::move(pool);
       (void)hipStreamEndCapture(ctx_.stream, &g);
       if (g) (void)hipGraphDestroy(g);
       throw;
     }
+    engine_ = std::move(pool);
     HIPCHECK(hipStreamEndCapture(ctx_.stream, &g));
     HIPCHECK(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
     (void)hipGraphDestroy(g);
