@@ -91,6 +91,26 @@ struct PPOp {
     if constexpr (KM) return s + I * 512;
     else return s + (I >> 4) * (64 * 128) + (I & 15) * 512;
   }
+  // pieces [i0, i0 + n) of this wave only (the 256 x 256 loop issues an
+  // operand's four pieces over two phases)
+  __device__ __forceinline__ void issue_part(const L& l, int k0, uint16_t* s,
+                                             int w, int i0, int n) {
+    if constexpr (KM) {
+      const bool kin = k0 + kc < l.K;
+      const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if (i >= i0 && i < i0 + n)
+          dma16(rs, dst(s, w * NS + i), kin ? v[i] + kbyte : kBufOOB);
+    } else {
+      const uint32_t kadv = (uint32_t)k0 * (uint32_t)l.ld * 2u;
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if (i >= i0 && i < i0 + n)
+          dma16(rs, dst(s, w * NS + i),
+                k0 + kr[i] < l.K ? v[i] + kadv : kBufOOB);
+    }
+  }
   __device__ __forceinline__ void issue(const L& l, int k0, uint16_t* s, int w) {
     if constexpr (KM) {
       const bool kin = k0 + kc < l.K;
@@ -320,6 +340,221 @@ gemm_pp_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
   }
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 tile, two LDS stages (2 x 64 KiB), four phases per K tile.
+// Waves: group g = w >> 2 owns rows 128 g .. +128, wave w & 3 columns
+// 64 (w & 3) .. +64; a wave tile is 128 x 64 (8 x 4 accumulators) split in
+// quadrants of 64 x 32: q0 (A0, B0) reads A0 + B0, q1 (A0, B1) reads B1,
+// q2 (A1, B1) reads A1 (into A0's registers), q3 (A1, B0) reads nothing.
+// DMA per tile t, two pieces per phase: A(t+1) in q0 / q1 (its stage held
+// tile t-1, fully read), B(t+2) in q2 / q3 (into tile t's stage: its B was
+// last read in q1), then vmcnt(4) retires tile t+1 with B(t+2) in flight.
+// Hazards by slot (group g, phase P = 4t + q: MEM slot 2P + g):
+//   RAW  A(t+1) issued in slots 8t..8t+3, B(t+1) in 8t-4..8t-1, waited in
+//        slots 8t+6 (g0) / 8t+7 (g1); first reads 8t+8 / 8t+9.
+//   WAR  B(t+2) issued from 8t+4 after B(t)'s last read in 8t+3 (g1, q1,
+//        lgkmcnt(0) before its barrier); A(t+2) from 8t+8 after A(t)'s last
+//        read in 8t+5 (q2, lgkmcnt(0) before its barrier).
+// The epilogue stages the f32 tile in four 64-row passes (66 KiB each).
+constexpr int PQ_B = 256, PQ_SA = PQ_B * BK, PQ_SST = 2 * PQ_SA;
+constexpr int PQ_LDC = PQ_B + 4;
+static_assert(64 * PQ_LDC * 4 <= 2 * PQ_SST * 2, "epilogue pass fits");
+
+template <class LP, bool PK, class LQ, bool QK>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp256_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
+                  int tiles_q, int tiles, int splits, int gm) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * PQ_SST];
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  const int gs = wgid / tiles;
+  const int gi = gs / splits;
+  int tp, tq;
+  if (gm > 1) {
+    const int tiles_p = tiles / tiles_q;
+    const int g = tile / (gm * tiles_q);
+    const int p0g = g * gm;
+    const int gh = min(tiles_p - p0g, gm);
+    const int r = tile - g * gm * tiles_q;
+    tp = p0g + r % gh;
+    tq = r / gh;
+  } else {
+    tp = tile / tiles_q;
+    tq = tile - tp * tiles_q;
+  }
+  const int kbeg = (gs - gi * splits) * k_split;
+  const int kend = min(K, kbeg + k_split);
+  if (kbeg >= kend) return;
+  lp.group(gi);
+  lq.group(gi);
+  const int p0 = tp * PQ_B, q0 = tq * PQ_B;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = w >> 2;
+  const int prow = grp * 128;        // wave's first P row
+  const int qrow = (w & 3) * 64;     // wave's first Q row
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PPOp<LP, PK, PQ_B> op;
+  PPOp<LQ, QK, PQ_B> oq;
+  op.init(lp, p0, w, lane);
+  oq.init(lq, q0, w, lane);
+  static_assert(PPOp<LP, PK, PQ_B>::NS == 4 && PPOp<LQ, QK, PQ_B>::NS == 4,
+                "four pieces per operand and tile");
+  // half h (0 / 1) of an operand's four pieces: pieces 2h, 2h + 1
+  auto issue_half = [&](auto& o, const auto& l, int k0, uint16_t* s, int h) {
+    o.issue_part(l, k0, s, w, 2 * h, 2);
+  };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  uint16_t* st0 = smem;
+  uint16_t* st1 = smem + PQ_SST;
+  // prologue: A(0), B(0), B(1); wait for tile 0
+  op.issue(lp, kbeg, st0, w);
+  oq.issue(lq, kbeg, st0 + PQ_SA, w);
+  if (nk > 1) {
+    oq.issue(lq, kbeg + BK, st1 + PQ_SA, w);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one slot
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  auto mfma = [&](int abase, bf16x8 (&bf)[2][2], int bbase) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[abase + i][bbase + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[i][ks], bf[j][ks], acc[abase + i][bbase + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto slot_end = [&]() {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* sP = (kt & 1) ? st1 : st0;
+    const uint16_t* sQ = sP + PQ_SA;
+    uint16_t* nxt = (kt & 1) ? st0 : st1;   // tile t+1's stage
+    uint16_t* cur = (kt & 1) ? st1 : st0;   // tile t+2's stage
+    const bool pa = kt + 1 < nk, pb = kt + 2 < nk;
+    const int ka = kbeg + (kt + 1) * BK, kb = kbeg + (kt + 2) * BK;
+    // ---- q0 MEM: A0, B0; A(t+1) pieces 0, 1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b0[j][ks] = pp_frag<QK>(sQ, qrow + j * 16, ks, fr, fq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i][ks] = pp_frag<PK>(sP, prow + i * 16, ks, fr, fq);
+    }
+    if (pa) issue_half(op, lp, ka, nxt, 0);
+    slot_end();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma(0, b0, 0);                       // q0 MFMA
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+    // ---- q1 MEM: B1; A(t+1) pieces 2, 3; B reads of this tile retired
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b1[j][ks] = pp_frag<QK>(sQ, qrow + 32 + j * 16, ks, fr, fq);
+    if (pa) issue_half(op, lp, ka, nxt, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    slot_end();
+    mfma(0, b1, 2);                       // q1 MFMA
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+    // ---- q2 MEM: A1; B(t+2) pieces 0, 1; A reads of this tile retired
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i][ks] = pp_frag<PK>(sP, prow + 64 + i * 16, ks, fr, fq);
+    if (pb) issue_half(oq, lq, kb, cur + PQ_SA, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    slot_end();
+    mfma(4, b1, 2);                       // q2 MFMA
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+    // ---- q3 MEM: B(t+2) pieces 2, 3; wait for tile t+1
+    if (pb) {
+      issue_half(oq, lq, kb, cur + PQ_SA, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    slot_end();
+    mfma(4, b0, 0);                       // q3 MFMA
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // group 1's last slot
+  asm volatile("" ::: "memory");
+
+  // epilogue: four passes of 64 rows; pass e holds group e / 2's m-tiles
+  // 4 (e % 2) .. +3
+  float* sC = (float*)smem;
+  constexpr int CH = PQ_B / 8;
+  const bool fast = epi.fast_ok();
+  // (unrolled: the accumulator indices must be compile-time constants, or
+  // acc goes to scratch)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __syncthreads();
+    if (grp == (e >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rb = i * 16 + fq * 4;
+          const int qc = qrow + j * 16 + fr;
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            sC[(rb + rr) * PQ_LDC + qc] = acc[(e & 1) * 4 + i][j][rr];
+          }
+        }
+    }
+    __syncthreads();
+    const int m0 = p0 + e * 64;
+    if (epi.atomic) {
+      const int c = t & 255;
+      for (int row = t >> 8; row < 64; row += 2)
+        epi.store(gi, m0 + row, q0 + c, sC[row * PQ_LDC + c]);
+      continue;
+    }
+    for (int q = t; q < 64 * CH; q += 512) {
+      const int row = q / CH, c8 = (q % CH) * 8;
+      if (m0 + row >= epi.M) continue;
+      const float4* src = (const float4*)(sC + row * PQ_LDC + c8);
+      float v[8];
+      const float4 lo = src[0], hi = src[1];
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      if (fast && q0 + c8 + 8 <= epi.N &&
+          (epi.ones_col < 0 || q0 + c8 + 8 <= epi.ones_col))
+        epi.store8_fast(gi, m0 + row, q0 + c8, v);
+      else
+        epi.store8(gi, m0 + row, q0 + c8, v);
+    }
+  }
+}
+
 // The ping-pong loop takes a dense NT / NN GEMM (buffer-DMA operands) with
 // a 128-wide column tile and at least one 256 x 128 tile per CU (one
 // workgroup per CU).  hvk_gemm_variant 30 (or 0) disables it, 31 runs
@@ -338,9 +573,37 @@ bool want_pp(const LA& la, const LB& lb, int M, int N, int bn, int splits,
   }
 }
 
+// the 256 x 256 loop where the output is wide and tall enough: at most 1/8
+// of a 256 column tile wasted, and a 256 x 256 tile per CU; variant 32
+// keeps 256 x 128 (A/B runs)
+inline bool want_pp256(int M, int N, int splits, int groups) {
+  if (hvk_gemm_variant == 32) return false;
+  const int wn = (N + 255) / 256 * 256 - N;
+  return N >= 256 && wn * 8 <= N &&
+         (long long)((M + 255) / 256) * ((N + 255) / 256) * splits * groups >=
+             256;
+}
+
+template <class LP, bool PK, class LQ, bool QK>
+hipError_t go_pp256(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
+                    int K, int k_split, int splits, int groups,
+                    hipStream_t s) {
+  const int tiles_p = (P + 255) / 256, tiles_q = (Q + 255) / 256;
+  const int tiles = tiles_p * tiles_q;
+  const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
+  dim3 grid((unsigned)((long long)tiles * splits * groups));
+  hipLaunchKernelGGL((gemm_pp256_kernel<LP, PK, LQ, QK>), grid, dim3(512), 0,
+                     s, lp, lq, epi, P, Q, K, k_split, tiles_q, tiles, splits,
+                     gm);
+  return launch_status(s);
+}
+
 template <class LP, bool PK, class LQ, bool QK>
 hipError_t go_pp(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
                  int K, int k_split, int splits, int groups, hipStream_t s) {
+  if (want_pp256(P, Q, splits, groups))
+    return go_pp256<LP, PK, LQ, QK>(lp, lq, epi, P, Q, K, k_split, splits,
+                                    groups, s);
   const int tiles_p = (P + PP_BM - 1) / PP_BM;
   const int tiles_q = (Q + PP_BN - 1) / PP_BN;
   const int tiles = tiles_p * tiles_q;
