@@ -13,6 +13,15 @@
 using namespace hvk;
 
 namespace {
+// 2^x as the bare v_exp_f32: the LRN exponents are (-beta [- 1]) log2(s)
+// with s >= k > 0, and denormal results flush to zero in these kernels
+// anyway (-fgpu-flush-denormals-to-zero), so the library exp2f's range
+// rescaling (a second v_exp plus compare / select / multiply per call) buys
+// nothing
+__device__ __forceinline__ float ex2(float x) {
+  return __builtin_amdgcn_exp2f(x);
+}
+
 inline int grid_for(long long n, int per_block = 256) {
   long long g = (n + per_block - 1) / per_block;
   if (g > 16384) g = 16384;
@@ -319,7 +328,7 @@ __global__ void lrn_fwd_kernel(const uint16_t* x, uint16_t* y, long long P,
       int c0 = max(0, c - half), c1 = min(C - 1, c + half);
       for (int j = c0; j <= c1; ++j) s += xs[j] * xs[j];
       s = k + alpha * s;
-      y[p * C + c] = f2bf(xs[c] * exp2f(-beta * log2f(s)));
+      y[p * C + c] = f2bf(xs[c] * ex2(-beta * log2f(s)));
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -349,7 +358,7 @@ __global__ void lrn_bwd_kernel(const uint16_t* x, const uint16_t* dy,
       int c0 = max(0, c - half), c1 = min(C - 1, c + half);
       for (int j = c0; j <= c1; ++j) s += xs[j] * xs[j];
       s = k + alpha * s;
-      float sb = exp2f(-beta * log2f(s));
+      float sb = ex2(-beta * log2f(s));
       float g = bf2f(dy[p * C + c]);
       ts[c] = g * xs[c] * sb / s;
       keep[idx] = g * sb;
@@ -433,7 +442,7 @@ __global__ void lrn_fwd_vec_kernel(const uint16_t* x, uint16_t* y, int P,
         s += (d >= -half && d <= half) ? t * t : 0.f;
       }
       s = k + alpha * s;
-      o[q] = f2bf(v[8 + q] * exp2f(-beta * __log2f(s)));
+      o[q] = f2bf(v[8 + q] * ex2(-beta * __log2f(s)));
     }
     *(uint4*)(y + (long long)p * C + c0) = *(uint4*)o;
   }
@@ -467,9 +476,9 @@ __global__ void lrn_bwd_vec_kernel(const uint16_t* x, const uint16_t* dy,
       }
       s = k + alpha * s;
       const float ls = __log2f(s);
-      float sb = exp2f(-beta * ls);
+      float sb = ex2(-beta * ls);
       // s^(-beta-1) as a second exp instead of a division
-      tj[j] = gv[4 + j] * xv[4 + j] * exp2f((-beta - 1.f) * ls);
+      tj[j] = gv[4 + j] * xv[4 + j] * ex2((-beta - 1.f) * ls);
       // keep s^-beta of the owned channels in gv's free slots? recompute
       // below instead (cheap)
       if (j >= 4 && j < 12) xv[(j - 4) + 0] = sb;  // xv[0..7] unused now
@@ -544,7 +553,7 @@ __global__ void lrn_pool3_fwd_kernel(const uint16_t* __restrict__ x,
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float s = lrn_s(v, 8 + q, half, alpha, k);
-        const float yv = v[8 + q] * exp2f(-beta * __log2f(s));
+        const float yv = v[8 + q] * ex2(-beta * __log2f(s));
         if (bi[q] < 0 || yv > best[q]) { best[q] = yv; bi[q] = off; }
       }
     }
@@ -625,8 +634,8 @@ __global__ void lrn_pool3_bwd_kernel(const uint16_t* __restrict__ x,
     for (int j = 0; j < 16; ++j) {
       const float s = lrn_s(xv, 4 + j, half, alpha, k);
       const float ls = __log2f(s);
-      tj[j] = g[4 + j] * xv[4 + j] * exp2f((-beta - 1.f) * ls);
-      if (j >= 4 && j < 12) sb[j - 4] = exp2f(-beta * ls);
+      tj[j] = g[4 + j] * xv[4 + j] * ex2((-beta - 1.f) * ls);
+      if (j >= 4 && j < 12) sb[j - 4] = ex2(-beta * ls);
     }
     float a[8];
     if (aux) load8(aux + base + c0, a);
@@ -721,7 +730,7 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_kernel(
       for (int j = 0; j < 16; ++j) {
         const float s = lrn_s(xv, 4 + j, half, alpha, k);
         const float ls = __log2f(s);
-        const float e1 = exp2f((-beta - 1.f) * ls);  // s^(-beta-1)
+        const float e1 = ex2((-beta - 1.f) * ls);  // s^(-beta-1)
         tj[j] = g[p][j] * xv[4 + j] * e1;
         if (j >= 4 && j < 12) sb[j - 4] = e1 * s;  // s^-beta
       }
@@ -897,7 +906,7 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8_kernel(
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float s = lrn_s(v, 8 + q, half, alpha, k);
-        const float yv = v[8 + q] * exp2f(-beta * __log2f(s));
+        const float yv = v[8 + q] * ex2(-beta * __log2f(s));
         if (i == 0 || yv > best[q]) { best[q] = yv; bi[q] = i; }
       }
     }
@@ -979,7 +988,7 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_fwd_u8p_kernel(
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const float sv = lrn_s(v, 8 + q, half, alpha, k);
-        const float yv = v[8 + q] * exp2f(-beta * __log2f(sv));
+        const float yv = v[8 + q] * ex2(-beta * __log2f(sv));
         if (i == 0 || (in && yv > best[q])) { best[q] = yv; bi[q] = i; }
       }
     }
@@ -1056,7 +1065,7 @@ __device__ __forceinline__ void lrn_pair(const LrnPx& a, const LrnPx& b,
     const f32x2v sv = k + alpha * w;
     f32x2v l2 = f32x2v{__log2f(sv.x), __log2f(sv.y)};
     l2 = -beta * l2;
-    y[q] = v[q + 2] * f32x2v{exp2f(l2.x), exp2f(l2.y)};
+    y[q] = v[q + 2] * f32x2v{ex2(l2.x), ex2(l2.y)};
   }
 }
 
@@ -1224,7 +1233,7 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_u8_kernel(
 #pragma unroll
       for (int j = JLO; j < JHI; ++j) {
         const float s = lrn_s(xv, j, half, alpha, k);
-        const float e1 = exp2f((-beta - 1.f) * __log2f(s));  // s^(-beta-1)
+        const float e1 = ex2((-beta - 1.f) * __log2f(s));  // s^(-beta-1)
         tj[j] = g[p][j] * xv[j] * e1;
         if (j >= 8 && j < 16) sb[j - 8] = e1 * s;  // s^-beta
       }
@@ -1338,14 +1347,19 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
         av = *(const uint2*)(argmax + yo);
       }
       const uint16_t* gh = (const uint16_t*)&gv;
-      const uint8_t* ah = (const uint8_t*)&av;
+      // window indices as 32-bit byte extracts (a byte view of the uint2
+      // compiled to 64-bit shifts and compares)
+      uint32_t ai[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        ai[q] = ((q < 4 ? av.x : av.y) >> (8 * (q & 3))) & 0xffu;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int r = 2 * (1 - a) + (p >> 1), c = 2 * (1 - b) + (p & 1);
         if (r > 2 || c > 2) continue;  // pixel outside this window
-        const int kexp = r * 3 + c;
+        const uint32_t kexp = r * 3 + c;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) g[p][q] += ah[q] == kexp ? bf2f(gh[q]) : 0.f;
+        for (int q = 0; q < 8; ++q) g[p][q] += ai[q] == kexp ? bf2f(gh[q]) : 0.f;
       }
     }
 #pragma unroll
@@ -1364,10 +1378,25 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
 #pragma unroll
         for (int q = 0; q < 8; ++q) xv[q] = 0.f;
       }
+      // The kernel is VALU-bound (~87 % of SIMD cycles at AlexNet conv1
+      // b1024): the per-channel products run on channel pairs (f32x2_t ->
+      // v_pk_mul_f32 / v_pk_fma_f32, two lanes' worth per instruction) and
+      // the (2 half + 1)-term window sums slide (w_{q+1} = w_q + e_{q+2h+1}
+      // - e_q: 2 ops per output instead of 2 half)
+      f32x2_t X2[4], G2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        X2[i] = f32x2_t{xv[2 * i], xv[2 * i + 1]};
+        G2[i] = f32x2_t{g[p][2 * i], g[p][2 * i + 1]};
+      }
       // squares of channels c0 - half .. c0 + 8 + half
       float e[8 + 2 * half];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) e[half + q] = xv[q] * xv[q];
+      for (int i = 0; i < 4; ++i) {
+        const f32x2_t sq2 = X2[i] * X2[i];
+        e[half + 2 * i] = sq2.x;
+        e[half + 2 * i + 1] = sq2.y;
+      }
 #pragma unroll
       for (int d = 0; d < half; ++d) {
         const float lo = lane_from_below(e[8 + d]);   // its channel 8-half+d
@@ -1375,16 +1404,28 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
         e[d] = first ? 0.f : lo;
         e[8 + half + d] = last ? 0.f : hi;
       }
-      float sb[8], tj[8 + 2 * half];
+      float w[8];
+      w[0] = e[0];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float w = 0.f;
+      for (int d = 1; d <= 2 * half; ++d) w[0] += e[d];
 #pragma unroll
-        for (int d = 0; d <= 2 * half; ++d) w += e[q + d];
-        const float sq = k + alpha * w;
-        const float e1 = exp2f((-beta - 1.f) * __log2f(sq));  // s^(-beta-1)
-        sb[q] = e1 * sq;                                     // s^-beta
-        tj[half + q] = g[p][q] * xv[q] * e1;
+      for (int q = 1; q < 8; ++q) w[q] = (w[q - 1] + e[q + 2 * half]) - e[q - 1];
+      const f32x2_t K2 = {k, k}, A2 = {alpha, alpha};
+      const f32x2_t NB1 = {-beta - 1.f, -beta - 1.f};
+      f32x2_t SB2[4], T2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x2_t S2 = K2 + A2 * f32x2_t{w[2 * i], w[2 * i + 1]};
+        f32x2_t L2 = f32x2_t{__log2f(S2.x), __log2f(S2.y)} * NB1;
+        const f32x2_t E2 = {ex2(L2.x), ex2(L2.y)};  // s^(-beta-1)
+        SB2[i] = E2 * S2;                               // s^-beta
+        T2[i] = G2[i] * X2[i] * E2;                     // t_j
+      }
+      float tj[8 + 2 * half];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        tj[half + 2 * i] = T2[i].x;
+        tj[half + 2 * i + 1] = T2[i].y;
       }
 #pragma unroll
       for (int d = 0; d < half; ++d) {
@@ -1393,13 +1434,21 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
         tj[d] = first ? 0.f : lo;
         tj[8 + half + d] = last ? 0.f : hi;
       }
+      float acc[8];
+      acc[0] = tj[0];
+#pragma unroll
+      for (int d = 1; d <= 2 * half; ++d) acc[0] += tj[d];
+#pragma unroll
+      for (int q = 1; q < 8; ++q)
+        acc[q] = (acc[q - 1] + tj[q + 2 * half]) - tj[q - 1];
+      const f32x2_t M2 = {-2.f * alpha * beta, -2.f * alpha * beta};
       float v[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float acc = 0.f;
-#pragma unroll
-        for (int d = 0; d <= 2 * half; ++d) acc += tj[q + d];
-        v[q] = g[p][q] * sb[q] - 2.f * alpha * beta * xv[q] * acc;
+      for (int i = 0; i < 4; ++i) {
+        const f32x2_t V2 =
+            G2[i] * SB2[i] + (M2 * X2[i]) * f32x2_t{acc[2 * i], acc[2 * i + 1]};
+        v[2 * i] = V2.x;
+        v[2 * i + 1] = V2.y;
       }
       if (aux && pv) {
         float av8[8];

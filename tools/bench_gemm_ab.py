@@ -78,7 +78,9 @@ def main():
              ("fc6_fwd", lambda: gemm(B, 4096, 9216)),
              ("fc6_dgrad", lambda: gemm(B, 9216, 4096, tb=False)),
              ("fc6_wgrad", lambda: gemm(4096, 9216, B, ta=True, tb=False))]
-    layers = {"conv2": (B, 27, 27, 96, 256, 5, 1, 2, 2),
+    # conv1 after space-to-depth (57 x 57 x 48 -> 55 x 55 x 96, 3 x 3)
+    layers = {"conv1s2d": (B, 57, 57, 48, 96, 3, 1, 0, 1),
+              "conv2": (B, 27, 27, 96, 256, 5, 1, 2, 2),
               "conv3": (B, 13, 13, 256, 384, 3, 1, 1, 1),
               "conv4": (B, 13, 13, 384, 384, 3, 1, 1, 2),
               "conv5": (B, 13, 13, 384, 256, 3, 1, 1, 2),
