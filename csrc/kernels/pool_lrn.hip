@@ -1069,8 +1069,11 @@ __device__ __forceinline__ void lrn_pair(const LrnPx& a, const LrnPx& b,
   }
 }
 
+// at most 128 VGPRs (4 waves per SIMD instead of 3 at the unconstrained
+// 151; no scratch)
 template <int half, bool PF>
-__global__ __launch_bounds__(256) void lrn_pool3s2_fwd_walk_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void lrn_pool3s2_fwd_walk_kernel(
     const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
     uint8_t* __restrict__ argmax, int N, int H, int W, int C, int OH, int OW,
     int R, int S, float alpha, float beta, float k, FastDiv fCV, FastDiv fOW,
