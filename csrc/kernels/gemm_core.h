@@ -891,12 +891,6 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     }
   };
   const int nk = (kend - kbeg + BK - 1) / BK;
-  // a wave whose rows all lie past M, or whose columns all lie past N (the
-  // ragged last tile: conv4's 192-row weight gradient in 128-row tiles,
-  // conv1's 432 columns in 128-wide ones) skips its fragment reads and
-  // MFMAs; it still issues its share of the DMA and meets every barrier
-  const bool live = __builtin_amdgcn_readfirstlane(
-      (m0 + wm * WMR < M) && (n0 + wn * (NC / WNC) < N));
 
   bool done = false;
   constexpr bool GL = LA::kGlds && LB::kGlds;
@@ -1054,7 +1048,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
         }
         if (ABL < 3 || kt == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (live) compute(smem + cur * SA, smem + 2 * SA + cur * SB);
+        compute(smem + cur * SA, smem + 2 * SA + cur * SB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (ABL < 3) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -1121,7 +1115,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) gload(kbeg + (kt + 1) * BK);
-    if (live) compute(smem + cur * SA, smem + 2 * SA + cur * SB);
+    compute(smem + cur * SA, smem + 2 * SA + cur * SB);
     if (more) sstore(smem + (cur ^ 1) * SA, smem + 2 * SA + (cur ^ 1) * SB);
     __syncthreads();
     cur ^= 1;
