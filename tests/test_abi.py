@@ -11,12 +11,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _decls():
+    """name -> (return type, argument declarations)"""
     out = {}
     for f in glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")):
         src = open(f).read()
-        for m in re.finditer(r"HVK_API\s+int\s+(hvk_\w+)\s*\(([^)]*)\)", src):
-            out[m.group(1)] = [a.strip() for a in m.group(2).split(",")
-                               if a.strip()]
+        for m in re.finditer(r"HVK_API\s+(int|void\s*\*)\s*(hvk_\w+)\s*"
+                             r"\(([^)]*)\)", src):
+            out[m.group(2)] = (m.group(1).replace(" ", ""),
+                               [a.strip() for a in m.group(3).split(",")
+                                if a.strip()])
     return out
 
 
@@ -40,7 +43,11 @@ def test_every_binding_matches_its_declaration():
     assert len(decls) >= 20
     for name, sig in _lib._SIGS.items():
         assert name in decls, "%s is bound but not declared" % name
-        want = [_kind(a) for a in decls[name]]
+        ret, args = decls[name]
+        # a pointer result read back as a C int would be truncated
+        assert (ret == "void*") == (name in _lib._PTR_RET), \
+            "%s returns %s" % (name, ret)
+        want = [_kind(a) for a in args]
         assert len(sig) == len(want), "%s: %d args bound, %d declared" % (
             name, len(sig), len(want))
         for i, (got, exp) in enumerate(zip(sig, want)):
@@ -48,4 +55,4 @@ def test_every_binding_matches_its_declaration():
             if {got, exp} <= {_lib.I, _lib.U}:
                 continue
             assert got == exp, "%s arg %d: %s vs %s (%s)" % (
-                name, i, got, exp, decls[name][i])
+                name, i, got, exp, args[i])

@@ -108,6 +108,8 @@ _SIGS = {
     "hvk_stream_create": [],
 }
 _OPTIONAL = {}
+# functions returning a pointer (every other one returns int)
+_PTR_RET = {"hvk_stream_create"}
 
 
 def _load():
@@ -125,8 +127,7 @@ def _load():
                                            "-m veles_amd.ops.build" %
                                            (LIB_PATH, name))
             fn.argtypes = sig
-            fn.restype = ctypes.c_int
-        lib.hvk_stream_create.restype = ctypes.c_void_p
+            fn.restype = ctypes.c_void_p if name in _PTR_RET else ctypes.c_int
         _lib = lib
         return lib
 
