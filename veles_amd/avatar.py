@@ -3,7 +3,18 @@ producer (usually the loader) can run ahead (reference veles/avatar.py:21-129).
 
 MI355X form: ``run()`` copies the source tensors device-to-device on the
 copy-stream and records an event the consumers' compute stream waits on;
-the compute stream never stalls on the host."""
+the compute stream never stalls on the host.
+
+What this does not do: let the producer's NEXT device fill run beside the
+current step's compute.  The full-batch loaders fill on the compute stream
+(one fused gather kernel: 0.18 ms of AlexNet's 7.35 ms b1024 step), and a
+real run-ahead would alternate two buffers - which a HIP-graph-captured
+forward cannot follow (it replays the pointers it captured) without one
+graph per buffer parity - while a single-buffer clone adds a copy of the
+whole minibatch (320 MB for the space-to-depth AlexNet input) to save the
+fill it hides.  Host-side run-ahead lives in the streaming image loaders
+(``loader/image.py``: threaded decode, pinned staging, side-stream copy,
+next-minibatch prefetch)."""
 from __future__ import annotations
 
 import torch
