@@ -574,14 +574,22 @@ bool want_pp(const LA& la, const LB& lb, int M, int N, int bn, int splits,
 }
 
 // the 256 x 256 loop where the output is wide and tall enough: at most 1/8
-// of a 256 column tile wasted, and a 256 x 256 tile per CU; variant 32
-// keeps 256 x 128 (A/B runs)
+// of a 256 column tile wasted, and a 256 x 256 tile per CU - or fewer tiles
+// than CUs when that still finishes first: in units of one 256 x 128 tile
+// at the measured loop rates (1.42 vs 1.19 PF, profiles/ab_gemm_pp256_r3.log)
+// ceil(t256 / 256) rounds cost 2 / 1.42 each, ceil(t128 / 256) 1 / 1.19 (AlexNet
+// b1024 fc6 backward-data: 144 tiles in one round against 288 in two);
+// variant 32 keeps 256 x 128 (A/B runs)
 inline bool want_pp256(int M, int N, int splits, int groups) {
   if (hvk_gemm_variant == 32) return false;
   const int wn = (N + 255) / 256 * 256 - N;
-  return N >= 256 && wn * 8 <= N &&
-         (long long)((M + 255) / 256) * ((N + 255) / 256) * splits * groups >=
-             256;
+  if (N < 256 || wn * 8 > N) return false;
+  const long long t256 =
+      (long long)((M + 255) / 256) * ((N + 255) / 256) * splits * groups;
+  if (t256 >= 256) return true;
+  const long long t128 =
+      (long long)((M + 255) / 256) * ((N + 127) / 128) * splits * groups;
+  return (t256 + 255) / 256 * 2 * 119 < (t128 + 255) / 256 * 142;
 }
 
 template <class LP, bool PK, class LQ, bool QK>
