@@ -41,24 +41,57 @@ __global__ void im2col_kernel(const uint16_t* x, uint16_t* col, ConvGeom g,
   }
 }
 
-// Split-K finishing pass: C = epilogue(ws), ws the f32 sum of the K splits
-// (N % 8 == 0 and Epi::fast_ok(): one 8-column chunk per thread)
-__global__ void splitk_finish_kernel(float* __restrict__ ws, int M, int N,
-                                     Epi e, int clear) {
+// Split-K finishing pass: C = epilogue(sum of the K splits' slices of ws),
+// summed in split order (deterministic; N % 8 == 0 and Epi::fast_ok(): one
+// 8-column chunk per thread)
+__global__ void splitk_finish_kernel(const float* __restrict__ ws, int M,
+                                     int N, int splits, Epi e) {
   const int CH = N >> 3;
   const long long total = (long long)M * CH;
+  const long long slice = (long long)M * N;
   for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
        q < total; q += (long long)gridDim.x * blockDim.x) {
     const int m = (int)(q / CH), c8 = (int)(q - (long long)m * CH) * 8;
-    float4* src = (float4*)(ws + (long long)m * N + c8);
-    const float4 lo = src[0], hi = src[1];
-    if (clear) {  // leave the workspace zeroed for the next split-K GEMM
-      src[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-      src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4* src = (const float4*)(ws + (long long)m * N + c8);
+    float4 lo = src[0], hi = src[1];
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4* p = (const float4*)((const float*)src + sp * slice);
+      const float4 a = p[0], b = p[1];
+      lo.x += a.x; lo.y += a.y; lo.z += a.z; lo.w += a.w;
+      hi.x += b.x; hi.y += b.y; hi.z += b.z; hi.w += b.w;
     }
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     e.store8_fast(0, m, c8, v);
   }
+}
+
+// the four operand orientations of hvk_gemm on one epilogue
+hipError_t gemm_dispatch(int transA, int transB, int M, int N, int K,
+                         const uint16_t* a, int lda, const uint16_t* b,
+                         int ldb, const Epi& e, int splits, int oc,
+                         hipStream_t s) {
+  const int Nk = oc >= 0 ? N + 1 : N;
+  const int va = al16(a) && (lda % 8 == 0), vb = al16(b) && (ldb % 8 == 0);
+  if (!transA && transB) {
+    DenseK la{a, 0, M, K, lda, va};
+    DenseK lb{b, 0, N, K, ldb, vb};
+    return launch<DenseK, true, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
+  }
+  if (!transA && !transB) {
+    DenseK la{a, 0, M, K, lda, va};
+    DenseMN lb{b, 0, N, K, ldb, vb, oc};
+    return launch<DenseK, true, DenseMN, false>(la, lb, e, M, Nk, K, splits, 1,
+                                                s);
+  }
+  if (transA && !transB) {
+    DenseMN la{a, 0, M, K, lda, va, -1};
+    DenseMN lb{b, 0, N, K, ldb, vb, oc};
+    return launch<DenseMN, false, DenseMN, false>(la, lb, e, M, Nk, K, splits,
+                                                  1, s);
+  }
+  DenseMN la{a, 0, M, K, lda, va, -1};
+  DenseK lb{b, 0, N, K, ldb, vb};
+  return launch<DenseMN, false, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
 }
 
 }  // namespace
@@ -131,62 +164,48 @@ HVK_API int hvk_gemm(int transA, int transB, int M, int N, int K,
     e.ones_col = N;
     e.bias_grad = bias_grad;
   }
-  const int oc = bias_grad ? N : -1;
-  const uint16_t* a = (const uint16_t*)A;
-  const uint16_t* b = (const uint16_t*)B;
-  int va = al16(a) && (lda % 8 == 0), vb = al16(b) && (ldb % 8 == 0);
-  hipError_t err;
-  if (!transA && transB) {
-    DenseK la{a, 0, M, K, lda, va};
-    DenseK lb{b, 0, N, K, ldb, vb};
-    err = launch<DenseK, true, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
-  } else if (!transA && !transB) {
-    DenseK la{a, 0, M, K, lda, va};
-    DenseMN lb{b, 0, N, K, ldb, vb, oc};
-    err = launch<DenseK, true, DenseMN, false>(la, lb, e, M, Nk, K, splits, 1, s);
-  } else if (transA && !transB) {
-    DenseMN la{a, 0, M, K, lda, va, -1};
-    DenseMN lb{b, 0, N, K, ldb, vb, oc};
-    err = launch<DenseMN, false, DenseMN, false>(la, lb, e, M, Nk, K, splits, 1, s);
-  } else {
-    DenseMN la{a, 0, M, K, lda, va, -1};
-    DenseK lb{b, 0, N, K, ldb, vb};
-    err = launch<DenseMN, false, DenseK, true>(la, lb, e, M, N, K, splits, 1, s);
-  }
-  return (int)err;
+  return (int)gemm_dispatch(transA, transB, M, N, K, (const uint16_t*)A, lda,
+                            (const uint16_t*)B, ldb, e, splits,
+                            bias_grad ? N : -1, s);
 }
 
 // Split-K GEMM for shapes with too few output tiles to fill 256 CUs (the FC
 // layers at batch 512: fc6 forward is 4 x 32 tiles of 128 x 128): the K range
-// is split `splits` ways, the partial products are summed by f32 atomics into
-// the workspace ws[M][N] (zeroed here), then one pass applies alpha, the
-// per-column bias, the activation and the aux derivative and casts to C.
-// Same arguments as hvk_gemm minus beta / accumulate / bias_grad; N % 8 == 0
-// and 16-B aligned C / bias / aux rows (-4 otherwise: use hvk_gemm).
-// ws_zero = 1: ws is all zeros on entry and is left all zeros (the finishing
-// pass clears what it read) - no memset launch per GEMM.
+// is split `splits` ways, each split STORES its partial product to its own
+// slice of the workspace ws[splits][M][N] (no f32 atomics, no zeroing), then
+// one pass sums the slices in split order and applies alpha, the per-column
+// bias, the activation and the aux derivative and casts to C.  ws holds
+// splits * M * N floats.  Same arguments as hvk_gemm minus beta /
+// accumulate / bias_grad; N % 8 == 0 and 16-B aligned C / bias / aux rows
+// (-4 otherwise: use hvk_gemm).  ws_zero is ignored (every slice element is
+// written before it is read).
 HVK_API int hvk_gemm_splitk(int transA, int transB, int M, int N, int K,
                             const void* A, int lda, const void* B, int ldb,
                             void* C, int ldc, int out_f32, float alpha,
                             const float* bias, int act, const void* aux,
                             int ld_aux, int aux_act, int splits, float* ws,
                             int ws_zero, hipStream_t s) {
+  (void)ws_zero;
   Epi e = make_epi(C, ldc, M, N, out_f32, 0, alpha, 0.f, bias, 1, act, aux,
                    ld_aux, aux_act);
   if (N % 8 || !e.fast_ok() || ((uintptr_t)ws & 15) || splits < 2) return -4;
-  if (!ws_zero) {
-    hipError_t err = hipMemsetAsync(ws, 0, (size_t)M * N * sizeof(float), s);
-    if (err != hipSuccess) return (int)err;
-  }
-  const int rc = hvk_gemm(transA, transB, M, N, K, A, lda, B, ldb, ws, N, 1,
-                          1, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0, splits,
-                          nullptr, s);
-  if (rc) return rc;
+  // the split count launch() derives (K per split rounded up to BK)
+  int ks = (K + splits - 1) / splits;
+  ks = (ks + BK - 1) / BK * BK;
+  const int sp = (K + ks - 1) / ks;
+  Epi w = make_epi(ws, N, M, N, 1, 0, 1.f, 0.f, nullptr, 0, 0, nullptr, 0, 0);
+  w.slice = 1;
+  w.grow = M;
+  const hipError_t err = gemm_dispatch(transA, transB, M, N, K,
+                                       (const uint16_t*)A, lda,
+                                       (const uint16_t*)B, ldb, w, splits, -1,
+                                       s);
+  if (err != hipSuccess) return (int)err;
   const long long total = (long long)M * (N / 8);
   long long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(splitk_finish_kernel, dim3((int)blocks), dim3(256), 0, s,
-                     ws, M, N, e, ws_zero);
+                     (const float*)ws, M, N, sp, e);
   return (int)launch_status(s);
 }
 

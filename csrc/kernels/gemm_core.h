@@ -610,6 +610,11 @@ struct Epi {
   float* bias_grad;
   int bias_store;  // 1: the bias-gradient column is stored, not added
   int run_in, run_out;  // column remap n = kh*run_in + j -> kh*run_out + j
+  // 1: split-K partial sums, each K split stored (not added) to its own
+  // slice of an f32 workspace [splits][M][ldc] (grow = M: the split index
+  // takes the group index's place in the row offset); 128-row gemm_kernel
+  // tiles only
+  int slice;
   // fused fp8 copy of the (bf16) output for the fp8 layer reading it
   // (store8_fast only; q8.q == nullptr: off)
   Q8 q8;
@@ -835,7 +840,8 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     tm = tile / tiles_n;
     tn = tile - tm * tiles_n;
   }
-  const int kbeg = (gs - gi * splits) * k_split;
+  const int split = gs - gi * splits;
+  const int kbeg = split * k_split;
   const int kend = min(K, kbeg + k_split);
   if (kbeg >= kend) return;
   la.group(gi);
@@ -1153,6 +1159,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
   const float qs = epi.q8.q ? fp8_scale(epi.q8.st, epi.q8.hist, epi.q8.fmax)
                             : 1.f;
   float amax = 0.f;
+  const int eg = epi.slice ? split : gi;  // row-offset index of the store
   for (int q = t; q < BMC * CH; q += NT) {
     int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
     if (m0 + row >= M) continue;
@@ -1163,9 +1170,9 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
     if (fast && n0 + c8 + 8 <= epi.N &&
         (epi.ones_col < 0 || n0 + c8 + 8 <= epi.ones_col))
-      epi.store8_fast(gi, m0 + row, n0 + c8, v, qs, &amax);
+      epi.store8_fast(eg, m0 + row, n0 + c8, v, qs, &amax);
     else
-      epi.store8(gi, m0 + row, n0 + c8, v);
+      epi.store8(eg, m0 + row, n0 + c8, v);
   }
   if (epi.q8.q) {  // block-uniform
     __syncthreads();   // sC reads done: its first words hold the reduction
@@ -1261,7 +1268,7 @@ hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
       ks = (ks + BK - 1) / BK * BK;
       sp = (K + ks - 1) / ks;
     }
-    if (want_pp<LA, AK, LB, BKM>(la, lb, M, N, bn, sp, groups))
+    if (!epi.slice && want_pp<LA, AK, LB, BKM>(la, lb, M, N, bn, sp, groups))
       return go_pp<LA, AK, LB, BKM>(la, lb, epi, M, N, K, ks, sp, groups, s);
   }
 #define HVK_GO(BNV, W8V, VARV)                                              \
@@ -1402,6 +1409,7 @@ Epi make_epi(void* c, int ldc, int M, int N, int out_f32, int atomic,
   e.grow = 0; e.gcol = 0; e.preact = nullptr;
   e.ones_col = -1; e.bias_grad = nullptr; e.run_in = 0; e.run_out = 0;
   e.bias_store = 0;
+  e.slice = 0;
   e.q8.q = nullptr;
   e.q8.st = nullptr;
   e.q8.shard = nullptr;

@@ -138,8 +138,9 @@ def test_gemm_epilogue_bias_act_aux():
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
 def test_gemm_auto_splitk_epilogue(tb, out_dtype):
     """Few output tiles and a long K (the FC layers at batch 512) take the
-    split-K path (hvk_gemm_splitk: f32 atomics into a workspace, then one
-    epilogue pass): bias, activation and aux derivative against fp32."""
+    split-K path (hvk_gemm_splitk: each K split stores to its own workspace
+    slice, one epilogue pass sums them in order): bias, activation and aux
+    derivative against fp32, and bit-identical across runs."""
     M, N, K = 256, 1000, 4096
     assert ops.auto_splitk(M, N, K, torch.empty(M, N, device=DEV)) > 1
     a, w = rnd(M, K), rnd(N, K, seed=2) if tb else rnd(K, N, seed=2)
@@ -153,6 +154,30 @@ def test_gemm_auto_splitk_epilogue(tb, out_dtype):
                        aux_act=3, out_dtype=out_dtype)
         close(got.float(), ref, 1e-2 if out_dtype == torch.bfloat16 else
               5e-3)
+        again = ops.gemm(a.to(DEV), w.to(DEV), trans_b=bool(tb),
+                         bias=bias.to(DEV), act=act, aux=aux.to(DEV),
+                         aux_act=3, out_dtype=out_dtype)
+        assert torch.equal(got, again)
+
+
+@pytest.mark.parametrize("M,N,K,sk", [(1024, 1000, 4096, 4), (200, 64, 3000, 3),
+                                      (130, 136, 1100, 7)])
+def test_gemm_splitk_slices(M, N, K, sk):
+    """Explicit split counts, including a K that leaves the last split short
+    and a split count launch() lowers (7 requested over 1100 -> 6 of 192):
+    the finishing pass sums exactly the slices the GEMM wrote."""
+    a, w = rnd(M, K), rnd(N, K, seed=5)
+    bias = torch.randn(N)
+    ref = ops.gemm(a, w, trans_b=True, bias=bias, act=1,
+                   out_dtype=torch.float32)
+    old = ops._splitk_forced
+    ops._splitk_forced = sk
+    try:
+        got = ops.gemm(a.to(DEV), w.to(DEV), trans_b=True, bias=bias.to(DEV),
+                       act=1, out_dtype=torch.float32)
+    finally:
+        ops._splitk_forced = old
+    close(got, ref, 5e-3)
 
 
 def test_gemm_splitk_accumulate():

@@ -273,10 +273,11 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         sk = 0 if accumulate or beta != 0.0 else \
             _splitk_for(a, b, trans_a, trans_b, out, M, N, K, bias, aux)
         if sk > 1:
-            # a persistent, self-clearing f32 workspace per size (zeroed once;
-            # the finishing pass zeroes what it reads)
-            ws = _workspace(("splitk_ws", M * N), (M * N,), torch.float32,
-                            dev, zero=True)
+            # a persistent f32 workspace of sk slices per size: each K split
+            # stores its partial product to its own slice, the finishing
+            # pass sums them in order (no atomics, nothing to zero)
+            ws = _workspace(("splitk_ws", M * N * sk), (M * N * sk,),
+                            torch.float32, dev)
             _lib_call("hvk_gemm_splitk", int(trans_a), int(trans_b), M, N, K,
                       _p(a), a.stride(0), _p(b), b.stride(0), _p(out),
                       out.stride(0), int(out.dtype == torch.float32),
