@@ -413,7 +413,10 @@ def _splitk_for(a, b, trans_a, trans_b, out, M, N, K, bias, aux):
     if _splitk_forced is not None:
         return _splitk_forced if _splitk_aligned(N, out, bias, aux) else 0
     sk = auto_splitk(M, N, K, out, bias, aux)
-    if _SPLITK_ENV == "0" or -(-M // 128) * -(-N // 128) >= 256 or \
+    # the table may also split a GEMM with 256..511 tiles (one 128 x 128
+    # tile per CU: AlexNet b1024 fc6 forward runs 2 splits 7 % faster,
+    # profiles/splitk_sweep_fc_r3.log)
+    if _SPLITK_ENV == "0" or -(-M // 128) * -(-N // 128) >= 512 or \
             K < 1024 or not _splitk_aligned(N, out, bias, aux):
         return sk
     from veles_amd.ops import autotune
