@@ -1,3 +1,4 @@
+#include <exception>
 #include "runtime.h"
 
 #include <algorithm>
@@ -70,17 +71,27 @@ class PoolEngine : public Engine {
   }
   // Tasks may schedule children (a unit fires its successors): drain until
   // no task scheduled while waiting is left, or Wait() could return while a
-  // child is still queued.
+  // child is still queued.  A task that throws does not stop the drain: the
+  // remaining tasks reference the caller's stack (Run's input) and outputs,
+  // so every one of them finishes before the first exception is rethrown.
   void Wait() override {
+    std::exception_ptr first;
     while (true) {
       std::vector<std::future<void>> f;
       {
         std::lock_guard<std::mutex> lk(mu_);
         f.swap(futs_);
       }
-      if (f.empty()) return;
-      for (auto& x : f) x.get();
+      if (f.empty()) break;
+      for (auto& x : f) {
+        try {
+          x.get();
+        } catch (...) {
+          if (!first) first = std::current_exception();
+        }
+      }
     }
+    if (first) std::rethrow_exception(first);
   }
 
  private:

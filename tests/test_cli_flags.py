@@ -163,6 +163,8 @@ def test_manhole_serves_a_console_on_sigusr2(tmp_path):
                 break
             except OSError:
                 time.sleep(0.05)
+        # owner-only socket whatever the umask
+        assert os.stat(path).st_mode & 0o077 == 0
         f = s.makefile("rw")
         assert f.read(4) == ">>> "
         f.write("print(len(units) >= 2, type(workflow).__name__)\n")
@@ -179,7 +181,9 @@ def test_manhole_flag(wf_file):
     old = signal.getsignal(signal.SIGUSR2)
     try:
         m = _main(path, "", "-a", "cpu", "--manhole", "--dry-run", "exec")
-        assert m.manhole_path.endswith("%d.sock" % os.getpid())
+        assert m.manhole_path.endswith("manhole.sock")
+        # a private directory, not a predictable name in shared /tmp
+        assert os.stat(os.path.dirname(m.manhole_path)).st_mode & 0o077 == 0
         assert signal.getsignal(signal.SIGUSR2) is not old
     finally:
         signal.signal(signal.SIGUSR2, old)

@@ -158,13 +158,17 @@ def test_full_batch_normalizer_sees_served_crops(tmp_path):
 
 
 # ------------------------------------------------------------- streaming
-@pytest.mark.parametrize("prefetch", [True, False])
-def test_streaming_file_image_loader_prefetches(tmp_path, prefetch):
+@pytest.mark.parametrize("prefetch,workers",
+                         [(True, 2), (False, 2), (True, 1)])
+@pytest.mark.timeout(60)
+def test_streaming_file_image_loader_prefetches(tmp_path, prefetch, workers):
+    """decode_workers=1 with prefetch: the prefetch job must not hold the
+    only decode worker while it waits on the decode pool (it deadlocked)."""
     root = _make_images(str(tmp_path / "train"), per=6)
     ld = _init(FileImageLoader(
         DummyWorkflow(), train_paths=[root], size=(12, 10), crop=(8, 8),
         mirror="random", minibatch_size=4, normalization_type="mean_disp",
-        prefetch=prefetch, decode_workers=2))
+        prefetch=prefetch, decode_workers=workers))
     assert ld.class_lengths == [0, 0, 12]
     assert ld.reversed_labels_mapping == ["cat", "dog"]
     served = _serve(ld, 6)          # two epochs of 3 minibatches

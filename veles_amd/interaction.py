@@ -12,10 +12,11 @@ inspected with ``nc -U``.
 from __future__ import annotations
 
 import code
-import contextlib
 import os
 import signal
 import socket
+import sys
+import tempfile
 import threading
 
 from veles_amd.units import Unit
@@ -24,14 +25,56 @@ from veles_amd.utils.config import get, root
 __all__ = ["Shell", "serve_console", "install_manhole"]
 
 
+class _ThreadStdout(object):
+    """sys.stdout proxy: writes from threads registered in ``sinks`` go to
+    their sink (a console client), every other thread's to the original
+    stream - so a console does not capture the training thread's output."""
+
+    def __init__(self, orig):
+        self.orig = orig
+        self.sinks = {}
+
+    def _target(self):
+        return self.sinks.get(threading.get_ident(), self.orig)
+
+    def write(self, data):
+        return self._target().write(data)
+
+    def flush(self):
+        return self._target().flush()
+
+    def __getattr__(self, name):
+        return getattr(self.orig, name)
+
+
+_stdout_lock = threading.Lock()
+
+
+def _route_stdout(sink):
+    with _stdout_lock:
+        if not isinstance(sys.stdout, _ThreadStdout):
+            sys.stdout = _ThreadStdout(sys.stdout)
+        sys.stdout.sinks[threading.get_ident()] = sink
+
+
+def _unroute_stdout():
+    with _stdout_lock:
+        if isinstance(sys.stdout, _ThreadStdout):
+            sys.stdout.sinks.pop(threading.get_ident(), None)
+
+
 def serve_console(path, namespace):
-    """Serve ONE Python console client on the UNIX socket ``path``."""
-    try:
-        os.remove(path)
-    except OSError:
-        pass
+    """Serve ONE Python console client on the UNIX socket ``path``.  The
+    socket is created owner-only (mode 0600) whatever the umask; ``path``
+    must not exist yet (a path in a shared directory that someone else
+    created is never removed or reused)."""
     srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
-    srv.bind(path)
+    old = os.umask(0o177)
+    try:
+        srv.bind(path)
+    finally:
+        os.umask(old)
+    os.chmod(path, 0o600)
     srv.listen(1)
     try:
         conn, _ = srv.accept()
@@ -40,13 +83,16 @@ def serve_console(path, namespace):
         console.write = lambda data: (f.write(data), f.flush())
         f.write(">>> ")
         f.flush()
-        for line in f:
-            # the client sees what the statement prints (stdout of the
-            # process while it runs: this is a debugging console)
-            with contextlib.redirect_stdout(f):
+        # what a statement prints goes to the client; other threads keep
+        # the process's stdout
+        _route_stdout(f)
+        try:
+            for line in f:
                 more = console.push(line.rstrip("\n"))
-            f.write("... " if more else ">>> ")
-            f.flush()
+                f.write("... " if more else ">>> ")
+                f.flush()
+        finally:
+            _unroute_stdout()
         conn.close()
     finally:
         srv.close()
@@ -59,9 +105,11 @@ def serve_console(path, namespace):
 def install_manhole(workflow, path=None):
     """``--manhole`` (reference thread_pool.py:139-142): on SIGUSR2 the
     process starts serving a console into ``workflow`` on a UNIX socket
-    (``/tmp/veles_amd_manhole_<pid>.sock`` by default; ``nc -U`` it).
-    Returns the socket path."""
-    path = path or "/tmp/veles_amd_manhole_%d.sock" % os.getpid()
+    (``manhole.sock`` in a fresh owner-only directory by default; ``nc -U``
+    it).  Returns the socket path."""
+    if path is None:
+        path = os.path.join(tempfile.mkdtemp(prefix="veles_amd_manhole_"),
+                            "manhole.sock")
 
     def handler(signum, frame):
         ns = {"workflow": workflow, "root": root,

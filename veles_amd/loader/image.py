@@ -466,6 +466,9 @@ class _Staging(object):
         self.dev = [torch.empty((n,) + shape, dtype=torch.uint8, device=tdev)
                     if gpu else self.host[i] for i in range(2)]
         self.copied = [None, None]
+        # recorded on the compute stream after the device twin was last read:
+        # the next copy into that twin waits for it on the copy stream
+        self.consumed = [None, None]
         self.stream = torch.cuda.Stream(tdev) if gpu else None
         self.gpu = gpu
 
@@ -497,6 +500,10 @@ class ImageLoader(_ImageMixin, Loader):
     def init_unpickled(self):
         super().init_unpickled()
         self._pool_ = None
+        # prefetch jobs run here, not on _pool_: a job that waits on the
+        # decode pool from inside it would hold one of its workers (and
+        # deadlock with decode_workers=1)
+        self._prefetch_pool_ = None
         self._stage_ = None
         self._pending_ = {}
         self._slot_ = 0
@@ -596,8 +603,14 @@ class ImageLoader(_ImageMixin, Loader):
         if self._pool_ is None:
             self._pool_ = cf.ThreadPoolExecutor(
                 self.decode_workers, thread_name_prefix="image-decode")
+        if self._prefetch_pool_ is None:
+            self._prefetch_pool_ = cf.ThreadPoolExecutor(
+                1, thread_name_prefix="image-prefetch")
 
     def stop(self):
+        if self._prefetch_pool_ is not None:
+            self._prefetch_pool_.shutdown(wait=True)
+            self._prefetch_pool_ = None
         if self._pool_ is not None:
             self._pool_.shutdown(wait=True)
             self._pool_ = None
@@ -635,7 +648,7 @@ class ImageLoader(_ImageMixin, Loader):
 
     def fill_indices(self, start_offset, count):
         import torch
-        if self._stage_ is None:
+        if self._stage_ is None or self._pool_ is None:
             self.on_initialized()
         st = self._stage_
         samples = tuple(int(v) for v in
@@ -656,6 +669,10 @@ class ImageLoader(_ImageMixin, Loader):
         tdev = self.minibatch_data.devmem.device
         cur = torch.cuda.current_stream(tdev) if st.gpu else None
         if st.gpu:
+            if st.consumed[slot] is not None:
+                # the compute stream may still be reading this twin (the host
+                # can run two minibatches ahead of the GPU)
+                st.stream.wait_event(st.consumed[slot])
             with torch.cuda.stream(st.stream):
                 st.dev[slot][:count].copy_(st.host[slot][:count],
                                            non_blocking=True)
@@ -677,6 +694,10 @@ class ImageLoader(_ImageMixin, Loader):
             tdev, non_blocking=True) if st.gpu else torch.from_numpy(a))
         self._image_batch(st.dev[slot], to(canv), to(params),
                           self.minibatch_data.devmem)
+        if st.gpu:
+            done = torch.cuda.Event()
+            done.record(cur)
+            st.consumed[slot] = done
         if self.has_labels and self.minibatch_labels.devmem is not None:
             lab = numpy.full(n, -1, numpy.int32)
             lab[:count] = [self.labels_mapping[self._key_labels_[
@@ -691,7 +712,7 @@ class ImageLoader(_ImageMixin, Loader):
         if self.prefetch:
             nxt = self._predict_next()
             if nxt:
-                self._pending_[nxt] = self._pool_.submit(
+                self._pending_[nxt] = self._prefetch_pool_.submit(
                     self._decode_into, self._slot_, nxt)
         return True
 
