@@ -1,0 +1,70 @@
+#!/bin/bash
+# One parameterised GPU job (replaces the per-experiment gpu_r3_*.sh
+# launchers).  Each argument is a step; steps run in order under their own
+# time limit (tools/gpu_step.sh) and the job stops at the first fault,
+# abort, segfault or timeout.  Logs go to gpurun_out/<step>.log.
+#
+#   tools/gpu_job.sh STEP [STEP ...]
+#
+# steps:
+#   tests[:PATTERN]          pytest -m gpu (PATTERN: test file(s) or -k expr,
+#                            e.g. tests:tests/test_gemm_t4_gpu.py)
+#   smoke                    __graft_entry__.smoke()
+#   bench[:ARGS]             python bench.py ARGS (comma-separated, e.g.
+#                            bench:--batch,512,--model,vgg16)
+#   solo[:ARGS]              bench.py with a one-rank RCCL process group
+#                            (VELES_AMD_DP_SOLO_COLLECTIVES=1)
+#   ab[:B:ROUNDS:VARIANTS]   tools/bench_gemm_ab.py (GEMM loop A/B)
+#   prof[:MODEL:BATCH:TAG:PREC]  step-only rocprofv3 kernel table
+#   py:SCRIPT[,ARGS]         python SCRIPT ARGS
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}
+  arg=""
+  [ "$kind" != "$step" ] && arg=${step#*:}
+  log=gpurun_out/job${n}_${kind}.log
+  echo "[gpu_job] step $n: $step -> $log"
+  case $kind in
+    tests)
+      sel=${arg:-tests}
+      tools/gpu_step.sh 900 "$log" python -u -m pytest $sel -m gpu -v \
+        --timeout 200 --timeout-method thread -x || exit 1
+      tail -3 "$log"
+      grep -E "FAILED|ERROR" "$log" | head -20 ;;
+    smoke)
+      tools/gpu_step.sh 300 "$log" python -c \
+        "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+      tail -2 "$log" ;;
+    bench)
+      tools/gpu_step.sh 600 "$log" python bench.py ${arg//,/ } || exit 1
+      grep metric "$log" || tail -5 "$log" ;;
+    solo)
+      tools/gpu_step.sh 600 "$log" env VELES_AMD_DP_SOLO_COLLECTIVES=1 \
+        python bench.py ${arg//,/ } || exit 1
+      grep metric "$log" || tail -5 "$log" ;;
+    ab)
+      IFS=: read -r b rounds vars <<< "$arg"
+      tools/gpu_step.sh 900 "$log" python -u tools/bench_gemm_ab.py \
+        "${b:-1024}" "${rounds:-3}" "${vars:--1}" || exit 1
+      cat "$log" | head -60 ;;
+    prof)
+      IFS=: read -r m b tag prec <<< "$arg"
+      M=${m:-alexnet} B=${b:-1024} T=${tag:-r4} P=${prec:-bfloat16}
+      tools/gpu_step.sh 600 "$log" rocprofv3 --kernel-trace --stats \
+        -d "$R/gpurun_out/prof_${M}_${T}" -o run --output-format csv -- \
+        python3 "$R/bench.py" --model $M --precision $P --steps 5 \
+        --warmup 2 --batch $B --mark-steps || exit 1
+      f=$(find gpurun_out/prof_${M}_${T} -name "*kernel_trace.csv" | head -1)
+      python tools/prof_summary.py "$f" gpurun_out/prof_${M}_${T}.md \
+        "$M b$B 1x MI355X ($P, $T)" --window --steps 5
+      head -40 gpurun_out/prof_${M}_${T}.md ;;
+    py)
+      tools/gpu_step.sh 900 "$log" python -u ${arg//,/ } || exit 1
+      tail -40 "$log" ;;
+    *)
+      echo "[gpu_job] unknown step $step"; exit 2 ;;
+  esac
+done
