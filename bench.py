@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--steps-per-epoch", type=int, default=16)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--profile-json", default=None)
+    ap.add_argument("--stats-steps", type=int, default=3,
+                    help="N > 1: untimed eager steps after the timed ones "
+                         "that record the per-bucket all-reduce timeline")
     ap.add_argument("--mark-steps", action="store_true",
                     help="bracket the timed steps with hvk_trace_marker "
                          "kernels (step-only rocprofv3 summaries)")
@@ -120,6 +123,15 @@ def main():
         dp.all_reduce_max(t)
     dt = float(t.cpu()[0])
     value = args.steps * global_batch / dt
+    if dp.multi and store is not None:
+        # untimed instrumented steps after the timed region: eager passes
+        # with per-bucket events (a captured backward records none)
+        from veles_amd import graphs
+        store.comm_report()
+        store.timeline_report()
+        with graphs.suspended():
+            wf.run_steps(args.stats_steps)
+        sync()
     dp_info = dp_report(dp, store, backend)
     if dp.rank == 0:
         base = None
@@ -186,7 +198,11 @@ def dp_report(dp, store, backend):
         info["buckets_mb"] = [mb for mb, _ in lay]
         info["grad_dtype"] = store.grad_dtype
         info["overlapped_update"] = bool(store._overlap_update())
+        info["graph_backward"] = bool(store.graph_safe())
         rep = store.comm_report()
+        tl = store.timeline_report()
+        if tl is not None:
+            info["bucket_timeline"] = tl
     ms = torch.tensor([rep["mean_ms"] if rep else -1.0], dtype=torch.float64)
     if dp.world_size > 1:
         if backend == "hip":
@@ -194,6 +210,7 @@ def dp_report(dp, store, backend):
         dp.all_reduce_max(ms)
     v = float(ms.cpu()[0])
     info["exposed_allreduce_ms_per_step"] = round(v, 4) if v >= 0 else None
+    info["stats_from"] = "untimed eager steps after the timed region"
     info["grad_allreduce"] = "bucketed %s all-reduce (%s, %d buckets), " \
         "launched per bucket during backward" % (
             "RCCL" if dp.backend == "nccl" else dp.backend,

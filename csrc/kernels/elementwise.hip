@@ -500,14 +500,18 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x, uint32_t seed) {
 }
 // seed_dev (optional): the seed is read from device memory instead, so a
 // captured HIP graph draws a fresh mask every replay (hvk_seed_advance).
+// element i's mask is hash32(base + i, seed): a rank passes the global index
+// of its shard's first element (rank x local elements), so the ranks of a
+// data-parallel step draw exactly the masks a single process would draw for
+// the whole global minibatch
 __global__ void dropout_kernel(const void* x, int xdt, void* y, int ydt,
                                long long n, uint32_t seed, uint32_t thresh,
                                float scale, uint8_t* mask_out,
-                               const uint32_t* seed_dev) {
+                               const uint32_t* seed_dev, long long base) {
   if (seed_dev) seed = __builtin_amdgcn_readfirstlane(seed_dev[0]);
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    bool keep = hash32((uint32_t)i, seed) >= thresh;
+    bool keep = hash32((uint32_t)(base + i), seed) >= thresh;
     st_any(y, i, ydt, keep ? ld_any(x, i, xdt) * scale : 0.f);
     if (mask_out) mask_out[i] = keep;
   }
@@ -1301,7 +1305,7 @@ HVK_API int hvk_dropout(const void* x, int xdt, void* y, int ydt, long long n,
   float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      y, ydt, n, seed, thresh, scale, (uint8_t*)mask_out,
-                     (const uint32_t*)nullptr);
+                     (const uint32_t*)nullptr, 0ll);
   return (int)launch_status(s);
 }
 
@@ -1314,7 +1318,19 @@ HVK_API int hvk_dropout_dev(const void* x, int xdt, void* y, int ydt,
   float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
                      y, ydt, n, 0u, thresh, scale, (uint8_t*)mask_out,
-                     (const uint32_t*)seed_dev);
+                     (const uint32_t*)seed_dev, 0ll);
+  return (int)launch_status(s);
+}
+
+// as hvk_dropout_dev, with the mask index of element i at base + i
+HVK_API int hvk_dropout_dev_at(const void* x, int xdt, void* y, int ydt,
+                               long long n, const void* seed_dev, float p,
+                               long long base, hipStream_t s) {
+  uint32_t thresh = (uint32_t)fminf(4294967295.f, p * 4294967296.f);
+  float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xdt,
+                     y, ydt, n, 0u, thresh, scale, (uint8_t*)nullptr,
+                     (const uint32_t*)seed_dev, base);
   return (int)launch_status(s);
 }
 

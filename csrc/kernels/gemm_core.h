@@ -404,13 +404,14 @@ struct ConvWgradB {
         (in & (d.kind == 2u ? 1u : 0u)) ? g_ones8 : g_zero8;
     return pick_src(x + (d.nbase + (ih * g.W + iw) * g.C + d.ch), v, zp);
   }
-  __device__ __forceinline__ void dnext(DCol& d) const {
-    d.p += BK;
-    d.rem += BK;
+  __device__ __forceinline__ void dnext_by(DCol& d, int step) const {
+    d.p += step;
+    d.rem += step;
     const bool w = d.rem >= g.OH * g.OW;
     d.rem -= w ? g.OH * g.OW : 0;
     d.nbase += w ? g.H * g.W * g.C : 0;
   }
+  __device__ __forceinline__ void dnext(DCol& d) const { dnext_by(d, BK); }
   __device__ __forceinline__ const uint16_t* src(const Ctx& cx, int p) const {
     if (!cx.ok || p >= K) return g_zero8;
     if (cx.ok == 2) return g_ones8;
@@ -1181,6 +1182,7 @@ gemm_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_split,
 }
 
 #include "gemm_pp.h"
+#include "gemm_t4.h"
 
 // Tile width: 128 unless it wastes more than 1/8 of the columns; then 64,
 // or 96 for a single 96-wide column tile (K-major B only: AlexNet conv1,
@@ -1253,6 +1255,15 @@ template <class LA, bool AK, class LB, bool BKM, bool BUF>
 hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles_n, int tiles, int splits,
                      int bn, dim3 grid, hipStream_t s) {
+  // implicit-GEMM convolutions: 256 x 128 tiles, two workgroups per CU
+  // (gemm_t4.h)
+  if constexpr (BUF && t4_pair_ok<LA, AK, LB, BKM>()) {
+    const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+    bool taken = false;
+    const hipError_t r = t4_launch<LA, AK, LB, BKM>(
+        la, lb, epi, M, N, K, k_split, tiles, splits, groups, s, &taken);
+    if (taken) return r;
+  }
   // large dense NT / NN GEMMs: the ping-pong 256 x 128 loop (gemm_pp.h)
   if constexpr (BUF && pp_loader_ok<LA, AK, true>() &&
                 pp_loader_ok<LB, BKM, false>()) {

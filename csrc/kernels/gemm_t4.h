@@ -1,0 +1,429 @@
+// gemm_t4.h - 256 x 128 (or 192 x 128) tiles at TWO workgroups per CU for
+// the implicit-GEMM convolutions.  Included by gemm_core.h inside its
+// anonymous namespace, after gemm_pp.h.
+//
+// Why: the convolutions' GEMMs are short along K (AlexNet: 36-75 K tiles of
+// 32) and narrow (128-384 output channels per group).  The 128 x 128 loop of
+// gemm_kernel (8 waves of 64 x 32) moves 0.0156 operand bytes per FLOP and
+// pays two barriers and four LDS-DMA pieces per 16 MFMAs of each wave: it is
+// bound by DMA issue and synchronisation (profiles/r3_experiments.md §10).
+// The one-workgroup-per-CU ping-pong loops (gemm_pp.h) move fewer bytes but
+// cannot hide a tile's prologue and epilogue (§12, §13).  This loop keeps
+// two independent workgroups per CU and gives each wave the 128 x 64 tile of
+// the 256 x 256 ping-pong loop:
+//
+//   * 4 waves (one per SIMD) per workgroup, 2 x 2, each PR/2 x 64 (8 x 4 or
+//     6 x 4 accumulators of MFMA 16x16x32); the other workgroup on the CU
+//     supplies the second wave per SIMD, so one workgroup's barrier waits,
+//     prologue and epilogue run under the other one's MFMAs;
+//   * BK = 32, 3-stage LDS ring of (PR + 128) x 32 bf16 (24 KiB at PR = 256,
+//     72 KiB per workgroup): tile t + 2 is issued at the top of step t,
+//     tile t + 1 is retired by one counted vmcnt at its end, ONE s_barrier
+//     per K step (32 MFMAs per wave);
+//   * 0.0117 operand bytes per FLOP (256 x 128), 12 fragment reads per 32
+//     MFMAs.
+//
+// Operand images (lane-linear LDS-DMA from pre-permuted source offsets, as
+// in gemm_kernel):
+//   K-major [rows][32 k], 64-B rows; 16-B chunk c of row r at c ^ t4_sw(r),
+//     t4_sw(r) = {0, 2, 3, 1}[(r >> 2) & 3]: the 16 lanes of each
+//     ds_read_b128 lane group hit 16 different 16-B bank slots;
+//   MN-major [32 k][IMG cols] (IMG = 128 or 256; a 192-row operand keeps a
+//     256-wide image whose upper columns read zeros), 32-B block b of k-row
+//     k at b ^ hk(k), read by ds_read_b64_tr_b16 (gemm_kernel's image with a
+//     wider row).
+// The MFMA accumulation order over K is the 128-row loop's (k ascending in
+// steps of 32): results are bit-identical to gemm_kernel.
+//
+// Orientation: the PR-row operand P and the 128-row operand Q are either
+// (A, B) - C[P][Q] - or (B, A) with TRANS - C[Q][P]; the epilogue stages the
+// f32 tile through the drained ring in two passes of PR/2 rows of P,
+// transposed for TRANS, so stores (and split-K atomics) always run along
+// C's contiguous dimension.
+
+constexpr int T4_BK = 32, T4_NST = 3, T4_QR = 128;
+
+__device__ __forceinline__ int t4_sw(int r) {
+  return (0x78 >> (2 * ((r >> 2) & 3))) & 3;
+}
+
+// One operand's DMA slots (ROWS = rows of the operand the tile computes)
+template <class L, bool KM, int ROWS>
+struct T4Op {
+  static constexpr int IMG = (KM || ROWS != 192) ? ROWS : 256;
+  static constexpr int NP = IMG / 16;   // 1-KiB pieces per stage
+  static constexpr int NS = NP / 4;     // per wave
+  static_assert(NS * 4 == NP, "pieces divide over the four waves");
+  static constexpr bool FAST = L::kFast;
+  static constexpr bool BUF = L::kBuf;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t v[NS];
+  int kr[NS];
+  int kc;
+  DRow fa[KM && FAST ? NS : 1];
+  typename DColOf<L, !KM && FAST>::type fb[!KM && FAST ? NS : 1];
+
+  __device__ __forceinline__ void init(const L& l, int r0, int kbeg, int w,
+                                       int lane) {
+    if constexpr (BUF) rs = dma_rsrc(l.dbase());
+    if constexpr (KM) {
+      kc = 8 * ((lane & 3) ^ t4_sw(lane >> 2));
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int row = r0 + 16 * (w * NS + i) + (lane >> 2);
+        if constexpr (FAST) fa[i] = l.drow(row);
+        else v[i] = l.row_voff(row);
+      }
+    } else {
+      constexpr int CPR = IMG / 8, RPP = 64 / CPR;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int I = w * NS + i;
+        kr[i] = RPP * I + lane / CPR;
+        const int pc = lane % CPR;
+        const int c = 16 * ((pc >> 1) ^ hk(kr[i])) + 8 * (pc & 1);
+        const bool cok = c < ROWS;
+        if constexpr (FAST) fb[i] = l.dcol(r0 + c, kbeg + kr[i], !cok);
+        else v[i] = cok ? l.col_voff(r0 + c, kr[i]) : kBufOOB;
+      }
+    }
+  }
+  // the K step at k0 into stage s (FAST MN-major slots track k0 themselves:
+  // steps must be issued in order)
+  __device__ __forceinline__ void issue(const L& l, int k0, uint16_t* s,
+                                        int w) {
+    if constexpr (KM && FAST) {
+      const DTap tp = l.dtap(k0 + kc);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        dma16(rs, s + (w * NS + i) * 512, l.dvoff(fa[i], tp));
+    } else if constexpr (KM) {
+      const bool kin = k0 + kc < l.K;
+      const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        dma16(rs, s + (w * NS + i) * 512, kin ? v[i] + kbyte : kBufOOB);
+    } else if constexpr (FAST) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        __builtin_amdgcn_global_load_lds(
+            (const void*)l.dsrc(fb[i]),
+            (__attribute__((address_space(3))) void*)(s + (w * NS + i) * 512),
+            16, 0, 0);
+        l.dnext_by(fb[i], T4_BK);
+      }
+    } else {
+      const uint32_t kadv = (uint32_t)k0 * (uint32_t)l.ld * 2u;
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        dma16(rs, s + (w * NS + i) * 512,
+              k0 + kr[i] < l.K ? v[i] + kadv : kBufOOB);
+    }
+  }
+};
+
+// fragment of the 16-row MFMA tile at `row` (16-row aligned)
+template <bool KM, int IMG>
+__device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int fr,
+                                          int fq) {
+  if constexpr (KM) {
+    const int r = row + fr;
+    return *(const bf16x8*)(s + r * 32 + ((fq ^ t4_sw(r)) << 3));
+  } else {
+    const int b = row >> 4;
+    const int trq = fr >> 2, trp = fr & 3;
+    const int k = fq * 8 + trq;
+    const uint16_t* p0 = s + k * IMG + ((b ^ hk(k)) << 4) + trp * 4;
+    const uint16_t* p1 = s + (k + 4) * IMG + ((b ^ hk(k + 4)) << 4) + trp * 4;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS>
+__global__ void __launch_bounds__(256, 2)
+gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
+               int tiles_q, int tiles, int splits, int gm) {
+  using OP = T4Op<LP, PK, PR>;
+  using OQ = T4Op<LQ, QK, T4_QR>;
+  constexpr int SP = OP::IMG * T4_BK, SQ = OQ::IMG * T4_BK;
+  constexpr int SST = SP + SQ;
+  constexpr int RING = T4_NST * SST * 2;
+  constexpr int HP = PR / 2;                 // P rows per epilogue pass
+  constexpr int LDC = TRANS ? HP + 4 : T4_QR + 4;
+  constexpr int EPI = (TRANS ? T4_QR : HP) * LDC * 4;
+  constexpr int SMEM = RING > EPI ? RING : EPI;
+  constexpr int MI = PR / 32;                // m-tiles per wave
+  constexpr int NSW = OP::NS + OQ::NS;       // DMA pieces per wave and step
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM / 2];
+
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  const int gs = wgid / tiles;
+  const int gi = gs / splits;
+  int tp, tq;
+  if (gm > 1) {  // grouped tile order, as in gemm_kernel
+    const int tiles_p = tiles / tiles_q;
+    const int g = tile / (gm * tiles_q);
+    const int p0g = g * gm;
+    const int gh = min(tiles_p - p0g, gm);
+    const int r = tile - g * gm * tiles_q;
+    tp = p0g + r % gh;
+    tq = r / gh;
+  } else {
+    tp = tile / tiles_q;
+    tq = tile - tp * tiles_q;
+  }
+  const int split = gs - gi * splits;
+  const int kbeg = split * k_split;
+  const int kend = min(K, kbeg + k_split);
+  if (kbeg >= kend) return;
+  lp.group(gi);
+  lq.group(gi);
+  const int p0 = tp * PR, q0 = tq * T4_QR;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int prow = (w >> 1) * HP;    // wave's first P row
+  const int qrow = (w & 1) * 64;     // wave's first Q row
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  OP op;
+  OQ oq;
+  op.init(lp, p0, kbeg, w, lane);
+  oq.init(lq, q0, kbeg, w, lane);
+
+  const int nk = (kend - kbeg + T4_BK - 1) / T4_BK;
+  // prologue: steps 0 and 1 in flight, wait for step 0
+  op.issue(lp, kbeg, smem, w);
+  oq.issue(lq, kbeg, smem + SP, w);
+  if (nk > 1) {
+    op.issue(lp, kbeg + T4_BK, smem + SST, w);
+    oq.issue(lq, kbeg + T4_BK, smem + SST + SP, w);
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  int scur = 0, spre = 2;  // stage of step t, of step t + 2
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* sP = smem + scur * SST;
+    const uint16_t* sQ = sP + SP;
+    // step t + 2 into the stage step t - 1 used (every wave finished reading
+    // it before the barrier that ended step t - 1)
+    const bool pre = kt + 2 < nk;
+    if (pre) {
+      uint16_t* d = smem + spre * SST;
+      const int k2 = kbeg + (kt + 2) * T4_BK;
+      op.issue(lp, k2, d, w);
+      oq.issue(lq, k2, d + SP, w);
+    }
+    bf16x8 bq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bq[j] = t4_frag<QK, OQ::IMG>(sQ, qrow + j * 16, fr, fq);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const bf16x8 a = t4_frag<PK, OP::IMG>(sP, prow + i * 16, fr, fq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j],
+                                                            acc[i][j], 0, 0, 0);
+    }
+    // retire step t + 1 (step t + 2 stays in flight), then one barrier:
+    // step t + 1 visible to every wave, every read of step t done
+    if (pre) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    scur = scur == 2 ? 0 : scur + 1;
+    spre = spre == 2 ? 0 : spre + 1;
+  }
+
+  // epilogue: the ring is drained (every DMA waited for, every fragment read
+  // consumed before the last barrier).  Two passes over the P rows; pass e
+  // holds the accumulators of the waves with (w >> 1) == e.
+  float* sC = (float*)smem;
+  const bool fast = epi.fast_ok();
+  const float qs = epi.q8.q ? fp8_scale(epi.q8.st, epi.q8.hist, epi.q8.fmax)
+                            : 1.f;
+  float amax = 0.f;
+  const int eg = epi.slice ? split : gi;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    if (e) __syncthreads();
+    if ((w >> 1) == e) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pl = i * 16 + fq * 4;           // pass-local P row
+          const int qc = qrow + j * 16 + fr;        // Q row
+          if constexpr (TRANS) {
+            *(float4*)(sC + qc * LDC + pl) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2],
+                            acc[i][j][3]);
+          } else {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+              sC[(pl + rr) * LDC + qc] = acc[i][j][rr];
+          }
+        }
+    }
+    __syncthreads();
+    // C rows / columns of this pass
+    constexpr int ROWS = TRANS ? T4_QR : HP;
+    constexpr int COLS = TRANS ? HP : T4_QR;
+    const int m0 = TRANS ? q0 : p0 + e * HP;
+    const int n0 = TRANS ? p0 + e * HP : q0;
+    if (epi.atomic) {
+      for (int q = t; q < ROWS * COLS; q += 256) {
+        const int row = q / COLS, c = q - (q / COLS) * COLS;
+        epi.store(eg, m0 + row, n0 + c, sC[row * LDC + c]);
+      }
+      continue;
+    }
+    constexpr int CH = COLS / 8;
+    for (int q = t; q < ROWS * CH; q += 256) {
+      const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
+      if (m0 + row >= epi.M) continue;
+      const float4* src = (const float4*)(sC + row * LDC + c8);
+      float v[8];
+      const float4 lo = src[0], hi = src[1];
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      if (fast && n0 + c8 + 8 <= epi.N &&
+          (epi.ones_col < 0 || n0 + c8 + 8 <= epi.ones_col))
+        epi.store8_fast(eg, m0 + row, n0 + c8, v, qs, &amax);
+      else
+        epi.store8(eg, m0 + row, n0 + c8, v);
+    }
+  }
+  if (epi.q8.q) {  // block-uniform
+    __syncthreads();   // sC reads done: its first words hold the reduction
+    q8_block_amax(epi.q8, amax, sC);
+  }
+}
+
+// ------------------------------------------------------------ dispatch
+// The operand pairs that take the T4 loop (LDS-DMA loaders with buffer
+// descriptors or the fast wgrad gather): conv forward / backward-data (A =
+// implicit im2col, K-major; B = weights, K-major) and the conv weight
+// gradient (A = dY MN-major, B = im2col MN-major).
+template <class LA, bool AK, class LB, bool BKM>
+constexpr bool t4_pair_ok() {
+  if constexpr (AK && BKM)
+    return std::is_same<LB, DenseK>::value &&
+           (std::is_same<LA, ConvFwdA>::value ||
+            std::is_same<LA, ConvDgradA>::value);
+  else if constexpr (!AK && !BKM)
+    return std::is_same<LA, DenseMN>::value &&
+           std::is_same<LB, ConvWgradB>::value;
+  else
+    return false;
+}
+
+// orientation options (M = A rows, N = B rows): 1 P = A (256), Q = B;
+// 2 P = A (192), Q = B; 3 P = B (256), Q = A, TRANS; 4 P = B (192), Q = A,
+// TRANS.  Forward / backward-data instantiate 1 and 4, the weight gradient
+// 3 and 2.  Cost = padded MFMA work (192-row tiles x 1.03: one more
+// accumulator-to-read ratio step); 0 = not worth it (the 128-row loop).
+inline long long t4_cost(int M, int N, int opt) {
+  auto up = [](long long x, long long b) { return (x + b - 1) / b * b; };
+  switch (opt) {
+    case 1: return up(M, 256) * up(N, 128) * 100;
+    case 2: return up(M, 192) * up(N, 128) * 103;
+    case 3: return up(N, 256) * up(M, 128) * 100;
+    case 4: return up(N, 192) * up(M, 128) * 103;
+  }
+  return 0;
+}
+
+template <class LA, bool AK, class LB, bool BKM>
+int t4_pick(int M, int N) {
+  if (hvk_gemm_variant == 50 || hvk_gemm_variant == 0) return 0;
+  const int o1 = (AK && BKM) ? 1 : 3, o2 = (AK && BKM) ? 4 : 2;
+  const long long c1 = t4_cost(M, N, o1), c2 = t4_cost(M, N, o2);
+  // the 128-row loop's padded work at its own tile (128 x 128 / 64)
+  const long long base = (long long)((M + 127) / 128 * 128) *
+                         ((N + 63) / 64 * 64) * 100;
+  const int best = c1 <= c2 ? o1 : o2;
+  const long long cb = c1 <= c2 ? c1 : c2;
+  // the T4 tile must not waste much more than the 128-row loop would
+  if (cb * 100 > base * 112) return 0;
+  if (hvk_gemm_variant == 51) return o1;
+  if (hvk_gemm_variant == 52) return o2;
+  return best;
+}
+
+template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS>
+hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
+                 int K, int k_split, int splits, int groups, hipStream_t s) {
+  const int tiles_p = (P + PR - 1) / PR, tiles_q = (Q + T4_QR - 1) / T4_QR;
+  const int tiles = tiles_p * tiles_q;
+  const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
+  dim3 grid((unsigned)((long long)tiles * splits * groups));
+  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS>), grid,
+                     dim3(256), 0, s, lp, lq, epi, P, Q, K, k_split, tiles_q,
+                     tiles, splits, gm);
+  return launch_status(s);
+}
+
+// Launch on the T4 loop if the shape takes it; *taken = false leaves the
+// call to the other loops.  A split-K launch is re-split so that the T4
+// tiles launch as many workgroups as the 128 x bn tiles would have.
+template <class LA, bool AK, class LB, bool BKM>
+hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
+                     int K, int k_split, int tiles, int splits, int groups,
+                     hipStream_t s, bool* taken) {
+  *taken = false;
+  if constexpr (!t4_pair_ok<LA, AK, LB, BKM>()) {
+    return hipSuccess;
+  } else {
+    if (!la.dma_ok() || !lb.dma_ok()) return hipSuccess;
+    if constexpr (std::is_same<LB, ConvWgradB>::value) {
+      // the gather's running pixel wraps into the next image at most once
+      // per 32-pixel step
+      if (lb.g.OH * lb.g.OW < T4_BK) return hipSuccess;
+    }
+    const int opt = t4_pick<LA, AK, LB, BKM>(M, N);
+    if (!opt) return hipSuccess;
+    const int pr = (opt == 2 || opt == 4) ? 192 : 256;
+    const long long t4t = (opt <= 2)
+        ? (long long)((M + pr - 1) / pr) * ((N + T4_QR - 1) / T4_QR)
+        : (long long)((N + pr - 1) / pr) * ((M + T4_QR - 1) / T4_QR);
+    int sp = splits, ks = k_split;
+    // (split-K through workspace slices keeps the caller's split: the
+    // finishing pass sums exactly `splits` slices)
+    if (splits > 1 && !epi.slice) {
+      const long long want = ((long long)tiles * splits + t4t - 1) / t4t;
+      ks = (int)((K + want - 1) / want);
+      ks = (ks + T4_BK - 1) / T4_BK * T4_BK;
+      sp = (K + ks - 1) / ks;
+    }
+    *taken = true;
+    if constexpr (AK && BKM) {
+      if (opt == 1)
+        return go_t4<LA, true, LB, true, 256, false>(la, lb, epi, M, N, K, ks,
+                                                     sp, groups, s);
+      return go_t4<LB, true, LA, true, 192, true>(lb, la, epi, N, M, K, ks,
+                                                  sp, groups, s);
+    } else {
+      if (opt == 3)
+        return go_t4<LB, false, LA, false, 256, true>(lb, la, epi, N, M, K,
+                                                      ks, sp, groups, s);
+      return go_t4<LA, false, LB, false, 192, false>(la, lb, epi, M, N, K, ks,
+                                                     sp, groups, s);
+    }
+  }
+}

@@ -38,21 +38,48 @@ any such unit in a segment keeps that segment eager.  A capture that fails
 (an op that synchronises, an unsupported call) re-runs the pass eagerly and
 pins that key to eager mode; host state that the discarded capture
 advanced (the parameter store's step counters, the fp8 history step) is
-restored first (``state_hooks``).  Multi-rank workflows capture the forward
-segment only (it issues no collective), so N = 1 and N > 1 run the same
-forward; their backward stays eager (the bucketed RCCL all-reduces are
-launched from the GD units as gradients become ready), as does any backward
-with gradient accumulation (``graph_safe`` of the parameter store).  Disable
-with ``root.common.engine.graphs = False`` or ``VELES_AMD_GRAPHS=0``.
+restored first (``state_hooks``).  Multi-rank workflows over RCCL capture
+the backward too, collectives included: the bucketed all-reduces are
+enqueued by the GD units in the same order at every rank and RCCL
+collectives are stream-capturable, so the graph holds the compute stream's
+kernels, each bucket's all-reduce on the process group's stream (forked
+from and joined back into the capture by events) and the per-bucket updates
+on the update stream - N = 1 and N > 1 replay the same kind of step.  A
+backward whose collectives block the host (gloo) or that accumulates
+gradients over micro-steps stays eager (``graph_safe`` of the parameter
+store); ``root.common.engine.dp.graph_backward = False`` (or
+``VELES_AMD_DP_GRAPH_BACKWARD=0``) keeps the multi-rank backward eager.
+:func:`suspended` runs passes eagerly for a while (per-bucket timing events
+of the instrumented steps cannot be captured).  Disable graphs with
+``root.common.engine.graphs = False`` or ``VELES_AMD_GRAPHS=0``.
 """
 from __future__ import annotations
 
 import logging
 import os
 
-__all__ = ["GraphSegment", "graphs_enabled", "install_step_graphs"]
+__all__ = ["GraphSegment", "graphs_enabled", "install_step_graphs",
+           "suspended"]
 
 _log = logging.getLogger("graphs")
+
+# > 0 while ``suspended()`` is active: every segment runs its passes eagerly
+_suspend = 0
+
+
+class suspended(object):
+    """Context manager: segments run eagerly inside it (their graphs are
+    kept and replayed again afterwards)."""
+
+    def __enter__(self):
+        global _suspend
+        _suspend += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _suspend
+        _suspend -= 1
+        return False
 
 # the GraphSegment whose capture is in progress (at most one: segments run
 # on the main thread, one after the other).  A unit outside it that runs
@@ -270,7 +297,7 @@ class GraphSegment(object):
             self._abort_capture()
         self.mode = "eager"
         self.pos = 0
-        if not self.safe:
+        if not self.safe or _suspend:
             return
         key = self.key_fn()
         if key is None or key in self.eager_keys:
@@ -432,11 +459,6 @@ def install_step_graphs(wf, warmup=2):
     if not graphs_enabled() or dev is None or not getattr(dev, "is_gpu",
                                                           False):
         return []
-    # multi-rank: the forward is captured as at N = 1; the backward stays
-    # eager (its GD units launch the bucketed all-reduces as they go)
-    from veles_amd.parallel import find_dp
-    dp = find_dp(wf)
-    multi = dp is not None and getattr(dp, "multi", dp.world_size > 1)
     ld = wf.loader
     ev = getattr(wf, "evaluator", None)
     fwd_units = list(wf.forwards) + ([ev] if ev is not None else [])
@@ -459,7 +481,7 @@ def install_step_graphs(wf, warmup=2):
                                  warmup=warmup))
     gds = [g for g in reversed(getattr(wf, "gds", []) or []) if g is not None]
     store = getattr(wf, "param_store_", None)
-    if gds and store is not None and _is_chain(gds) and not multi:
+    if gds and store is not None and _is_chain(gds):
         def bkey():
             if not store.graph_safe():
                 return None

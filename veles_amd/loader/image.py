@@ -237,6 +237,26 @@ class _ImageMixin(object):
         a = numpy.asarray(sample_idx, numpy.int64)
         return a // infl, a % infl
 
+    def _rank_params(self, start_offset, count, slot_bbox):
+        """Augmentation parameters of this rank's ``count`` samples from
+        ``start_offset``: drawn for the whole GLOBAL minibatch and sliced,
+        so every rank draws the same sequence from the workflow PRNG and N
+        ranks augment exactly as one process over the global minibatch.
+        ``slot_bbox(sample) -> (distortion slot, bbox)``."""
+        gsize = int(getattr(self, "global_minibatch_size", 0) or 0)
+        b = 0
+        if gsize > count:
+            b, _ = self.shard_bounds(gsize)
+        else:
+            gsize = count
+        g0 = start_offset - b
+        samples = self.shuffled_indices.mem[g0:g0 + gsize]
+        sb = [slot_bbox(int(v)) for v in samples]
+        H, W = self.canvas_shape[:2]
+        p = self.augment.params((H, W), [x[0] for x in sb], self.prng,
+                                [x[1] for x in sb])
+        return p[b:b + count]
+
 
 # ------------------------------------------------------------- full batch
 class _FullBatchImages(_ImageMixin, FullBatchLoader):
@@ -362,9 +382,12 @@ class _FullBatchImages(_ImageMixin, FullBatchLoader):
         params[:, 2] = 1.0
         if count:
             H, W = self.canvas_shape[:2]
-            bboxes = [self.get_image_bbox(int(i), (H, W)) for i in img]
-            params[:count] = self.augment.params((H, W), slot, self.prng,
-                                                 bboxes)
+
+            def slot_bbox(sample):
+                im, sl = self._split_sample([sample])
+                return int(sl[0]), self.get_image_bbox(int(im[0]), (H, W))
+            params[:count] = self._rank_params(start_offset, count,
+                                               slot_bbox)
         tdev = self.minibatch_data.devmem.device
         to = (lambda a: torch.from_numpy(a).to(tdev, non_blocking=True)
               if tdev.type != "cpu" else torch.from_numpy(a))
@@ -686,10 +709,12 @@ class ImageLoader(_ImageMixin, Loader):
         params[:, 2] = 1.0
         if count:
             H, W = self.canvas_shape[:2]
-            kk = [self._key_of(s) for s in samples]
-            params[:count] = self.augment.params(
-                (H, W), [k[1] for k in kk], self.prng,
-                [self.get_image_bbox(k[0], (H, W)) for k in kk])
+
+            def slot_bbox(sample):
+                key, sl = self._key_of(sample)
+                return sl, self.get_image_bbox(key, (H, W))
+            params[:count] = self._rank_params(start_offset, count,
+                                               slot_bbox)
         to = (lambda a: torch.from_numpy(a).pin_memory().to(
             tdev, non_blocking=True) if st.gpu else torch.from_numpy(a))
         self._image_batch(st.dev[slot], to(canv), to(params),

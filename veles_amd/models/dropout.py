@@ -2,7 +2,12 @@
 (``hvk_dropout``).  The forward unit draws a fresh 32-bit seed per minibatch;
 the backward unit re-applies the same mask to err_output from that seed -
 no mask tensor is stored.  Identity when the workflow is testing or for
-non-TRAIN minibatches (``forward_mode``)."""
+non-TRAIN minibatches (``forward_mode``).
+
+Data parallel: the mask of element i of a rank's shard is drawn at index
+rank x (shard elements) + i, so N ranks draw exactly the masks one process
+draws over the global minibatch (the seed sequence is the same at every
+rank: seeded from the unit's reproducible generator)."""
 from __future__ import annotations
 
 from veles_amd.accelerated_units import AcceleratedUnit
@@ -69,10 +74,18 @@ class DropoutForward(AcceleratedUnit):
                 self.seed_dev_ = sd = torch.tensor(
                     [self.seed], dtype=torch.int32, device=x.device)
             ops.seed_advance(sd)
-            ops.dropout(x, self.dropout_ratio, None, out=y, seed_dev=sd)
+            ops.dropout(x, self.dropout_ratio, None, out=y, seed_dev=sd,
+                        base=self.index_base(x))
             return
         self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
-        ops.dropout(x, self.dropout_ratio, self.seed, out=y)
+        ops.dropout(x, self.dropout_ratio, self.seed, out=y,
+                    base=self.index_base(x))
+
+    def index_base(self, x):
+        """Mask index of this rank's first element (see the module doc)."""
+        ld = getattr(self.workflow, "loader", None)
+        rank = int(getattr(ld, "rank", 0) or 0) if ld is not None else 0
+        return rank * x.numel()
 
     def init_unpickled(self):
         super().init_unpickled()
@@ -95,7 +108,8 @@ class DropoutBackward(GradientDescentBase):
             ei = self.alloc_err_input(tuple(err.shape))
             out = ops.dropout(err, fwd.dropout_ratio, fwd.seed, out=ei,
                               seed_dev=getattr(fwd, "seed_dev_", None)
-                              if err.is_cuda else None)
+                              if err.is_cuda else None,
+                              base=fwd.index_base(err))
         aux, aux_act = self.aux_tensor()
         if aux is not None:
             ei = self.alloc_err_input(tuple(err.shape))

@@ -110,6 +110,14 @@ class ParameterStore(object):
         # collectives / per-bucket updates, per step
         self.comm_stats = os.environ.get("VELES_AMD_DP_STATS", "0") == "1"
         self._comm_events = []
+        # per-bucket timeline of the same instrumented steps: [(t0, [(launch,
+        # reduced)] per bucket, end)] events; t0 = the first GD unit's
+        # gradients enqueued, launch = the compute stream reaching bucket i's
+        # all-reduce, reduced = that all-reduce done (seen from the stream
+        # that consumes it), end = the compute stream's join before the next
+        # forward.  Eager passes only (graphs.suspended()).
+        self._tl = None
+        self._timelines = []
 
     # -- registration -------------------------------------------------------
     def register(self, owner, name, host):
@@ -183,6 +191,10 @@ class ParameterStore(object):
             if tail:
                 self.zero_tail = min(tail)
         self.finalized = True
+        if self.device is not None and getattr(self.device, "fp8", False) \
+                and self._multi() and self._amax_sync():
+            from veles_amd.ops import fp8
+            fp8.registry(self.device.torch_device).dp = self.dp
         for p in order:
             if hasattr(p.owner, "on_params_finalized"):
                 p.owner.on_params_finalized()
@@ -252,8 +264,24 @@ class ParameterStore(object):
         return self.grad[lo:hi]
 
     # -- step ---------------------------------------------------------------
+    def _timing(self):
+        """Per-bucket events for this pass (stats mode, eager, GPU)."""
+        if not (self.comm_stats and self._multi() and self.master is not None
+                and self.master.is_cuda):
+            return False
+        import torch
+        return not torch.cuda.is_current_stream_capturing()
+
+    def _event(self, stream=None):
+        import torch
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        return ev
+
     def grads_ready(self, params):
         """Called by a GD unit once its gradients are enqueued."""
+        if not self._ready and self._timing():
+            self._tl = (self._event(), {}, {})
         for p in params:
             self._ready.add(id(p))
         if not self._multi():
@@ -274,6 +302,8 @@ class ParameterStore(object):
 
     def _launch_bucket(self, i):
         self._launched.add(i)
+        if self._tl is not None:
+            self._tl[1][i] = self._event()
         view = self.bucket_view(i)
         if self.grad_dtype == "bfloat16":
             import torch
@@ -303,6 +333,34 @@ class ParameterStore(object):
         """[(MB, parameter count)] per all-reduce bucket, launch order."""
         return [(round(self.bucket_view(i).numel() * 4 / (1 << 20), 3),
                  len(b)) for i, b in enumerate(self.buckets)]
+
+    def timeline_report(self, reset=True):
+        """Per-bucket timeline of the instrumented steps since the last
+        report (ms from the first gradient enqueued, mean over steps):
+        [{"bucket", "mb", "launch_ms", "reduced_ms"}], plus the compute
+        stream's end and the wait exposed after it.  Synchronises."""
+        tls = self._timelines
+        if reset:
+            self._timelines = []
+        tls = [t for t in tls if len(t[1]) == len(self.buckets)]
+        if not tls:
+            return None
+        tls[-1][3].synchronize()
+        out = []
+        for i in range(len(self.buckets)):
+            la = [t[0].elapsed_time(t[1][i]) for t in tls]
+            rd = [t[0].elapsed_time(t[2][i]) for t in tls if i in t[2]]
+            out.append({"bucket": i,
+                        "mb": round(self.bucket_view(i).numel() * 4 / 2 ** 20,
+                                    2),
+                        "launch_ms": round(sum(la) / len(la), 4),
+                        "reduced_ms": round(sum(rd) / len(rd), 4)
+                        if rd else None})
+        end = [t[0].elapsed_time(t[3]) for t in tls]
+        last = max((b["launch_ms"] for b in out), default=0.0)
+        return {"steps": len(tls), "buckets": out,
+                "backward_enqueued_ms": round(last, 4),
+                "step_join_ms": round(sum(end) / len(end), 4)}
 
     def comm_report(self, reset=True):
         """Mean exposed all-reduce wait (ms per step) of the compute stream
@@ -422,6 +480,8 @@ class ParameterStore(object):
         with torch.cuda.stream(self._upd_stream):
             if work is not None:
                 work.wait()
+                if self._tl is not None:
+                    self._tl[2][i] = self._event(self._upd_stream)
                 self._finish_bucket(i)
             if segs:
                 ops.sgd_update(*args, **kw)
@@ -480,9 +540,10 @@ class ParameterStore(object):
                 torch.cuda.current_stream(self.master.device).wait_stream(
                     self._upd_stream)
         elif self._multi():
+            import torch
             ev = None
-            if self.comm_stats and self.master.is_cuda:
-                import torch
+            if self.comm_stats and self.master.is_cuda and \
+                    not torch.cuda.is_current_stream_capturing():
                 ev = (torch.cuda.Event(enable_timing=True),
                       torch.cuda.Event(enable_timing=True))
                 ev[0].record()
@@ -494,6 +555,10 @@ class ParameterStore(object):
             if not overlapped:
                 for w in self._works:
                     w.wait()
+                if self._tl is not None:
+                    done = self._event()
+                    for i in range(len(self.buckets)):
+                        self._tl[2].setdefault(i, done)
                 for i in list(self._pending):
                     self._finish_bucket(i)
             elif self._upd_stream is not None:
@@ -502,10 +567,14 @@ class ParameterStore(object):
                 import torch
                 torch.cuda.current_stream(self.master.device).wait_stream(
                     self._upd_stream)
-            if ev is not None:
+            if ev is not None and not torch.cuda.is_current_stream_capturing():
                 ev[1].record()
                 self._comm_events.append(ev)
                 del self._comm_events[:-256]
+            if self._tl is not None:
+                self._timelines.append(self._tl + (self._event(),))
+                del self._timelines[:-64]
+                self._tl = None
         segs = [] if overlapped else self._cached_segments()
         if segs and self._seg_table is None:
             self._seg_table = ops.SegmentTable(self.master.device)
@@ -537,12 +606,19 @@ class ParameterStore(object):
         self._accum_count = 0
         self.steps += 1
         if self.device is not None and getattr(self.device, "fp8", False):
-            # fp8 delayed scaling: this step's amaxes enter the history
+            # fp8 delayed scaling: this step's amaxes enter the history (the
+            # GLOBAL batch's amaxes at N > 1: ``engine.dp.fp8_amax_sync``)
             from veles_amd.ops import fp8
-            fp8.registry(self.device.torch_device).roll()
+            fp8.registry(self.device.torch_device).roll(
+                dp=self.dp if self._multi() and self._amax_sync() else None)
         for hook in self.post_update_hooks:
             hook()
         return True
+
+    def _amax_sync(self):
+        from veles_amd.utils.config import root, get
+        return os.environ.get("VELES_AMD_DP_FP8_AMAX_SYNC", "1" if get(
+            root.common.engine.dp.fp8_amax_sync, True) else "0") != "0"
 
     def _zero_arg(self):
         # everything (accumulating GDs) or the split-K tail (overwrite mode)
@@ -551,9 +627,18 @@ class ParameterStore(object):
     # -- HIP-graph replay support (veles_amd/graphs.py) ----------------------
     def graph_safe(self):
         """A captured backward may contain the update only when one step is
-        one launch sequence: no gradient accumulation over micro-steps and
-        no collectives (multi-rank steps run eagerly)."""
-        return self.accumulate == 1 and not self._multi()
+        one launch sequence: no gradient accumulation over micro-steps, and
+        collectives only if they are stream-ordered (RCCL; gloo's block the
+        host) and multi-rank capture is not turned off
+        (``engine.dp.graph_backward``)."""
+        if self.accumulate != 1:
+            return False
+        if not self._multi():
+            return True
+        from veles_amd.utils.config import root, get
+        on = os.environ.get("VELES_AMD_DP_GRAPH_BACKWARD", "1" if get(
+            root.common.engine.dp.graph_backward, True) else "0") != "0"
+        return on and not getattr(self.dp, "host_blocking_wait", True)
 
     def _multi(self):
         """Gradients go through collectives (``DataParallel.multi``)."""

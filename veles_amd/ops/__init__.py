@@ -1706,32 +1706,40 @@ def _hash32(i, seed):
     return x
 
 
-def dropout_mask_ref(n, seed, p):
-    i = torch.arange(n, dtype=torch.int64)
+def dropout_mask_ref(n, seed, p, base=0):
+    i = (torch.arange(n, dtype=torch.int64) + int(base)) & 0xFFFFFFFF
     h = _hash32(i, int(seed) & 0xFFFFFFFF)
     thresh = min(0xFFFFFFFF, int(p * 4294967296.0))
     return h >= thresh
 
 
-def dropout(x, p, seed, out=None, seed_dev=None):
+def dropout(x, p, seed, out=None, seed_dev=None, base=0):
     """y = x * keep / (1-p) with a counter-based mask (same seed -> same mask:
     the backward pass calls this on dy).  ``seed_dev``: a 1-element int32
     device tensor holding the seed instead (graph-safe, see
-    :func:`seed_advance`); ``seed`` is then ignored."""
+    :func:`seed_advance`); ``seed`` is then ignored.  ``base``: mask index
+    of element 0 (a data-parallel rank's offset in the global minibatch)."""
     if out is None:
         out = torch.empty_like(x)
     if seed_dev is not None and not _gpu(x):
         seed = int(seed_dev.reshape(-1)[0]) & 0xFFFFFFFF
     if _gpu(x):
         if seed_dev is not None:
+            if base:
+                _lib_call("hvk_dropout_dev_at", _p(x), DT[x.dtype], _p(out),
+                          DT[out.dtype], x.numel(), _p(seed_dev), float(p),
+                          int(base), _s(x))
+                return out
             _lib_call("hvk_dropout_dev", _p(x), DT[x.dtype], _p(out),
                       DT[out.dtype], x.numel(), _p(seed_dev), float(p), None,
                       _s(x))
             return out
+        if base:
+            raise ValueError("dropout: base needs the device seed path")
         _lib_call("hvk_dropout", _p(x), DT[x.dtype], _p(out), DT[out.dtype],
                   x.numel(), int(seed) & 0xFFFFFFFF, float(p), None, _s(x))
         return out
-    keep = dropout_mask_ref(x.numel(), seed, p).view(x.shape)
+    keep = dropout_mask_ref(x.numel(), seed, p, base).view(x.shape)
     scale = 1.0 / (1.0 - p) if p < 1 else 0.0
     out.copy_((x.float() * keep * scale).to(out.dtype))
     return out

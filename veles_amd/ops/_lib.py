@@ -61,6 +61,7 @@ _SIGS = {
     "hvk_act_bwd": [P, I, P, I, P, I, L, I, P],
     "hvk_dropout": [P, I, P, I, L, U, F, P, P],
     "hvk_dropout_dev": [P, I, P, I, L, P, F, P, P],
+    "hvk_dropout_dev_at": [P, I, P, I, L, P, F, L, P],
     "hvk_seed_advance": [P, P],
     "hvk_trace_marker": [I, P],
     "hvk_xact": [P, I, P, I, P, I, L, I, F, L, I, P],

@@ -62,6 +62,9 @@ class _Registry(object):
         self.used = 0
         self.step = 0
         self.step_dev = None  # device mirror of ``step`` (GPU roll)
+        # multi-rank DataParallel whose ranks share the amaxes (set by the
+        # parameter store with engine.dp.fp8_amax_sync): primes are reduced
+        self.dp = None
 
     def allocate(self):
         """(state row [HIST + 1], shard row [1024]) of a new scaler."""
@@ -77,11 +80,26 @@ class _Registry(object):
         return (self.blocks[i // _CHUNK][i % _CHUNK],
                 self.shard_blocks[i // _CHUNK][i % _CHUNK])
 
-    def roll(self):
+    def roll(self, dp=None):
         """End of step: current amax -> history slot; current = 0.  On the
         GPU the slot index comes from a device step counter advanced in the
         same stream, so a captured HIP graph of the step rolls correctly on
-        every replay."""
+        every replay.
+
+        ``dp`` (a multi-rank DataParallel): the current amaxes are first
+        all-reduced with MAX over the ranks, so every rank scales with the
+        amax of the GLOBAL minibatch - the scales, and so the quantisation,
+        of a 1-rank run over the same global batch (one small stream-ordered
+        collective per step: the scalers' state and shard rows)."""
+        if dp is not None and getattr(dp, "multi", False):
+            import torch.distributed as dist
+            for bi, blk in enumerate(self.blocks):
+                count = min(_CHUNK, self.used - bi * _CHUNK)
+                if count <= 0:
+                    break
+                dist.all_reduce(blk[:count], op=dist.ReduceOp.MAX)
+                dist.all_reduce(self.shard_blocks[bi][:count],
+                                op=dist.ReduceOp.MAX)
         idx = self.step % HIST
         gpu_step = None
         for bi, blk in enumerate(self.blocks):
@@ -162,6 +180,11 @@ class Scaler(object):
         else:
             st[:HIST] = x.float().abs().max()
             st[HIST] = 0
+        dp = self.registry.dp
+        if dp is not None and getattr(dp, "multi", False):
+            # the first scale of every rank from the GLOBAL batch's amax
+            import torch.distributed as dist
+            dist.all_reduce(st, op=dist.ReduceOp.MAX)
 
 
 def quantize(x, scaler, out=None, record=True):
