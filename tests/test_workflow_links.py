@@ -194,3 +194,51 @@ def test_image_saver_keeps_only_misclassified(tmp_path):
     assert files == ["0_as_2.1.png", "0_as_4.3.png", "0_as_5.4.png"]
     from PIL import Image
     assert Image.open(tmp_path / "validation" / files[0]).size == (28, 28)
+
+
+def test_avatar_snapshots_host_state():
+    """Avatar (reference veles/avatar.py:38-73): non-Array attributes are
+    snapshots taken when the avatar runs - the producer can advance (its
+    flags, offsets, lists, dicts, arrays) without the avatar's copy, or the
+    identity of the objects consumers hold, changing."""
+    from veles_amd.avatar import Avatar
+    from veles_amd.dummy import DummyWorkflow
+    from veles_amd.memory import Array
+    from veles_amd.mutable import Bool
+    from veles_amd.units import TrivialUnit
+
+    wf = DummyWorkflow()
+    src = TrivialUnit(wf)
+    src.flag = Bool(False)
+    src.offset = 10
+    src.lengths = [1, 2, 3]
+    src.table = {"a": 1}
+    src.hist = numpy.arange(4, dtype=numpy.float32)
+    src.data = Array(numpy.arange(6, dtype=numpy.float32))
+    dev = Device(backend="cpu")
+    src.data.initialize(dev)
+    av = Avatar(wf)
+    av.clone(src, "flag", "offset", "lengths", "table", "hist", "data")
+    av.initialize(device=dev)
+    held = (av.flag, av.lengths, av.table, av.hist)
+    av.run()
+    assert not av.flag and av.offset == 10 and av.lengths == [1, 2, 3]
+    assert av.flag is not src.flag and av.lengths is not src.lengths
+    # the producer runs ahead
+    src.flag <<= True
+    src.offset = 11
+    src.lengths.append(4)
+    src.table["b"] = 2
+    src.hist += 1
+    src.data.map_write()
+    src.data.mem[:] = -1
+    assert not av.flag and av.offset == 10 and av.lengths == [1, 2, 3]
+    assert av.table == {"a": 1} and av.hist[0] == 0
+    assert float(av.data.devmem[1]) == 1.0
+    # the next run takes the new snapshot into the SAME objects
+    av.run()
+    assert av.flag and av.offset == 11 and av.lengths == [1, 2, 3, 4]
+    assert av.table == {"a": 1, "b": 2} and av.hist[0] == 1
+    assert float(av.data.devmem[1]) == -1.0
+    assert all(a is b for a, b in zip(held, (av.flag, av.lengths, av.table,
+                                             av.hist)))
