@@ -1255,13 +1255,13 @@ template <class LA, bool AK, class LB, bool BKM, bool BUF>
 hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles_n, int tiles, int splits,
                      int bn, dim3 grid, hipStream_t s) {
-  // implicit-GEMM convolutions: 256 x 128 tiles, two workgroups per CU
+  // implicit-GEMM convolutions: 192 x 128 tiles, two workgroups per CU
   // (gemm_t4.h)
   if constexpr (BUF && t4_pair_ok<LA, AK, LB, BKM>()) {
     const int groups = (int)(grid.x / ((unsigned)tiles * splits));
     bool taken = false;
     const hipError_t r = t4_launch<LA, AK, LB, BKM>(
-        la, lb, epi, M, N, K, k_split, tiles, splits, groups, s, &taken);
+        la, lb, epi, M, N, K, k_split, tiles, splits, groups, bn, s, &taken);
     if (taken) return r;
   }
   // large dense NT / NN GEMMs: the ping-pong 256 x 128 loop (gemm_pp.h)

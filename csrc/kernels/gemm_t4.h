@@ -1,58 +1,72 @@
-// gemm_t4.h - 256 x 128 (or 192 x 128) tiles at TWO workgroups per CU for
-// the implicit-GEMM convolutions.  Included by gemm_core.h inside its
-// anonymous namespace, after gemm_pp.h.
+// gemm_t4.h - 192 x 128 tiles at TWO workgroups per CU for the
+// implicit-GEMM convolutions.  Included by gemm_core.h inside its anonymous
+// namespace, after gemm_pp.h.
 //
-// Why: the convolutions' GEMMs are short along K (AlexNet: 36-75 K tiles of
-// 32) and narrow (128-384 output channels per group).  The 128 x 128 loop of
+// Why: the convolutions' GEMMs are short along K (AlexNet: 19-36 K tiles of
+// 64) and narrow (128-384 output channels per group).  The 128 x 128 loop of
 // gemm_kernel (8 waves of 64 x 32) moves 0.0156 operand bytes per FLOP and
 // pays two barriers and four LDS-DMA pieces per 16 MFMAs of each wave: it is
 // bound by DMA issue and synchronisation (profiles/r3_experiments.md §10).
 // The one-workgroup-per-CU ping-pong loops (gemm_pp.h) move fewer bytes but
 // cannot hide a tile's prologue and epilogue (§12, §13).  This loop keeps
-// two independent workgroups per CU and gives each wave the 128 x 64 tile of
-// the 256 x 256 ping-pong loop:
+// two independent workgroups per CU and gives each wave a 96 x 64 tile:
 //
-//   * 4 waves (one per SIMD) per workgroup, 2 x 2, each PR/2 x 64 (8 x 4 or
-//     6 x 4 accumulators of MFMA 16x16x32); the other workgroup on the CU
-//     supplies the second wave per SIMD, so one workgroup's barrier waits,
-//     prologue and epilogue run under the other one's MFMAs;
-//   * BK = 32, 3-stage LDS ring of (PR + 128) x 32 bf16 (24 KiB at PR = 256,
-//     72 KiB per workgroup): tile t + 2 is issued at the top of step t,
-//     tile t + 1 is retired by one counted vmcnt at its end, ONE s_barrier
-//     per K step (32 MFMAs per wave);
-//   * 0.0117 operand bytes per FLOP (256 x 128), 12 fragment reads per 32
-//     MFMAs.
+//   * 4 waves (one per SIMD) per workgroup, 2 x 2, each 96 x 64 (6 x 4
+//     accumulators of MFMA 16x16x32); the other workgroup on the CU supplies
+//     the second wave per SIMD, so one workgroup's barrier waits, prologue
+//     and epilogue run under the other one's MFMAs;
+//   * BK = 64, two LDS stages of (192 + 128) x 64 bf16 = 40 KiB: the two
+//     workgroups take the whole 160 KiB.  Step t + 1 is issued at the top of
+//     step t and retired at its end, ONE s_barrier per K step (48 MFMAs per
+//     wave, 10 LDS-DMA pieces, 20 fragment reads);
+//   * 0.013 operand bytes per FLOP (0.0156 for 128 x 128), and every K-major
+//     DMA piece reads whole 128-B lines (8 rows x 64 k).
+//
+// Measured first with BK = 32 / 256 x 128 / three 24-KiB stages
+// (profiles/r4/ab_t4_256x128_bk32_vs_128row.log): a 32-deep K-major step reads
+// half of each 128-B line per row, so the L2 serves twice the requests per
+// byte, and the convolutions gained at most 6 % (conv3 forward) - rejected.
+// The BK template parameter keeps that configuration for A/B builds.
 //
 // Operand images (lane-linear LDS-DMA from pre-permuted source offsets, as
 // in gemm_kernel):
-//   K-major [rows][32 k], 64-B rows; 16-B chunk c of row r at c ^ t4_sw(r),
-//     t4_sw(r) = {0, 2, 3, 1}[(r >> 2) & 3]: the 16 lanes of each
-//     ds_read_b128 lane group hit 16 different 16-B bank slots;
-//   MN-major [32 k][IMG cols] (IMG = 128 or 256; a 192-row operand keeps a
-//     256-wide image whose upper columns read zeros), 32-B block b of k-row
-//     k at b ^ hk(k), read by ds_read_b64_tr_b16 (gemm_kernel's image with a
-//     wider row).
+//   K-major [rows][64 k], 128-B rows, 16-B chunk c of row r at c ^ (r & 7)
+//     (BK 32: [rows][32 k], chunk c at c ^ t4_sw(r));
+//   MN-major [64 k][IMG cols] (IMG = 128, 192), 32-B block b of k-row k at
+//     b ^ t4_mnsw(k), read by ds_read_b64_tr_b16.
 // The MFMA accumulation order over K is the 128-row loop's (k ascending in
 // steps of 32): results are bit-identical to gemm_kernel.
 //
-// Orientation: the PR-row operand P and the 128-row operand Q are either
+// Orientation: the 192-row operand P and the 128-row operand Q are either
 // (A, B) - C[P][Q] - or (B, A) with TRANS - C[Q][P]; the epilogue stages the
-// f32 tile through the drained ring in two passes of PR/2 rows of P,
+// f32 tile through the drained ring in two passes of 96 rows of P,
 // transposed for TRANS, so stores (and split-K atomics) always run along
 // C's contiguous dimension.
 
-constexpr int T4_BK = 32, T4_NST = 3, T4_QR = 128;
+constexpr int T4_QR = 128;
 
 __device__ __forceinline__ int t4_sw(int r) {
   return (0x78 >> (2 * ((r >> 2) & 3))) & 3;
 }
+// MN-major images: XOR mask of k-row k's 32-B blocks.  Pitch 256 / 512 B
+// (128 / 256 columns): hk(k), 8 distinct slots for the k-rows {0..3, 8..11}
+// a ds_read_b64_tr_b16 lane group reads; pitch 384 B (192 columns): rows
+// alternate between two bank halves, the 2-bit mask (XOR inside a group of
+// four blocks, so a block never leaves its row) separates the four rows of
+// each half
+template <int IMG>
+__device__ __forceinline__ int t4_mnsw(int k) {
+  if constexpr (IMG == 192) return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);
+  else return hk(k);
+}
 
-// One operand's DMA slots (ROWS = rows of the operand the tile computes)
-template <class L, bool KM, int ROWS>
+// One operand's DMA slots (ROWS = rows of the operand the tile computes,
+// BKT = K step: 32 (three stages) or 64 (two stages))
+template <class L, bool KM, int ROWS, int BKT>
 struct T4Op {
-  static constexpr int IMG = (KM || ROWS != 192) ? ROWS : 256;
-  static constexpr int NP = IMG / 16;   // 1-KiB pieces per stage
-  static constexpr int NS = NP / 4;     // per wave
+  static constexpr int IMG = ROWS;
+  static constexpr int NP = IMG * BKT / 512;   // 1-KiB pieces per stage
+  static constexpr int NS = NP / 4;            // per wave
   static_assert(NS * 4 == NP, "pieces divide over the four waves");
   static constexpr bool FAST = L::kFast;
   static constexpr bool BUF = L::kBuf;
@@ -67,24 +81,27 @@ struct T4Op {
                                        int lane) {
     if constexpr (BUF) rs = dma_rsrc(l.dbase());
     if constexpr (KM) {
-      kc = 8 * ((lane & 3) ^ t4_sw(lane >> 2));
+      // BKT 32: a piece is 16 rows x 64 B, lane L -> row L >> 2, chunk L & 3;
+      // BKT 64: 8 rows x 128 B (whole cache lines), row L >> 3, chunk L & 7
+      constexpr int RPP = 64 / (BKT / 8);
+      constexpr int CPRW = BKT / 8;
+      kc = BKT == 32 ? 8 * ((lane & 3) ^ t4_sw(lane >> 2))
+                     : 8 * ((lane & 7) ^ ((lane >> 3) & 7));
 #pragma unroll
       for (int i = 0; i < NS; ++i) {
-        const int row = r0 + 16 * (w * NS + i) + (lane >> 2);
+        const int row = r0 + RPP * (w * NS + i) + lane / CPRW;
         if constexpr (FAST) fa[i] = l.drow(row);
         else v[i] = l.row_voff(row);
       }
     } else {
-      constexpr int CPR = IMG / 8, RPP = 64 / CPR;
 #pragma unroll
       for (int i = 0; i < NS; ++i) {
-        const int I = w * NS + i;
-        kr[i] = RPP * I + lane / CPR;
-        const int pc = lane % CPR;
-        const int c = 16 * ((pc >> 1) ^ hk(kr[i])) + 8 * (pc & 1);
-        const bool cok = c < ROWS;
-        if constexpr (FAST) fb[i] = l.dcol(r0 + c, kbeg + kr[i], !cok);
-        else v[i] = cok ? l.col_voff(r0 + c, kr[i]) : kBufOOB;
+        const int off = (w * NS + i) * 1024 + 16 * lane;   // image byte
+        kr[i] = off / (IMG * 2);
+        const int pc = (off - kr[i] * IMG * 2) >> 4;        // 16-B chunk
+        const int c = 16 * ((pc >> 1) ^ t4_mnsw<IMG>(kr[i])) + 8 * (pc & 1);
+        if constexpr (FAST) fb[i] = l.dcol(r0 + c, kbeg + kr[i], false);
+        else v[i] = l.col_voff(r0 + c, kr[i]);
       }
     }
   }
@@ -110,7 +127,7 @@ struct T4Op {
             (const void*)l.dsrc(fb[i]),
             (__attribute__((address_space(3))) void*)(s + (w * NS + i) * 512),
             16, 0, 0);
-        l.dnext_by(fb[i], T4_BK);
+        l.dnext_by(fb[i], BKT);
       }
     } else {
       const uint32_t kadv = (uint32_t)k0 * (uint32_t)l.ld * 2u;
@@ -122,19 +139,25 @@ struct T4Op {
   }
 };
 
-// fragment of the 16-row MFMA tile at `row` (16-row aligned)
-template <bool KM, int IMG>
-__device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int fr,
-                                          int fq) {
+// fragment of the 16-row MFMA tile at `row` (16-row aligned), 32-deep k
+// half ks of the stage
+template <bool KM, int IMG, int BKT>
+__device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int ks,
+                                          int fr, int fq) {
   if constexpr (KM) {
     const int r = row + fr;
-    return *(const bf16x8*)(s + r * 32 + ((fq ^ t4_sw(r)) << 3));
+    if constexpr (BKT == 32)
+      return *(const bf16x8*)(s + r * 32 + ((fq ^ t4_sw(r)) << 3));
+    else
+      return *(const bf16x8*)(s + r * 64 + (((ks * 4 + fq) ^ (r & 7)) << 3));
   } else {
     const int b = row >> 4;
     const int trq = fr >> 2, trp = fr & 3;
-    const int k = fq * 8 + trq;
-    const uint16_t* p0 = s + k * IMG + ((b ^ hk(k)) << 4) + trp * 4;
-    const uint16_t* p1 = s + (k + 4) * IMG + ((b ^ hk(k + 4)) << 4) + trp * 4;
+    const int k = ks * 32 + fq * 8 + trq;
+    const uint16_t* p0 =
+        s + k * IMG + ((b ^ t4_mnsw<IMG>(k)) << 4) + trp * 4;
+    const uint16_t* p1 =
+        s + (k + 4) * IMG + ((b ^ t4_mnsw<IMG>(k + 4)) << 4) + trp * 4;
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
     typedef __attribute__((ext_vector_type(8))) short s16x8;
@@ -143,19 +166,21 @@ __device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int fr,
   }
 }
 
-template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS>
+template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS, int BKT>
 __global__ void __launch_bounds__(256, 2)
 gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
                int tiles_q, int tiles, int splits, int gm) {
-  using OP = T4Op<LP, PK, PR>;
-  using OQ = T4Op<LQ, QK, T4_QR>;
-  constexpr int SP = OP::IMG * T4_BK, SQ = OQ::IMG * T4_BK;
+  constexpr int NST = BKT == 32 ? 3 : 2;     // LDS ring stages
+  using OP = T4Op<LP, PK, PR, BKT>;
+  using OQ = T4Op<LQ, QK, T4_QR, BKT>;
+  constexpr int SP = OP::IMG * BKT, SQ = OQ::IMG * BKT;
   constexpr int SST = SP + SQ;
-  constexpr int RING = T4_NST * SST * 2;
+  constexpr int RING = NST * SST * 2;
   constexpr int HP = PR / 2;                 // P rows per epilogue pass
   constexpr int LDC = TRANS ? HP + 4 : T4_QR + 4;
   constexpr int EPI = (TRANS ? T4_QR : HP) * LDC * 4;
   constexpr int SMEM = RING > EPI ? RING : EPI;
+  static_assert(2 * SMEM <= 160 * 1024, "two workgroups per CU");
   constexpr int MI = PR / 32;                // m-tiles per wave
   constexpr int NSW = OP::NS + OQ::NS;       // DMA pieces per wave and step
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM / 2];
@@ -201,13 +226,13 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
   op.init(lp, p0, kbeg, w, lane);
   oq.init(lq, q0, kbeg, w, lane);
 
-  const int nk = (kend - kbeg + T4_BK - 1) / T4_BK;
-  // prologue: steps 0 and 1 in flight, wait for step 0
+  const int nk = (kend - kbeg + BKT - 1) / BKT;
+  // prologue: NST - 1 steps in flight, wait for step 0
   op.issue(lp, kbeg, smem, w);
   oq.issue(lq, kbeg, smem + SP, w);
-  if (nk > 1) {
-    op.issue(lp, kbeg + T4_BK, smem + SST, w);
-    oq.issue(lq, kbeg + T4_BK, smem + SST + SP, w);
+  if (NST == 3 && nk > 1) {
+    op.issue(lp, kbeg + BKT, smem + SST, w);
+    oq.issue(lq, kbeg + BKT, smem + SST + SP, w);
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -215,39 +240,43 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  int scur = 0, spre = 2;  // stage of step t, of step t + 2
+  int scur = 0, spre = NST - 1;  // stage of step t, of step t + NST - 1
   for (int kt = 0; kt < nk; ++kt) {
     const uint16_t* sP = smem + scur * SST;
     const uint16_t* sQ = sP + SP;
-    // step t + 2 into the stage step t - 1 used (every wave finished reading
-    // it before the barrier that ended step t - 1)
-    const bool pre = kt + 2 < nk;
+    // step t + NST - 1 into the stage step t - 1 used (every wave finished
+    // reading it before the barrier that ended step t - 1)
+    const bool pre = kt + NST - 1 < nk;
     if (pre) {
       uint16_t* d = smem + spre * SST;
-      const int k2 = kbeg + (kt + 2) * T4_BK;
+      const int k2 = kbeg + (kt + NST - 1) * BKT;
       op.issue(lp, k2, d, w);
       oq.issue(lq, k2, d + SP, w);
     }
-    bf16x8 bq[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bq[j] = t4_frag<QK, OQ::IMG>(sQ, qrow + j * 16, fr, fq);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const bf16x8 a = t4_frag<PK, OP::IMG>(sP, prow + i * 16, fr, fq);
+    for (int ks = 0; ks < BKT / 32; ++ks) {
+      bf16x8 bq[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[j],
-                                                            acc[i][j], 0, 0, 0);
+        bq[j] = t4_frag<QK, OQ::IMG, BKT>(sQ, qrow + j * 16, ks, fr, fq);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bf16x8 a = t4_frag<PK, OP::IMG, BKT>(sP, prow + i * 16, ks, fr,
+                                                   fq);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              a, bq[j], acc[i][j], 0, 0, 0);
+      }
     }
-    // retire step t + 1 (step t + 2 stays in flight), then one barrier:
-    // step t + 1 visible to every wave, every read of step t done
-    if (pre) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
+    // retire step t + 1 (three stages: step t + 2 stays in flight), then one
+    // barrier: step t + 1 visible to every wave, every read of step t done
+    if (NST == 3 && pre) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    scur = scur == 2 ? 0 : scur + 1;
-    spre = spre == 2 ? 0 : spre + 1;
+    scur = scur == NST - 1 ? 0 : scur + 1;
+    spre = spre == NST - 1 ? 0 : spre + 1;
   }
 
   // epilogue: the ring is drained (every DMA waited for, every fragment read
@@ -333,47 +362,37 @@ constexpr bool t4_pair_ok() {
     return false;
 }
 
-// orientation options (M = A rows, N = B rows): 1 P = A (256), Q = B;
-// 2 P = A (192), Q = B; 3 P = B (256), Q = A, TRANS; 4 P = B (192), Q = A,
-// TRANS.  Forward / backward-data instantiate 1 and 4, the weight gradient
-// 3 and 2.  Cost = padded MFMA work (192-row tiles x 1.03: one more
-// accumulator-to-read ratio step); 0 = not worth it (the 128-row loop).
+// orientation options (M = A rows, N = B rows), both 192 x 128 tiles at
+// BK 64: 1 P = A, Q = B; 2 P = B, Q = A, TRANS.  Cost = padded MFMA work;
+// the T4 loop is taken when its padded work is at most 1.10x that of the
+// 128-row loop (which pads to 128 x bn tiles).  hvk_gemm_variant 50 turns
+// the loop off, 51 / 52 force option 1 / 2 (A/B runs, tests).
 inline long long t4_cost(int M, int N, int opt) {
   auto up = [](long long x, long long b) { return (x + b - 1) / b * b; };
-  switch (opt) {
-    case 1: return up(M, 256) * up(N, 128) * 100;
-    case 2: return up(M, 192) * up(N, 128) * 103;
-    case 3: return up(N, 256) * up(M, 128) * 100;
-    case 4: return up(N, 192) * up(M, 128) * 103;
-  }
-  return 0;
+  return opt == 1 ? up(M, 192) * up(N, 128) : up(N, 192) * up(M, 128);
 }
 
-template <class LA, bool AK, class LB, bool BKM>
-int t4_pick(int M, int N) {
+inline int t4_pick(int M, int N, int bn) {
   if (hvk_gemm_variant == 50 || hvk_gemm_variant == 0) return 0;
-  const int o1 = (AK && BKM) ? 1 : 3, o2 = (AK && BKM) ? 4 : 2;
-  const long long c1 = t4_cost(M, N, o1), c2 = t4_cost(M, N, o2);
-  // the 128-row loop's padded work at its own tile (128 x 128 / 64)
+  if (hvk_gemm_variant == 51) return 1;
+  if (hvk_gemm_variant == 52) return 2;
+  const long long c1 = t4_cost(M, N, 1), c2 = t4_cost(M, N, 2);
   const long long base = (long long)((M + 127) / 128 * 128) *
-                         ((N + 63) / 64 * 64) * 100;
-  const int best = c1 <= c2 ? o1 : o2;
+                         ((N + bn - 1) / bn * bn);
+  const int best = c1 <= c2 ? 1 : 2;
   const long long cb = c1 <= c2 ? c1 : c2;
-  // the T4 tile must not waste much more than the 128-row loop would
-  if (cb * 100 > base * 112) return 0;
-  if (hvk_gemm_variant == 51) return o1;
-  if (hvk_gemm_variant == 52) return o2;
-  return best;
+  return cb * 100 <= base * 110 ? best : 0;
 }
 
-template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS>
+template <class LP, bool PK, class LQ, bool QK, bool TRANS>
 hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
                  int K, int k_split, int splits, int groups, hipStream_t s) {
+  constexpr int PR = 192;
   const int tiles_p = (P + PR - 1) / PR, tiles_q = (Q + T4_QR - 1) / T4_QR;
   const int tiles = tiles_p * tiles_q;
   const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS>), grid,
+  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64>), grid,
                      dim3(256), 0, s, lp, lq, epi, P, Q, K, k_split, tiles_q,
                      tiles, splits, gm);
   return launch_status(s);
@@ -385,7 +404,7 @@ hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
 template <class LA, bool AK, class LB, bool BKM>
 hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles, int splits, int groups,
-                     hipStream_t s, bool* taken) {
+                     int bn, hipStream_t s, bool* taken) {
   *taken = false;
   if constexpr (!t4_pair_ok<LA, AK, LB, BKM>()) {
     return hipSuccess;
@@ -393,37 +412,28 @@ hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
     if (!la.dma_ok() || !lb.dma_ok()) return hipSuccess;
     if constexpr (std::is_same<LB, ConvWgradB>::value) {
       // the gather's running pixel wraps into the next image at most once
-      // per 32-pixel step
-      if (lb.g.OH * lb.g.OW < T4_BK) return hipSuccess;
+      // per 64-pixel step
+      if (lb.g.OH * lb.g.OW < 64) return hipSuccess;
     }
-    const int opt = t4_pick<LA, AK, LB, BKM>(M, N);
+    const int opt = t4_pick(M, N, bn);
     if (!opt) return hipSuccess;
-    const int pr = (opt == 2 || opt == 4) ? 192 : 256;
-    const long long t4t = (opt <= 2)
-        ? (long long)((M + pr - 1) / pr) * ((N + T4_QR - 1) / T4_QR)
-        : (long long)((N + pr - 1) / pr) * ((M + T4_QR - 1) / T4_QR);
+    const long long t4t = opt == 1
+        ? (long long)((M + 191) / 192) * ((N + T4_QR - 1) / T4_QR)
+        : (long long)((N + 191) / 192) * ((M + T4_QR - 1) / T4_QR);
     int sp = splits, ks = k_split;
     // (split-K through workspace slices keeps the caller's split: the
     // finishing pass sums exactly `splits` slices)
     if (splits > 1 && !epi.slice) {
       const long long want = ((long long)tiles * splits + t4t - 1) / t4t;
       ks = (int)((K + want - 1) / want);
-      ks = (ks + T4_BK - 1) / T4_BK * T4_BK;
+      ks = (ks + 63) / 64 * 64;
       sp = (K + ks - 1) / ks;
     }
     *taken = true;
-    if constexpr (AK && BKM) {
-      if (opt == 1)
-        return go_t4<LA, true, LB, true, 256, false>(la, lb, epi, M, N, K, ks,
-                                                     sp, groups, s);
-      return go_t4<LB, true, LA, true, 192, true>(lb, la, epi, N, M, K, ks,
-                                                  sp, groups, s);
-    } else {
-      if (opt == 3)
-        return go_t4<LB, false, LA, false, 256, true>(lb, la, epi, N, M, K,
-                                                      ks, sp, groups, s);
-      return go_t4<LA, false, LB, false, 192, false>(la, lb, epi, M, N, K, ks,
-                                                     sp, groups, s);
-    }
+    if (opt == 1)
+      return go_t4<LA, AK, LB, BKM, false>(la, lb, epi, M, N, K, ks, sp,
+                                           groups, s);
+    return go_t4<LB, BKM, LA, AK, true>(lb, la, epi, N, M, K, ks, sp, groups,
+                                        s);
   }
 }

@@ -105,9 +105,71 @@ class _Scheduler(object):
 
     def drain(self):
         pending = self.pending
+        tls = _Branches._tls
         while pending:
-            dst, src = pending.popleft()
-            dst._check_gate_and_run(src)
+            ent = pending.popleft()
+            if len(ent) == 3:
+                dst, src, br = ent
+            else:
+                (dst, src), br = ent, None
+            tls.br = br
+            try:
+                dst._check_gate_and_run(src)
+            finally:
+                tls.br = None
+
+
+class _Branches(object):
+    """Independent branches of a fan-out on HIP streams (SURVEY §2.6
+    "intra-process graph concurrency"; the reference runs fan-out successors
+    on its thread pool, veles/units.py:485-505).
+
+    With ``root.common.engine.parallel_fanout`` on a GPU workflow, a unit
+    whose control links fan out to several runnable successors forks: every
+    successor gets a stream of a small per-device pool that first waits on
+    the forking stream (an event), and everything that runs downstream of it
+    inherits that stream - its kernels run concurrently with the sibling
+    branches.  A unit with several control parents (an InputJoiner diamond,
+    the join) waits for every parent's stream on the stream the fork came
+    from and runs there; its successors continue in the enclosing branch.
+    Everything stays on the engine's thread (kernel launches are
+    asynchronous: the concurrency is on the device), so a HIP-graph capture
+    follows the fork (streams that wait on a captured event join the capture)
+    and the join (the capture stream waits on them again).
+
+    A branch context is (stream, enclosing context, fork stream)."""
+    _tls = threading.local()
+    _pools = {}
+    PER_FORK = 4
+
+    @classmethod
+    def current(cls):
+        return getattr(cls._tls, "br", None)
+
+    @classmethod
+    def depth(cls, br):
+        d = 0
+        while br is not None:
+            d, br = d + 1, br[1]
+        return d
+
+    @classmethod
+    def fork(cls, device, n):
+        """n branch contexts forked from the current stream."""
+        import torch
+        parent = cls.current()
+        base = torch.cuda.current_stream(device)
+        pool = cls._pools.setdefault(str(device), [])
+        d = cls.depth(parent)
+        need = (d + 1) * cls.PER_FORK
+        while len(pool) < need:
+            pool.append(torch.cuda.Stream(device))
+        out = []
+        for i in range(n):
+            st = pool[d * cls.PER_FORK + i % cls.PER_FORK]
+            st.wait_stream(base)
+            out.append((st, parent, base))
+        return out
 
 
 _ROCTX = [None, False]
@@ -589,20 +651,39 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
             for dst in targets:
                 self.debug("%s -> %s @%s", self, dst,
                            threading.current_thread().name)
+        brs = None
         if len(targets) > 1 and get(root.common.engine.parallel_fanout,
                                     False) is True:
-            for dst in targets:
-                self.thread_pool.callInThread(_run_in_pool, dst, self)
-            return
+            dev = self._branch_device()
+            if dev is None:
+                for dst in targets:
+                    self.thread_pool.callInThread(_run_in_pool, dst, self)
+                return
+            brs = _Branches.fork(dev, len(targets))
+        if brs is None:
+            brs = [_Branches.current()] * len(targets)
         sched = _Scheduler.current()
         if sched is None:
             with _Scheduler() as sched:
-                for dst in targets:
-                    sched.pending.append((dst, self))
+                for dst, br in zip(targets, brs):
+                    sched.pending.append((dst, self, br))
                 sched.drain()
         else:
-            for dst in targets:
-                sched.pending.append((dst, self))
+            for dst, br in zip(targets, brs):
+                sched.pending.append((dst, self, br))
+
+    def _branch_device(self):
+        """The torch device of a GPU workflow with engine.branch_streams
+        (default on), else None (fan-out on the thread pool)."""
+        if get(root.common.engine.branch_streams, True) is not True:
+            return None
+        wf = self.workflow
+        while wf is not None and getattr(wf, "device", None) is None:
+            wf = getattr(wf, "workflow", None)
+        dev = getattr(wf, "device", None) if wf is not None else None
+        if dev is None or not getattr(dev, "is_gpu", False):
+            return None
+        return dev.torch_device
 
     def _check_gate_and_run(self, src):
         if not self.open_gate(src):
@@ -611,14 +692,44 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
         pool = getattr(wf, "_thread_pool_", None) if wf is not None else None
         if pool is not None and pool.failure is not None:
             return
+        br = _Branches.current()
         if not self._gate_skip:
             if not self._run_lock_.acquire(False):
                 return
             try:
-                self.do_run()
+                if br is None:
+                    self.ran_on_ = None
+                    self.do_run()
+                else:
+                    br = self._run_on_branch(br)
             finally:
                 self._run_lock_.release()
+        if br is not _Branches.current():
+            # a join: the successors continue in the enclosing branch
+            _Branches._tls.br = br
+            try:
+                self.run_dependent()
+            finally:
+                _Branches._tls.br = None
+            return
         self.run_dependent()
+
+    def _run_on_branch(self, br):
+        """do_run() on branch br's stream; a unit with several control
+        parents joins them on the fork stream first.  Returns the branch
+        context its successors inherit."""
+        import torch
+        stream, parent, base = br
+        if len(self._links_from) > 1:
+            for u in self._links_from:
+                s = u.__dict__.get("ran_on_")
+                if s is not None and s is not base:
+                    base.wait_stream(s)
+            stream, br = base, parent
+        with torch.cuda.stream(stream):
+            self.do_run()
+        self.ran_on_ = stream
+        return br
 
     def dependent_units(self, with_open_gate=False):
         """BFS over links_to, children sorted by name."""
