@@ -955,6 +955,100 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
   }
 }
 
+// Row-staged form (the default): a workgroup builds RPB output rows Y of one
+// sample.  Their S input rows are S * W * C CONTIGUOUS bytes, loaded into
+// LDS by 16-B loads (unaligned addresses are fine on gfx950), out-of-image
+// rows zero-filled; each lane then assembles 16-B output chunks (8 s2d
+// elements) from LDS bytes and stores them, a wave writing 1 KiB
+// contiguous.  Global traffic is two streams of whole lines (the per-chunk
+// kernel above read three dwords per row piece per lane).
+extern int hvk_gemm_variant;
+
+template <int S, int C, int RPB>
+__global__ void __launch_bounds__(256)
+fill_s2d_rows_kernel(const uint8_t* __restrict__ src, long long src_bytes,
+                     const int* shuffled, int start, int count, int max_mb,
+                     int H, int W, int pt, int pl, int H2, int W2,
+                     const float* __restrict__ mean2,
+                     const float* __restrict__ rdisp2,
+                     uint16_t* __restrict__ dst, const int* labels,
+                     int* labels_out, int* idx_out) {
+  constexpr int PIX = S * S * C, CPP = PIX / 8;
+  static_assert(PIX % 8 == 0, "16-B chunks");
+  extern __shared__ __attribute__((aligned(16))) uint8_t rows_lds[];
+  const int i = blockIdx.y;
+  const int Y0 = blockIdx.x * RPB;
+  const int WC = W * C;
+  const int RB = (S * WC + 15) & ~15;   // LDS bytes per output row's input
+  const int sid = i < count ? shuffled[start + i] : -1;
+  const int t = threadIdx.x;
+  if (blockIdx.x == 0 && t == 0) {
+    if (labels_out) labels_out[i] = (sid >= 0 && labels) ? labels[sid] : -1;
+    if (idx_out) idx_out[i] = sid;
+  }
+  const int nrow = min(RPB, H2 - Y0);
+  const int cpr = W2 * CPP;             // output chunks per row
+  uint16_t* out = dst + (long long)i * H2 * cpr * 8;
+  if (sid < 0) {
+    for (int q = t; q < nrow * cpr; q += 256)
+      *(uint4*)(out + ((long long)Y0 * cpr + q) * 8) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  // stage: for each of the nrow output rows, its S input rows
+  const long long base = (long long)sid * H * WC;
+  const int nch = RB / 16;
+  for (int q = t; q < nrow * nch; q += 256) {
+    const int r = q / nch, c = q - (q / nch) * nch;
+    const int byte = c * 16;                 // within the S rows
+    const int dy = byte / WC;
+    const int iy = S * (Y0 + r) - pt + dy;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    // the chunk may straddle input rows: load it whole when every row it
+    // touches is in the image and the 16 bytes stay inside the buffer,
+    // else byte by byte
+    const long long g = base + (long long)(S * (Y0 + r) - pt) * WC + byte;
+    const int dy2 = min(byte + 15, S * WC - 1) / WC;
+    const int iy2 = S * (Y0 + r) - pt + dy2;
+    if (iy >= 0 && iy2 < H && g + 16 <= src_bytes) {
+      __builtin_memcpy(&v, src + g, 16);
+    } else {
+      uint8_t b[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int bb = byte + e;
+        const int ry = S * (Y0 + r) - pt + bb / WC;
+        b[e] = (bb < S * WC && ry >= 0 && ry < H) ? src[g + e] : 0;
+      }
+      __builtin_memcpy(&v, b, 16);
+    }
+    *(uint4*)(rows_lds + r * RB + byte) = v;
+  }
+  __syncthreads();
+  for (int q = t; q < nrow * cpr; q += 256) {
+    const int r = q / cpr, cc = q - (q / cpr) * cpr;
+    const int X = cc / CPP, j = cc - (cc / CPP) * CPP;
+    const long long ch = ((long long)(Y0 + r) * W2 * CPP + cc);
+    const float4* m4 = (const float4*)(mean2 + ch * 8);
+    const float4* r4 = (const float4*)(rdisp2 + ch * 8);
+    const float4 ma = m4[0], mb = m4[1], ra = r4[0], rb = r4[1];
+    const float mm[8] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
+    const float rr[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int el = 8 * j + e;
+      const int dy = el / (S * C), rem = el - dy * (S * C);
+      const int dx = rem / C, c = rem - dx * C;
+      const int ix = S * X + dx - pl;
+      // outside the image: the affine map is (0, 1) there, the byte 0
+      const uint8_t b = (ix >= 0 && ix < W)
+          ? rows_lds[r * RB + dy * WC + ix * C + c] : (uint8_t)0;
+      f[e] = ((float)b - mm[e]) * rr[e];
+    }
+    *(uint4*)(out + ch * 8) = pack_bf16x8(f);
+  }
+}
+
 HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
                                    const int* shuffled, int start, int count,
                                    int max_mb, int H, int W, int C, int S,
@@ -966,6 +1060,16 @@ HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
   if (S != 4 || C != 3 || ((uintptr_t)dst & 15) || ((uintptr_t)mean2 & 15) ||
       ((uintptr_t)rdisp2 & 15) || max_mb > 65535 * 4)
     return -1;
+  if (hvk_gemm_variant != 60 && max_mb <= 65535) {
+    constexpr int RPB = 2;
+    const size_t lds = (size_t)RPB * ((S * W * C + 15) & ~15);
+    hipLaunchKernelGGL((fill_s2d_rows_kernel<4, 3, RPB>),
+                       dim3((H2 + RPB - 1) / RPB, max_mb), dim3(256), lds, s,
+                       (const uint8_t*)src, src_bytes, shuffled, start, count,
+                       max_mb, H, W, pt, pl, H2, W2, mean2, rdisp2,
+                       (uint16_t*)dst, labels, labels_out, idx_out);
+    return (int)launch_status(s);
+  }
   constexpr int SPT = 4;
   const int chunks = H2 * W2 * (4 * 4 * 3 / 8);
   hipLaunchKernelGGL((fill_s2d_u8_bf16_kernel<4, 3, SPT>),
