@@ -202,3 +202,76 @@ def test_single_rank_overlapped_update_matches_serial(graphs):
     assert st.steps == ser.param_store_.steps == steps
     assert _rel(st.master, ser.param_store_.master) < 2e-2
     assert torch.equal(st.lp, st.master.to(st.lp.dtype))
+
+
+def _solo_run(out, solo, steps, port):
+    import os
+    import numpy
+    import torch
+    os.environ["VELES_AMD_DP_SOLO_COLLECTIVES"] = "1" if solo else "0"
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    from veles_amd.utils.config import root
+    root.common.disable.snapshotting = True
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    from veles_amd.models.zoo import lenet
+    from veles_amd.parallel.dp import DataParallel
+    import veles_amd.loader  # noqa: F401
+    dp = DataParallel(backend="nccl")
+    la = DummyLauncher()
+    la.dp_ = dp
+    wf = StandardWorkflow(
+        la, loader_name="synthetic_images",
+        loader_config={"dataset": "mnist", "class_lengths": (0, 0, 2560),
+                       "minibatch_size": 256,
+                       "normalization_type": "mean_disp", "seed": 4},
+        layers=lenet(0.01), decision_config={"max_epochs": None,
+                                             "fail_iterations": None})
+    wf.initialize(device=Device(backend="hip"))
+    wf.run_steps(steps)
+    torch.cuda.synchronize()
+    segs = {s.name: (s.captures, s.replays) for s in wf.graph_segments_}
+    w = [f.weights_master.float().cpu().numpy().copy() for f in wf.forwards
+         if getattr(f, "_pw_", None) is not None]
+    numpy.savez(out, *w)
+    with open(out + ".json", "w") as f:
+        import json
+        json.dump({"segs": segs, "multi": bool(dp.multi),
+                   "graph_safe": bool(wf.param_store_.graph_safe())}, f)
+    dp.shutdown()
+
+
+@pytest.mark.gpu
+def test_solo_rccl_path_captures_backward_and_matches_dp1(tmp_path):
+    """The multi-rank step through a one-rank RCCL process group
+    (VELES_AMD_DP_SOLO_COLLECTIVES=1): bucketed all-reduces and per-bucket
+    updates on the side stream, all captured in the backward HIP graph and
+    replayed - ends 6 steps with the weights of the plain single-GPU step
+    (split-K atomics make runs differ in the last bits only)."""
+    import json
+    import socket
+    import numpy
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    res = {}
+    for solo in (True, False):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        out = str(tmp_path / ("solo%d.npz" % solo))
+        p = ctx.Process(target=_solo_run, args=(out, solo, 6, port))
+        p.start()
+        p.join(300)
+        assert p.exitcode == 0
+        res[solo] = (numpy.load(out), json.load(open(out + ".json")))
+    (ws, js), (wp, jp) = res[True], res[False]
+    assert js["multi"] and js["graph_safe"]
+    assert not jp["multi"]
+    cap, rep = js["segs"]["backward"]
+    assert cap == 1 and rep >= 2, js["segs"]
+    for k in ws.files:
+        assert numpy.isfinite(ws[k]).all()
+        numpy.testing.assert_allclose(ws[k], wp[k], rtol=1e-4, atol=1e-6)

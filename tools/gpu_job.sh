@@ -16,6 +16,9 @@
 #                            (VELES_AMD_DP_SOLO_COLLECTIVES=1)
 #   ab[:B:ROUNDS:VARIANTS]   tools/bench_gemm_ab.py (GEMM loop A/B)
 #   prof[:MODEL:BATCH:TAG:PREC]  step-only rocprofv3 kernel table
+#   pmc[:TAG[:BENCHARGS]]    four rocprofv3 --pmc passes (instruction mix,
+#                            wave states, HBM read + TA, HBM write + L2 hit)
+#                            on bench.py --mark-steps, step-only summaries
 #   py:SCRIPT[,ARGS]         python SCRIPT ARGS
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -61,6 +64,27 @@ for step in "$@"; do
       python tools/prof_summary.py "$f" gpurun_out/prof_${M}_${T}.md \
         "$M b$B 1x MI355X ($P, $T)" --window --steps 5
       head -40 gpurun_out/prof_${M}_${T}.md ;;
+    pmc)
+      IFS=: read -r tag bargs <<< "$arg"
+      T=${tag:-r4}
+      for pass in A B C D; do
+        case $pass in
+          A) ctr="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_BF16" ;;
+          B) ctr="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" ;;
+          C) ctr="FETCH_SIZE TA_BUSY_avr GRBM_GUI_ACTIVE" ;;
+          D) ctr="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" ;;
+        esac
+        tools/gpu_step.sh 200 gpurun_out/pmc_${T}_$pass.log timeout -s KILL 150 \
+          rocprofv3 --kernel-trace --pmc $ctr -d "$R/gpurun_out/pmc_${T}_$pass" \
+          -o run --output-format csv -- python3 "$R/bench.py" --steps 2 \
+          --warmup 2 --mark-steps ${bargs//,/ } || exit 1
+      done
+      f() { find gpurun_out/pmc_${T}_$1 -name "*counter_collection.csv" | head -1; }
+      python tools/pmc_mix_summary.py --window "$(f A)" "$(f B)" \
+        gpurun_out/pmc_mix_$T.md "step kernels: instruction mix and wave states ($T)"
+      python tools/pmc_mem_summary.py --window "$(f C)" "$(f D)" \
+        gpurun_out/pmc_mem_$T.md "step kernels: HBM traffic, L2 hit rate, TA busy ($T)"
+      head -30 gpurun_out/pmc_mix_$T.md; head -30 gpurun_out/pmc_mem_$T.md ;;
     py)
       tools/gpu_step.sh 900 "$log" python -u ${arg//,/ } || exit 1
       tail -40 "$log" ;;

@@ -5,12 +5,21 @@ kernel's own time, L2 hit rate, texture-address (TA) busy share.
 FETCH_SIZE / WRITE_SIZE are in KiB."""
 import collections
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_common import load_rows  # noqa: E402
+
+# --window: step kernels only (between the bench's trace markers)
+WINDOW = "--window" in sys.argv
+if WINDOW:
+    sys.argv.remove("--window")
 
 
 def load(path):
     agg = collections.OrderedDict()
-    for r in csv.DictReader(open(path)):
+    for r in load_rows(path, WINDOW):
         n = r["Kernel_Name"].replace("void ", "").replace(
             "(anonymous namespace)::", "").split("(")[0][:64]
         d = agg.setdefault((n, r["Grid_Size"]),

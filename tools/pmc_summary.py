@@ -8,11 +8,20 @@ SQ_BUSY_CYCLES / (time x 2.4 GHz) = 30 ~ the 32 shader engines).  Under load
 the clock can sit below 2.4 GHz, so the figure is a lower bound."""
 import collections
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_common import load_rows  # noqa: E402
+
+# --window: step kernels only (between the bench's trace markers)
+WINDOW = "--window" in sys.argv
+if WINDOW:
+    sys.argv.remove("--window")
 
 
 def main(path, out, title):
-    rows = list(csv.DictReader(open(path)))
+    rows = list(load_rows(path, WINDOW))
     agg = collections.OrderedDict()
     for r in rows:
         n = r["Kernel_Name"].replace("void ", "").replace(
