@@ -26,12 +26,18 @@
 // the fully-connected forward.  Weight gradients and the fully-connected
 // dgrad (whose fp8 B operand would be W^T) stay on the bf16 kernels
 // (docs/OPS.md §FP8).
+#include <type_traits>
+
 #include "fp8_common.h"
 #include "conv_geom.h"
 
 using namespace hvk;
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+// fp8 schedule selector for A/B runs (hvk_set_fp8_variant): 70 keeps dense
+// GEMMs on the 128-row loop
+int hvk_fp8_variant = -1;
 
 namespace {
 
@@ -58,6 +64,13 @@ struct Dense8 {
   __device__ __forceinline__ const uint8_t* src(const Ctx& c, int k) const {
     // bitwise condition + pinned address: no exec-mask branch per slot
     return pick_ptr(c.row + k, (c.ok != 0) & (k < K), g_zero16);
+  }
+  // buffer-descriptor DMA (the ping-pong loop): byte offset of row r
+  bool buf_ok() const {
+    return (long long)(rows - 1) * ld + K < kBufMaxBytes;
+  }
+  __device__ __forceinline__ uint32_t row_voff(int r) const {
+    return r < rows ? (uint32_t)r * (uint32_t)ld : kBufOOB;
   }
 };
 
@@ -449,6 +462,248 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
   }
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 fp8 tile on the bf16 four-phase ping-pong schedule (gemm_pp.h
+// gemm_pp256_kernel: 1.42 PF bf16 at 8192^3).  A K tile of 128 fp8 bytes is
+// byte-for-byte the bf16 loop's 64-element tile (128-B rows, chunk c at
+// c ^ (row & 7), 1-KiB LDS-DMA pieces of 8 rows), and a 16x16x128 f8f6f4
+// MFMA (32 cycles) consumes the 32 B a lane holds for both halves of the
+// bf16 K tile: per K tile a wave issues the same 24 fragment reads and 8
+// DMA pieces against 32 MFMAs that each do twice the bf16 work - the same
+// schedule at the fp8 rate.  Two groups of four waves, group 1 one barrier
+// behind; quadrant phases q0..q3 read A0 + B0 / B1 / A1 / nothing, A(t+1)
+// is DMAed in q0 / q1 into the stage tile t-1 left, B(t+2) in q2 / q3 into
+// tile t's stage once its B reads are retired, one vmcnt(4) per tile (the
+// slot-numbered RAW / WAR argument of gemm_pp.h holds unchanged).
+struct PP8Op {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t v[4];
+  int kc;
+  __device__ __forceinline__ void init(const Dense8& l, int r0, int w,
+                                       int lane) {
+    rs = dma_rsrc(l.p);
+    kc = 16 * ((lane & 7) ^ ((lane >> 3) & 7));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      v[i] = l.row_voff(r0 + 8 * (w * 4 + i) + (lane >> 3));
+  }
+  __device__ __forceinline__ void issue(const Dense8& l, int k0, uint8_t* s,
+                                        int w, int i0, int n) {
+    const bool kin = k0 + kc < l.K;
+    const uint32_t kb = (uint32_t)(k0 + kc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i >= i0 && i < i0 + n)
+        dma16(rs, s + (w * 4 + i) * 1024, kin ? v[i] + kb : kBufOOB);
+  }
+};
+
+template <int FA, int FB>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
+                      int tiles_q, int tiles, int gm) {
+  constexpr int TB = 256 * BK;           // bytes per operand stage
+  constexpr int SST = 2 * TB;            // A + B
+  constexpr int LDC = 256 + 4;
+  static_assert(64 * LDC * 4 <= 2 * SST, "epilogue pass fits");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * SST];
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  int tp, tq;
+  if (gm > 1) {
+    const int tiles_p = tiles / tiles_q;
+    const int g = tile / (gm * tiles_q);
+    const int p0g = g * gm;
+    const int gh = min(tiles_p - p0g, gm);
+    const int r = tile - g * gm * tiles_q;
+    tp = p0g + r % gh;
+    tq = r / gh;
+  } else {
+    tp = tile / tiles_q;
+    tq = tile - tp * tiles_q;
+  }
+  const int p0 = tp * 256, q0 = tq * 256;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = w >> 2;
+  const int prow = grp * 128, qrow = (w & 3) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  PP8Op op, oq;
+  op.init(lp, p0, w, lane);
+  oq.init(lq, q0, w, lane);
+  // 32 bytes of row (rowbase + fr): chunks 2fq, 2fq + 1 at c ^ (row & 7)
+  auto frag = [&](const uint8_t* sb, int rowbase) -> i32x8 {
+    const int row = rowbase + fr;
+    const int sw = row & 7;
+    const uint8_t* base = sb + row * BK;
+    const uint4 lo = *(const uint4*)(base + (((2 * fq) ^ sw) << 4));
+    const uint4 hi = *(const uint4*)(base + (((2 * fq + 1) ^ sw) << 4));
+    i32x8 v;
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    return v;
+  };
+  const int nk = (K + BK - 1) / BK;
+  uint8_t* st0 = smem;
+  uint8_t* st1 = smem + SST;
+  op.issue(lp, 0, st0, w, 0, 4);
+  oq.issue(lq, 0, st0 + TB, w, 0, 4);
+  if (nk > 1) {
+    oq.issue(lq, BK, st1 + TB, w, 0, 4);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger group 1
+  asm volatile("" ::: "memory");
+
+  i32x8 af[4], b0[2], b1[2];
+  auto mfma = [&](int abase, i32x8 (&bf)[2], int bbase) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[abase + i][bbase + j] =
+            __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                af[i], bf[j], acc[abase + i][bbase + j], FA, FB, 0, 127, 0,
+                127);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto slot_end = [&]() {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint8_t* sP = (kt & 1) ? st1 : st0;
+    const uint8_t* sQ = sP + TB;
+    uint8_t* nxt = (kt & 1) ? st0 : st1;
+    uint8_t* cur = (kt & 1) ? st1 : st0;
+    const bool pa = kt + 1 < nk, pb = kt + 2 < nk;
+    const int ka = (kt + 1) * BK, kb = (kt + 2) * BK;
+    // q0 MEM: A0, B0; A(t+1) pieces 0, 1
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b0[j] = frag(sQ, qrow + j * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(sP, prow + i * 16);
+    if (pa) op.issue(lp, ka, nxt, w, 0, 2);
+    slot_end();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    mfma(0, b0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+    // q1 MEM: B1; A(t+1) pieces 2, 3
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b1[j] = frag(sQ, qrow + 32 + j * 16);
+    if (pa) op.issue(lp, ka, nxt, w, 2, 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    slot_end();
+    mfma(0, b1, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+    // q2 MEM: A1; B(t+2) pieces 0, 1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(sP, prow + 64 + i * 16);
+    if (pb) oq.issue(lq, kb, cur + TB, w, 0, 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    slot_end();
+    mfma(4, b1, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+    // q3 MEM: B(t+2) pieces 2, 3; wait for tile t+1
+    if (pb) {
+      oq.issue(lq, kb, cur + TB, w, 2, 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    slot_end();
+    mfma(4, b0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    slot_end();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // group 1's last slot
+  asm volatile("" ::: "memory");
+
+  const float alpha = 1.f / (fp8_scale(epi.sa, epi.hist, epi.fa) *
+                             fp8_scale(epi.sb, epi.hist, epi.fb));
+  const float qs = epi.q8 ? fp8_scale(epi.q8_st, epi.hist, epi.q8_fmax) : 1.f;
+  float amax = 0.f;
+  float* sC = (float*)smem;
+  constexpr int CH = 256 / 8;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __syncthreads();
+    if (grp == (e >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rb = i * 16 + fq * 4;
+          const int qc = qrow + j * 16 + fr;
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            sC[(rb + rr) * LDC + qc] = acc[(e & 1) * 4 + i][j][rr];
+        }
+    }
+    __syncthreads();
+    const int m0 = p0 + e * 64;
+    for (int q = t; q < 64 * CH; q += 512) {
+      const int row = q / CH, c8 = (q % CH) * 8;
+      if (m0 + row >= P) continue;
+      const float4* src = (const float4*)(sC + row * LDC + c8);
+      float v[8];
+      const float4 lo = src[0], hi = src[1];
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      store8(epi, alpha, 0, m0 + row, q0 + c8, v, qs, &amax);
+    }
+  }
+  if (epi.q8) {
+    amax = wave_max(amax);
+    __syncthreads();
+    float* red = (float*)smem;
+    if (lane == 0) red[w] = amax;
+    __syncthreads();
+    if (t == 0) {
+      float mx = 0.f;
+      for (int i = 0; i < 8; ++i) mx = fmaxf(mx, red[i]);
+      if (mx > 0.f)
+        atomicMax((unsigned int*)(epi.q8_shard + (blockIdx.x & 31) * 32),
+                  __float_as_uint(mx));
+    }
+  }
+}
+
+// the 256 x 256 loop for dense fp8 GEMMs with at least one tile per CU
+// (hvk_gemm_variant 70 keeps the 128-row loop: A/B runs)
+inline bool want_pp256_fp8(const Dense8& la, const Dense8& lb, int M, int N) {
+  if (hvk_fp8_variant == 70) return false;
+  if (!la.buf_ok() || !lb.buf_ok()) return false;
+  const long long t = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  const int wn = (N + 255) / 256 * 256 - N;
+  return t >= 256 && wn * 8 <= N;
+}
+
+template <int FA, int FB>
+hipError_t go_pp256_fp8(const Dense8& la, const Dense8& lb, const Epi8& e,
+                        int M, int N, int K, hipStream_t s) {
+  const int tiles_q = (N + 255) / 256;
+  const int tiles = (M + 255) / 256 * tiles_q;
+  const int gm = tiles_q >= 8 ? 8 : 1;
+  hipLaunchKernelGGL((gemm_pp256_fp8_kernel<FA, FB>), dim3(tiles), dim3(512),
+                     0, s, la, lb, e, M, N, K, tiles_q, tiles, gm);
+  return launch_status(s);
+}
+
 inline bool use_bn64(int N) {
   int w128 = (N + 127) / 128 * 128 - N;
   int w64 = (N + 63) / 64 * 64 - N;
@@ -458,6 +713,11 @@ inline bool use_bn64(int N) {
 template <class LA, class LB, int FA, int FB>
 hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
                    int K, int groups, hipStream_t s) {
+  if constexpr (std::is_same<LA, Dense8>::value &&
+                std::is_same<LB, Dense8>::value) {
+    if (groups == 1 && want_pp256_fp8(la, lb, M, N))
+      return go_pp256_fp8<FA, FB>(la, lb, e, M, N, K, s);
+  }
   const bool n64 = use_bn64(N);
   const int bn = n64 ? 64 : 128;
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + bn - 1) / bn;
@@ -689,6 +949,8 @@ inline void set_q8(Epi8& e, void* q8, const float* st, float* shard,
   e.q8_fmax = fmax;
   e.q8_fmt = fmt;
 }
+
+HVK_API void hvk_set_fp8_variant(int v) { hvk_fp8_variant = v; }
 
 // C[M][N] (bf16) = act(A[M][K] . B[N][K]^T / (sA sB) + bias) * f'(aux)
 HVK_API int hvk_gemm_fp8(int M, int N, int K, const void* A, int lda, int fa,

@@ -432,3 +432,30 @@ def test_fused_quantisation_pool2(bwd):
     r.roll()
     torch.cuda.synchronize()
     assert nxt.state[step % fp8.HIST].item() == y.float().abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 1024), (4100, 4000, 384),
+                                   (8192, 2304, 128), (4096, 4096, 256 + 16)])
+def test_gemm_fp8_pingpong_256(M, N, K):
+    """The 256 x 256 fp8 ping-pong loop (gemm_pp256_fp8_kernel; >= 256 tiles)
+    against the 128-row fp8 loop (hvk_set_fp8_variant(70)): the same MFMAs
+    over the same K order, so bit-identical - and both against the float32
+    product of the dequantised operands.  Covers partial row / column tiles,
+    a one-tile K (prologue only) and a K tail."""
+    a8, sa, a8c, sac = _pair(rnd(M, K))
+    b8, sb, b8c, sbc = _pair(rnd(N, K, seed=1, scale=0.1))
+    bias = torch.randn(N, device=DEV)
+    lib = ops._lib.lib()
+    outs = []
+    try:
+        for v in (70, -1):
+            lib.hvk_set_fp8_variant(v)
+            outs.append(fp8.gemm(a8, sa, b8, sb, bias=bias, act=3).clone())
+    finally:
+        lib.hvk_set_fp8_variant(-1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.relu(fp8.dequantize(a8, sa).float() @
+                     fp8.dequantize(b8, sb).float().t() + bias)
+    close(outs[1], ref, 1e-2)
