@@ -275,3 +275,54 @@ def test_solo_rccl_path_captures_backward_and_matches_dp1(tmp_path):
     for k in ws.files:
         assert numpy.isfinite(ws[k]).all()
         numpy.testing.assert_allclose(ws[k], wp[k], rtol=1e-4, atol=1e-6)
+
+
+def _runahead_run(on, steps):
+    import os
+    os.environ["VELES_AMD_LOADER_RUNAHEAD"] = "1" if on else "0"
+    from veles_amd.backends import Device
+    from veles_amd.dummy import DummyLauncher
+    from veles_amd.models import StandardWorkflow
+    from veles_amd.prng import random_generator
+    from test_e2e_gpu import _small_alexnet
+    import veles_amd.loader  # noqa: F401
+    random_generator.get().seed(21)
+    torch.manual_seed(21)
+    wf = StandardWorkflow(
+        DummyLauncher(), loader_name="synthetic_images",
+        loader_config={"dataset": "imagenet", "n_classes": 16,
+                       "class_lengths": (0, 0, 96), "minibatch_size": 32,
+                       "normalization_type": "mean_disp", "seed": 5},
+        layers=_small_alexnet(), decision_config={"max_epochs": None,
+                                                  "fail_iterations": None},
+        graph_warmup=1)
+    wf.initialize(device=Device(backend="hip"))
+    wf.run_steps(steps)
+    torch.cuda.synchronize()
+    ld = wf.loader
+    w = [f.weights_master.float().cpu().clone() for f in wf.forwards
+         if getattr(f, "_pw_", None) is not None]
+    segs = {s.name: (s.captures, s.replays) for s in wf.graph_segments_}
+    return w, ld.runahead_hits, ld.runahead_misses, segs
+
+
+def test_loader_runahead_matches_serial_gather():
+    """The double-buffered gather (the next minibatch's fill on a side
+    stream, forward / backward graphs keyed by buffer parity) trains like
+    the serial gather over 3 epochs of 3 minibatches (every epoch end is a
+    reshuffle: a prediction miss), with the space-to-depth conv1 input."""
+    import os
+    old = os.environ.get("VELES_AMD_LOADER_RUNAHEAD")
+    try:
+        ws, _, _, _ = _runahead_run(False, 9)
+        wr, hits, misses, segs = _runahead_run(True, 9)
+    finally:
+        if old is None:
+            os.environ.pop("VELES_AMD_LOADER_RUNAHEAD", None)
+        else:
+            os.environ["VELES_AMD_LOADER_RUNAHEAD"] = old
+    assert hits >= 5 and misses >= 2, (hits, misses)
+    assert segs["forward"][0] == 2, segs   # one graph per buffer set
+    for a, b in zip(ws, wr):
+        assert torch.isfinite(b).all()
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-5)

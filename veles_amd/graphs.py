@@ -445,8 +445,12 @@ def _is_chain(units):
 
 def _full_key(wf):
     ld = wf.loader
+    # buffer_parity_: which of a run-ahead loader's two minibatch buffer
+    # sets this pass reads (one graph per set: a graph replays the pointers
+    # it captured)
     return (int(ld.minibatch_class), int(ld.minibatch_size),
-            bool(getattr(wf, "testing", False)))
+            bool(getattr(wf, "testing", False)),
+            int(getattr(ld, "buffer_parity_", 0)))
 
 
 def install_step_graphs(wf, warmup=2):

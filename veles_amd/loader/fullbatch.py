@@ -54,6 +54,15 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         # space-to-depth layout (request_s2d_input)
         self.s2d_layout_ = None
         self._dev_s2d_affine_ = None
+        # run-ahead state (``_runahead``): two output buffer sets, the parity
+        # of the one served, the prefetched minibatch (key, parity, event)
+        self._ra_bufs_ = None
+        self._ra_pending_ = None
+        self._ra_stream_ = None
+        self._ra_gen_ = 0
+        self.buffer_parity_ = 0
+        self.runahead_hits = 0
+        self.runahead_misses = 0
 
     def __getstate__(self):
         st = super().__getstate__()
@@ -84,6 +93,9 @@ class FullBatchLoader(Loader, IFullBatchLoader):
     def create_minibatch_data(self):
         import torch
         from veles_amd import ops
+        self._ra_bufs_ = None       # run-ahead sets follow the new buffers
+        self._ra_pending_ = None
+        self.buffer_parity_ = 0
         n = self.local_minibatch_size
         dev = self.device
         shape = (n,) + self.sample_shape
@@ -241,6 +253,7 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         self._upload_shuffled()
 
     def on_shuffled(self):
+        self._ra_gen_ += 1   # a prefetch of the old order is stale
         if self._dev_labels_ is not None or self.original_data.devmem is not None:
             self._upload_shuffled()
 
@@ -255,28 +268,114 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         else:
             self._dev_shuffled_.copy_(src, non_blocking=False)
 
-    def fill_indices(self, start_offset, count):
+    def _gather(self, start_offset, count, data_out, labels_out, idx_out):
         from veles_amd import ops
-        if self._dev_shuffled_ is None:
-            self.on_initialized()
         data = self.original_data.devmem
         if self.s2d_layout_ is not None:
             s, KH, KW, padding = self.s2d_layout_
             ops.fill_minibatch_s2d(
-                data, self._dev_shuffled_, start_offset, count,
-                self.minibatch_data.devmem, s, KH, KW, padding,
-                *self._dev_s2d_affine_, labels=self._dev_labels_,
-                labels_out=self.minibatch_labels.devmem
-                if self.has_labels else None,
-                idx_out=self.minibatch_indices.devmem)
-            return True
+                data, self._dev_shuffled_, start_offset, count, data_out, s,
+                KH, KW, padding, *self._dev_s2d_affine_,
+                labels=self._dev_labels_, labels_out=labels_out,
+                idx_out=idx_out)
+            return
         ops.fill_minibatch(
-            data, self._dev_shuffled_, start_offset, count,
-            self.minibatch_data.devmem, mean=self._dev_mean_,
-            rdisp=self._dev_rdisp_, labels=self._dev_labels_,
-            labels_out=self.minibatch_labels.devmem
-            if self.has_labels else None,
-            idx_out=self.minibatch_indices.devmem)
+            data, self._dev_shuffled_, start_offset, count, data_out,
+            mean=self._dev_mean_, rdisp=self._dev_rdisp_,
+            labels=self._dev_labels_, labels_out=labels_out,
+            idx_out=idx_out)
+
+    def fill_indices(self, start_offset, count):
+        if self._dev_shuffled_ is None:
+            self.on_initialized()
+        if self._runahead():
+            return self._fill_runahead(start_offset, count)
+        self._gather(start_offset, count, self.minibatch_data.devmem,
+                     self.minibatch_labels.devmem
+                     if self.has_labels else None,
+                     self.minibatch_indices.devmem)
+        return True
+
+    # -- run-ahead (SURVEY §2.6 "loader / compute overlap") ----------------
+    def _runahead(self):
+        """Double-buffered device gather: the NEXT minibatch's gather runs
+        on a side stream into the other buffer set while this step computes
+        (GPU, ``root.common.engine.loader_runahead`` / env
+        VELES_AMD_LOADER_RUNAHEAD, default on; not for MSE targets).  The
+        step's HIP graphs are keyed by ``buffer_parity_`` (graphs.py), one
+        per buffer set."""
+        dev = self.device
+        if dev is None or not getattr(dev, "is_gpu", False) or \
+                getattr(self, "original_targets", None) is not None:
+            return False
+        import os
+        from veles_amd.utils.config import root, get
+        return os.environ.get("VELES_AMD_LOADER_RUNAHEAD", "1" if get(
+            root.common.engine.loader_runahead, True) else "0") != "0"
+
+    def _ra_views(self, parity):
+        import torch
+        if self._ra_bufs_ is None:
+            cur = (self.minibatch_data.devmem,
+                   self.minibatch_labels.devmem if self.has_labels else None,
+                   self.minibatch_indices.devmem)
+            other = tuple(None if t is None else torch.empty_like(t)
+                          for t in cur)
+            self._ra_bufs_ = [cur, other]
+            self._ra_stream_ = torch.cuda.Stream(cur[0].device)
+        return self._ra_bufs_[parity]
+
+    def _peek_next(self):
+        """(start, count) of the minibatch this rank serves next, when it is
+        known now without side effects (no reshuffle and no failed
+        minibatch in between), else None."""
+        if self.failed_minibatches:
+            return None
+        off = self.global_offset
+        if off >= self.effective_total_samples:
+            return None
+        _, rem = self.class_index_by_sample_index(off)
+        size = min(rem, self.max_minibatch_size)
+        b, e = self.shard_bounds(size)
+        return off + b, e - b
+
+    def _fill_runahead(self, start_offset, count):
+        import torch
+        cur = torch.cuda.current_stream(self.minibatch_data.devmem.device)
+        key = (self._ra_gen_, start_offset, count)
+        pend, self._ra_pending_ = self._ra_pending_, None
+        if pend is not None and pend[0] == key:
+            parity = pend[1]
+            cur.wait_event(pend[2])
+            self.runahead_hits += 1
+        else:
+            self.runahead_misses += 1
+            parity = self.buffer_parity_ ^ 1 if pend is not None else \
+                self.buffer_parity_
+            d, lab, idx = self._ra_views(parity)
+            if pend is not None:
+                cur.wait_event(pend[2])   # the stale prefetch's writes
+            self._gather(start_offset, count, d, lab, idx)
+        d, lab, idx = self._ra_views(parity)
+        self.minibatch_data.devmem = d
+        if lab is not None:
+            self.minibatch_labels.devmem = lab
+        self.minibatch_indices.devmem = idx
+        self.buffer_parity_ = parity
+        nxt = self._peek_next()
+        if nxt is not None and nxt[1] > 0:
+            # the other set's readers (the previous step) are all enqueued
+            # on the compute stream before this point
+            free = torch.cuda.Event()
+            free.record(cur)
+            side = self._ra_stream_
+            side.wait_event(free)
+            od, ol, oi = self._ra_views(parity ^ 1)
+            with torch.cuda.stream(side):
+                self._gather(nxt[0], nxt[1], od, ol, oi)
+                done = torch.cuda.Event()
+                done.record(side)
+            self._ra_pending_ = ((self._ra_gen_,) + nxt, parity ^ 1, done)
         return True
 
     def fill_minibatch(self):
