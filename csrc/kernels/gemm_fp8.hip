@@ -463,6 +463,191 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
 }
 
 // ---------------------------------------------------------------------------
+// fp8 implicit-GEMM convolution on the bf16 T4 loop (gemm_t4.h): 192 x 128
+// tiles, 4 waves (2 x 2, each 96 x 64), two 40-KiB LDS stages of a 128-byte
+// K tile (= the bf16 loop's 64-element tile, byte for byte), TWO
+// workgroups per CU, one barrier per K tile, the next tile's DMA in flight
+// during the MFMAs.  Per K tile a wave issues 10 LDS-DMA pieces and 20
+// fragment reads (32 B each: two ds_read_b128) against 24 MFMAs of
+// 16x16x128 (32 cycles each, twice the bf16 work per cycle).  P = the
+// implicit im2col / gathered-dY rows (fast DRow / DTap addressing), Q = the
+// weights (Dense8).
+template <class LP, int FA, int FB>
+__global__ void __launch_bounds__(256, 2)
+gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
+                   int tiles_q, int tiles, int gm) {
+  constexpr int PR = 192, QR = 128;
+  constexpr int SP = PR * BK, SQ = QR * BK, SST = SP + SQ;   // bytes
+  constexpr int NSP = PR / 8 / 4, NSQ = QR / 8 / 4;          // per wave
+  constexpr int HP = PR / 2, LDC = QR + 4;
+  static_assert(HP * LDC * 4 <= 2 * SST, "epilogue pass fits");
+  static_assert(2 * 2 * SST <= 160 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * SST];
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  const int gi = wgid / tiles;
+  int tp, tq;
+  if (gm > 1) {
+    const int tiles_p = tiles / tiles_q;
+    const int g = tile / (gm * tiles_q);
+    const int p0g = g * gm;
+    const int gh = min(tiles_p - p0g, gm);
+    const int r = tile - g * gm * tiles_q;
+    tp = p0g + r % gh;
+    tq = r / gh;
+  } else {
+    tp = tile / tiles_q;
+    tq = tile - tp * tiles_q;
+  }
+  lp.group(gi);
+  lq.group(gi);
+  const int p0 = tp * PR, q0 = tq * QR;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int prow = (w >> 1) * HP, qrow = (w & 1) * 64;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[6][4];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // DMA slots: piece I = rows 8I .. 8I + 7 of the operand, lane -> row
+  // 8I + (lane >> 3), chunk (lane & 7) ^ (row & 7)
+  const int kc = 16 * ((lane & 7) ^ ((lane >> 3) & 7));
+  DRow fa[NSP];
+  typename Dense8::Ctx db[NSQ];
+#pragma unroll
+  for (int i = 0; i < NSP; ++i)
+    fa[i] = lp.drow(p0 + 8 * (w * NSP + i) + (lane >> 3));
+#pragma unroll
+  for (int i = 0; i < NSQ; ++i)
+    db[i] = lq.row_ctx(q0 + 8 * (w * NSQ + i) + (lane >> 3));
+  auto issue = [&](int k0, uint8_t* sP) {
+    const DTap tpk = lp.dtap(k0 + kc);
+#pragma unroll
+    for (int i = 0; i < NSP; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)lp.dsrc(fa[i], tpk),
+          (__attribute__((address_space(3))) void*)(sP + (w * NSP + i) * 1024),
+          16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NSQ; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)lq.src(db[i], k0 + kc),
+          (__attribute__((address_space(3))) void*)(sP + SP +
+                                                    (w * NSQ + i) * 1024),
+          16, 0, 0);
+  };
+  auto frag = [&](const uint8_t* sb, int rowbase) -> i32x8 {
+    const int row = rowbase + fr;
+    const int sw = row & 7;
+    const uint8_t* base = sb + row * BK;
+    const uint4 lo = *(const uint4*)(base + (((2 * fq) ^ sw) << 4));
+    const uint4 hi = *(const uint4*)(base + (((2 * fq + 1) ^ sw) << 4));
+    i32x8 v;
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    return v;
+  };
+  const int nk = (K + BK - 1) / BK;
+  issue(0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint8_t* sP = smem + (kt & 1) * SST;
+    const uint8_t* sQ = sP + SP;
+    // tile t + 1 into the stage tile t - 1 used (read before the barrier
+    // that ended step t - 1)
+    if (kt + 1 < nk) issue((kt + 1) * BK, smem + ((kt + 1) & 1) * SST);
+    i32x8 bq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bq[j] = frag(sQ, qrow + j * 16);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const i32x8 a = frag(sP, prow + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            a, bq[j], acc[i][j], FA, FB, 0, 127, 0, 127);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  const float alpha = 1.f / (fp8_scale(epi.sa, epi.hist, epi.fa) *
+                             fp8_scale(epi.sb, epi.hist, epi.fb));
+  const float qs = epi.q8 ? fp8_scale(epi.q8_st, epi.hist, epi.q8_fmax) : 1.f;
+  float amax = 0.f;
+  float* sC = (float*)smem;
+  constexpr int CH = QR / 8;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    if (e) __syncthreads();
+    if ((w >> 1) == e) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rb = i * 16 + fq * 4;
+          const int qc = qrow + j * 16 + fr;
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + qc] = acc[i][j][rr];
+        }
+    }
+    __syncthreads();
+    const int m0 = p0 + e * HP;
+    for (int q = t; q < HP * CH; q += 256) {
+      const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
+      if (m0 + row >= P) continue;
+      const float4* src = (const float4*)(sC + row * LDC + c8);
+      float v[8];
+      const float4 lo = src[0], hi = src[1];
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      store8(epi, alpha, gi, m0 + row, q0 + c8, v, qs, &amax);
+    }
+  }
+  if (epi.q8) {
+    amax = wave_max(amax);
+    __syncthreads();
+    float* red = (float*)smem;
+    if (lane == 0) red[w] = amax;
+    __syncthreads();
+    if (t == 0) {
+      float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (mx > 0.f)
+        atomicMax((unsigned int*)(epi.q8_shard + (blockIdx.x & 31) * 32),
+                  __float_as_uint(mx));
+    }
+  }
+}
+
+// convolutions on the T4 fp8 loop when the output channels per group fill
+// 128-wide tiles (<= 1/8 wasted) - VGG's 128..512; hvk_fp8_variant 71
+// keeps the 128-row loop (A/B runs)
+inline bool want_t4_fp8(int N) {
+  if (hvk_fp8_variant == 71) return false;
+  const int w = (N + 127) / 128 * 128 - N;
+  return N >= 128 && w * 8 <= N;
+}
+
+template <class LP, int FA, int FB>
+hipError_t go_t4_fp8(const LP& lp, const Dense8& lq, const Epi8& e, int M,
+                     int N, int K, int groups, hipStream_t s) {
+  const int tiles_q = (N + 127) / 128;
+  const int tiles = (M + 191) / 192 * tiles_q;
+  const int gm = tiles_q >= 8 ? 8 : 1;
+  hipLaunchKernelGGL((gemm_t4_fp8_kernel<LP, FA, FB>),
+                     dim3((unsigned)((long long)tiles * groups)), dim3(256), 0,
+                     s, lp, lq, e, M, N, K, tiles_q, tiles, gm);
+  return launch_status(s);
+}
+
+// ---------------------------------------------------------------------------
 // 256 x 256 fp8 tile on the bf16 four-phase ping-pong schedule (gemm_pp.h
 // gemm_pp256_kernel: 1.42 PF bf16 at 8192^3).  A K tile of 128 fp8 bytes is
 // byte-for-byte the bf16 loop's 64-element tile (128-B rows, chunk c at
@@ -717,6 +902,12 @@ hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
                 std::is_same<LB, Dense8>::value) {
     if (groups == 1 && want_pp256_fp8(la, lb, M, N))
       return go_pp256_fp8<FA, FB>(la, lb, e, M, N, K, s);
+  }
+  if constexpr ((std::is_same<LA, ConvFwdA8>::value ||
+                 std::is_same<LA, ConvDgradA8>::value) &&
+                std::is_same<LB, Dense8>::value) {
+    if (want_t4_fp8(N)) return go_t4_fp8<LA, FA, FB>(la, lb, e, M, N, K,
+                                                      groups, s);
   }
   const bool n64 = use_bn64(N);
   const int bn = n64 ? 64 : 128;

@@ -459,3 +459,52 @@ def test_gemm_fp8_pingpong_256(M, N, K):
     ref = torch.relu(fp8.dequantize(a8, sa).float() @
                      fp8.dequantize(b8, sb).float().t() + bias)
     close(outs[1], ref, 1e-2)
+
+
+T4CONVS8 = [
+    # N, H, W, C, OC, k, pad, groups, stride: VGG-like (128 / 256 / 512 outputs),
+    # the AlexNet conv2 grouping, a stride-2 forward, partial row tiles
+    (2, 28, 28, 64, 128, 3, 1, 1, 1),
+    (3, 14, 14, 128, 256, 3, 1, 1, 1),
+    (1, 7, 7, 256, 512, 3, 1, 1, 1),
+    (2, 27, 27, 96, 256, 5, 2, 2, 1),
+    (2, 16, 16, 64, 128, 3, 1, 1, 2),   # stride 2: forward only
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", T4CONVS8)
+def test_conv_fp8_t4_loop(cfg):
+    """The 192 x 128 two-workgroups-per-CU fp8 loop (gemm_t4_fp8_kernel)
+    against the 128-row fp8 loop (hvk_set_fp8_variant(71)): forward and
+    backward-data bit-identical (same MFMAs, same K order), and against the
+    float32 reference."""
+    N, H, W, C, OC, k, p, g, s = cfg
+    pad = (p, p, p, p)
+    x8, sx, x8c, sxc = _pair(rnd(N, H, W, C))
+    w8, sw, w8c, swc = _pair(rnd(OC, k, k, C // g, seed=1, scale=0.1))
+    b = torch.randn(OC)
+    lib = ops._lib.lib()
+    try:
+        outs = []
+        for v in (71, -1):
+            lib.hvk_set_fp8_variant(v)
+            outs.append(fp8.conv_fwd(x8, sx, w8, sw, b.to(DEV), (s, s), pad,
+                                     g, 3).clone())
+        assert torch.equal(outs[0], outs[1])
+        close(outs[1], fp8.conv_fwd(x8c, sxc, w8c, swc, b, (s, s), pad, g, 3),
+              1e-2)
+        if s == 1:
+            OH, OW = ops.conv_out_size(H, W, k, k, (1, 1), pad)
+            d8, sd, d8c, sdc = _pair(rnd(N, OH, OW, OC, seed=2, scale=1e-2),
+                                     fp8.E5M2)
+            outs = []
+            for v in (71, -1):
+                lib.hvk_set_fp8_variant(v)
+                outs.append(fp8.conv_dgrad(d8, sd, w8, sw, (N, H, W, C),
+                                           (1, 1), pad, g).clone())
+            assert torch.equal(outs[0], outs[1])
+            close(outs[1], fp8.conv_dgrad(d8c, sdc, w8c, swc, (N, H, W, C),
+                                          (1, 1), pad, g), 1e-2)
+    finally:
+        lib.hvk_set_fp8_variant(-1)
