@@ -408,6 +408,67 @@ __global__ void col_sum_bf16x8_kernel(const uint16_t* in, int R, int C,
   }
 }
 
+// bf16 column sums of any C % 8 == 0 (the FC bias gradients: C = 4096 and
+// more): a block is 64 chunks (512 columns) x 4 row lanes over a slab of
+// rows, each thread keeping four 16-B loads in flight; the row lanes meet in
+// LDS and each column takes one atomic per slab.  Enough slabs that the
+// grid covers the CUs several times (an 8 MB read is otherwise latency-
+// bound at a few hundred GB/s).
+__global__ void __launch_bounds__(256)
+col_sum_bf16_wide_kernel(const uint16_t* __restrict__ in, int R, int C,
+                         float* out, int rows_per_slab, float scale) {
+  const int CH = C >> 3;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * rows_per_slab;
+  const int r1 = min(R, r0 + rows_per_slab);
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  if (ch < CH) {
+    const uint16_t* p = in + (long long)ch * 8;
+    int r = r0 + rl;
+    for (; r + 12 < r1; r += 16) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = *(const uint4*)(p + (long long)(r + 4 * u) * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[2 * q] += __uint_as_float(w[q] << 16);
+          acc[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+        }
+      }
+    }
+    for (; r < r1; r += 4) {
+      const uint4 v = *(const uint4*)(p + (long long)r * C);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += __uint_as_float(w[q] << 16);
+        acc[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+      }
+    }
+  }
+  __shared__ float red[3][64][9];
+  if (rl > 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[rl - 1][cl][q] = acc[q];
+  }
+  __syncthreads();
+  if (rl == 0 && ch < CH) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += red[k][cl][q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) atomicAdd(&out[ch * 8 + q], acc[q] * scale);
+  }
+}
+
 // out[r] = sum_c in[r][c] * scale  (one wave per row)
 __global__ void row_sum_kernel(const void* in, int dt, int R, int C, float* out,
                                float scale) {
@@ -1341,6 +1402,19 @@ HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
 
 HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
                         float scale, hipStream_t s) {
+  if (dt == DT_BF16 && C % 8 == 0 && C >= 512 &&
+      ((uintptr_t)in & 15) == 0) {
+    // >= ~1024 blocks: slabs of 16+ rows
+    const int cgroups = (C / 8 + 63) / 64;
+    int slabs = (1024 + cgroups - 1) / cgroups;
+    int rps = (R + slabs - 1) / slabs;
+    if (rps < 16) rps = 16;
+    slabs = (R + rps - 1) / rps;
+    hipLaunchKernelGGL(col_sum_bf16_wide_kernel, dim3(cgroups, slabs),
+                       dim3(256), 0, s, (const uint16_t*)in, R, C, out, rps,
+                       scale);
+    return (int)launch_status(s);
+  }
   if (dt == DT_BF16 && C % 8 == 0 && C / 8 <= 256 &&
       ((uintptr_t)in & 15) == 0) {
     // ~2048 blocks over the rows

@@ -486,9 +486,12 @@ def test_conv_im2col_path_fwd_and_wgrad():
     close(dgot, 2 * dref, 1e-2)
 
 
-@pytest.mark.parametrize("C", [96, 256, 8])
-def test_col_sum_vectorised(C):
-    x = rnd(3001, C)
+@pytest.mark.parametrize("C,R", [(96, 3001), (256, 3001), (8, 3001),
+                                 (4096, 1024), (1000 * 8, 37), (520, 5)])
+def test_col_sum_vectorised(C, R):
+    """narrow (<= 2048 columns: chunk per thread), wide (the FC bias
+    gradients: slabs of rows, four loads in flight) and tiny slabs"""
+    x = rnd(R, C)
     close(ops.col_sum(x.to(DEV)), ops.col_sum(x), 1e-4)
 
 

@@ -15,6 +15,15 @@ __all__ = ["GradientDescent", "GDTanh", "GDRELU", "GDStrictRELU",
            "GDSigmoid", "GDSoftmax"]
 
 
+def _bias_colsum():
+    """FC bias gradient by ops.col_sum instead of the fused ones column
+    (root.common.engine.fc_bias_colsum / VELES_AMD_FC_BIAS_COLSUM)."""
+    import os
+    from veles_amd.utils.config import root, get
+    return os.environ.get("VELES_AMD_FC_BIAS_COLSUM", "1" if get(
+        root.common.engine.fc_bias_colsum, False) else "0") != "0"
+
+
 class GradientDescent(GradientDescentBase):
     MAPPING = "all2all"
     OVERWRITES_GRADS = True  # see ParameterStore.overwrite
@@ -40,7 +49,14 @@ class GradientDescent(GradientDescentBase):
         # the step's only contribution: write, not read-modify-write
         ow = self.store_.overwrite
         mode = "overwrite" if ow else True
-        if not fwd.weights_transposed:
+        if not fwd.weights_transposed and bg is not None and \
+                _bias_colsum() and e2.is_cuda:
+            # grad_b by the column-sum kernel: the ones column costs the
+            # weight-gradient GEMM one more column tile and its buffer-DMA
+            # path (engine.fc_bias_colsum)
+            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode)
+            ops.col_sum(e2, out=bg, accumulate=not ow)
+        elif not fwd.weights_transposed:
             # grad_W and grad_b (ones column) from one GEMM
             ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode,
                      bias_grad=bg)
