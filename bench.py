@@ -89,8 +89,11 @@ def main():
                        "generate_on_device": backend == "hip"},
         layers=layers_fn(), decision_config={"max_epochs": None,
                                              "fail_iterations": None},
-        # capture the forward / backward segments inside the warmup steps
-        graph_warmup=max(0, min(2, args.warmup - 1)))
+        # capture the forward / backward segments inside the warmup steps:
+        # the run-ahead loader alternates two buffer sets, one graph each,
+        # so every set needs its eager warmup pass(es) and its capture
+        # before the timed region (a capture synchronises the device)
+        graph_warmup=max(0, min(2, args.warmup // 2 - 1)))
     wf.initialize(device=device)
 
     def sync():

@@ -364,8 +364,11 @@ constexpr bool t4_pair_ok() {
 
 // orientation options (M = A rows, N = B rows), both 192 x 128 tiles at
 // BK 64: 1 P = A, Q = B; 2 P = B, Q = A, TRANS.  Cost = padded MFMA work;
-// the T4 loop is taken when its padded work is at most 1.10x that of the
-// 128-row loop (which pads to 128 x bn tiles).  hvk_gemm_variant 50 turns
+// the T4 loop is taken when its padded work is at most 1.04x that of the
+// 128-row loop (which pads to 128 x bn tiles): measured at AlexNet b1024
+// (profiles/r4/ab_t4_192x128_bk64_vs_128row.log) it wins 3-27 % on every
+// convolution it takes at <= 1.0x and loses 2 % (conv2 weight gradient,
+// 1.05x: the bias column's extra tile) and 7 % (conv5, 1.07x).  hvk_gemm_variant 50 turns
 // the loop off, 51 / 52 force option 1 / 2 (A/B runs, tests).
 inline long long t4_cost(int M, int N, int opt) {
   auto up = [](long long x, long long b) { return (x + b - 1) / b * b; };
@@ -381,7 +384,7 @@ inline int t4_pick(int M, int N, int bn) {
                          ((N + bn - 1) / bn * bn);
   const int best = c1 <= c2 ? 1 : 2;
   const long long cb = c1 <= c2 ? c1 : c2;
-  return cb * 100 <= base * 110 ? best : 0;
+  return cb * 100 <= base * 104 ? best : 0;
 }
 
 template <class LP, bool PK, class LQ, bool QK, bool TRANS>

@@ -129,6 +129,13 @@ def _load():
                                            (LIB_PATH, name))
             fn.argtypes = sig
             fn.restype = ctypes.c_void_p if name in _PTR_RET else ctypes.c_int
+        # A/B schedule selectors for whole-run experiments (bench.py under
+        # an environment setting; tests and tools call the setters directly)
+        for env, fn in (("VELES_AMD_GEMM_VARIANT", "hvk_set_gemm_variant"),
+                        ("VELES_AMD_FP8_VARIANT", "hvk_set_fp8_variant")):
+            v = os.environ.get(env)
+            if v is not None and hasattr(lib, fn):
+                getattr(lib, fn)(ctypes.c_int(int(v)))
         _lib = lib
         return lib
 
