@@ -82,7 +82,10 @@ def test_diamond_branches_on_streams(graph):
                 wf.run()          # warm-up (allocations, library state)
                 torch.cuda.synchronize()
                 # the unit graph itself on the capturing stream (wf.run()
-                # would switch to the device's compute stream)
+                # would switch to the device's compute stream); the
+                # finished pass left every unit stopped
+                for u in wf:
+                    u.stopped = False
                 with torch.cuda.stream(s):
                     g.capture_begin()
                     with _Scheduler() as sched:

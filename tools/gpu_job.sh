@@ -12,6 +12,8 @@
 #   smoke                    __graft_entry__.smoke()
 #   bench[:ARGS]             python bench.py ARGS (comma-separated, e.g.
 #                            bench:--batch,512,--model,vgg16)
+#   benv:VAR=VAL[+VAR=VAL][:ARGS]  bench.py under extra environment settings
+#                            (A/B of whole steps, e.g. benv:VELES_AMD_GEMM_VARIANT=50)
 #   solo[:ARGS]              bench.py with a one-rank RCCL process group
 #                            (VELES_AMD_DP_SOLO_COLLECTIVES=1)
 #   ab[:B:ROUNDS:VARIANTS]   tools/bench_gemm_ab.py (GEMM loop A/B)
@@ -44,6 +46,10 @@ for step in "$@"; do
     bench)
       tools/gpu_step.sh 600 "$log" python bench.py ${arg//,/ } || exit 1
       grep metric "$log" || tail -5 "$log" ;;
+    benv)
+      IFS=: read -r envs bargs <<< "$arg"
+      tools/gpu_step.sh 600 "$log" env ${envs//+/ } python bench.py ${bargs//,/ } || exit 1
+      echo "$envs"; grep metric "$log" || tail -5 "$log" ;;
     solo)
       tools/gpu_step.sh 600 "$log" env VELES_AMD_DP_SOLO_COLLECTIVES=1 \
         python bench.py ${arg//,/ } || exit 1
