@@ -15,10 +15,12 @@
 // move by global_load_lds_dwordx4 with the next tile in flight across the
 // (raw) barrier, one counted vmcnt per tile.
 //
-// Operand lane map: lane l feeds row (l & 15) with the 32 bytes
-// k = 32*(l >> 4) ... +31 of both A and B.  The k order inside an MFMA is a
-// permutation shared by A and B, so the sum over k is the same whatever
-// order the hardware assigns (tests/test_fp8.py checks it against fp32).
+// Operand lane map: lane l feeds row (l & 15) with the 16-B chunks
+// q = l >> 4 and q + 4 (k = 16q .. 16q + 15 and 64 + 16q ..) of both A and
+// B.  The k order inside an MFMA is a permutation shared by A and B, so the
+// sum over k is the same whatever order the hardware assigns
+// (tests/test_fp8.py checks it against fp32); this pair keeps the
+// ds_read_b128 lane groups conflict-free, as the bf16 loop's fragments.
 //
 // Only K-major operands exist here (fp8 has no transposed LDS read that the
 // bf16 MN-major path relies on), which covers conv forward (A = im2col(X),
@@ -318,14 +320,18 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // 32 bytes of row (rowbase + fr): chunks 2fq and 2fq+1 at their swizzled
-  // slots (c ^ (row & 7)) of the 128-B row
+  // 32 bytes of row (rowbase + fr): chunks fq and fq + 4 at their swizzled
+  // slots (c ^ (row & 7)) of the 128-B row.  Which k a lane holds only has
+  // to agree between A and B (the MFMA sums every product); this pair is
+  // the bf16 loop's two 32-deep fragments, conflict-free per ds_read_b128
+  // lane group (chunks 2fq, 2fq + 1 put two lanes of a group on one bank
+  // slot)
   auto frag = [&](const uint8_t* s, int rowbase) -> i32x8 {
     const int row = rowbase + fr;
     const int sw = row & 7;
     const uint8_t* base = s + row * BK;
-    uint4 lo = *(const uint4*)(base + (((2 * fq) ^ sw) << 4));
-    uint4 hi = *(const uint4*)(base + (((2 * fq + 1) ^ sw) << 4));
+    uint4 lo = *(const uint4*)(base + ((fq ^ sw) << 4));
+    uint4 hi = *(const uint4*)(base + (((fq + 4) ^ sw) << 4));
     i32x8 v;
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
@@ -544,8 +550,8 @@ gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
     const int row = rowbase + fr;
     const int sw = row & 7;
     const uint8_t* base = sb + row * BK;
-    const uint4 lo = *(const uint4*)(base + (((2 * fq) ^ sw) << 4));
-    const uint4 hi = *(const uint4*)(base + (((2 * fq + 1) ^ sw) << 4));
+    const uint4 lo = *(const uint4*)(base + ((fq ^ sw) << 4));
+    const uint4 hi = *(const uint4*)(base + (((fq + 4) ^ sw) << 4));
     i32x8 v;
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
@@ -723,13 +729,14 @@ gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
   PP8Op op, oq;
   op.init(lp, p0, w, lane);
   oq.init(lq, q0, w, lane);
-  // 32 bytes of row (rowbase + fr): chunks 2fq, 2fq + 1 at c ^ (row & 7)
+  // 32 bytes of row (rowbase + fr): chunks fq, fq + 4 at c ^ (row & 7)
+  // (the k assignment the 128-row loop uses; conflict-free reads)
   auto frag = [&](const uint8_t* sb, int rowbase) -> i32x8 {
     const int row = rowbase + fr;
     const int sw = row & 7;
     const uint8_t* base = sb + row * BK;
-    const uint4 lo = *(const uint4*)(base + (((2 * fq) ^ sw) << 4));
-    const uint4 hi = *(const uint4*)(base + (((2 * fq + 1) ^ sw) << 4));
+    const uint4 lo = *(const uint4*)(base + ((fq ^ sw) << 4));
+    const uint4 hi = *(const uint4*)(base + (((fq + 4) ^ sw) << 4));
     i32x8 v;
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
