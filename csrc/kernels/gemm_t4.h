@@ -166,10 +166,20 @@ __device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int ks,
   }
 }
 
-template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS, int BKT>
+// BIAS (weight gradients): the bias gradient sum_k of one operand's
+// columns, from extra MFMAs against an all-ones operand in the first tile
+// of the other side instead of a ones column appended to the GEMM (which
+// costs a whole extra tile when KK fills the tiles: AlexNet conv5 1728 =
+// 9 x 192).  1: over the Q operand (ones as A; waves with prow = 0 of the
+// workgroups with tp = 0); 2: over the P operand (ones as B; waves with
+// qrow = 0 of the workgroups with tq = 0).  bgrad[row + gi * grow] is
+// stored (bg_store, an unsplit overwrite) or atomically added.
+template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS, int BKT,
+          int BIAS = 0>
 __global__ void __launch_bounds__(256, 2)
 gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
-               int tiles_q, int tiles, int splits, int gm) {
+               int tiles_q, int tiles, int splits, int gm, float* bgrad,
+               int bg_store) {
   constexpr int NST = BKT == 32 ? 3 : 2;     // LDS ring stages
   using OP = T4Op<LP, PK, PR, BKT>;
   using OQ = T4Op<LQ, QK, T4_QR, BKT>;
@@ -220,6 +230,14 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int NBA = BIAS == 1 ? 4 : (BIAS == 2 ? MI : 1);
+  f32x4 accb[NBA];
+#pragma unroll
+  for (int i = 0; i < NBA; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool bwave = BIAS == 1 ? (tp == 0 && prow == 0)
+                   : BIAS == 2 ? (tq == 0 && qrow == 0) : false;
+  const bf16x8 ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                       (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
 
   OP op;
   OQ oq;
@@ -267,6 +285,19 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               a, bq[j], acc[i][j], 0, 0, 0);
+        if constexpr (BIAS == 2) {
+          if (bwave)
+            accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones,
+                                                              accb[i], 0, 0, 0);
+        }
+      }
+      if constexpr (BIAS == 1) {
+        if (bwave) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bq[j],
+                                                              accb[j], 0, 0, 0);
+        }
       }
     }
     // retire step t + 1 (three stages: step t + 2 stays in flight), then one
@@ -277,6 +308,37 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
     asm volatile("" ::: "memory");
     scur = scur == NST - 1 ? 0 : scur + 1;
     spre = spre == NST - 1 ? 0 : spre + 1;
+  }
+
+  if constexpr (BIAS != 0) {
+    // every row (BIAS 1) / column (BIAS 2) of the ones-MFMA tile holds the
+    // same sums: lanes of row 0 / column 0 write them
+    if (bwave) {
+      const int eg0 = epi.slice ? 0 : gi;
+#pragma unroll
+      for (int i = 0; i < NBA; ++i) {
+        if constexpr (BIAS == 1) {
+          const int r = q0 + qrow + i * 16 + fr;      // Q index = C row
+          if (fq == 0 && r < Q) {
+            const float v = accb[i][0] * epi.alpha;
+            float* d = bgrad + r + eg0 * epi.grow;
+            if (bg_store) *d = v;
+            else atomicAdd(d, v);
+          }
+        } else {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int r = p0 + prow + i * 16 + fq * 4 + rr;  // P = C row
+            if (fr == 0 && r < P) {
+              const float v = accb[i][rr] * epi.alpha;
+              float* d = bgrad + r + eg0 * epi.grow;
+              if (bg_store) *d = v;
+              else atomicAdd(d, v);
+            }
+          }
+        }
+      }
+    }
   }
 
   // epilogue: the ring is drained (every DMA waited for, every fragment read
@@ -375,11 +437,13 @@ inline long long t4_cost(int M, int N, int opt) {
   return opt == 1 ? up(M, 192) * up(N, 128) : up(N, 192) * up(M, 128);
 }
 
-inline int t4_pick(int M, int N, int bn) {
+// Nt: the N the T4 tiles cover (a weight gradient's bias comes from ones-
+// MFMAs instead of the ones column the 128-row loop pads N with)
+inline int t4_pick(int M, int N, int bn, int Nt) {
   if (hvk_gemm_variant == 50 || hvk_gemm_variant == 0) return 0;
   if (hvk_gemm_variant == 51) return 1;
   if (hvk_gemm_variant == 52) return 2;
-  const long long c1 = t4_cost(M, N, 1), c2 = t4_cost(M, N, 2);
+  const long long c1 = t4_cost(M, Nt, 1), c2 = t4_cost(M, Nt, 2);
   const long long base = (long long)((M + 127) / 128 * 128) *
                          ((N + bn - 1) / bn * bn);
   const int best = c1 <= c2 ? 1 : 2;
@@ -387,17 +451,18 @@ inline int t4_pick(int M, int N, int bn) {
   return cb * 100 <= base * 104 ? best : 0;
 }
 
-template <class LP, bool PK, class LQ, bool QK, bool TRANS>
+template <class LP, bool PK, class LQ, bool QK, bool TRANS, int BIAS = 0>
 hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
-                 int K, int k_split, int splits, int groups, hipStream_t s) {
+                 int K, int k_split, int splits, int groups, hipStream_t s,
+                 float* bgrad = nullptr, int bg_store = 0) {
   constexpr int PR = 192;
   const int tiles_p = (P + PR - 1) / PR, tiles_q = (Q + T4_QR - 1) / T4_QR;
   const int tiles = tiles_p * tiles_q;
   const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64>), grid,
-                     dim3(256), 0, s, lp, lq, epi, P, Q, K, k_split, tiles_q,
-                     tiles, splits, gm);
+  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64, BIAS>),
+                     grid, dim3(256), 0, s, lp, lq, epi, P, Q, K, k_split,
+                     tiles_q, tiles, splits, gm, bgrad, bg_store);
   return launch_status(s);
 }
 
@@ -418,11 +483,16 @@ hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
       // per 64-pixel step
       if (lb.g.OH * lb.g.OW < 64) return hipSuccess;
     }
-    const int opt = t4_pick(M, N, bn);
+    // weight gradient with a fused bias gradient: the bias comes from ones-
+    // MFMAs (BIAS), not from the ones column at index N - 1
+    const bool wbias = std::is_same<LB, ConvWgradB>::value &&
+                       epi.ones_col >= 0 && epi.ones_col == N - 1;
+    const int Nt = wbias ? N - 1 : N;
+    const int opt = t4_pick(M, N, bn, Nt);
     if (!opt) return hipSuccess;
     const long long t4t = opt == 1
-        ? (long long)((M + 191) / 192) * ((N + T4_QR - 1) / T4_QR)
-        : (long long)((N + 191) / 192) * ((M + T4_QR - 1) / T4_QR);
+        ? (long long)((M + 191) / 192) * ((Nt + T4_QR - 1) / T4_QR)
+        : (long long)((Nt + 191) / 192) * ((M + T4_QR - 1) / T4_QR);
     int sp = splits, ks = k_split;
     // (split-K through workspace slices keeps the caller's split: the
     // finishing pass sums exactly `splits` slices)
@@ -433,6 +503,24 @@ hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
       sp = (K + ks - 1) / ks;
     }
     *taken = true;
+    if constexpr (std::is_same<LB, ConvWgradB>::value) {
+      if (wbias) {
+        LB lb2 = lb;
+        lb2.ones = 0;
+        Epi e2 = epi;
+        e2.ones_col = -1;
+        e2.N = Nt;
+        // an unsplit overwrite stores the bias, else adds it (split-K /
+        // accumulation; the caller zeroed it for a split overwrite)
+        const int bst = (!epi.atomic && epi.bias_store) ? 1 : 0;
+        if (opt == 1)
+          return go_t4<LA, AK, LB, BKM, false, 2>(la, lb2, e2, M, Nt, K, ks,
+                                                  sp, groups, s,
+                                                  epi.bias_grad, bst);
+        return go_t4<LB, BKM, LA, AK, true, 1>(lb2, la, e2, Nt, M, K, ks, sp,
+                                               groups, s, epi.bias_grad, bst);
+      }
+    }
     if (opt == 1)
       return go_t4<LA, AK, LB, BKM, false>(la, lb, epi, M, N, K, ks, sp,
                                            groups, s);
