@@ -281,7 +281,7 @@ def test_solo_rccl_path_captures_backward_and_matches_dp1(tmp_path):
 
 def _runahead_run(on, steps):
     import os
-    os.environ["VELES_AMD_LOADER_RUNAHEAD"] = "1" if on else "0"
+    os.environ["VELES_AMD_LOADER_RUNAHEAD"] = "1" if on else "0"   # opt-in
     from veles_amd.backends import Device
     from veles_amd.dummy import DummyLauncher
     from veles_amd.models import StandardWorkflow

@@ -301,9 +301,11 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         """Double-buffered device gather: the NEXT minibatch's gather runs
         on a side stream into the other buffer set while this step computes
         (GPU, ``root.common.engine.loader_runahead`` / env
-        VELES_AMD_LOADER_RUNAHEAD, default on; not for MSE targets).  The
-        step's HIP graphs are keyed by ``buffer_parity_`` (graphs.py), one
-        per buffer set."""
+        VELES_AMD_LOADER_RUNAHEAD; not for MSE targets).  The step's HIP
+        graphs are keyed by ``buffer_parity_`` (graphs.py), one per buffer
+        set.  Off by default: on AlexNet b1024 the side-stream gather ran
+        beside conv1 (0.50 -> 0.65 ms) and the step was 0.8 % slower
+        (144.3k vs 145.4k img/s, profiles/r4/runahead_ab.md)."""
         dev = self.device
         if dev is None or not getattr(dev, "is_gpu", False) or \
                 getattr(self, "original_targets", None) is not None:
@@ -311,7 +313,7 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         import os
         from veles_amd.utils.config import root, get
         return os.environ.get("VELES_AMD_LOADER_RUNAHEAD", "1" if get(
-            root.common.engine.loader_runahead, True) else "0") != "0"
+            root.common.engine.loader_runahead, False) else "0") != "0"
 
     def _ra_views(self, parity):
         import torch
