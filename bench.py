@@ -89,11 +89,12 @@ def main():
                        "generate_on_device": backend == "hip"},
         layers=layers_fn(), decision_config={"max_epochs": None,
                                              "fail_iterations": None},
-        # capture the forward / backward segments inside the warmup steps:
-        # the run-ahead loader alternates two buffer sets, one graph each,
-        # so every set needs its eager warmup pass(es) and its capture
-        # before the timed region (a capture synchronises the device)
-        graph_warmup=max(0, min(2, args.warmup // 2 - 1)))
+        # capture the forward / backward segments inside the warmup steps,
+        # after two eager passes (buffers a unit allocates lazily on its
+        # second pass would otherwise be zero-filled inside the captured
+        # graph, i.e. on every replay); the run-ahead loader alternates two
+        # buffer sets, one graph each, so each set needs its passes
+        graph_warmup=_graph_warmup(args.warmup))
     wf.initialize(device=device)
 
     def sync():
@@ -175,6 +176,14 @@ def main():
                 json.dump({"result": out, "unit_stats": stats}, f, indent=1)
     dp.barrier()
     dp.shutdown()
+
+
+def _graph_warmup(warmup):
+    from veles_amd.utils.config import root, get
+    ra = os.environ.get("VELES_AMD_LOADER_RUNAHEAD", "1" if get(
+        root.common.engine.loader_runahead, False) else "0") != "0"
+    per = warmup // 2 if ra else warmup
+    return max(0, min(2, per - 1))
 
 
 def dp_report(dp, store, backend):

@@ -327,4 +327,5 @@ def test_loader_runahead_matches_serial_gather():
     assert segs["forward"][0] == 2, segs   # one graph per buffer set
     for a, b in zip(ws, wr):
         assert torch.isfinite(b).all()
-        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-5)
+        # split-K atomics: the runs differ in the last bits, not by a step
+        assert _rel(b, a) < 2e-3
