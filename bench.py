@@ -33,8 +33,10 @@ def main():
     # GEMMs, half the per-sample update / launch cost) and halves the
     # all-reduce-to-compute ratio for the multi-GPU points
     # (profiles/batch_sweep_r2.md)
-    ap.add_argument("--batch", type=int, default=1024,
-                    help="per-GPU minibatch (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU minibatch (weak scaling); default 1024, "
+                         "512 for vgg16 (the fp8 and bf16 throughput "
+                         "plateau: profiles/r4/vgg16_batch_sweep.md)")
     ap.add_argument("--model", default="alexnet")
     ap.add_argument("--precision", default="bfloat16",
                     choices=("bfloat16", "float8"),
@@ -50,6 +52,8 @@ def main():
                     help="bracket the timed steps with hvk_trace_marker "
                          "kernels (step-only rocprofv3 summaries)")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 512 if args.model == "vgg16" else 1024
 
     import torch
     from veles_amd.utils.config import root
