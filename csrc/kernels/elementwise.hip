@@ -1016,16 +1016,18 @@ fill_s2d_u8_bf16_kernel(const uint8_t* __restrict__ src, long long src_bytes,
   }
 }
 
-// Row-staged form (the default): a workgroup builds RPB output rows Y of one
-// sample.  Their S input rows are S * W * C CONTIGUOUS bytes, loaded into
+// Row-staged form (the default): a workgroup builds RPB output rows Y of
+// IPB samples (4; hvk_gemm_variant 61: one).  Their S input rows are S * W * C CONTIGUOUS bytes, loaded into
 // LDS by 16-B loads (unaligned addresses are fine on gfx950), out-of-image
 // rows zero-filled; each lane then assembles 16-B output chunks (8 s2d
 // elements) from LDS bytes and stores them, a wave writing 1 KiB
 // contiguous.  Global traffic is two streams of whole lines (the per-chunk
-// kernel above read three dwords per row piece per lane).
+// kernel above read three dwords per row piece per lane).  The chunk's
+// mean / 1/dispersion (32 B of loads per 16 B written) and its LDS byte
+// offsets serve all IPB samples.
 extern int hvk_gemm_variant;
 
-template <int S, int C, int RPB>
+template <int S, int C, int RPB, int IPB>
 __global__ void __launch_bounds__(256)
 fill_s2d_rows_kernel(const uint8_t* __restrict__ src, long long src_bytes,
                      const int* shuffled, int start, int count, int max_mb,
@@ -1037,54 +1039,62 @@ fill_s2d_rows_kernel(const uint8_t* __restrict__ src, long long src_bytes,
   constexpr int PIX = S * S * C, CPP = PIX / 8;
   static_assert(PIX % 8 == 0, "16-B chunks");
   extern __shared__ __attribute__((aligned(16))) uint8_t rows_lds[];
-  const int i = blockIdx.y;
+  const int i0 = blockIdx.y * IPB;
   const int Y0 = blockIdx.x * RPB;
   const int WC = W * C;
   const int RB = (S * WC + 15) & ~15;   // LDS bytes per output row's input
-  const int sid = i < count ? shuffled[start + i] : -1;
   const int t = threadIdx.x;
-  if (blockIdx.x == 0 && t == 0) {
-    if (labels_out) labels_out[i] = (sid >= 0 && labels) ? labels[sid] : -1;
-    if (idx_out) idx_out[i] = sid;
+  int sid[IPB];
+#pragma unroll
+  for (int b = 0; b < IPB; ++b) {
+    const int i = i0 + b;
+    sid[b] = (i < max_mb && i < count) ? shuffled[start + i] : -1;
+    if (blockIdx.x == 0 && t == 0 && i < max_mb) {
+      if (labels_out) labels_out[i] = (sid[b] >= 0 && labels) ? labels[sid[b]] : -1;
+      if (idx_out) idx_out[i] = sid[b];
+    }
   }
   const int nrow = min(RPB, H2 - Y0);
   const int cpr = W2 * CPP;             // output chunks per row
-  uint16_t* out = dst + (long long)i * H2 * cpr * 8;
-  if (sid < 0) {
-    for (int q = t; q < nrow * cpr; q += 256)
-      *(uint4*)(out + ((long long)Y0 * cpr + q) * 8) = make_uint4(0, 0, 0, 0);
-    return;
-  }
-  // stage: for each of the nrow output rows, its S input rows
-  const long long base = (long long)sid * H * WC;
+  // stage: for each image and each of the nrow output rows, its S input rows
   const int nch = RB / 16;
-  for (int q = t; q < nrow * nch; q += 256) {
-    const int r = q / nch, c = q - (q / nch) * nch;
+  for (int q = t; q < IPB * nrow * nch; q += 256) {
+    const int b = q / (nrow * nch);
+    const int q2 = q - b * (nrow * nch);
+    const int r = q2 / nch, c = q2 - (q2 / nch) * nch;
     const int byte = c * 16;                 // within the S rows
-    const int dy = byte / WC;
-    const int iy = S * (Y0 + r) - pt + dy;
     uint4 v = make_uint4(0, 0, 0, 0);
-    // the chunk may straddle input rows: load it whole when every row it
-    // touches is in the image and the 16 bytes stay inside the buffer,
-    // else byte by byte
-    const long long g = base + (long long)(S * (Y0 + r) - pt) * WC + byte;
-    const int dy2 = min(byte + 15, S * WC - 1) / WC;
-    const int iy2 = S * (Y0 + r) - pt + dy2;
-    if (iy >= 0 && iy2 < H && g + 16 <= src_bytes) {
-      __builtin_memcpy(&v, src + g, 16);
-    } else {
-      uint8_t b[16];
+    int sidb = -1;   // sid[b] (a register array: no dynamic index)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int bb = byte + e;
-        const int ry = S * (Y0 + r) - pt + bb / WC;
-        b[e] = (bb < S * WC && ry >= 0 && ry < H) ? src[g + e] : 0;
+    for (int bb = 0; bb < IPB; ++bb)
+      if (bb == b) sidb = sid[bb];
+    if (sidb >= 0) {
+      const long long base = (long long)sidb * H * WC;
+      const int iy = S * (Y0 + r) - pt + byte / WC;
+      // the chunk may straddle input rows: load it whole when every row it
+      // touches is in the image and the 16 bytes stay inside the buffer,
+      // else byte by byte
+      const long long g = base + (long long)(S * (Y0 + r) - pt) * WC + byte;
+      const int dy2 = min(byte + 15, S * WC - 1) / WC;
+      const int iy2 = S * (Y0 + r) - pt + dy2;
+      if (iy >= 0 && iy2 < H && g + 16 <= src_bytes) {
+        __builtin_memcpy(&v, src + g, 16);
+      } else {
+        uint8_t e8[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int bb2 = byte + e;
+          const int ry = S * (Y0 + r) - pt + bb2 / WC;
+          e8[e] = (bb2 < S * WC && ry >= 0 && ry < H) ? src[g + e] : 0;
+        }
+        __builtin_memcpy(&v, e8, 16);
       }
-      __builtin_memcpy(&v, b, 16);
     }
-    *(uint4*)(rows_lds + r * RB + byte) = v;
+    *(uint4*)(rows_lds + (b * RPB + r) * RB + byte) = v;
   }
   __syncthreads();
+  // each output chunk: its 8 LDS byte offsets, mean and 1/dispersion once,
+  // then the IPB images
   for (int q = t; q < nrow * cpr; q += 256) {
     const int r = q / cpr, cc = q - (q / cpr) * cpr;
     const int X = cc / CPP, j = cc - (cc / CPP) * CPP;
@@ -1094,7 +1104,8 @@ fill_s2d_rows_kernel(const uint8_t* __restrict__ src, long long src_bytes,
     const float4 ma = m4[0], mb = m4[1], ra = r4[0], rb = r4[1];
     const float mm[8] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
     const float rr[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-    float f[8];
+    int off[8];
+    bool in[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int el = 8 * j + e;
@@ -1102,11 +1113,26 @@ fill_s2d_rows_kernel(const uint8_t* __restrict__ src, long long src_bytes,
       const int dx = rem / C, c = rem - dx * C;
       const int ix = S * X + dx - pl;
       // outside the image: the affine map is (0, 1) there, the byte 0
-      const uint8_t b = (ix >= 0 && ix < W)
-          ? rows_lds[r * RB + dy * WC + ix * C + c] : (uint8_t)0;
-      f[e] = ((float)b - mm[e]) * rr[e];
+      in[e] = ix >= 0 && ix < W;
+      off[e] = r * RB + dy * WC + ix * C + c;
     }
-    *(uint4*)(out + ch * 8) = pack_bf16x8(f);
+#pragma unroll
+    for (int b = 0; b < IPB; ++b) {
+      if (i0 + b >= max_mb) break;
+      uint16_t* out = dst + (long long)(i0 + b) * H2 * cpr * 8;
+      uint4 o = make_uint4(0, 0, 0, 0);
+      if (sid[b] >= 0) {
+        const uint8_t* lb = rows_lds + b * RPB * RB;
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t v = in[e] ? lb[off[e]] : (uint8_t)0;
+          f[e] = ((float)v - mm[e]) * rr[e];
+        }
+        o = pack_bf16x8(f);
+      }
+      *(uint4*)(out + ch * 8) = o;
+    }
   }
 }
 
@@ -1121,11 +1147,24 @@ HVK_API int hvk_fill_minibatch_s2d(const void* src, long long src_bytes,
   if (S != 4 || C != 3 || ((uintptr_t)dst & 15) || ((uintptr_t)mean2 & 15) ||
       ((uintptr_t)rdisp2 & 15) || max_mb > 65535 * 4)
     return -1;
-  if (hvk_gemm_variant != 60 && max_mb <= 65535) {
+  if (hvk_gemm_variant == 61 && max_mb <= 65535) {   // one image per block
     constexpr int RPB = 2;
     const size_t lds = (size_t)RPB * ((S * W * C + 15) & ~15);
-    hipLaunchKernelGGL((fill_s2d_rows_kernel<4, 3, RPB>),
+    hipLaunchKernelGGL((fill_s2d_rows_kernel<4, 3, RPB, 1>),
                        dim3((H2 + RPB - 1) / RPB, max_mb), dim3(256), lds, s,
+                       (const uint8_t*)src, src_bytes, shuffled, start, count,
+                       max_mb, H, W, pt, pl, H2, W2, mean2, rdisp2,
+                       (uint16_t*)dst, labels, labels_out, idx_out);
+    return (int)launch_status(s);
+  }
+  if (hvk_gemm_variant != 60 && max_mb <= 65535 * 4) {
+    // four images per block: the mean / dispersion loads and the chunk's
+    // byte offsets once for all four
+    constexpr int RPB = 2, IPB = 4;
+    const size_t lds = (size_t)IPB * RPB * ((S * W * C + 15) & ~15);
+    hipLaunchKernelGGL((fill_s2d_rows_kernel<4, 3, RPB, IPB>),
+                       dim3((H2 + RPB - 1) / RPB, (max_mb + IPB - 1) / IPB),
+                       dim3(256), lds, s,
                        (const uint8_t*)src, src_bytes, shuffled, start, count,
                        max_mb, H, W, pt, pl, H2, W2, mean2, rdisp2,
                        (uint16_t*)dst, labels, labels_out, idx_out);

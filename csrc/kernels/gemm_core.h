@@ -713,6 +713,76 @@ struct Epi {
       if (amax && q8.q) q8_store8(q8, idx, ob, qs, *amax);
     }
   }
+  // 4 consecutive columns of one row from a lane's accumulator register
+  // quad (the T4 loop's direct epilogue: no LDS staging); fast_ok(), no
+  // fused fp8 copy, n % 4 == 0 and n + 4 <= N (v is scratch)
+  __device__ __forceinline__ void store4_fast(int gi, int m, int n,
+                                              float* v) const {
+    const int gm = m + gi * grow, gn = n + gi * gcol;
+    const long long idx = (long long)gm * ldc + gn;
+    if (alpha != 1.f) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= alpha;
+    }
+    if (beta != 0.f) {
+      float o[4];
+      if (out_f32) {
+        const float4 d = *(const float4*)((const float*)c + idx);
+        o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = d.w;
+      } else {
+        const uint2 ov = *(const uint2*)((const uint16_t*)c + idx);
+        const uint16_t* oh = (const uint16_t*)&ov;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = bf2f(oh[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += beta * o[q];
+    }
+    if (bias_mode == 1) {
+      const float4 b = *(const float4*)(bias + gn);
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    act_fwd_n<4>(v, act);
+    if (aux) {
+      const uint2 av = *(const uint2*)(aux + (long long)gm * ld_aux + gn);
+      const uint16_t* ah = (const uint16_t*)&av;
+      float a[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = bf2f(ah[q]);
+      act_bwd_mul_n<4>(v, a, aux_act);
+    }
+    if (out_f32) {
+      *(float4*)((float*)c + idx) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      *(uint2*)((uint16_t*)c + idx) =
+          make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+  }
+  // 4 consecutive columns of one row, finished in registers and packed to
+  // bf16 (the T4 register epilogue): alpha, per-column bias, activation,
+  // derivative of the layer below; fast_ok(), beta == 0, n % 4 == 0
+  __device__ __forceinline__ uint2 pre4(int gi, int m, int n, float* v) const {
+    const int gm = m + gi * grow, gn = n + gi * gcol;
+    if (alpha != 1.f) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= alpha;
+    }
+    if (bias_mode == 1) {
+      const float4 b = *(const float4*)(bias + gn);
+      v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+    }
+    act_fwd_n<4>(v, act);
+    if (aux) {
+      const uint2 av = *(const uint2*)(aux + (long long)gm * ld_aux + gn);
+      float a[4];
+      a[0] = __uint_as_float(av.x << 16);
+      a[1] = __uint_as_float(av.x & 0xffff0000u);
+      a[2] = __uint_as_float(av.y << 16);
+      a[3] = __uint_as_float(av.y & 0xffff0000u);
+      act_bwd_mul_n<4>(v, a, aux_act);
+    }
+    return make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
   // 8 consecutive columns of one row: 16-B vector stores when possible
   __device__ __forceinline__ void store8(int gi, int m, int n,
                                          const float* v) const {
@@ -1255,6 +1325,23 @@ template <class LA, bool AK, class LB, bool BKM, bool BUF>
 hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                      int K, int k_split, int tiles_n, int tiles, int splits,
                      int bn, dim3 grid, hipStream_t s) {
+  // implicit-GEMM convolution forward / backward-data with >= 256 output
+  // channels per group (VGG conv3-5, AlexNet conv3 backward-data): the
+  // 256 x 256 ping-pong loop, 0.0078 operand bytes per FLOP against the T4
+  // loop's 0.013 (gemm_pp.h).  Default settings only (any A/B variant keeps
+  // them on T4 / the 128-row loop); hvk_gemm_variant 56 takes it for every
+  // conv with >= 256 outputs per group (tests)
+  if constexpr (BUF && AK && BKM && std::is_same<LB, DenseK>::value &&
+                (std::is_same<LA, ConvFwdA>::value ||
+                 std::is_same<LA, ConvDgradA>::value)) {
+    const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+    const bool force = hvk_gemm_variant == 56 && N >= 256;
+    if ((hvk_gemm_variant < 0 || force) && splits == 1 && !epi.atomic &&
+        !epi.slice && la.dma_ok() && lb.dma_ok() &&
+        (force || want_pp256(M, N, 1, groups)))
+      return go_pp256<LA, AK, LB, BKM>(la, lb, epi, M, N, K, k_split, 1,
+                                       groups, s);
+  }
   // implicit-GEMM convolutions: 192 x 128 tiles, two workgroups per CU
   // (gemm_t4.h)
   if constexpr (BUF && t4_pair_ok<LA, AK, LB, BKM>()) {

@@ -193,6 +193,31 @@ struct Epi8 {
   int q8_fmt;
 };
 
+// the fused fp8 copy of 8 stored bf16 outputs: quantise what the consumer
+// would read (the bf16-rounded values), amax of them into *amax
+__device__ __forceinline__ void q8_out8(const Epi8& e, long long idx,
+                                        const uint4& ob, float qs,
+                                        float* amax) {
+  const uint32_t w4[4] = {ob.x, ob.y, ob.z, ob.w};
+  float r[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    r[2 * q] = __uint_as_float(w4[q] << 16);
+    r[2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
+  }
+  const float lim = e.q8_fmt == 0 ? 448.f : 57344.f;
+  float mx = *amax;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) mx = fmaxf(mx, fabsf(r[q]));
+  *amax = mx;
+  uint2 qv;
+  qv.x = pack4_fp8(sat(r[0] * qs, lim), sat(r[1] * qs, lim),
+                   sat(r[2] * qs, lim), sat(r[3] * qs, lim), e.q8_fmt);
+  qv.y = pack4_fp8(sat(r[4] * qs, lim), sat(r[5] * qs, lim),
+                   sat(r[6] * qs, lim), sat(r[7] * qs, lim), e.q8_fmt);
+  *(uint2*)(e.q8 + idx) = qv;
+}
+
 __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
                                        int m, int n, const float* v,
                                        float qs = 1.f, float* amax = nullptr) {
@@ -244,27 +269,7 @@ __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
   if (vec) {
     const uint4 ob = pack_bf16x8(o);
     *(uint4*)(e.c + idx) = ob;
-    if (e.q8) {
-      // quantise what the consumer would read: the bf16-rounded output
-      const uint32_t w4[4] = {ob.x, ob.y, ob.z, ob.w};
-      float r[8];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        r[2 * q] = __uint_as_float(w4[q] << 16);
-        r[2 * q + 1] = __uint_as_float(w4[q] & 0xffff0000u);
-      }
-      const float lim = e.q8_fmt == 0 ? 448.f : 57344.f;
-      float mx = *amax;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) mx = fmaxf(mx, fabsf(r[q]));
-      *amax = mx;
-      uint2 qv;
-      qv.x = pack4_fp8(sat(r[0] * qs, lim), sat(r[1] * qs, lim),
-                       sat(r[2] * qs, lim), sat(r[3] * qs, lim), e.q8_fmt);
-      qv.y = pack4_fp8(sat(r[4] * qs, lim), sat(r[5] * qs, lim),
-                       sat(r[6] * qs, lim), sat(r[7] * qs, lim), e.q8_fmt);
-      *(uint2*)(e.q8 + idx) = qv;
-    }
+    if (e.q8) q8_out8(e, idx, ob, qs, amax);
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -281,6 +286,93 @@ __device__ __forceinline__ void store8(const Epi8& e, float alpha, int gi,
         }
     }
   }
+}
+
+// 4 consecutive columns of one row from a lane's accumulator quad (the T4
+// loop's direct epilogue); the launch checked store4_ok: 4-aligned rows,
+// columns and aux rows, a 16-B aligned bias, n % 4 == 0 and N % 4 == 0
+__host__ __device__ __forceinline__ bool store4_ok(const Epi8& e) {
+  return (e.ldc & 3) == 0 && (e.gcol & 3) == 0 && (e.N & 3) == 0 &&
+         (!e.aux || (e.ld_aux & 3) == 0) &&
+         (!e.bias || (((uintptr_t)e.bias) & 15) == 0);
+}
+__device__ __forceinline__ void store4(const Epi8& e, float alpha, int gi,
+                                       int m, int n, const float* v,
+                                       float qs, float* amax) {
+  const int gn = n + gi * e.gcol;
+  const long long idx = (long long)m * e.ldc + gn;
+  float o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = v[q] * alpha;
+  if (e.bias) {
+    const float4 b = *(const float4*)(e.bias + gn);
+    o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w;
+  }
+  act_fwd_n<4>(o, e.act);
+  if (e.aux) {
+    const uint2 av = *(const uint2*)(e.aux + (long long)m * e.ld_aux + gn);
+    const uint16_t* ah = (const uint16_t*)&av;
+    float y[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = bf2f(ah[q]);
+    act_bwd_mul_n<4>(o, y, e.aux_act);
+  }
+  const uint2 ob = make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+  *(uint2*)(e.c + idx) = ob;
+  if (e.q8) {
+    // quantise what the consumer would read: the bf16-rounded output
+    float r[4];
+    r[0] = __uint_as_float(ob.x << 16);
+    r[1] = __uint_as_float(ob.x & 0xffff0000u);
+    r[2] = __uint_as_float(ob.y << 16);
+    r[3] = __uint_as_float(ob.y & 0xffff0000u);
+    const float lim = e.q8_fmt == 0 ? 448.f : 57344.f;
+    float mx = *amax;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mx = fmaxf(mx, fabsf(r[q]));
+    *amax = mx;
+    *(uint32_t*)(e.q8 + idx) =
+        pack4_fp8(sat(r[0] * qs, lim), sat(r[1] * qs, lim),
+                  sat(r[2] * qs, lim), sat(r[3] * qs, lim), e.q8_fmt);
+  }
+}
+
+// 4 consecutive columns of one row finished in registers and packed to
+// bf16 (the T4 register epilogue): alpha, bias, activation, derivative of
+// the layer below - store8's arithmetic per element
+__device__ __forceinline__ uint2 pre4_8(const Epi8& e, float alpha, int gi,
+                                        int m, int n, const float* v) {
+  const int gn = n + gi * e.gcol;
+  float o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = v[q] * alpha;
+  if (e.bias) {
+    const float4 b = *(const float4*)(e.bias + gn);
+    o[0] += b.x; o[1] += b.y; o[2] += b.z; o[3] += b.w;
+  }
+  float a[4] = {1.f, 1.f, 1.f, 1.f};
+  if (e.aux) {
+    const uint2 av = *(const uint2*)(e.aux + (long long)m * e.ld_aux + gn);
+    float y[4];
+    y[0] = __uint_as_float(av.x << 16);
+    y[1] = __uint_as_float(av.x & 0xffff0000u);
+    y[2] = __uint_as_float(av.y << 16);
+    y[3] = __uint_as_float(av.y & 0xffff0000u);
+    act_bwd_mul_n<4>(a, y, e.aux_act);   // a = act_bwd(y), as store8
+  }
+  act_fwd_n<4>(o, e.act);
+  if (e.aux) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] *= a[q];
+  }
+  return make_uint2(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]));
+}
+// the register epilogue applies: 8-aligned rows, columns and N, 4-aligned
+// aux rows, a 16-B aligned bias
+__host__ __device__ __forceinline__ bool regepi_ok(const Epi8& e) {
+  return (e.ldc & 7) == 0 && (e.gcol & 7) == 0 && (e.N & 7) == 0 &&
+         (((uintptr_t)e.c) & 15) == 0 && (!e.aux || (e.ld_aux & 3) == 0) &&
+         (!e.bias || (((uintptr_t)e.bias) & 15) == 0);
 }
 
 // ------------------------------------------------------------------ kernel
@@ -478,11 +570,24 @@ gemm_fp8_kernel(LA la, LB lb, Epi8 epi, int M, int N, int K, int tiles_n,
 // 16x16x128 (32 cycles each, twice the bf16 work per cycle).  P = the
 // implicit im2col / gathered-dY rows (fast DRow / DTap addressing), Q = the
 // weights (Dense8).
-template <class LP, int FA, int FB>
+//
+// QR = 64 (outputs of 64 channels per group: VGG conv1_2 forward, conv1_2 /
+// conv2_1 backward-data) takes PR = 256 rows and stacks the four waves
+// along P (each 64 x 64, 16 MFMAs per K tile): the same 40-KiB stage.
+//
+// DIR: the direct epilogue - the MFMAs compute the transposed tile (same
+// values), so a lane's accumulator quad is 4 consecutive output channels of
+// one pixel and goes straight to global memory (no LDS staging).
+template <class LP, int FA, int FB, int PR = 192, int QR = 128,
+          int EP = 0>
 __global__ void __launch_bounds__(256, 2)
 gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
                    int tiles_q, int tiles, int gm) {
-  constexpr int PR = 192, QR = 128;
+  static_assert((PR == 192 && QR == 128) || (PR == 256 && QR == 64),
+                "tile shapes");
+  constexpr bool STK = QR == 64;        // waves stacked along P
+  constexpr int MI = STK ? PR / 64 : PR / 32;   // m-tiles per wave
+  constexpr int NJ = 4;                         // n-tiles per wave (64 cols)
   constexpr int SP = PR * BK, SQ = QR * BK, SST = SP + SQ;   // bytes
   constexpr int NSP = PR / 8 / 4, NSQ = QR / 8 / 4;          // per wave
   constexpr int HP = PR / 2, LDC = QR + 4;
@@ -510,14 +615,15 @@ gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
   const int p0 = tp * PR, q0 = tq * QR;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int prow = (w >> 1) * HP, qrow = (w & 1) * 64;
+  const int prow = STK ? w * (PR / 4) : (w >> 1) * HP;
+  const int qrow = STK ? 0 : (w & 1) * 64;
   const int fr = lane & 15, fq = lane >> 4;
 
-  f32x4 acc[6][4];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // DMA slots: piece I = rows 8I .. 8I + 7 of the operand, lane -> row
   // 8I + (lane >> 3), chunk (lane & 7) ^ (row & 7)
@@ -568,16 +674,21 @@ gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
     // tile t + 1 into the stage tile t - 1 used (read before the barrier
     // that ended step t - 1)
     if (kt + 1 < nk) issue((kt + 1) * BK, smem + ((kt + 1) & 1) * SST);
-    i32x8 bq[4];
+    i32x8 bq[NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bq[j] = frag(sQ, qrow + j * 16);
+    for (int j = 0; j < NJ; ++j) bq[j] = frag(sQ, qrow + j * 16);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const i32x8 a = frag(sP, prow + i * 16);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-            a, bq[j], acc[i][j], FA, FB, 0, 127, 0, 127);
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (EP != 0)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              bq[j], a, acc[i][j], FB, FA, 0, 127, 0, 127);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              a, bq[j], acc[i][j], FA, FB, 0, 127, 0, 127);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -590,15 +701,59 @@ gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
   float amax = 0.f;
   float* sC = (float*)smem;
   constexpr int CH = QR / 8;
+  if constexpr (EP == 1) {
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int m = p0 + prow + i * 16 + fr;
+        const int n = q0 + qrow + j * 16 + fq * 4;
+        if (m < P && n < Q) {
+          const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2],
+                              acc[i][j][3]};
+          store4(epi, alpha, gi, m, n, v, qs, &amax);
+        }
+      }
+  }
+  if constexpr (EP == 2) {
+    // register epilogue: lane quads finished and packed to bf16 into a bf16
+    // image of the C tile (one pass), then whole 16-B row chunks out (and
+    // the fp8 copy from the same bf16 values)
+    constexpr int LDO = QR + 8;
+    static_assert(PR * LDO * 2 <= 2 * SST, "bf16 C tile fits the ring");
+    uint16_t* sO = (uint16_t*)smem;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int ml = prow + i * 16 + fr, nl = qrow + j * 16 + fq * 4;
+        const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2],
+                            acc[i][j][3]};
+        uint2 o = make_uint2(0u, 0u);
+        if (p0 + ml < P && q0 + nl < Q)
+          o = pre4_8(epi, alpha, gi, p0 + ml, q0 + nl, v);
+        *(uint2*)(sO + ml * LDO + nl) = o;
+      }
+    __syncthreads();
+    for (int q = t; q < PR * CH; q += 256) {
+      const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
+      if (p0 + row >= P || q0 + c8 >= Q) continue;
+      const uint4 ob = *(const uint4*)(sO + row * LDO + c8);
+      const long long idx =
+          (long long)(p0 + row) * epi.ldc + q0 + c8 + gi * epi.gcol;
+      *(uint4*)(epi.c + idx) = ob;
+      if (epi.q8) q8_out8(epi, idx, ob, qs, &amax);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < (EP != 0 ? 0 : 2); ++e) {
     if (e) __syncthreads();
-    if ((w >> 1) == e) {
+    if ((w >> 1) == e) {    // the waves holding P rows e*HP .. +HP-1
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int rb = i * 16 + fq * 4;
+        for (int j = 0; j < NJ; ++j) {
+          const int rb = prow - e * HP + i * 16 + fq * 4;
           const int qc = qrow + j * 16 + fr;
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) sC[(rb + rr) * LDC + qc] = acc[i][j][rr];
@@ -637,20 +792,44 @@ gemm_t4_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
 // keeps the 128-row loop (A/B runs)
 inline bool want_t4_fp8(int N) {
   if (hvk_fp8_variant == 71) return false;
+  if (N > 48 && N <= 64) return hvk_fp8_variant != 72;   // 256 x 64 tiles
   const int w = (N + 127) / 128 * 128 - N;
   return N >= 128 && w * 8 <= N;
 }
 
-template <class LP, int FA, int FB>
-hipError_t go_t4_fp8(const LP& lp, const Dense8& lq, const Epi8& e, int M,
-                     int N, int K, int groups, hipStream_t s) {
+template <class LP, int FA, int FB, int EP>
+hipError_t go_t4_fp8_(const LP& lp, const Dense8& lq, const Epi8& e, int M,
+                      int N, int K, int groups, hipStream_t s) {
+  if (N <= 64) {
+    const int tiles = (M + 255) / 256;
+    hipLaunchKernelGGL((gemm_t4_fp8_kernel<LP, FA, FB, 256, 64, EP>),
+                       dim3((unsigned)((long long)tiles * groups)), dim3(256),
+                       0, s, lp, lq, e, M, N, K, 1, tiles, 1);
+    return launch_status(s);
+  }
   const int tiles_q = (N + 127) / 128;
   const int tiles = (M + 191) / 192 * tiles_q;
   const int gm = tiles_q >= 8 ? 8 : 1;
-  hipLaunchKernelGGL((gemm_t4_fp8_kernel<LP, FA, FB>),
+  hipLaunchKernelGGL((gemm_t4_fp8_kernel<LP, FA, FB, 192, 128, EP>),
                      dim3((unsigned)((long long)tiles * groups)), dim3(256), 0,
                      s, lp, lq, e, M, N, K, tiles_q, tiles, gm);
   return launch_status(s);
+}
+
+// the direct epilogue is opt-in (hvk_fp8_variant 74): measured slower than
+// the LDS-staged one (VGG b512 conv2_2 forward 1241 -> 868 TF, conv1_2
+// 640 -> 581; the 8-B lane quads leave 32-B pieces of each output row per
+// store instruction)
+template <class LP, int FA, int FB>
+hipError_t go_t4_fp8(const LP& lp, const Dense8& lq, const Epi8& e, int M,
+                     int N, int K, int groups, hipStream_t s) {
+  if (hvk_fp8_variant == 74 && store4_ok(e))
+    return go_t4_fp8_<LP, FA, FB, 1>(lp, lq, e, M, N, K, groups, s);
+  // the register epilogue with a bf16 C image (hvk_fp8_variant 73 keeps the
+  // f32-staged one)
+  if (hvk_fp8_variant != 73 && regepi_ok(e))
+    return go_t4_fp8_<LP, FA, FB, 2>(lp, lq, e, M, N, K, groups, s);
+  return go_t4_fp8_<LP, FA, FB, 0>(lp, lq, e, M, N, K, groups, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -689,9 +868,37 @@ struct PP8Op {
   }
 };
 
-template <int FA, int FB>
+// the implicit-GEMM conv operand (ConvFwdA8 / ConvDgradA8) of the same
+// loop: pieces as PP8Op, addresses from the row's DRow and the K tile's
+// DTap (fast conv addressing, conv_geom.h)
+template <class L>
+struct PP8OpC {
+  DRow fa[4];
+  int kc;
+  __device__ __forceinline__ void init(const L& l, int r0, int w, int lane) {
+    kc = 16 * ((lane & 7) ^ ((lane >> 3) & 7));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      fa[i] = l.drow(r0 + 8 * (w * 4 + i) + (lane >> 3));
+  }
+  __device__ __forceinline__ void issue(const L& l, int k0, uint8_t* s, int w,
+                                        int i0, int n) {
+    const DTap tp = l.dtap(k0 + kc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i >= i0 && i < i0 + n)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)l.dsrc(fa[i], tp),
+            (__attribute__((address_space(3))) void*)(s + (w * 4 + i) * 1024),
+            16, 0, 0);
+  }
+};
+
+// LP: Dense8 (dense GEMMs) or a conv A loader (groups: blockIdx over
+// tiles x groups)
+template <class LP, int FA, int FB>
 __global__ void __launch_bounds__(512, 1)
-gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
+gemm_pp256_fp8_kernel(LP lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
                       int tiles_q, int tiles, int gm) {
   constexpr int TB = 256 * BK;           // bytes per operand stage
   constexpr int SST = 2 * TB;            // A + B
@@ -700,6 +907,7 @@ gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * SST];
   const int wgid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wgid % tiles;
+  const int gi = wgid / tiles;
   int tp, tq;
   if (gm > 1) {
     const int tiles_p = tiles / tiles_q;
@@ -713,6 +921,8 @@ gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
     tp = tile / tiles_q;
     tq = tile - tp * tiles_q;
   }
+  if constexpr (!std::is_same<LP, Dense8>::value) lp.group(gi);
+  lq.group(gi);
   const int p0 = tp * 256, q0 = tq * 256;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -726,7 +936,9 @@ gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  PP8Op op, oq;
+  typename std::conditional<std::is_same<LP, Dense8>::value, PP8Op,
+                            PP8OpC<LP>>::type op;
+  PP8Op oq;
   op.init(lp, p0, w, lane);
   oq.init(lq, q0, w, lane);
   // 32 bytes of row (rowbase + fr): chunks fq, fq + 4 at c ^ (row & 7)
@@ -856,7 +1068,7 @@ gemm_pp256_fp8_kernel(Dense8 lp, Dense8 lq, Epi8 epi, int P, int Q, int K,
       const float4 lo = src[0], hi = src[1];
       v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
       v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-      store8(epi, alpha, 0, m0 + row, q0 + c8, v, qs, &amax);
+      store8(epi, alpha, gi, m0 + row, q0 + c8, v, qs, &amax);
     }
   }
   if (epi.q8) {
@@ -885,15 +1097,29 @@ inline bool want_pp256_fp8(const Dense8& la, const Dense8& lb, int M, int N) {
   return t >= 256 && wn * 8 <= N;
 }
 
-template <int FA, int FB>
-hipError_t go_pp256_fp8(const Dense8& la, const Dense8& lb, const Epi8& e,
-                        int M, int N, int K, hipStream_t s) {
+template <class LA, int FA, int FB>
+hipError_t go_pp256_fp8(const LA& la, const Dense8& lb, const Epi8& e, int M,
+                        int N, int K, int groups, hipStream_t s) {
   const int tiles_q = (N + 255) / 256;
   const int tiles = (M + 255) / 256 * tiles_q;
   const int gm = tiles_q >= 8 ? 8 : 1;
-  hipLaunchKernelGGL((gemm_pp256_fp8_kernel<FA, FB>), dim3(tiles), dim3(512),
-                     0, s, la, lb, e, M, N, K, tiles_q, tiles, gm);
+  hipLaunchKernelGGL((gemm_pp256_fp8_kernel<LA, FA, FB>),
+                     dim3((unsigned)((long long)tiles * groups)), dim3(512), 0,
+                     s, la, lb, e, M, N, K, tiles_q, tiles, gm);
   return launch_status(s);
+}
+
+// fp8 convolutions with >= 256 outputs per group (VGG conv3-5 forward and
+// backward-data) on the 256 x 256 loop where it fills the CUs (<= 1/8 of the
+// column tile wasted, >= one tile per CU); default settings only,
+// hvk_fp8_variant 75 forces it (tests)
+inline bool want_pp256_fp8_conv(const Dense8& lb, int M, int N, int groups) {
+  if (!lb.buf_ok()) return false;
+  const int wn = (N + 255) / 256 * 256 - N;
+  if (N < 256 || wn * 8 > N) return false;
+  if (hvk_fp8_variant == 75) return true;
+  if (hvk_fp8_variant >= 0) return false;
+  return (long long)((M + 255) / 256) * ((N + 255) / 256) * groups >= 256;
 }
 
 inline bool use_bn64(int N) {
@@ -908,11 +1134,13 @@ hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
   if constexpr (std::is_same<LA, Dense8>::value &&
                 std::is_same<LB, Dense8>::value) {
     if (groups == 1 && want_pp256_fp8(la, lb, M, N))
-      return go_pp256_fp8<FA, FB>(la, lb, e, M, N, K, s);
+      return go_pp256_fp8<Dense8, FA, FB>(la, lb, e, M, N, K, 1, s);
   }
   if constexpr ((std::is_same<LA, ConvFwdA8>::value ||
                  std::is_same<LA, ConvDgradA8>::value) &&
                 std::is_same<LB, Dense8>::value) {
+    if (want_pp256_fp8_conv(lb, M, N, groups))
+      return go_pp256_fp8<LA, FA, FB>(la, lb, e, M, N, K, groups, s);
     if (want_t4_fp8(N)) return go_t4_fp8<LA, FA, FB>(la, lb, e, M, N, K,
                                                       groups, s);
   }

@@ -63,20 +63,27 @@ constexpr bool pp_loader_ok() {
 // One operand's DMA slots.  ROWS (256 / 128) x 64 k of bf16 = ROWS / 64
 // pieces of 1 KiB per wave.  K-major slot I: rows 8I .. 8I+7, all 8 chunks;
 // MN-major slot I: image I / 16 (128 columns each), k-rows 4 (I % 16) .. +3.
+// K-major implicit-GEMM conv operands (ConvFwdA / ConvDgradA, kFast): the
+// row's pixel and tap masks once (DRow), the lane's tap once per K tile
+// (DTap), as in the T4 loop
 template <class L, bool KM, int ROWS>
 struct PPOp {
   static constexpr int NS = ROWS / 64;
+  static constexpr bool FAST = KM && L::kFast;
   __amdgpu_buffer_rsrc_t rs;
   uint32_t v[NS];
   int kr[NS];
   int kc;
+  DRow fa[FAST ? NS : 1];
   __device__ __forceinline__ void init(const L& l, int r0, int w, int lane) {
     rs = dma_rsrc(l.dbase());
     kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       const int I = w * NS + i;
-      if constexpr (KM) {
+      if constexpr (FAST) {
+        fa[i] = l.drow(r0 + 8 * I + (lane >> 3));
+      } else if constexpr (KM) {
         v[i] = l.row_voff(r0 + 8 * I + (lane >> 3));
       } else {
         const int Ii = I & 15, h = I >> 4;
@@ -95,7 +102,13 @@ struct PPOp {
   // operand's four pieces over two phases)
   __device__ __forceinline__ void issue_part(const L& l, int k0, uint16_t* s,
                                              int w, int i0, int n) {
-    if constexpr (KM) {
+    if constexpr (FAST) {
+      const DTap tp = l.dtap(k0 + kc);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if (i >= i0 && i < i0 + n)
+          dma16(rs, dst(s, w * NS + i), l.dvoff(fa[i], tp));
+    } else if constexpr (KM) {
       const bool kin = k0 + kc < l.K;
       const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
 #pragma unroll
@@ -112,7 +125,12 @@ struct PPOp {
     }
   }
   __device__ __forceinline__ void issue(const L& l, int k0, uint16_t* s, int w) {
-    if constexpr (KM) {
+    if constexpr (FAST) {
+      const DTap tp = l.dtap(k0 + kc);
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        dma16(rs, dst(s, w * NS + i), l.dvoff(fa[i], tp));
+    } else if constexpr (KM) {
       const bool kin = k0 + kc < l.K;
       const uint32_t kbyte = 2u * (uint32_t)(k0 + kc);
 #pragma unroll

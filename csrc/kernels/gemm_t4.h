@@ -45,6 +45,16 @@
 
 constexpr int T4_QR = 128;
 
+// Diagnostic builds only (tools/build_abl.py; wrong results by design): bit 1
+// skips the main loop's LDS-DMA, bit 2 the epilogue (the accumulators are
+// kept live by a never-taken store), bit 4 the main loop's waits and
+// barriers, bit 8 re-reads the first K step's sources every step (the same
+// LDS-DMA traffic, all of it L1 / L2 hits), bit 16 as 8 for the im2col
+// operands with the addresses computed once (no per-step addressing VALU).
+#ifndef HVK_T4_ABL
+#define HVK_T4_ABL 0
+#endif
+
 __device__ __forceinline__ int t4_sw(int r) {
   return (0x78 >> (2 * ((r >> 2) & 3))) & 3;
 }
@@ -76,6 +86,9 @@ struct T4Op {
   int kc;
   DRow fa[KM && FAST ? NS : 1];
   typename DColOf<L, !KM && FAST>::type fb[!KM && FAST ? NS : 1];
+  // ABL 16 (diagnostic): the first step's sources, reused every step
+  uint32_t v0[(HVK_T4_ABL & 16) && KM && FAST ? NS : 1];
+  const uint16_t* p0[(HVK_T4_ABL & 16) && !KM && FAST ? NS : 1];
 
   __device__ __forceinline__ void init(const L& l, int r0, int kbeg, int w,
                                        int lane) {
@@ -93,6 +106,11 @@ struct T4Op {
         if constexpr (FAST) fa[i] = l.drow(row);
         else v[i] = l.row_voff(row);
       }
+      if constexpr ((HVK_T4_ABL & 16) && FAST) {
+        const DTap tp = l.dtap(kbeg + kc);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) v0[i] = l.dvoff(fa[i], tp);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NS; ++i) {
@@ -102,6 +120,7 @@ struct T4Op {
         const int c = 16 * ((pc >> 1) ^ t4_mnsw<IMG>(kr[i])) + 8 * (pc & 1);
         if constexpr (FAST) fb[i] = l.dcol(r0 + c, kbeg + kr[i], false);
         else v[i] = l.col_voff(r0 + c, kr[i]);
+        if constexpr ((HVK_T4_ABL & 16) && FAST) p0[i] = l.dsrc(fb[i]);
       }
     }
   }
@@ -109,6 +128,21 @@ struct T4Op {
   // steps must be issued in order)
   __device__ __forceinline__ void issue(const L& l, int k0, uint16_t* s,
                                         int w) {
+    if constexpr ((HVK_T4_ABL & 16) && FAST) {
+      // diagnostic: the same LDS-DMA traffic without per-step addressing
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        if constexpr (KM) {
+          dma16(rs, s + (w * NS + i) * 512, v0[i]);
+        } else {
+          __builtin_amdgcn_global_load_lds(
+              (const void*)p0[i],
+              (__attribute__((address_space(3))) void*)(s + (w * NS + i) * 512),
+              16, 0, 0);
+        }
+      }
+      return;
+    }
     if constexpr (KM && FAST) {
       const DTap tp = l.dtap(k0 + kc);
 #pragma unroll
@@ -175,7 +209,7 @@ __device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int ks,
 // qrow = 0 of the workgroups with tq = 0).  bgrad[row + gi * grow] is
 // stored (bg_store, an unsplit overwrite) or atomically added.
 template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS, int BKT,
-          int BIAS = 0>
+          int BIAS = 0, int EP = 0>
 __global__ void __launch_bounds__(256, 2)
 gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
                int tiles_q, int tiles, int splits, int gm, float* bgrad,
@@ -258,58 +292,151 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  int scur = 0, spre = NST - 1;  // stage of step t, of step t + NST - 1
-  for (int kt = 0; kt < nk; ++kt) {
-    const uint16_t* sP = smem + scur * SST;
-    const uint16_t* sQ = sP + SP;
-    // step t + NST - 1 into the stage step t - 1 used (every wave finished
-    // reading it before the barrier that ended step t - 1)
-    const bool pre = kt + NST - 1 < nk;
-    if (pre) {
-      uint16_t* d = smem + spre * SST;
-      const int k2 = kbeg + (kt + NST - 1) * BKT;
-      op.issue(lp, k2, d, w);
-      oq.issue(lq, k2, d + SP, w);
-    }
+  // the main loop, unswitched on the wave-uniform bias flag: a branch around
+  // the bias MFMAs inside the loop split it into one basic block per m-tile
+  // and serialised the MFMA schedule (BIAS variants only)
+  auto main_loop = [&](auto with_bias) {
+    constexpr bool WB = decltype(with_bias)::value;
+    int scur = 0, spre = NST - 1;  // stage of step t, of step t + NST - 1
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint16_t* sP = smem + scur * SST;
+      const uint16_t* sQ = sP + SP;
+      // step t + NST - 1 into the stage step t - 1 used (every wave finished
+      // reading it before the barrier that ended step t - 1)
+      const bool pre = kt + NST - 1 < nk;
+      if (pre && !(HVK_T4_ABL & 1)) {
+        uint16_t* d = smem + spre * SST;
+        const int k2 = (HVK_T4_ABL & 8) ? kbeg
+                                        : kbeg + (kt + NST - 1) * BKT;
+        op.issue(lp, k2, d, w);
+        oq.issue(lq, k2, d + SP, w);
+      }
 #pragma unroll
-    for (int ks = 0; ks < BKT / 32; ++ks) {
-      bf16x8 bq[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bq[j] = t4_frag<QK, OQ::IMG, BKT>(sQ, qrow + j * 16, ks, fr, fq);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const bf16x8 a = t4_frag<PK, OP::IMG, BKT>(sP, prow + i * 16, ks, fr,
-                                                   fq);
+      for (int ks = 0; ks < BKT / 32; ++ks) {
+        bf16x8 bq[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              a, bq[j], acc[i][j], 0, 0, 0);
-        if constexpr (BIAS == 2) {
-          if (bwave)
+          bq[j] = t4_frag<QK, OQ::IMG, BKT>(sQ, qrow + j * 16, ks, fr, fq);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bf16x8 a = t4_frag<PK, OP::IMG, BKT>(sP, prow + i * 16, ks,
+                                                     fr, fq);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            // EP 1 / 2: the transposed product (a lane then holds 4
+            // consecutive C columns of one row); same K order, same values
+            if constexpr (EP != 0 && !TRANS)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  bq[j], a, acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  a, bq[j], acc[i][j], 0, 0, 0);
+          }
+          if constexpr (WB && BIAS == 2)
             accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, ones,
                                                               accb[i], 0, 0, 0);
         }
-      }
-      if constexpr (BIAS == 1) {
-        if (bwave) {
+        if constexpr (WB && BIAS == 1) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bq[j],
                                                               accb[j], 0, 0, 0);
         }
       }
+      // retire step t + 1 (three stages: step t + 2 stays in flight), then
+      // one barrier: step t + 1 visible to every wave, every read of step t
+      // done
+      if constexpr (!(HVK_T4_ABL & 4)) {
+        if (NST == 3 && pre)
+          asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      asm volatile("" ::: "memory");
+      scur = scur == NST - 1 ? 0 : scur + 1;
+      spre = spre == NST - 1 ? 0 : spre + 1;
     }
-    // retire step t + 1 (three stages: step t + 2 stays in flight), then one
-    // barrier: step t + 1 visible to every wave, every read of step t done
-    if (NST == 3 && pre) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    scur = scur == NST - 1 ? 0 : scur + 1;
-    spre = spre == NST - 1 ? 0 : spre + 1;
-  }
+  };
+  if (BIAS != 0 && bwave)
+    main_loop(std::integral_constant<bool, BIAS != 0>{});
+  else
+    main_loop(std::false_type{});
 
+  if constexpr ((HVK_T4_ABL & 2) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 1234.5f && P < 0) epi.store(0, 0, 0, sum);
+    return;
+  }
+  if constexpr (EP == 1) {
+    // direct epilogue (no atomics, slices, fp8 copy or bias column): every
+    // lane stores its accumulator quads as 4 consecutive columns of a C row
+    // - no LDS staging, no barriers
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = TRANS ? q0 + qrow + j * 16 + fr : p0 + prow + i * 16 + fr;
+        const int n = TRANS ? p0 + prow + i * 16 + fq * 4
+                            : q0 + qrow + j * 16 + fq * 4;
+        if (m < epi.M && n < epi.N) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2],
+                        acc[i][j][3]};
+          epi.store4_fast(gi, m, n, v);
+        }
+      }
+    return;
+  }
+  if constexpr (EP == 2) {
+    // register epilogue: each lane finishes its accumulator quads (4
+    // consecutive C columns of one row: alpha, bias, activation, derivative
+    // of the layer below, bf16) and writes 8 B into a bf16 image of the
+    // whole C tile in the drained ring (one pass, 48 KiB); then whole 16-B
+    // row chunks go out as in the staged epilogue (and the fp8 copy).  A
+    // quarter of the LDS traffic and of the epilogue VALU of the f32 staging
+    constexpr int OR_ = TRANS ? T4_QR : PR;      // C rows of the tile
+    constexpr int OC_ = TRANS ? PR : T4_QR;      // C columns
+    constexpr int LDO = OC_ + 8;                 // bf16 elements per row
+    static_assert(OR_ * LDO * 2 <= RING, "bf16 C tile fits the ring");
+    uint16_t* sO = smem;
+    const int m0 = TRANS ? q0 : p0, n0 = TRANS ? p0 : q0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = TRANS ? qrow + j * 16 + fr : prow + i * 16 + fr;
+        const int nl = TRANS ? prow + i * 16 + fq * 4 : qrow + j * 16 + fq * 4;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        uint2 o = make_uint2(0u, 0u);
+        if (m0 + ml < epi.M && n0 + nl < epi.N)
+          o = epi.pre4(gi, m0 + ml, n0 + nl, v);
+        *(uint2*)(sO + ml * LDO + nl) = o;
+      }
+    __syncthreads();
+    const float qs = epi.q8.q ? fp8_scale(epi.q8.st, epi.q8.hist, epi.q8.fmax)
+                              : 1.f;
+    float amax = 0.f;
+    constexpr int CH = OC_ / 8;
+    for (int q = t; q < OR_ * CH; q += 256) {
+      const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
+      if (m0 + row >= epi.M || n0 + c8 >= epi.N) continue;
+      const uint4 ob = *(const uint4*)(sO + row * LDO + c8);
+      const long long idx = (long long)(m0 + row + gi * epi.grow) * epi.ldc +
+                            n0 + c8 + gi * epi.gcol;
+      *(uint4*)((uint16_t*)epi.c + idx) = ob;
+      if (epi.q8.q) q8_store8(epi.q8, idx, ob, qs, amax);
+    }
+    if (epi.q8.q) {  // block-uniform
+      __syncthreads();   // sO reads done: its first words hold the reduction
+      q8_block_amax(epi.q8, amax, (float*)smem);
+    }
+    return;
+  }
   if constexpr (BIAS != 0) {
     // every row (BIAS 1) / column (BIAS 2) of the ones-MFMA tile holds the
     // same sums: lanes of row 0 / column 0 write them
@@ -426,20 +553,24 @@ constexpr bool t4_pair_ok() {
 
 // orientation options (M = A rows, N = B rows), both 192 x 128 tiles at
 // BK 64: 1 P = A, Q = B; 2 P = B, Q = A, TRANS.  Cost = padded MFMA work;
-// the T4 loop is taken when its padded work is at most 1.04x that of the
-// 128-row loop (which pads to 128 x bn tiles): measured at AlexNet b1024
-// (profiles/r4/ab_t4_192x128_bk64_vs_128row.log) it wins 3-27 % on every
-// convolution it takes at <= 1.0x and loses 2 % (conv2 weight gradient,
-// 1.05x: the bias column's extra tile) and 7 % (conv5, 1.07x).  hvk_gemm_variant 50 turns
-// the loop off, 51 / 52 force option 1 / 2 (A/B runs, tests).
+// the T4 loop is taken when its padded work is at most 1.04x (weight
+// gradients: 0.90x, see t4_pick) that of the 128-row loop (which pads to
+// 128 x bn tiles): measured at AlexNet b1024
+// (profiles/r4/ab_t4_192x128_bk64_vs_128row.log) the forward and
+// backward-data convolutions gain 3-27 % at <= 1.0x.  hvk_gemm_variant 50
+// turns the loop off, 51 / 52 force option 1 / 2 (A/B runs, tests).
 inline long long t4_cost(int M, int N, int opt) {
   auto up = [](long long x, long long b) { return (x + b - 1) / b * b; };
   return opt == 1 ? up(M, 192) * up(N, 128) : up(N, 192) * up(M, 128);
 }
 
 // Nt: the N the T4 tiles cover (a weight gradient's bias comes from ones-
-// MFMAs instead of the ones column the 128-row loop pads N with)
-inline int t4_pick(int M, int N, int bn, int Nt) {
+// MFMAs instead of the ones column the 128-row loop pads N with).  pct: the
+// padded-work ratio (percent) up to which T4 is taken.  Weight gradients
+// need <= 0.90: at equal padding the 8-wave 128-row loop is faster on them
+// (AlexNet b1024: conv3 wgrad 0.947x -> T4 825 vs 882 TF, conv5 0.964x ->
+// 773 vs 839; conv4 at 0.75x gains 696 -> 855; profiles/r4/t4_ablation/).
+inline int t4_pick(int M, int N, int bn, int Nt, int pct = 104) {
   if (hvk_gemm_variant == 50 || hvk_gemm_variant == 0) return 0;
   if (hvk_gemm_variant == 51) return 1;
   if (hvk_gemm_variant == 52) return 2;
@@ -448,10 +579,31 @@ inline int t4_pick(int M, int N, int bn, int Nt) {
                          ((N + bn - 1) / bn * bn);
   const int best = c1 <= c2 ? 1 : 2;
   const long long cb = c1 <= c2 ? c1 : c2;
-  return cb * 100 <= base * 104 ? best : 0;
+  return cb * 100 <= base * pct ? best : 0;
 }
 
-template <class LP, bool PK, class LQ, bool QK, bool TRANS, int BIAS = 0>
+// the direct (register -> global) epilogue: one K split, plain vector
+// stores (no atomics, workspace slices, fp8 copy or bias column), 4-column
+// groups.  Opt-in (hvk_gemm_variant 53): measured SLOWER than the staged
+// epilogue on every AlexNet / VGG conv it applies to (conv5 dgrad 967 ->
+// 713 TF, conv2 fwd 834 -> 688; profiles/r4/t4_ablation/README.md): a lane's
+// 8-B quads leave 32-B pieces of each output row per store instruction,
+// where the staged epilogue writes whole 256-B row runs.
+inline bool t4_direct_ok(const Epi& e, int splits) {
+  return hvk_gemm_variant == 53 && splits == 1 && e.fast_ok() && !e.slice &&
+         !e.q8.q && e.ones_col < 0 && (e.N & 3) == 0;
+}
+
+// the register epilogue with a bf16 C image (EP 2): one K split, bf16
+// output written once (no beta, atomics, slices or bias column), 8-column
+// groups; hvk_gemm_variant 54 keeps the f32-staged epilogue
+inline bool t4_regepi_ok(const Epi& e, int splits) {
+  return hvk_gemm_variant != 54 && splits == 1 && e.fast_ok() && !e.slice &&
+         !e.out_f32 && e.beta == 0.f && e.ones_col < 0 && (e.N & 7) == 0;
+}
+
+template <class LP, bool PK, class LQ, bool QK, bool TRANS, int BIAS = 0,
+          int EP = 0>
 hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
                  int K, int k_split, int splits, int groups, hipStream_t s,
                  float* bgrad = nullptr, int bg_store = 0) {
@@ -460,7 +612,7 @@ hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
   const int tiles = tiles_p * tiles_q;
   const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64, BIAS>),
+  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64, BIAS, EP>),
                      grid, dim3(256), 0, s, lp, lq, epi, P, Q, K, k_split,
                      tiles_q, tiles, splits, gm, bgrad, bg_store);
   return launch_status(s);
@@ -488,7 +640,8 @@ hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
     const bool wbias = std::is_same<LB, ConvWgradB>::value &&
                        epi.ones_col >= 0 && epi.ones_col == N - 1;
     const int Nt = wbias ? N - 1 : N;
-    const int opt = t4_pick(M, N, bn, Nt);
+    const int opt = t4_pick(M, N, bn, Nt,
+                            std::is_same<LB, ConvWgradB>::value ? 90 : 104);
     if (!opt) return hipSuccess;
     const long long t4t = opt == 1
         ? (long long)((M + 191) / 192) * ((Nt + T4_QR - 1) / T4_QR)
@@ -519,6 +672,24 @@ hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                                                   epi.bias_grad, bst);
         return go_t4<LB, BKM, LA, AK, true, 1>(lb2, la, e2, Nt, M, K, ks, sp,
                                                groups, s, epi.bias_grad, bst);
+      }
+    }
+    if constexpr (!std::is_same<LB, ConvWgradB>::value) {
+      // convolution forward / backward-data outputs: the direct epilogue
+      // when selected (t4_direct_ok)
+      if (t4_direct_ok(epi, sp)) {
+        if (opt == 1)
+          return go_t4<LA, AK, LB, BKM, false, 0, 1>(la, lb, epi, M, N, K,
+                                                     ks, sp, groups, s);
+        return go_t4<LB, BKM, LA, AK, true, 0, 1>(lb, la, epi, N, M, K, ks,
+                                                  sp, groups, s);
+      }
+      if (t4_regepi_ok(epi, sp)) {
+        if (opt == 1)
+          return go_t4<LA, AK, LB, BKM, false, 0, 2>(la, lb, epi, M, N, K,
+                                                     ks, sp, groups, s);
+        return go_t4<LB, BKM, LA, AK, true, 0, 2>(lb, la, epi, N, M, K, ks,
+                                                  sp, groups, s);
       }
     }
     if (opt == 1)

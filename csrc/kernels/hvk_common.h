@@ -107,31 +107,35 @@ __device__ __forceinline__ float act_fwd(float x, int act) {
     default: return x;
   }
 }
-// act_fwd over 8 values with ONE switch on the (wave-uniform) code: the
+// act_fwd over NV values with ONE switch on the (wave-uniform) code: the
 // per-element switch of an unrolled loop costs a branch ladder per element
-__device__ __forceinline__ void act_fwd8(float* v, int act) {
+template <int NV>
+__device__ __forceinline__ void act_fwd_n(float* v, int act) {
   switch (act) {
     case ACT_LINEAR: return;
     case ACT_STRICT_RELU:
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : 0.f;
+      for (int q = 0; q < NV; ++q) v[q] = v[q] > 0.f ? v[q] : 0.f;
       return;
     case ACT_TANH:
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = 1.7159f * tanhf(0.6666f * v[q]);
+      for (int q = 0; q < NV; ++q) v[q] = 1.7159f * tanhf(0.6666f * v[q]);
       return;
     case ACT_RELU:
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < NV; ++q)
         v[q] = v[q] > 15.f ? v[q] : log1pf(__expf(v[q]));
       return;
     case ACT_SIGMOID:
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = 1.f / (1.f + __expf(-v[q]));
+      for (int q = 0; q < NV; ++q) v[q] = 1.f / (1.f + __expf(-v[q]));
       return;
     default:
       return;
   }
+}
+__device__ __forceinline__ void act_fwd8(float* v, int act) {
+  act_fwd_n<8>(v, act);
 }
 // derivative expressed through the activation OUTPUT y
 __device__ __forceinline__ float act_bwd(float y, int act) {
@@ -147,19 +151,24 @@ __device__ __forceinline__ float act_bwd(float y, int act) {
 }  // namespace hvk
 
 namespace hvk {
-// v[q] *= act_bwd(y[q], act) for 8 values, one switch (see act_fwd8)
-__device__ __forceinline__ void act_bwd_mul8(float* v, const float* y,
-                                             int act) {
+// v[q] *= act_bwd(y[q], act) for NV values, one switch (see act_fwd_n)
+template <int NV>
+__device__ __forceinline__ void act_bwd_mul_n(float* v, const float* y,
+                                              int act) {
   switch (act) {
     case ACT_LINEAR: return;
     case ACT_STRICT_RELU:
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] *= y[q] > 0.f ? 1.f : 0.f;
+      for (int q = 0; q < NV; ++q) v[q] *= y[q] > 0.f ? 1.f : 0.f;
       return;
     default:
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] *= act_bwd(y[q], act);
+      for (int q = 0; q < NV; ++q) v[q] *= act_bwd(y[q], act);
       return;
   }
+}
+__device__ __forceinline__ void act_bwd_mul8(float* v, const float* y,
+                                             int act) {
+  act_bwd_mul_n<8>(v, y, act);
 }
 }  // namespace hvk

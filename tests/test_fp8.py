@@ -469,14 +469,19 @@ T4CONVS8 = [
     (1, 7, 7, 256, 512, 3, 1, 1, 1),
     (2, 27, 27, 96, 256, 5, 2, 2, 1),
     (2, 16, 16, 64, 128, 3, 1, 1, 2),   # stride 2: forward only
+    # 64 outputs per group: the 256 x 64 tiles (VGG conv1_2), partial tiles,
+    # grouped
+    (2, 30, 30, 64, 64, 3, 1, 1, 1),
+    (2, 14, 14, 128, 128, 3, 1, 2, 1),
 ]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", T4CONVS8)
 def test_conv_fp8_t4_loop(cfg):
-    """The 192 x 128 two-workgroups-per-CU fp8 loop (gemm_t4_fp8_kernel)
-    against the 128-row fp8 loop (hvk_set_fp8_variant(71)): forward and
+    """The 192 x 128 (and 256 x 64) two-workgroups-per-CU fp8 loop
+    (gemm_t4_fp8_kernel) against the 128-row fp8 loop
+    (hvk_set_fp8_variant(71)): forward and
     backward-data bit-identical (same MFMAs, same K order), and against the
     float32 reference."""
     N, H, W, C, OC, k, p, g, s = cfg
@@ -487,19 +492,95 @@ def test_conv_fp8_t4_loop(cfg):
     lib = ops._lib.lib()
     try:
         outs = []
-        for v in (71, -1):
+        # 71: 128-row loop; T4 with -1: the register epilogue (bf16 C
+        # image), 73: the f32-staged epilogue, 74: the direct epilogue
+        for v in (71, -1, 73, 74):
             lib.hvk_set_fp8_variant(v)
             outs.append(fp8.conv_fwd(x8, sx, w8, sw, b.to(DEV), (s, s), pad,
                                      g, 3).clone())
-        assert torch.equal(outs[0], outs[1])
+        for o in outs[1:]:
+            assert torch.equal(outs[0], o)
         close(outs[1], fp8.conv_fwd(x8c, sxc, w8c, swc, b, (s, s), pad, g, 3),
               1e-2)
+        # the fused e4m3 copy for the next layer: direct and staged epilogue
+        # write the same bytes and the same amax
+        q8s = []
+        for v in (-1, 73, 74):
+            lib.hvk_set_fp8_variant(v)
+            nxt = fp8.Scaler(DEV, fp8.E4M3)
+            nxt.prime(torch.full((16,), 3.0, device=DEV))
+            q8 = torch.zeros(outs[0].shape, dtype=torch.float8_e4m3fn,
+                             device=DEV)
+            fp8.conv_fwd(x8, sx, w8, sw, b.to(DEV), (s, s), pad, g, 3,
+                         q8=q8, q8_scaler=nxt)
+            torch.cuda.synchronize()
+            q8s.append((q8.view(torch.uint8).clone(), nxt.shard.max().item()))
+        for q in q8s[1:]:
+            assert torch.equal(q8s[0][0], q[0])
+            assert q8s[0][1] == q[1] > 0
         if s == 1:
             OH, OW = ops.conv_out_size(H, W, k, k, (1, 1), pad)
             d8, sd, d8c, sdc = _pair(rnd(N, OH, OW, OC, seed=2, scale=1e-2),
                                      fp8.E5M2)
             outs = []
-            for v in (71, -1):
+            for v in (71, -1, 73, 74):
+                lib.hvk_set_fp8_variant(v)
+                outs.append(fp8.conv_dgrad(d8, sd, w8, sw, (N, H, W, C),
+                                           (1, 1), pad, g).clone())
+            for o in outs[1:]:
+                assert torch.equal(outs[0], o)
+            close(outs[1], fp8.conv_dgrad(d8c, sdc, w8c, swc, (N, H, W, C),
+                                          (1, 1), pad, g), 1e-2)
+    finally:
+        lib.hvk_set_fp8_variant(-1)
+
+
+PP8CONVS = [
+    # N, H, W, C, OC, k, pad, groups: >= 256 outputs (inputs, for the
+    # backward-data) per group
+    (3, 14, 14, 128, 256, 3, 1, 1),     # forward only: C = 128
+    (1, 7, 7, 256, 512, 3, 1, 1),
+    (2, 7, 7, 512, 512, 3, 1, 2),
+    (2, 13, 13, 384, 256, 3, 1, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", PP8CONVS)
+def test_conv_fp8_pp256_loop(cfg):
+    """fp8 convolutions on the 256 x 256 ping-pong loop (forced by
+    hvk_set_fp8_variant(75)) against the 128-row fp8 loop (71): forward and
+    backward-data bit-identical, the fused e4m3 copy too, and against the
+    float32 reference"""
+    N, H, W, C, OC, k, p, g = cfg
+    pad = (p, p, p, p)
+    x8, sx, x8c, sxc = _pair(rnd(N, H, W, C))
+    w8, sw, w8c, swc = _pair(rnd(OC, k, k, C // g, seed=1, scale=0.1))
+    b = torch.randn(OC)
+    lib = ops._lib.lib()
+    try:
+        outs = []
+        for v in (71, 75):
+            lib.hvk_set_fp8_variant(v)
+            nxt = fp8.Scaler(DEV, fp8.E4M3)
+            nxt.prime(torch.full((16,), 3.0, device=DEV))
+            q8 = torch.zeros(N, H, W, OC, dtype=torch.float8_e4m3fn,
+                             device=DEV)
+            y = fp8.conv_fwd(x8, sx, w8, sw, b.to(DEV), (1, 1), pad, g, 3,
+                             q8=q8, q8_scaler=nxt)
+            torch.cuda.synchronize()
+            outs.append((y.clone(), q8.view(torch.uint8).clone(),
+                         nxt.shard.max().item()))
+        assert torch.equal(outs[0][0], outs[1][0])
+        assert torch.equal(outs[0][1], outs[1][1])
+        assert outs[0][2] == outs[1][2]
+        close(outs[1][0], fp8.conv_fwd(x8c, sxc, w8c, swc, b, (1, 1), pad, g,
+                                       3), 1e-2)
+        if C // g >= 256:
+            d8, sd, d8c, sdc = _pair(rnd(N, H, W, OC, seed=2, scale=1e-2),
+                                     fp8.E5M2)
+            outs = []
+            for v in (71, 75):
                 lib.hvk_set_fp8_variant(v)
                 outs.append(fp8.conv_dgrad(d8, sd, w8, sw, (N, H, W, C),
                                            (1, 1), pad, g).clone())

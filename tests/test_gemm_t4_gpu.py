@@ -4,7 +4,9 @@ reference of the same op.
 
 Both loops accumulate every output over the same 16x16x32 MFMAs in the same K
 order, so without split-K the forward and backward-data outputs must be
-bit-identical.  hvk_set_gemm_variant(50) turns the T4 loop off; 51 / 52 force
+bit-identical.  hvk_set_gemm_variant(50) turns the T4 loop off, 53 runs it
+with the direct (register -> global) epilogue and 54 with the f32-staged one
+instead of the default register epilogue (bf16 C image); 51 / 52 force
 its first / second orientation (forward and backward-data: P = pixels (256)
 or P = channels (192, transposed epilogue); weight gradient: P = im2col
 columns (256, transposed) or P = output channels (192)).  The shapes are the
@@ -62,7 +64,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("cfg", CASES)
-@pytest.mark.parametrize("force", [-1, 51, 52])
+@pytest.mark.parametrize("force", [-1, 51, 52, 53, 54])
 def test_t4_conv_fwd(cfg, force):
     N, H, W, C, OC, k, p, g = cfg
     x = rnd(N, H, W, C, seed=1)
@@ -78,7 +80,7 @@ def test_t4_conv_fwd(cfg, force):
 
 
 @pytest.mark.parametrize("cfg", CASES)
-@pytest.mark.parametrize("force", [-1, 51, 52])
+@pytest.mark.parametrize("force", [-1, 51, 52, 53, 54])
 def test_t4_conv_dgrad(cfg, force):
     N, H, W, C, OC, k, p, g = cfg
     w = rnd(OC, k, k, C // g, seed=4, scale=0.05)
@@ -98,7 +100,7 @@ def test_t4_conv_dgrad(cfg, force):
 
 
 @pytest.mark.parametrize("cfg", CASES)
-@pytest.mark.parametrize("force", [-1, 51, 52])
+@pytest.mark.parametrize("force", [-1, 51, 52, 53, 54])
 @pytest.mark.parametrize("splits", [1, 5])
 def test_t4_conv_wgrad(cfg, force, splits):
     """accumulating weight gradient + fused bias gradient; split-K through
@@ -123,3 +125,45 @@ def test_t4_conv_wgrad(cfg, force, splits):
     ref = torch.cat([ref_w.reshape(-1), ref_b])
     close(new, ref, 2e-3)
     close(old, ref, 2e-3)
+
+
+PP_CASES = [
+    # N, H, W, C, OC, k, pad, groups: >= 256 outputs per group (forward) /
+    # inputs per group (backward-data), partial 256-row tiles, K tails
+    (2, 14, 14, 256, 256, 3, 1, 1),
+    (3, 13, 13, 384, 256, 3, 1, 1),     # AlexNet conv3 backward-data
+    (2, 7, 7, 512, 512, 3, 1, 2),       # 256 per group
+    (1, 28, 28, 128, 512, 3, 1, 1),     # forward only: C = 128
+]
+
+
+@pytest.mark.parametrize("cfg", PP_CASES)
+def test_pp256_conv_fwd_dgrad(cfg):
+    """The 256 x 256 ping-pong loop with the implicit-GEMM loaders
+    (hvk_set_gemm_variant(56) forces it for >= 256 outputs per group; the
+    default takes it where it fills the CUs) against the 128-row loop:
+    bit-identical, and against the float32 reference"""
+    N, H, W, C, OC, k, p, g = cfg
+    pad = (p, p, p, p)
+    x = rnd(N, H, W, C, seed=11)
+    w = rnd(OC, k, k, C // g, seed=12, scale=0.05)
+    b = torch.randn(OC, device=DEV)
+    old, new = run_variants(lambda: ops.conv_fwd(x, w, b, (1, 1), pad, g, 3),
+                            (50, 56))
+    assert torch.equal(old, new)
+    ref = F.relu(F.conv2d(nchw(x), nchw(w), b, padding=p,
+                          groups=g)).permute(0, 2, 3, 1)
+    close(new, ref, 1e-2)
+    if C // g < 256:
+        return
+    dy = rnd(N, H, W, OC, seed=13)
+    aux = rnd(N, H, W, C, seed=14)
+
+    def run():
+        return ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1), pad, g, aux=aux,
+                              aux_act=3)
+    old, new = run_variants(run, (50, 56))
+    assert torch.equal(old, new)
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), nchw(w), nchw(dy),
+                                     padding=p, groups=g).permute(0, 2, 3, 1)
+    close(new, ref * (aux.float() > 0).float(), 1e-2)

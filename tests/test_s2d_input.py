@@ -67,12 +67,15 @@ def test_fill_minibatch_s2d_reference_cpu(s, KH, KW, pad, H, W):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 61, 60])
 @pytest.mark.parametrize("s,KH,KW,pad,H,W", GEOM)
 def test_fill_minibatch_s2d_kernel_matches_fill_then_s2d(s, KH, KW, pad, H,
-                                                        W):
+                                                        W, variant):
     """hvk_fill_minibatch_s2d == hvk_space_to_depth(hvk_fill_minibatch(.))
     bit for bit (same f32 affine map, same bf16 rounding), tail rows of a
-    short minibatch zero, labels / indices gathered."""
+    short minibatch zero, labels / indices gathered - for the row-staged
+    kernel with four samples per block (default), one sample per block (61)
+    and the per-chunk kernel (60)."""
     dev = torch.device("cuda")
     src, mean, rdisp, labels, shuffled = (t.to(dev) for t in _data(13, H, W))
     n, start, count = 11, 1, 9
@@ -87,9 +90,15 @@ def test_fill_minibatch_s2d_kernel_matches_fill_then_s2d(s, KH, KW, pad, H,
     idx = torch.zeros(n, dtype=torch.int32, device=dev)
     m2 = ops.s2d_affine(mean.cpu(), (H, W, 3), s, KH, KW, pad, 0.0).to(dev)
     r2 = ops.s2d_affine(rdisp.cpu(), (H, W, 3), s, KH, KW, pad, 1.0).to(dev)
-    ops.fill_minibatch_s2d(src, shuffled, start, count, out, s, KH, KW, pad,
-                           m2, r2, labels=labels, labels_out=lb, idx_out=idx)
-    torch.cuda.synchronize()
+    lib = ops._lib.lib()
+    try:
+        lib.hvk_set_gemm_variant(variant)
+        ops.fill_minibatch_s2d(src, shuffled, start, count, out, s, KH, KW,
+                               pad, m2, r2, labels=labels, labels_out=lb,
+                               idx_out=idx)
+        torch.cuda.synchronize()
+    finally:
+        lib.hvk_set_gemm_variant(-1)
     assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
     assert torch.equal(la, lb)
     assert idx.cpu()[count:].tolist() == [-1] * (n - count)

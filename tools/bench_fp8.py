@@ -1,6 +1,11 @@
 """FP8 vs bf16 kernel micro-benchmarks on square GEMMs and VGG-16 layer
 shapes (random operands, one process, interleaved; cdna_hip_programming.md
-§5.4 rules 24/25).  Writes gpurun_out/bench_fp8.json."""
+§5.4 rules 24/25).  Writes gpurun_out/bench_fp8.json.
+
+    python tools/bench_fp8.py [batch] [fp8 variant ...]
+
+With a variant list the fp8 convolutions are timed once per
+hvk_set_fp8_variant setting (A/B of the fp8 loops)."""
 import json
 import sys
 
@@ -11,6 +16,7 @@ import veles_amd.ops as ops  # noqa: E402
 from veles_amd.ops import fp8  # noqa: E402
 
 dev = "cuda"
+VARS = [int(v) for v in sys.argv[2:]] or [-1]
 BF = torch.bfloat16
 res = {}
 
@@ -62,13 +68,18 @@ def conv_case(name, N, H, W, C, OC, k=3, p=1):
     r = {
         "fwd_bf16_TF": fl / timeit(lambda: ops.conv_fwd(
             x, w, b, (1, 1), pad, 1, 3)) / 1e12,
-        "fwd_fp8_TF": fl / timeit(lambda: fp8.conv_fwd(
-            x8, sx, w8, sw, b, (1, 1), pad, 1, 3)) / 1e12,
         "dgrad_bf16_TF": fl / timeit(lambda: ops.conv_dgrad(
             dy, w, (N, H, W, C), (1, 1), pad, 1)) / 1e12,
-        "dgrad_fp8_TF": fl / timeit(lambda: fp8.conv_dgrad(
-            d8, sd, w8, sw, (N, H, W, C), (1, 1), pad, 1, wt8=wt8)) / 1e12,
     }
+    lib = ops._lib.lib()
+    for v in VARS:
+        sfx = "" if VARS == [-1] else "_v%d" % v
+        lib.hvk_set_fp8_variant(v)
+        r["fwd_fp8_TF" + sfx] = fl / timeit(lambda: fp8.conv_fwd(
+            x8, sx, w8, sw, b, (1, 1), pad, 1, 3)) / 1e12
+        r["dgrad_fp8_TF" + sfx] = fl / timeit(lambda: fp8.conv_dgrad(
+            d8, sd, w8, sw, (N, H, W, C), (1, 1), pad, 1, wt8=wt8)) / 1e12
+    lib.hvk_set_fp8_variant(-1)
     res[name] = r
     print(name, r, flush=True)
 

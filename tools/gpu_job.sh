@@ -17,6 +17,9 @@
 #   solo[:ARGS]              bench.py with a one-rank RCCL process group
 #                            (VELES_AMD_DP_SOLO_COLLECTIVES=1)
 #   ab[:B:ROUNDS:VARIANTS]   tools/bench_gemm_ab.py (GEMM loop A/B)
+#   abenv:VAR=VAL[+VAR=VAL]:B:ROUNDS:VARIANTS  the same under extra environment
+#                            settings (e.g. HVK_LIBRARY=build/abl/libhvk_abl1.so,
+#                            a tools/build_abl.py diagnostic build)
 #   prof[:MODEL:BATCH:TAG:PREC]  step-only rocprofv3 kernel table
 #   pmc[:TAG[:BENCHARGS]]    four rocprofv3 --pmc passes (instruction mix,
 #                            wave states, HBM read + TA, HBM write + L2 hit)
@@ -59,6 +62,11 @@ for step in "$@"; do
       tools/gpu_step.sh 900 "$log" python -u tools/bench_gemm_ab.py \
         "${b:-1024}" "${rounds:-3}" "${vars:--1}" || exit 1
       cat "$log" | head -60 ;;
+    abenv)
+      IFS=: read -r envs b rounds vars <<< "$arg"
+      tools/gpu_step.sh 900 "$log" env ${envs//+/ } python -u \
+        tools/bench_gemm_ab.py "${b:-1024}" "${rounds:-3}" "${vars:--1}" || exit 1
+      echo "$envs"; cat "$log" | head -60 ;;
     prof)
       IFS=: read -r m b tag prec <<< "$arg"
       M=${m:-alexnet} B=${b:-1024} T=${tag:-r4} P=${prec:-bfloat16}

@@ -60,6 +60,27 @@ def _gpu(t):
     return t is not None and t.is_cuda
 
 
+# The LDS-DMA loaders address an operand through 32-bit buffer offsets
+# (csrc/kernels/conv_geom.h kBufMaxBytes); a larger operand drops the kernel
+# to its per-lane-address loader (VGG-16 b512 conv1_2: 3.3 GB activations,
+# forward 3.1 ms on that path).  Convolutions over larger batches therefore
+# run in image chunks that keep every operand under the limit.
+_BUF_MAX = (1 << 31) - 64
+
+
+def _image_chunks(N, *tensors):
+    """Equal image ranges [(n0, n1)] whose slices of ``tensors`` (leading
+    dimension = images) each stay under ``_BUF_MAX`` bytes."""
+    per = max([t.numel() // max(t.shape[0], 1) * t.element_size()
+               for t in tensors if t is not None] + [1])
+    if N * per < _BUF_MAX or N < 2:
+        return [(0, N)]
+    n = max(1, (_BUF_MAX - 1) // per)
+    k = -(-N // n)
+    step = -(-N // k)
+    return [(i, min(N, i + step)) for i in range(0, N, step)]
+
+
 # --------------------------------------------------------------- activations
 def act_fwd_ref(x, act):
     act = act_code(act)
@@ -715,6 +736,18 @@ def _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
     """``q8``: the kernel arguments of a fused fp8 copy of ``out``
     (``fp8._q8_args`` + history length) or None.  Returns whether the fp8
     copy was written (the fused epilogue needs aligned rows and bias)."""
+    chunks = _image_chunks(N, x)
+    if len(chunks) > 1:
+        fused = True
+        for n0, n1 in chunks:
+            qc = None
+            if q8 is not None:
+                qc = list(q8)
+                qc[0] += n0 * OH * OW * OC     # one byte per element
+            fused = _conv_fwd_call(
+                x[n0:n1], w, bias, out[n0:n1], n1 - n0, H, W, C, OC, KH, KW,
+                sy, sx, pt, pl, OH, OW, groups, act, stream, q8=qc) and fused
+        return fused
     sfx = "" if q8 is None else "_q8"
     extra = [] if q8 is None else list(q8)
     if _HALO and sy == 1 and sx == 1 and out.is_contiguous():
@@ -852,6 +885,21 @@ def _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out, fq):
     return out
 
 
+def _dgrad_call(dy, wt, out, aux, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
+                OH, OW, groups, aux_act):
+    if _HALO_DGRAD and sx == 1 and sy == 1 and out.is_contiguous():
+        rc = _lib.lib().hvk_conv_dgrad_halo(
+            _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH,
+            OW, groups, _p(aux), aux_act, _s(dy))
+        if rc == 0:
+            return
+        if rc != -2:
+            _lib.check(rc, "hvk_conv_dgrad_halo")
+    _lib_call("hvk_conv_dgrad_t", _p(dy), _p(wt), _p(out), N, H, W, C,
+              OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, _p(aux),
+              aux_act, _s(dy))
+
+
 def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
                groups=1, aux=None, aux_act=0, out=None):
     """dx [N,H,W,C] = conv^T(dy, w) [* f'(aux)]."""
@@ -883,17 +931,10 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
             wt = _workspace(("dgrad_wt", id(w)), (groups, Cg, KH, KW, OCg),
                             w.dtype, w.device)
             wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1))
-        if _HALO_DGRAD and sx == 1 and sy == 1 and out.is_contiguous():
-            rc = _lib.lib().hvk_conv_dgrad_halo(
-                _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH,
-                OW, groups, _p(aux), aux_act, _s(dy))
-            if rc == 0:
-                return out
-            if rc != -2:
-                _lib.check(rc, "hvk_conv_dgrad_halo")
-        _lib_call("hvk_conv_dgrad_t", _p(dy), _p(wt), _p(out), N, H, W, C,
-                  OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, _p(aux),
-                  aux_act, _s(dy))
+        for n0, n1 in _image_chunks(N, dy):
+            _dgrad_call(dy[n0:n1], wt, out[n0:n1],
+                        None if aux is None else aux[n0:n1], n1 - n0, H, W,
+                        C, OC, KH, KW, sy, sx, pt, pl, OH, OW, groups, aux_act)
         return out
     Hp, Wp = H + pt + pb, W + pl + pr
     dxp = torch.nn.grad.conv2d_input((N, C, Hp, Wp),
@@ -923,6 +964,26 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     if dw.dtype != torch.float32:
         raise TypeError("conv_wgrad accumulates into float32")
     if _gpu(x):
+        xt = col.x if isinstance(col, (S2DImage, PaddedImage)) else x
+        chunks = _image_chunks(N, xt, dy)
+        if len(chunks) > 1:
+            # a sum over pixels: the image chunks accumulate into dw / dbias
+            for n0, n1 in chunks:
+                c = col
+                if isinstance(col, S2DImage):
+                    c = S2DImage(col.x[n0:n1], col.s, (n1 - n0,) +
+                                 tuple(col.shape[1:]))
+                elif isinstance(col, PaddedImage):
+                    c = PaddedImage(col.x[n0:n1], col.C)
+                elif col is not None:
+                    c = col[n0 * OH * OW:n1 * OH * OW]
+                if isinstance(col, S2DImage) and col.x is x:
+                    xc = c            # the loader-made s2d input itself
+                else:
+                    xc = x[n0:n1]
+                conv_wgrad(xc, dy[n0:n1], dw, sliding, padding, groups,
+                           None, c, dbias)
+            return dw
         s2 = s2d_factor(C, groups, sliding, KH, KW)
         if s2:
             x2 = col.x if isinstance(col, S2DImage) else \

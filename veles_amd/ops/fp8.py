@@ -299,12 +299,17 @@ def conv_fwd(x8, sx, w8, sw, bias=None, sliding=(1, 1), padding=(0, 0, 0, 0),
         out = torch.empty(N, OH, OW, OC, dtype=torch.bfloat16 if x8.is_cuda
                           else torch.float32, device=x8.device)
     if x8.is_cuda:
-        _call("hvk_conv_fwd_fp8", x8.data_ptr(), w8.data_ptr(), ops._p(bias),
-              out.data_ptr(), N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH,
-              OW, groups, ops.act_code(act), sx.fmt, sw.fmt,
-              sx.state.data_ptr(), sw.state.data_ptr(), HIST,
-              float(sx.fmax_eff), float(sw.fmax_eff),
-              *_q8_args(q8, q8_scaler), _s(x8))
+        # image chunks under the 32-bit buffer offsets (ops._image_chunks)
+        for n0, n1 in ops._image_chunks(N, x8):
+            qa = _q8_args(q8, q8_scaler)
+            if q8 is not None:
+                qa[0] += n0 * OH * OW * OC
+            _call("hvk_conv_fwd_fp8", x8[n0:n1].data_ptr(), w8.data_ptr(),
+                  ops._p(bias), out[n0:n1].data_ptr(), n1 - n0, H, W, C, OC,
+                  KH, KW, syy, sxx, pt, pl, OH, OW, groups,
+                  ops.act_code(act), sx.fmt, sw.fmt, sx.state.data_ptr(),
+                  sw.state.data_ptr(), HIST, float(sx.fmax_eff),
+                  float(sw.fmax_eff), *qa, _s(x8))
         return out
     y = ops.conv_fwd(dequantize(x8, sx), dequantize(w8, sw), bias, sliding,
                      padding, groups, act, out=out)
@@ -329,12 +334,17 @@ def conv_dgrad(dy8, sdy, w8, sw, x_shape, sliding=(1, 1),
     if dy8.is_cuda:
         if wt8 is None:
             wt8 = permute_for_dgrad(w8, groups)
-        _call("hvk_conv_dgrad_fp8", dy8.data_ptr(), wt8.data_ptr(),
-              out.data_ptr(), N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH,
-              OW, groups, ops._p(aux), ops.act_code(aux_act), sdy.fmt,
-              sw.fmt, sdy.state.data_ptr(), sw.state.data_ptr(), HIST,
-              float(sdy.fmax_eff), float(sw.fmax_eff),
-              *_q8_args(q8, q8_scaler), _s(dy8))
+        for n0, n1 in ops._image_chunks(N, dy8):
+            qa = _q8_args(q8, q8_scaler)
+            if q8 is not None:
+                qa[0] += n0 * H * W * C
+            _call("hvk_conv_dgrad_fp8", dy8[n0:n1].data_ptr(), wt8.data_ptr(),
+                  out[n0:n1].data_ptr(), n1 - n0, H, W, C, OC, KH, KW, syy,
+                  sxx, pt, pl, OH, OW, groups,
+                  ops._p(None if aux is None else aux[n0:n1]),
+                  ops.act_code(aux_act), sdy.fmt, sw.fmt,
+                  sdy.state.data_ptr(), sw.state.data_ptr(), HIST,
+                  float(sdy.fmax_eff), float(sw.fmax_eff), *qa, _s(dy8))
         return out
     dx = ops.conv_dgrad(dequantize(dy8, sdy), dequantize(w8, sw), x_shape,
                         sliding, padding, groups, aux=aux, aux_act=aux_act,
@@ -358,15 +368,18 @@ def conv_wgrad(x8, sx, dy8, sdy, dw, sliding=(1, 1), padding=(0, 0, 0, 0),
     sxx, syy = sliding
     pl, pt, pr, pb = padding
     if x8.is_cuda:
-        if splits is None:
-            splits = ops.wgrad_splits(N * OH * OW, OC // groups, KH * KW * Cg,
-                                      groups)
-        _call("hvk_conv_wgrad_fp8", x8.data_ptr(), dy8.data_ptr(),
-              dw.data_ptr(), None if dbias is None else dbias.data_ptr(),
-              N, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH, OW,
-              groups, int(splits), sx.fmt, sdy.fmt, sx.state.data_ptr(),
-              sdy.state.data_ptr(), HIST, float(sx.fmax_eff),
-              float(sdy.fmax_eff), _s(x8))
+        # a sum over pixels: image chunks (32-bit buffer offsets) accumulate
+        for n0, n1 in ops._image_chunks(N, x8, dy8):
+            n = n1 - n0
+            sp = splits if splits is not None else ops.wgrad_splits(
+                n * OH * OW, OC // groups, KH * KW * Cg, groups)
+            _call("hvk_conv_wgrad_fp8", x8[n0:n1].data_ptr(),
+                  dy8[n0:n1].data_ptr(), dw.data_ptr(),
+                  None if dbias is None else dbias.data_ptr(),
+                  n, H, W, C, OC, KH, KW, syy, sxx, pt, pl, OH, OW,
+                  groups, int(sp), sx.fmt, sdy.fmt, sx.state.data_ptr(),
+                  sdy.state.data_ptr(), HIST, float(sx.fmax_eff),
+                  float(sdy.fmax_eff), _s(x8))
         return dw
     acc = torch.zeros_like(dw)
     dq = dequantize(dy8, sdy)
