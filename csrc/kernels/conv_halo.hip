@@ -39,7 +39,12 @@ struct HaloGeom {
   FastDiv fTW, fHW, fCP, fCh, fKW, fTX, fTSP;
 };
 
-template <int BN_, bool W8, int VAR>
+// EP 2: the register epilogue (as the T4 loop's, gemm_t4.h): the MFMAs
+// compute the transposed tile, each lane finishes 4 consecutive output
+// channels of one pixel in registers (bias, activation, derivative of the
+// layer below, bf16) into a bf16 image of the tile, then whole 16-B chunks
+// go out; EP 0 stages the f32 tile (hvk_gemm_variant 54)
+template <int BN_, bool W8, int VAR, int EP = 0>
 __global__ void __launch_bounds__(W8 ? 512 : NTHR, 2)
 conv_halo_kernel(HaloGeom hg, const uint16_t* __restrict__ src, DenseK lb,
                  Epi epi, int K, int tiles_n) {
@@ -158,9 +163,14 @@ conv_halo_kernel(HaloGeom hg, const uint16_t* __restrict__ src, DenseK lb,
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j],
-                                                              acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (EP == 2)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                bfv[j], af[i], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                af[i], bfv[j], acc[i][j], 0, 0, 0);
+        }
     }
   };
 
@@ -185,6 +195,52 @@ conv_halo_kernel(HaloGeom hg, const uint16_t* __restrict__ src, DenseK lb,
     asm volatile("" ::: "memory");
   }
 
+  if constexpr (EP == 2) {
+    constexpr int LDO = NC + 8;
+    static_assert(BM * LDO * 2 <= 80 * 1024, "bf16 tile fits");
+    uint16_t* sO = smem;
+    const int rows = hg.TH * hg.TW;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int ml = wm * WMR + i * 16 + fr;     // tile pixel of this lane
+      uint32_t py, px;
+      fdivmod((uint32_t)ml, hg.fTW, py, px);
+      const int oh = oh0 + (int)py, ow = ow0 + (int)px;
+      const bool pin = ml < rows && oh < hg.OH && ow < hg.OW;
+      const int P = ((int)img * hg.OH + oh) * hg.OW + ow;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int nl = wn * (NC / WNC) + j * 16 + fq * 4;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        uint2 o = make_uint2(0u, 0u);
+        if (pin && n0 + nl < epi.N) o = epi.pre4((int)gi, P, n0 + nl, v);
+        *(uint2*)(sO + ml * LDO + nl) = o;
+      }
+    }
+    __syncthreads();
+    constexpr int CH = NC / 8;
+    const float qs = epi.q8.q ? fp8_scale(epi.q8.st, epi.q8.hist, epi.q8.fmax)
+                              : 1.f;
+    float amax = 0.f;
+    for (int q = t; q < rows * CH; q += NT) {
+      const int row = q / CH, c8 = (q - (q / CH) * CH) * 8;
+      uint32_t py, px;
+      fdivmod((uint32_t)row, hg.fTW, py, px);
+      const int oh = oh0 + (int)py, ow = ow0 + (int)px;
+      if (oh >= hg.OH || ow >= hg.OW || n0 + c8 >= epi.N) continue;
+      const int P = ((int)img * hg.OH + oh) * hg.OW + ow;
+      const uint4 ob = *(const uint4*)(sO + row * LDO + c8);
+      const long long idx = (long long)(P + (int)gi * epi.grow) * epi.ldc +
+                            n0 + c8 + (int)gi * epi.gcol;
+      *(uint4*)((uint16_t*)epi.c + idx) = ob;
+      if (epi.q8.q) q8_store8(epi.q8, idx, ob, qs, amax);
+    }
+    if (epi.q8.q) {  // block-uniform
+      __syncthreads();
+      q8_block_amax(epi.q8, amax, (float*)smem);
+    }
+    return;
+  }
   // ---- epilogue: f32 tile through LDS, then row-contiguous stores of the
   // tile's in-image pixels
   constexpr int LDC = BN_ + 4;
@@ -276,12 +332,13 @@ size_t halo_lds(const HaloGeom& g, int bn) {
   return std::max(ops, ctile);
 }
 
-template <int BN_, bool W8, int VAR>
-hipError_t launch_halo(const HaloGeom& g, const uint16_t* src, const DenseK& lb,
-                       const Epi& e, int K, int N, int groups, hipStream_t s) {
+template <int BN_, bool W8, int VAR, int EP>
+hipError_t launch_halo_(const HaloGeom& g, const uint16_t* src,
+                        const DenseK& lb, const Epi& e, int K, int N,
+                        int groups, hipStream_t s) {
   const int tiles_n = (N + (VAR == 2 ? 48 : BN_) - 1) / (VAR == 2 ? 48 : BN_);
   const size_t lds = halo_lds(g, BN_);
-  auto kern = conv_halo_kernel<BN_, W8, VAR>;
+  auto kern = conv_halo_kernel<BN_, W8, VAR, EP>;
   static bool attr = false;  // once per instantiation, before any capture
   if (!attr) {
     hipError_t err = hipFuncSetAttribute(
@@ -294,6 +351,17 @@ hipError_t launch_halo(const HaloGeom& g, const uint16_t* src, const DenseK& lb,
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(W8 ? 512 : NTHR), lds, s,
                      g, src, lb, e, K, tiles_n);
   return launch_status(s);
+}
+
+// the register epilogue where the output takes it (bf16, written once,
+// 8-column groups: Epi::pre4); hvk_gemm_variant 54 keeps the f32 staging
+template <int BN_, bool W8, int VAR>
+hipError_t launch_halo(const HaloGeom& g, const uint16_t* src, const DenseK& lb,
+                       const Epi& e, int K, int N, int groups, hipStream_t s) {
+  if (hvk_gemm_variant != 54 && e.fast_ok() && !e.out_f32 && e.beta == 0.f &&
+      e.ones_col < 0 && (e.N & 7) == 0)
+    return launch_halo_<BN_, W8, VAR, 2>(g, src, lb, e, K, N, groups, s);
+  return launch_halo_<BN_, W8, VAR, 0>(g, src, lb, e, K, N, groups, s);
 }
 
 // the halo path applies: stride 1, 16-B channel chunks, a halo that fits LDS

@@ -589,3 +589,33 @@ def test_conv_fp8_pp256_loop(cfg):
                                           (1, 1), pad, g), 1e-2)
     finally:
         lib.hvk_set_fp8_variant(-1)
+
+
+@pytest.mark.gpu
+def test_fp8_fc_dgrad_transposed_weights():
+    """The fp8 FC backward-data of models/gd.py: e5m2 err against the
+    transposed e4m3 weight copy (same scaler) equals the float32 product of
+    the dequantised operands, with the derivative of the layer below"""
+    from veles_amd.models.gd import GradientDescent
+    B, n_in, n_out = 256, 1024, 512
+    err = (rnd(B, n_out, scale=1e-2)).to(DEV).to(torch.bfloat16)
+    W = (rnd(n_out, n_in, seed=1, scale=0.05)).to(DEV).to(torch.bfloat16)
+    aux = rnd(B, n_in, seed=3).to(DEV).to(torch.bfloat16)
+
+    class _Fwd:
+        fp8_ = True
+
+    fwd = _Fwd()
+    fwd.fp8_sw_ = fp8.Scaler(DEV, fp8.E4M3)
+    fwd.w8_ = fp8.quantize(W, fwd.fp8_sw_)
+    gd = GradientDescent.__new__(GradientDescent)
+    gd.e8_ = gd.wt8_ = gd.fp8_se_ = None
+    out = torch.empty(B, n_in, dtype=torch.bfloat16, device=DEV)
+    gd._fp8_dgrad(fwd, err, out, aux, 3)
+    torch.cuda.synchronize()
+    ref = (fp8.dequantize(gd.e8_, gd.fp8_se_).float() @
+           fp8.dequantize(fwd.w8_, fwd.fp8_sw_).float()) * \
+        (aux.float() > 0).float()
+    close(out, ref, 1e-2)
+    assert torch.equal(gd.wt8_.view(torch.uint8).cpu(),
+                       fwd.w8_.view(torch.uint8).t().cpu())

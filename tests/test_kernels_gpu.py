@@ -292,18 +292,24 @@ def test_conv_halo_matches_implicit_gemm(cfg):
     dy = rnd(N, OH, OW, OC, seed=2).to(DEV)
     aux = rnd(N, H, W, C, seed=3).to(DEV)
     res = {}
-    for halo in (False, True):
-        ops.set_conv_halo(halo, dgrad=halo)
-        try:
-            y = ops.conv_fwd(x, w, b, sl, pad, g, 3)
-            dx = ops.conv_dgrad(dy, w, (N, H, W, C), sl, pad, g, aux=aux,
-                                aux_act=3)
-            torch.cuda.synchronize()
-        finally:
-            ops.set_conv_halo(True, dgrad=False)
-        res[halo] = (y.cpu(), dx.cpu())
-    assert torch.equal(res[False][0], res[True][0])
-    assert torch.equal(res[False][1], res[True][1])
+    lib = ops._lib.lib()
+    # -1: register epilogues (bf16 C image), 54: f32-staged epilogues
+    for v in (-1, 54):
+        for halo in (False, True):
+            ops.set_conv_halo(halo, dgrad=halo)
+            try:
+                lib.hvk_set_gemm_variant(v)
+                y = ops.conv_fwd(x, w, b, sl, pad, g, 3)
+                dx = ops.conv_dgrad(dy, w, (N, H, W, C), sl, pad, g, aux=aux,
+                                    aux_act=3)
+                torch.cuda.synchronize()
+            finally:
+                lib.hvk_set_gemm_variant(-1)
+                ops.set_conv_halo(True, dgrad=False)
+            res[(v, halo)] = (y.cpu(), dx.cpu())
+    for k in res:
+        assert torch.equal(res[(-1, False)][0], res[k][0])
+        assert torch.equal(res[(-1, False)][1], res[k][1])
 
 
 @pytest.mark.parametrize("cfg", CONVS)

@@ -25,6 +25,8 @@
 #                            wave states, HBM read + TA, HBM write + L2 hit)
 #                            on bench.py --mark-steps, step-only summaries
 #   py:SCRIPT[,ARGS]         python SCRIPT ARGS
+#   rocprof:TAG:SCRIPT[,ARGS]  rocprofv3 --kernel-trace of python3 SCRIPT ARGS
+#                            into gpurun_out/rp_TAG (csv)
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 n=0
@@ -102,6 +104,12 @@ for step in "$@"; do
     py)
       tools/gpu_step.sh 900 "$log" python -u ${arg//,/ } || exit 1
       tail -40 "$log" ;;
+    rocprof)
+      IFS=: read -r tag script <<< "$arg"
+      tools/gpu_step.sh 600 "$log" rocprofv3 --kernel-trace \
+        -d "$R/gpurun_out/rp_$tag" -o run --output-format csv -- \
+        python3 ${script//,/ } || exit 1
+      find gpurun_out/rp_$tag -name "*kernel_trace.csv" | head -1 ;;
     *)
       echo "[gpu_job] unknown step $step"; exit 2 ;;
   esac

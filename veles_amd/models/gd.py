@@ -5,11 +5,20 @@ grad_b[out]     += colsum(err)      (hvk_col_sum)
 err_input       =  err . W  [* f'(below.output)]   (GEMM, NN layout, fused
                                                     derivative epilogue)
 where err = err_output * f'(output) unless the unit above already fused it.
+
+Under precision_type "float8" the backward-data of an fp8 layer runs on the
+fp8 MFMA too (round 4): err quantised to e5m2, against an e4m3 W^T made by
+transposing the forward's weight copy (same scaler) - the fp8 GEMM takes
+K-major operands only.  ``root.common.engine.fp8_fc_dgrad = False`` keeps
+the bf16 GEMM.
 """
 from __future__ import annotations
 
+import torch
+
 from veles_amd.models.nn_units import GradientDescentBase
 from veles_amd import ops
+from veles_amd.ops import fp8
 
 __all__ = ["GradientDescent", "GDTanh", "GDRELU", "GDStrictRELU",
            "GDSigmoid", "GDSoftmax"]
@@ -68,11 +77,37 @@ class GradientDescent(GradientDescentBase):
             ei = self.alloc_err_input(self.input.devmem.shape)
             aux, aux_act = self.aux_tensor()
             aux2 = None if aux is None else aux.reshape(B, -1)
-            # stays bf16 under float8 as well: an fp8 dgrad would need W^T
-            # materialised every step, which costs more than the GEMM
-            ops.gemm(e2, fwd.weights_lp, trans_b=fwd.weights_transposed,
-                     out=ei.view(B, -1), aux=aux2, aux_act=aux_act)
+            if self._fp8_dgrad_ok(fwd):
+                self._fp8_dgrad(fwd, e2, ei.view(B, -1), aux2, aux_act)
+            else:
+                ops.gemm(e2, fwd.weights_lp, trans_b=fwd.weights_transposed,
+                         out=ei.view(B, -1), aux=aux2, aux_act=aux_act)
         self.report_gradients()
+
+    def init_unpickled(self):
+        super().init_unpickled()
+        self.e8_ = self.wt8_ = self.fp8_se_ = None
+
+    def _fp8_dgrad_ok(self, fwd):
+        from veles_amd.utils.config import root, get
+        return getattr(fwd, "fp8_", False) and \
+            getattr(fwd, "w8_", None) is not None and \
+            get(root.common.engine.fp8_fc_dgrad, True)
+
+    def _fp8_dgrad(self, fwd, e2, out, aux, aux_act):
+        """err_input = deq(e5m2(err)) . deq(e4m3(W)) on the fp8 MFMA: the
+        forward's e4m3 weight copy transposed once per step into a K-major
+        [in][out] image (the scale is the copy's)"""
+        if self.fp8_se_ is None:
+            self.fp8_se_ = fp8.Scaler(e2.device, fp8.E5M2)
+        self.e8_ = fp8.quantize(e2, self.fp8_se_, out=self.e8_)
+        w8 = fwd.w8_
+        if self.wt8_ is None or self.wt8_.shape != (w8.shape[1], w8.shape[0]):
+            self.wt8_ = torch.empty(w8.shape[1], w8.shape[0], dtype=w8.dtype,
+                                    device=w8.device)
+        self.wt8_.view(torch.uint8).copy_(w8.view(torch.uint8).t())
+        fp8.gemm(self.e8_, self.fp8_se_, self.wt8_, fwd.fp8_sw_, aux=aux,
+                 aux_act=aux_act, out=out)
 
 
 class GDTanh(GradientDescent):
