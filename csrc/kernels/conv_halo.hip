@@ -43,7 +43,7 @@ struct HaloGeom {
 // compute the transposed tile, each lane finishes 4 consecutive output
 // channels of one pixel in registers (bias, activation, derivative of the
 // layer below, bf16) into a bf16 image of the tile, then whole 16-B chunks
-// go out; EP 0 stages the f32 tile (hvk_gemm_variant 54)
+// go out (opt-in, hvk_gemm_variant 54); EP 0 stages the f32 tile
 template <int BN_, bool W8, int VAR, int EP = 0>
 __global__ void __launch_bounds__(W8 ? 512 : NTHR, 2)
 conv_halo_kernel(HaloGeom hg, const uint16_t* __restrict__ src, DenseK lb,
@@ -354,11 +354,12 @@ hipError_t launch_halo_(const HaloGeom& g, const uint16_t* src,
 }
 
 // the register epilogue where the output takes it (bf16, written once,
-// 8-column groups: Epi::pre4); hvk_gemm_variant 54 keeps the f32 staging
+// 8-column groups: Epi::pre4) - opt-in (hvk_gemm_variant 54): AlexNet conv1
+// measured 536 -> 491 TF with it
 template <int BN_, bool W8, int VAR>
 hipError_t launch_halo(const HaloGeom& g, const uint16_t* src, const DenseK& lb,
                        const Epi& e, int K, int N, int groups, hipStream_t s) {
-  if (hvk_gemm_variant != 54 && e.fast_ok() && !e.out_f32 && e.beta == 0.f &&
+  if (hvk_gemm_variant == 54 && e.fast_ok() && !e.out_f32 && e.beta == 0.f &&
       e.ones_col < 0 && (e.N & 7) == 0)
     return launch_halo_<BN_, W8, VAR, 2>(g, src, lb, e, K, N, groups, s);
   return launch_halo_<BN_, W8, VAR, 0>(g, src, lb, e, K, N, groups, s);

@@ -1335,10 +1335,12 @@ hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                 (std::is_same<LA, ConvFwdA>::value ||
                  std::is_same<LA, ConvDgradA>::value)) {
     const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+    // long reductions only (K >= 3072): AlexNet conv3 backward-data (K =
+    // 3456) 996 -> 1067 TF, VGG conv3_2 (K = 2304) 987 -> 902 forward
     const bool force = hvk_gemm_variant == 56 && N >= 256;
     if ((hvk_gemm_variant < 0 || force) && splits == 1 && !epi.atomic &&
         !epi.slice && la.dma_ok() && lb.dma_ok() &&
-        (force || want_pp256(M, N, 1, groups)))
+        (force || (K >= 3072 && want_pp256(M, N, 1, groups))))
       return go_pp256<LA, AK, LB, BKM>(la, lb, epi, M, N, K, k_split, 1,
                                        groups, s);
   }

@@ -596,9 +596,13 @@ inline bool t4_direct_ok(const Epi& e, int splits) {
 
 // the register epilogue with a bf16 C image (EP 2): one K split, bf16
 // output written once (no beta, atomics, slices or bias column), 8-column
-// groups; hvk_gemm_variant 54 keeps the f32-staged epilogue
+// groups.  Opt-in (hvk_gemm_variant 54): measured slower than the f32
+// staging at AlexNet b1024 (conv4 dgrad 1025 -> 862 TF, conv5 dgrad 960 ->
+// 758, conv5 fwd 901 -> 847; profiles/r4/t4_ablation/README.md) - the lane
+// quads read the derivative of the layer below in 32-B pieces per row and
+// write the bf16 image with 4-way bank conflicts
 inline bool t4_regepi_ok(const Epi& e, int splits) {
-  return hvk_gemm_variant != 54 && splits == 1 && e.fast_ok() && !e.slice &&
+  return hvk_gemm_variant == 54 && splits == 1 && e.fast_ok() && !e.slice &&
          !e.out_f32 && e.beta == 0.f && e.ones_col < 0 && (e.N & 7) == 0;
 }
 

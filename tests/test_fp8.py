@@ -492,8 +492,8 @@ def test_conv_fp8_t4_loop(cfg):
     lib = ops._lib.lib()
     try:
         outs = []
-        # 71: 128-row loop; T4 with -1: the register epilogue (bf16 C
-        # image), 73: the f32-staged epilogue, 74: the direct epilogue
+        # 71: 128-row loop; T4 with -1: the f32-staged epilogue, 73: the
+        # register epilogue (bf16 C image), 74: the direct epilogue
         for v in (71, -1, 73, 74):
             lib.hvk_set_fp8_variant(v)
             outs.append(fp8.conv_fwd(x8, sx, w8, sw, b.to(DEV), (s, s), pad,

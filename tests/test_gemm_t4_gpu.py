@@ -5,8 +5,8 @@ reference of the same op.
 Both loops accumulate every output over the same 16x16x32 MFMAs in the same K
 order, so without split-K the forward and backward-data outputs must be
 bit-identical.  hvk_set_gemm_variant(50) turns the T4 loop off, 53 runs it
-with the direct (register -> global) epilogue and 54 with the f32-staged one
-instead of the default register epilogue (bf16 C image); 51 / 52 force
+with the direct (register -> global) epilogue and 54 with the register
+epilogue (bf16 C image) instead of the default f32-staged one; 51 / 52 force
 its first / second orientation (forward and backward-data: P = pixels (256)
 or P = channels (192, transposed epilogue); weight gradient: P = im2col
 columns (256, transposed) or P = output channels (192)).  The shapes are the

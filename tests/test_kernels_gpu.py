@@ -293,7 +293,7 @@ def test_conv_halo_matches_implicit_gemm(cfg):
     aux = rnd(N, H, W, C, seed=3).to(DEV)
     res = {}
     lib = ops._lib.lib()
-    # -1: register epilogues (bf16 C image), 54: f32-staged epilogues
+    # -1: f32-staged epilogues, 54: register epilogues (bf16 C image)
     for v in (-1, 54):
         for halo in (False, True):
             ops.set_conv_halo(halo, dgrad=halo)
