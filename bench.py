@@ -28,13 +28,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # 1024 per GPU: AlexNet's activations at b1024 take ~10 GB of the 288 GB
-    # HBM; b512 -> b1024 lifts 1-GPU throughput 114k -> 126k img/s (longer
-    # GEMMs, half the per-sample update / launch cost) and halves the
-    # all-reduce-to-compute ratio for the multi-GPU points
-    # (profiles/batch_sweep_r2.md)
+    # 2048 per GPU (round 4 sweep, profiles/r4/alexnet_batch_sweep.md):
+    # b1024 144.9k, b2048 154.3k, b3072 156.2k, b4096 157.2k img/s on one
+    # MI355X; b2048 takes ~20 GB of the 288 GB HBM with every activation
+    # tensor under 2 GB (the 32-bit buffer offsets of the LDS-DMA loaders;
+    # b4096's conv1 output is 2.4 GB), and halves the all-reduce-to-compute
+    # ratio of b1024 for the multi-GPU points
     ap.add_argument("--batch", type=int, default=None,
-                    help="per-GPU minibatch (weak scaling); default 1024, "
+                    help="per-GPU minibatch (weak scaling); default 2048, "
                          "512 for vgg16 (the fp8 and bf16 throughput "
                          "plateau: profiles/r4/vgg16_batch_sweep.md)")
     ap.add_argument("--model", default="alexnet")
@@ -53,7 +54,7 @@ def main():
                          "kernels (step-only rocprofv3 summaries)")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = 512 if args.model == "vgg16" else 1024
+        args.batch = 512 if args.model == "vgg16" else 2048
 
     import torch
     from veles_amd.utils.config import root
@@ -82,7 +83,13 @@ def main():
     device = Device(backend=backend)
     layers_fn, dataset = MODELS[args.model]
     global_batch = args.batch * dp.world_size
-    n_train = global_batch * args.steps_per_epoch
+    # the resident synthetic set: --steps-per-epoch minibatches of ONE
+    # rank's batch, at least two global minibatches - so the per-rank HBM
+    # it takes stays fixed as N grows (every rank holds the whole set: the
+    # global shuffle may hand any sample to any rank); at N >= 8 an epoch
+    # is two steps, measured as cheap as sixteen (152.9k vs 154.3k img/s
+    # at b2048, profiles/r4/alexnet_batch_sweep.md)
+    n_train = max(2 * global_batch, args.batch * args.steps_per_epoch)
     launcher = DummyLauncher()
     launcher.dp_ = dp
     wf = StandardWorkflow(
