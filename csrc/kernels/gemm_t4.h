@@ -208,24 +208,32 @@ __device__ __forceinline__ bf16x8 t4_frag(const uint16_t* s, int row, int ks,
 // workgroups with tp = 0); 2: over the P operand (ones as B; waves with
 // qrow = 0 of the workgroups with tq = 0).  bgrad[row + gi * grow] is
 // stored (bg_store, an unsplit overwrite) or atomically added.
+//
+// QR = 64 (outputs of 33-64 channels per group: AlexNet conv2 backward-data,
+// VGG conv1_2 / conv2_1 backward-data): PR = 256 and the four waves stacked
+// along P (64 x 64 each, NJ = 3 computed n-tiles for <= 48 columns) - the
+// same 40-KiB stage; orientation 1 only, no bias MFMAs, staged epilogue.
 template <class LP, bool PK, class LQ, bool QK, int PR, bool TRANS, int BKT,
-          int BIAS = 0, int EP = 0>
+          int BIAS = 0, int EP = 0, int QR = T4_QR, int NJ = 4>
 __global__ void __launch_bounds__(256, 2)
 gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
                int tiles_q, int tiles, int splits, int gm, float* bgrad,
                int bg_store) {
+  constexpr bool STK = QR == 64;             // waves stacked along P
+  static_assert(!STK || (!TRANS && BIAS == 0 && EP == 0 && PR == 256),
+                "stacked waves: orientation 1, staged epilogue");
   constexpr int NST = BKT == 32 ? 3 : 2;     // LDS ring stages
   using OP = T4Op<LP, PK, PR, BKT>;
-  using OQ = T4Op<LQ, QK, T4_QR, BKT>;
+  using OQ = T4Op<LQ, QK, QR, BKT>;
   constexpr int SP = OP::IMG * BKT, SQ = OQ::IMG * BKT;
   constexpr int SST = SP + SQ;
   constexpr int RING = NST * SST * 2;
   constexpr int HP = PR / 2;                 // P rows per epilogue pass
-  constexpr int LDC = TRANS ? HP + 4 : T4_QR + 4;
-  constexpr int EPI = (TRANS ? T4_QR : HP) * LDC * 4;
+  constexpr int LDC = TRANS ? HP + 4 : QR + 4;
+  constexpr int EPI = (TRANS ? QR : HP) * LDC * 4;
   constexpr int SMEM = RING > EPI ? RING : EPI;
   static_assert(2 * SMEM <= 160 * 1024, "two workgroups per CU");
-  constexpr int MI = PR / 32;                // m-tiles per wave
+  constexpr int MI = STK ? PR / 64 : PR / 32;   // m-tiles per wave
   constexpr int NSW = OP::NS + OQ::NS;       // DMA pieces per wave and step
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM / 2];
 
@@ -252,11 +260,11 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
   if (kbeg >= kend) return;
   lp.group(gi);
   lq.group(gi);
-  const int p0 = tp * PR, q0 = tq * T4_QR;
+  const int p0 = tp * PR, q0 = tq * QR;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int prow = (w >> 1) * HP;    // wave's first P row
-  const int qrow = (w & 1) * 64;     // wave's first Q row
+  const int prow = STK ? w * (PR / 4) : (w >> 1) * HP;   // first P row
+  const int qrow = STK ? 0 : (w & 1) * 64;               // first Q row
   const int fr = lane & 15, fq = lane >> 4;
 
   f32x4 acc[MI][4];
@@ -315,14 +323,14 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
       for (int ks = 0; ks < BKT / 32; ++ks) {
         bf16x8 bq[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           bq[j] = t4_frag<QK, OQ::IMG, BKT>(sQ, qrow + j * 16, ks, fr, fq);
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const bf16x8 a = t4_frag<PK, OP::IMG, BKT>(sP, prow + i * 16, ks,
                                                      fr, fq);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < NJ; ++j) {
             // EP 1 / 2: the transposed product (a lane then holds 4
             // consecutive C columns of one row); same K order, same values
             if constexpr (EP != 0 && !TRANS)
@@ -484,9 +492,9 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int pl = i * 16 + fq * 4;           // pass-local P row
-          const int qc = qrow + j * 16 + fr;        // Q row
+        for (int j = 0; j < NJ; ++j) {
+          const int pl = prow - e * HP + i * 16 + fq * 4;  // pass-local P row
+          const int qc = qrow + j * 16 + fr;               // Q row
           if constexpr (TRANS) {
             *(float4*)(sC + qc * LDC + pl) =
                 make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2],
@@ -500,8 +508,8 @@ gemm_t4_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
     }
     __syncthreads();
     // C rows / columns of this pass
-    constexpr int ROWS = TRANS ? T4_QR : HP;
-    constexpr int COLS = TRANS ? HP : T4_QR;
+    constexpr int ROWS = TRANS ? QR : HP;
+    constexpr int COLS = TRANS ? HP : QR;
     const int m0 = TRANS ? q0 : p0 + e * HP;
     const int n0 = TRANS ? p0 + e * HP : q0;
     if (epi.atomic) {
@@ -607,16 +615,17 @@ inline bool t4_regepi_ok(const Epi& e, int splits) {
 }
 
 template <class LP, bool PK, class LQ, bool QK, bool TRANS, int BIAS = 0,
-          int EP = 0>
+          int EP = 0, int QR = T4_QR, int NJ = 4>
 hipError_t go_t4(const LP& lp, const LQ& lq, const Epi& epi, int P, int Q,
                  int K, int k_split, int splits, int groups, hipStream_t s,
                  float* bgrad = nullptr, int bg_store = 0) {
-  constexpr int PR = 192;
-  const int tiles_p = (P + PR - 1) / PR, tiles_q = (Q + T4_QR - 1) / T4_QR;
+  constexpr int PR = QR == 64 ? 256 : 192;
+  const int tiles_p = (P + PR - 1) / PR, tiles_q = (Q + QR - 1) / QR;
   const int tiles = tiles_p * tiles_q;
   const int gm = (tiles_q >= 8 && hvk_gemm_variant != 20) ? 8 : 1;
   dim3 grid((unsigned)((long long)tiles * splits * groups));
-  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64, BIAS, EP>),
+  hipLaunchKernelGGL((gemm_t4_kernel<LP, PK, LQ, QK, PR, TRANS, 64, BIAS, EP,
+                                     QR, NJ>),
                      grid, dim3(256), 0, s, lp, lq, epi, P, Q, K, k_split,
                      tiles_q, tiles, splits, gm, bgrad, bg_store);
   return launch_status(s);
@@ -644,6 +653,22 @@ hipError_t t4_launch(const LA& la, const LB& lb, const Epi& epi, int M, int N,
     const bool wbias = std::is_same<LB, ConvWgradB>::value &&
                        epi.ones_col >= 0 && epi.ones_col == N - 1;
     const int Nt = wbias ? N - 1 : N;
+    if constexpr (!std::is_same<LB, ConvWgradB>::value) {
+      // 33-64 output channels per group: 256 x 64 tiles with the waves
+      // stacked along the pixels (the 128-row loop's VAR 3 / 4 tile shape on
+      // the T4 schedule).  Opt-in (hvk_gemm_variant 58): slower than VAR 3 /
+      // 4's eight waves per workgroup at AlexNet b1024 (conv2 backward-data
+      // 737 -> 705 TF; profiles/r4/t4_ablation/ab_t4_64.log)
+      if (N > 32 && N <= 64 && splits == 1 && !epi.slice &&
+          hvk_gemm_variant == 58) {
+        *taken = true;
+        if (N <= 48)
+          return go_t4<LA, AK, LB, BKM, false, 0, 0, 64, 3>(
+              la, lb, epi, M, N, K, k_split, 1, groups, s);
+        return go_t4<LA, AK, LB, BKM, false, 0, 0, 64, 4>(
+            la, lb, epi, M, N, K, k_split, 1, groups, s);
+      }
+    }
     const int opt = t4_pick(M, N, bn, Nt,
                             std::is_same<LB, ConvWgradB>::value ? 90 : 104);
     if (!opt) return hipSuccess;

@@ -167,3 +167,41 @@ def test_pp256_conv_fwd_dgrad(cfg):
     ref = torch.nn.grad.conv2d_input((N, C, H, W), nchw(w), nchw(dy),
                                      padding=p, groups=g).permute(0, 2, 3, 1)
     close(new, ref * (aux.float() > 0).float(), 1e-2)
+
+
+T4_64_CASES = [
+    # N, H, W, C, OC, k, pad, groups: 33-64 outputs (forward) / inputs
+    # (backward-data) per group - the stacked-wave 256 x 64 T4 tiles
+    (3, 27, 27, 96, 256, 5, 2, 2),      # AlexNet conv2 backward-data (48)
+    (2, 30, 30, 64, 64, 3, 1, 1),       # VGG conv1_2 (64), partial tiles
+    (2, 14, 14, 128, 48, 3, 1, 1),      # forward with 48 outputs
+]
+
+
+@pytest.mark.parametrize("cfg", T4_64_CASES)
+def test_t4_64_conv_fwd_dgrad(cfg):
+    """hvk_set_gemm_variant(58) selects the (opt-in) 256 x 64 T4 tiles;
+    against the 128-row loop (50): bit-identical, and the float32
+    reference"""
+    N, H, W, C, OC, k, p, g = cfg
+    pad = (p, p, p, p)
+    x = rnd(N, H, W, C, seed=21)
+    w = rnd(OC, k, k, C // g, seed=22, scale=0.05)
+    b = torch.randn(OC, device=DEV)
+    old, new = run_variants(lambda: ops.conv_fwd(x, w, b, (1, 1), pad, g, 3),
+                            (50, 58))
+    assert torch.equal(old, new)
+    ref = F.relu(F.conv2d(nchw(x), nchw(w), b, padding=p,
+                          groups=g)).permute(0, 2, 3, 1)
+    close(new, ref, 1e-2)
+    dy = rnd(N, H, W, OC, seed=23)
+    aux = rnd(N, H, W, C, seed=24)
+
+    def run():
+        return ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1), pad, g, aux=aux,
+                              aux_act=3)
+    old, new = run_variants(run, (50, 58))
+    assert torch.equal(old, new)
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), nchw(w), nchw(dy),
+                                     padding=p, groups=g).permute(0, 2, 3, 1)
+    close(new, ref * (aux.float() > 0).float(), 1e-2)

@@ -718,7 +718,7 @@ def im2col(x, KH, KW, sliding, padding, out=None):
 _HALO = True
 # the backward-data halo kernel measured slower than the implicit GEMM on
 # every AlexNet shape (profiles/r3_experiments.md §9): off unless asked for
-_HALO_DGRAD = False
+_HALO_DGRAD = os.environ.get("VELES_AMD_HALO_DGRAD", "0") != "0"
 
 
 def set_conv_halo(on, dgrad=None):
