@@ -1141,8 +1141,14 @@ hipError_t launch8(const LA& la, const LB& lb, const Epi8& e, int M, int N,
                 std::is_same<LB, Dense8>::value) {
     if (want_pp256_fp8_conv(lb, M, N, groups))
       return go_pp256_fp8<LA, FA, FB>(la, lb, e, M, N, K, groups, s);
-    if (want_t4_fp8(N)) return go_t4_fp8<LA, FA, FB>(la, lb, e, M, N, K,
-                                                      groups, s);
+    // the 256 x 64 tiles for forward convolutions only: VGG b512 conv1_2
+    // backward-data (with the derivative of the layer below in the
+    // epilogue) took 3.97 ms on them against 3.55 ms on the 128-row loop,
+    // the forward 3.02 against 3.19 (profiles/r4/vgg16_b512_fp8_step_r4h.md)
+    const bool t4_64_dgrad = std::is_same<LA, ConvDgradA8>::value && N <= 64 &&
+                             hvk_fp8_variant != 75;
+    if (want_t4_fp8(N) && !t4_64_dgrad)
+      return go_t4_fp8<LA, FA, FB>(la, lb, e, M, N, K, groups, s);
   }
   const bool n64 = use_bn64(N);
   const int bn = n64 ? 64 : 128;
