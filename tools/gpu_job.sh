@@ -21,6 +21,8 @@
 #                            settings (e.g. HVK_LIBRARY=build/abl/libhvk_abl1.so,
 #                            a tools/build_abl.py diagnostic build)
 #   prof[:MODEL:BATCH:TAG:PREC]  step-only rocprofv3 kernel table
+#   profenv:VAR=VAL[+VAR=VAL]:MODEL:BATCH:TAG:PREC  the same under extra
+#                            environment settings (set before rocprofv3)
 #   pmc[:TAG[:BENCHARGS]]    four rocprofv3 --pmc passes (instruction mix,
 #                            wave states, HBM read + TA, HBM write + L2 hit)
 #                            on bench.py --mark-steps, step-only summaries
@@ -64,6 +66,17 @@ for step in "$@"; do
       tools/gpu_step.sh 900 "$log" python -u tools/bench_gemm_ab.py \
         "${b:-1024}" "${rounds:-3}" "${vars:--1}" || exit 1
       cat "$log" | head -60 ;;
+    profenv)
+      IFS=: read -r envs m b tag prec <<< "$arg"
+      M=${m:-alexnet} B=${b:-2048} T=${tag:-r4} P=${prec:-bfloat16}
+      tools/gpu_step.sh 600 "$log" env ${envs//+/ } rocprofv3 --kernel-trace \
+        --stats -d "$R/gpurun_out/prof_${M}_${T}" -o run --output-format csv -- \
+        python3 "$R/bench.py" --model $M --precision $P --steps 5 \
+        --warmup 2 --batch $B --mark-steps || exit 1
+      f=$(find gpurun_out/prof_${M}_${T} -name "*kernel_trace.csv" | head -1)
+      python tools/prof_summary.py "$f" gpurun_out/prof_${M}_${T}.md \
+        "$M b$B 1x MI355X ($P, $T, $envs)" --window --steps 5
+      head -40 gpurun_out/prof_${M}_${T}.md ;;
     abenv)
       IFS=: read -r envs b rounds vars <<< "$arg"
       tools/gpu_step.sh 900 "$log" env ${envs//+/ } python -u \
