@@ -1344,6 +1344,27 @@ hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
       return go_pp256<LA, AK, LB, BKM>(la, lb, epi, M, N, K, k_split, 1,
                                        groups, s);
   }
+  // conv weight gradients with >= 256 output channels per group (VGG
+  // conv3-5): the 256 x 256 ping-pong loop with the MN-major dY and im2col
+  // loaders, split over pixels as the 128-row loop.  Opt-in
+  // (hvk_gemm_variant 63): VGG conv3_2 at b1024 ran 820 -> 666 TF on it,
+  // the VGG-16 b512 step 8.06k -> 7.88k img/s
+  // (profiles/r4/t4_ablation/ab_pp256_wgrad.log)
+  if constexpr (!AK && !BKM && std::is_same<LA, DenseMN>::value &&
+                std::is_same<LB, ConvWgradB>::value) {
+    const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+    const int wm = (M + 255) / 256 * 256 - M;
+    if (hvk_gemm_variant == 63 && M >= 256 && wm * 8 <= M && epi.atomic &&
+        !epi.slice && la.dma_ok() && lb.dma_ok() && lb.g.OH * lb.g.OW >= 64) {
+      const long long pt = (long long)((M + 255) / 256) * ((N + 255) / 256);
+      const long long want = ((long long)tiles * splits + pt - 1) / pt;
+      int ks = (int)((K + want - 1) / want);
+      ks = (ks + BK - 1) / BK * BK;
+      const int sp = (K + ks - 1) / ks;
+      return go_pp256<LA, AK, LB, BKM>(la, lb, epi, M, N, K, ks, sp, groups,
+                                       s);
+    }
+  }
   // implicit-GEMM convolutions: 192 x 128 tiles, two workgroups per CU
   // (gemm_t4.h)
   if constexpr (BUF && t4_pair_ok<LA, AK, LB, BKM>()) {

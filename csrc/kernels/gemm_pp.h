@@ -66,17 +66,24 @@ constexpr bool pp_loader_ok() {
 // K-major implicit-GEMM conv operands (ConvFwdA / ConvDgradA, kFast): the
 // row's pixel and tap masks once (DRow), the lane's tap once per K tile
 // (DTap), as in the T4 loop
+// The MN-major conv weight-gradient operand (ConvWgradB, kFast: the im2col
+// column's tap fixed, a running pixel advanced by BK per K tile, pointer
+// LDS-DMA as in the T4 loop): MNFAST.  Its pieces must be issued once per K
+// tile, in K order (the 256 x 256 loop issues each piece exactly once).
 template <class L, bool KM, int ROWS>
 struct PPOp {
   static constexpr int NS = ROWS / 64;
   static constexpr bool FAST = KM && L::kFast;
+  static constexpr bool MNFAST = !KM && L::kFast;
   __amdgpu_buffer_rsrc_t rs;
   uint32_t v[NS];
   int kr[NS];
   int kc;
   DRow fa[FAST ? NS : 1];
-  __device__ __forceinline__ void init(const L& l, int r0, int w, int lane) {
-    rs = dma_rsrc(l.dbase());
+  typename DColOf<L, MNFAST>::type fb[MNFAST ? NS : 1];
+  __device__ __forceinline__ void init(const L& l, int r0, int w, int lane,
+                                       int kbeg = 0) {
+    if constexpr (L::kBuf) rs = dma_rsrc(l.dbase());
     kc = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
@@ -90,7 +97,10 @@ struct PPOp {
         const int hkv = ((lane >> 4) & 3) | (((Ii >> 1) & 1) << 2);
         const int c = ((((lane & 15) >> 1) ^ hkv) << 1) | (lane & 1);
         kr[i] = 4 * Ii + (lane >> 4);
-        v[i] = l.col_voff(r0 + h * 128 + 8 * c, kr[i]);
+        if constexpr (MNFAST)
+          fb[i] = l.dcol(r0 + h * 128 + 8 * c, kbeg + kr[i], false);
+        else
+          v[i] = l.col_voff(r0 + h * 128 + 8 * c, kr[i]);
       }
     }
   }
@@ -115,6 +125,16 @@ struct PPOp {
       for (int i = 0; i < NS; ++i)
         if (i >= i0 && i < i0 + n)
           dma16(rs, dst(s, w * NS + i), kin ? v[i] + kbyte : kBufOOB);
+    } else if constexpr (MNFAST) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        if (i >= i0 && i < i0 + n) {
+          __builtin_amdgcn_global_load_lds(
+              (const void*)l.dsrc(fb[i]),
+              (__attribute__((address_space(3))) void*)dst(s, w * NS + i), 16,
+              0, 0);
+          l.dnext_by(fb[i], BK);
+        }
     } else {
       const uint32_t kadv = (uint32_t)k0 * (uint32_t)l.ld * 2u;
 #pragma unroll
@@ -125,7 +145,9 @@ struct PPOp {
     }
   }
   __device__ __forceinline__ void issue(const L& l, int k0, uint16_t* s, int w) {
-    if constexpr (FAST) {
+    if constexpr (MNFAST) {
+      issue_part(l, k0, s, w, 0, NS);
+    } else if constexpr (FAST) {
       const DTap tp = l.dtap(k0 + kc);
 #pragma unroll
       for (int i = 0; i < NS; ++i)
@@ -421,8 +443,8 @@ gemm_pp256_kernel(LP lp, LQ lq, Epi epi, int P, int Q, int K, int k_split,
 
   PPOp<LP, PK, PQ_B> op;
   PPOp<LQ, QK, PQ_B> oq;
-  op.init(lp, p0, w, lane);
-  oq.init(lq, q0, w, lane);
+  op.init(lp, p0, w, lane, kbeg);
+  oq.init(lq, q0, w, lane, kbeg);
   static_assert(PPOp<LP, PK, PQ_B>::NS == 4 && PPOp<LQ, QK, PQ_B>::NS == 4,
                 "four pieces per operand and tile");
   // half h (0 / 1) of an operand's four pieces: pieces 2h, 2h + 1

@@ -205,3 +205,34 @@ def test_t4_64_conv_fwd_dgrad(cfg):
     ref = torch.nn.grad.conv2d_input((N, C, H, W), nchw(w), nchw(dy),
                                      padding=p, groups=g).permute(0, 2, 3, 1)
     close(new, ref * (aux.float() > 0).float(), 1e-2)
+
+
+@pytest.mark.parametrize("cfg", [
+    (2, 14, 14, 256, 256, 3, 1, 1),
+    (4, 13, 13, 384, 256, 3, 1, 1),     # KK = 3456 + bias column
+    (2, 9, 9, 512, 512, 3, 1, 2),       # 256 per group
+])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_pp256_conv_wgrad(cfg, splits):
+    """weight gradient (+ fused bias gradient) on the 256 x 256 ping-pong
+    loop with the MN-major dY / im2col loaders (hvk_set_gemm_variant(63))
+    against the 128-row loop and the float32 reference (f32 atomics: not
+    bit-identical)"""
+    N, H, W, C, OC, k, p, g = cfg
+    x = rnd(N, H, W, C, seed=31)
+    dy = rnd(N, H, W, OC, seed=32)
+    pad = (p, p, p, p)
+
+    def run():
+        dw = torch.full((OC, k, k, C // g), 0.25, device=DEV)
+        db = torch.full((OC,), 0.5, device=DEV)
+        ops.conv_wgrad(x, dy, dw, (1, 1), pad, g, splits=splits, dbias=db)
+        return torch.cat([dw.reshape(-1), db])
+    old, new = run_variants(run, (50, 63))
+    ref_w = torch.nn.grad.conv2d_weight(nchw(x), (OC, C // g, k, k),
+                                        nchw(dy), padding=p,
+                                        groups=g).permute(0, 2, 3, 1) + 0.25
+    ref_b = dy.float().reshape(-1, OC).sum(0) + 0.5
+    ref = torch.cat([ref_w.reshape(-1), ref_b])
+    close(new, ref, 2e-3)
+    close(old, ref, 2e-3)
