@@ -114,3 +114,59 @@ def test_tune_keeps_numerics(tab):
     torch.testing.assert_close(y1.float(), y0.float(), rtol=2e-2, atol=2e-2)
     ref = (a.float() @ w.float().t())
     torch.testing.assert_close(y1.float(), ref, rtol=2e-2, atol=0.5)
+
+
+def test_wgrad_geometry_checked_and_logical_shape_logged(tab):
+    """A weight gradient whose x / dy / dw disagree raises on the host (the
+    kernels would read out of bounds); a call logged with a shape tuple (the
+    s2d path logs the logical image, not the s2d data) keeps it."""
+    x = torch.zeros(2, 9, 9, 16)
+    dw = torch.zeros(32, 3, 3, 16)
+    with pytest.raises(ValueError):   # dy 6x6, geometry says 7x7
+        ops.conv_wgrad(x, torch.zeros(2, 6, 6, 32), dw)
+    with pytest.raises(ValueError):   # dw for 3 input channels
+        ops.conv_wgrad(x, torch.zeros(2, 7, 7, 32), torch.zeros(32, 3, 3, 3))
+    shape = (2 * 7 * 7, 32, 3 * 3 * 16 + 1, 1)
+    autotune.record(True)
+    try:
+        ops._wgrad_splits_for((2, 9, 9, 16), torch.zeros(2, 7, 7, 32), dw,
+                              (1, 1), (0, 0, 0, 0), 1, shape)
+        log = autotune.recorded()
+    finally:
+        autotune.record(False)
+    assert log[autotune.key("wgrad", *shape)][1]["x"] == (2, 9, 9, 16)
+
+
+@pytest.mark.gpu
+def test_tune_replays_s2d_weight_gradient(tab):
+    """AlexNet conv1's weight gradient takes the loader's space-to-depth image
+    (ops.S2DImage).  The autotuner must replay it on a plain image of the
+    logical shape (it once replayed the s2d data as the image and faulted)."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(4, 227, 227, 3, device=dev, generator=g).bfloat16()
+    pad = (0, 0, 0, 0)
+    OH, OW = ops.conv_out_size(227, 227, 11, 11, (4, 4), pad)
+    dy = torch.randn(4, OH, OW, 96, device=dev, generator=g).bfloat16()
+    s2 = ops.S2DImage(ops.space_to_depth(x, 4, 11, 11, pad), 4, x.shape)
+
+    def run(inp):
+        dw = torch.zeros(96, 11, 11, 3, device=dev)
+        ops.conv_wgrad(inp, dy, dw, (4, 4), pad)
+        torch.cuda.synchronize()
+        return dw
+
+    autotune.record(True)
+    try:
+        dw0 = run(s2)
+        log = autotune.recorded()
+    finally:
+        autotune.record(False)
+    (k, (kind, gm)), = log.items()
+    assert kind == "wgrad" and gm["x"] == (4, 227, 227, 3)
+    autotune.tune(log, repeats=2, tab=tab, verbose=False)
+    torch.testing.assert_close(run(x), dw0, rtol=1e-4, atol=1e-2)
+    ref = torch.nn.grad.conv2d_weight(
+        x.permute(0, 3, 1, 2).float(), (96, 3, 11, 11),
+        dy.permute(0, 3, 1, 2).float(), stride=4).permute(0, 2, 3, 1)
+    torch.testing.assert_close(dw0, ref, rtol=2e-2, atol=0.5)

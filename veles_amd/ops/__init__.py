@@ -963,6 +963,15 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     pl, pt, pr, pb = padding
     if dw.dtype != torch.float32:
         raise TypeError("conv_wgrad accumulates into float32")
+    # the kernels index x, dy and dw with this geometry: a mismatch would
+    # read out of bounds on the device
+    if (Cg * groups != C or OC % groups or dy.shape[0] != N or
+            OH != (H + pt + pb - KH) // sy + 1 or
+            OW != (W + pl + pr - KW) // sx + 1):
+        raise ValueError(
+            "conv_wgrad geometry: x %s, dy %s, dw %s, sliding %s, padding "
+            "%s, groups %d" % ((N, H, W, C), tuple(dy.shape), tuple(dw.shape),
+                               sliding, padding, groups))
     if _gpu(x):
         xt = col.x if isinstance(col, (S2DImage, PaddedImage)) else x
         chunks = _image_chunks(N, xt, dy)
@@ -993,8 +1002,10 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             # self-clearing workspace: zeroed once, cleared again by the fold
             dw2 = _workspace(("s2dg", dw.data_ptr()), (OC, KH2, KW2, C2),
                              torch.float32, dw.device, zero=True)
+            # logged with the logical image shape: the autotuner replays
+            # the call on a plain image (the s2d data has C2 channels)
             sp = splits or _wgrad_splits_for(
-                x, dy, dw, sliding, padding, groups,
+                (N, H, W, C), dy, dw, sliding, padding, groups,
                 (N * OH * OW, OC, KH2 * KW2 * C2 + 1, 1))
             _lib_call("hvk_conv_wgrad", _p(x2), _p(dy), _p(dw2), N, H2, W2,
                       C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, int(sp),
@@ -1071,7 +1082,7 @@ def _wgrad_splits_for(x, dy, dw, sliding, padding, groups, shape):
     from veles_amd.ops import autotune
     default = wgrad_splits(*shape)
     autotune.log_call("wgrad", shape, {
-        "x": tuple(x.shape), "dy": tuple(dy.shape), "dw": tuple(dw.shape),
+        "x": tuple(x if isinstance(x, tuple) else x.shape), "dy": tuple(dy.shape), "dw": tuple(dw.shape),
         "sliding": tuple(sliding), "padding": tuple(padding),
         "groups": groups, "default": default})
     t = autotune.lookup("wgrad", *shape)
