@@ -170,3 +170,17 @@ def test_tune_replays_s2d_weight_gradient(tab):
         x.permute(0, 3, 1, 2).float(), (96, 3, 11, 11),
         dy.permute(0, 3, 1, 2).float(), stride=4).permute(0, 2, 3, 1)
     torch.testing.assert_close(dw0, ref, rtol=2e-2, atol=0.5)
+
+
+def test_conv_fwd_dgrad_geometry_checked():
+    x = torch.zeros(2, 9, 9, 16)
+    w = torch.zeros(32, 3, 3, 16)
+    with pytest.raises(ValueError):
+        ops.conv_fwd(x, w, out=torch.zeros(2, 6, 6, 32))
+    with pytest.raises(ValueError):   # dy 6x6 for a 9x9 input, 3x3 kernel
+        ops.conv_dgrad(torch.zeros(2, 6, 6, 32), w, (2, 9, 9, 16))
+    with pytest.raises(ValueError):   # aux of the wrong shape
+        ops.conv_dgrad(torch.zeros(2, 7, 7, 32), w, (2, 9, 9, 16),
+                       aux=torch.zeros(2, 8, 8, 16), aux_act=1)
+    assert ops.conv_dgrad(torch.zeros(2, 7, 7, 32), w,
+                          (2, 9, 9, 16)).shape == (2, 9, 9, 16)

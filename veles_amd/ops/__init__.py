@@ -822,6 +822,9 @@ def _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out, fq):
         x = pre.x
     if out is None:
         out = torch.empty(N, OH, OW, OC, dtype=x.dtype, device=x.device)
+    elif tuple(out.shape) != (N, OH, OW, OC):
+        raise ValueError("conv_fwd: out %s, expected %s" % (
+            tuple(out.shape), (N, OH, OW, OC)))
     if _gpu(x):
         def call(*a):
             q = None
@@ -909,6 +912,17 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
     sx, sy = sliding
     pl, pt, pr, pb = padding
     aux_act = act_code(aux_act)
+    # the kernels index dy, w, aux and out with this geometry: a mismatch
+    # would read or write out of bounds on the device
+    if (Cg * groups != C or OC % groups or dy.shape[0] != N or
+            w.shape[0] != OC or
+            (OH, OW) != conv_out_size(H, W, KH, KW, sliding, padding) or
+            (out is not None and tuple(out.shape) != (N, H, W, C)) or
+            (aux is not None and tuple(aux.shape) != (N, H, W, C))):
+        raise ValueError(
+            "conv_dgrad geometry: x %s, dy %s, w %s, sliding %s, padding %s, "
+            "groups %d" % (tuple(x_shape), tuple(dy.shape), tuple(w.shape),
+                           sliding, padding, groups))
     if out is None:
         out = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
     if _gpu(dy):
