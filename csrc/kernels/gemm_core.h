@@ -1365,6 +1365,28 @@ hipError_t launch_bn(const LA& la, const LB& lb, const Epi& epi, int M, int N,
                                        s);
     }
   }
+  // TN GEMMs without the bias-gradient ones column (FC weight gradients
+  // whose bias gradient is a separate col_sum, engine.fc_bias_colsum):
+  // both operands MN-major, the 256 x 256 loop where want_pp256 takes it;
+  // a split-K accumulation is re-split as the 256 x 128 path below does.
+  // hvk_gemm_variant 64 turns it off (A/B runs)
+  if constexpr (BUF && !AK && !BKM && std::is_same<LA, DenseMN>::value &&
+                std::is_same<LB, DenseMN>::value) {
+    const int groups = (int)(grid.x / ((unsigned)tiles * splits));
+    if (hvk_gemm_variant != 64 && groups == 1 && !epi.slice &&
+        epi.ones_col < 0 && la.dma_ok() && lb.dma_ok()) {
+      int sp = splits, ks = k_split;
+      if (epi.atomic == 1 && splits > 1) {
+        const long long pt = (long long)((M + 255) / 256) * ((N + 255) / 256);
+        const long long want = ((long long)tiles * splits + pt - 1) / pt;
+        ks = (int)((K + want - 1) / want);
+        ks = (ks + BK - 1) / BK * BK;
+        sp = (K + ks - 1) / ks;
+      }
+      if ((epi.atomic == 1 || sp == 1) && want_pp256(M, N, sp, 1))
+        return go_pp256<LA, AK, LB, BKM>(la, lb, epi, M, N, K, ks, sp, 1, s);
+    }
+  }
   // implicit-GEMM convolutions: 192 x 128 tiles, two workgroups per CU
   // (gemm_t4.h)
   if constexpr (BUF && t4_pair_ok<LA, AK, LB, BKM>()) {

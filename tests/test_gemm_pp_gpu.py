@@ -123,3 +123,28 @@ def test_256_row_narrow_tiles(cfg):
                           w.float().permute(0, 3, 1, 2), b, padding=p,
                           groups=g)).permute(0, 2, 3, 1)
     close(new, ref, 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K,mode,splits", [
+    (4096, 4096, 256, "overwrite", 1),     # fc7-like weight gradient
+    (4096, 4352, 520, True, 1),            # partial K tile, accumulate
+    (4096, 4096, 4096, True, 4),           # split-K f32 atomics (re-split)
+    (4000, 4104, 96, "overwrite", 1)])     # partial row / column tiles
+def test_pp256_tn_weight_gradient(M, N, K, mode, splits):
+    """TN GEMMs without a bias-gradient column (FC weight gradients with
+    engine.fc_bias_colsum) take the 256 x 256 loop with both operands
+    MN-major; hvk_gemm_variant 64 keeps the 128-row loop.  Same K order
+    without split-K: bit-identical; with split-K: the atomics' order."""
+    a = rnd(K, M, seed=3)
+    b = rnd(K, N, seed=4)
+    init = torch.randn(M, N, device=DEV)
+
+    def run():
+        out = init.clone()
+        ops.gemm(a, b, trans_a=True, out=out, accumulate=mode, splits=splits)
+        return out
+    old, new = run_variants(run, (64, -1))
+    ref = a.float().t() @ b.float() + (0 if mode == "overwrite" else init)
+    if splits == 1:
+        assert torch.equal(old, new)
+    close(new, ref, 1e-3)
