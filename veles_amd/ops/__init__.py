@@ -714,8 +714,9 @@ def im2col(x, KH, KW, sliding, padding, out=None):
 
 
 # stride-1 convolutions with the input tile held in LDS
-# (csrc/kernels/conv_halo.hip); False runs every conv on the implicit GEMM
-_HALO = True
+# (csrc/kernels/conv_halo.hip); False (VELES_AMD_HALO=0) runs every conv on
+# the implicit GEMM
+_HALO = os.environ.get("VELES_AMD_HALO", "1") != "0"
 # the backward-data halo kernel measured slower than the implicit GEMM on
 # every AlexNet shape (profiles/r3_experiments.md §9): off unless asked for
 _HALO_DGRAD = os.environ.get("VELES_AMD_HALO_DGRAD", "0") != "0"
