@@ -1612,7 +1612,10 @@ HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
 
 // forward kernel selector for A/B runs (hvk_set_lrn_fwd_variant): 0 the
 // vertical walk with the next row prefetched, 1 the per-output preloading
-// kernel, 2 the walk without the prefetch
+// kernel, 2 the walk without the prefetch, 3 / 4 the walk with the prefetch
+// over strips of about 5 / 9 output rows (0: about 14; AlexNet b2048,
+// tools/bench_lrn.py: conv2 273 -> 256 us from 9 to 14, conv1 419 / 423,
+// 5 rows 469 / 287: profiles/r4/lrn_fwd_strips_b2048.json)
 static int g_lrn_fwd_variant = 0;
 HVK_API void hvk_set_lrn_fwd_variant(int v) { g_lrn_fwd_variant = v; }
 // backward selector (hvk_set_lrn_bwd_variant): 0 every load of an
@@ -1632,11 +1635,12 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
   const int h = n / 2;
   const long long total = (long long)N * OH * OW * (C / 8);
   if (h >= 1 && h <= 2 && g_lrn_fwd_variant != 1) {
-    // vertical walk over strips of about 9 output rows (enough threads to
-    // fill the chip at batch >= 64)
-    const int S = (OH + 8) / 9, R = (OH + S - 1) / S;
+    // vertical walk over strips of about 14 output rows (AlexNet: one strip
+    // for conv2's 13 rows, two for conv1's 27)
+    const int t = g_lrn_fwd_variant == 3 ? 5 : g_lrn_fwd_variant == 4 ? 9 : 14;
+    const int S = (OH + t - 1) / t, R = (OH + S - 1) / S;
     const long long tw = (long long)N * S * OW * (C / 8);
-    const bool pf = g_lrn_fwd_variant == 0;
+    const bool pf = g_lrn_fwd_variant != 2;
     auto kw = h == 1 ? (pf ? lrn_pool3s2_fwd_walk_kernel<1, true>
                            : lrn_pool3s2_fwd_walk_kernel<1, false>)
                      : (pf ? lrn_pool3s2_fwd_walk_kernel<2, true>
