@@ -5,8 +5,14 @@ parallelism over RCCL (one process per MI355X).
 
     python bench.py --gpus N --steps K --warmup W [--batch B]
 
-For N > 1 launch under torch.distributed.run (one rank per GPU; the driver
-does this).  Every timed step is a full training step through the veles_amd
+For N > 1 the driver launches it under torch.distributed.run (one rank per
+GPU).  Started with --gpus N > 1 and no WORLD_SIZE, it spawns the N ranks
+itself (veles_amd.parallel.launch.spawn_ranks, from a parent that makes no
+GPU call) and exits with the group's code; it never reports a 1-rank result
+for --gpus N.  At N > 1 every rank runs a step watchdog
+(veles_amd.parallel.faults.Watchdog): a rank that makes no progress for
+VELES_AMD_BENCH_WATCHDOG_S seconds (default 600) - e.g. a collective whose
+peer never arrives - prints a [watchdog] line and exits 124.  Every timed step is a full training step through the veles_amd
 StandardWorkflow: device minibatch gather + normalisation, forward, softmax
 evaluator, decision, backward, bucketed gradient all-reduce, fused SGD.
 Prints ONE JSON line on rank 0.
@@ -55,6 +61,8 @@ def main():
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 512 if args.model == "vgg16" else 2048
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn(args)
 
     import torch
     from veles_amd.utils.config import root
@@ -68,9 +76,10 @@ def main():
     import veles_amd.loader  # noqa: F401 (registers loaders)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus and args.gpus > 1:
-        print("bench.py: --gpus %d but WORLD_SIZE=%d; launch with "
-              "torch.distributed.run" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world),
+              file=sys.stderr)
+        return 2
     backend = "cpu" if args.cpu or not torch.cuda.is_available() else "hip"
     # exposed all-reduce wait per step (models/params.py comm_report)
     os.environ.setdefault("VELES_AMD_DP_STATS", "1")
@@ -84,12 +93,13 @@ def main():
     layers_fn, dataset = MODELS[args.model]
     global_batch = args.batch * dp.world_size
     # the resident synthetic set: --steps-per-epoch minibatches of ONE
-    # rank's batch, at least two global minibatches - so the per-rank HBM
-    # it takes stays fixed as N grows (every rank holds the whole set: the
-    # global shuffle may hand any sample to any rank); at N >= 8 an epoch
-    # is two steps, measured as cheap as sixteen (152.9k vs 154.3k img/s
-    # at b2048, profiles/r4/alexnet_batch_sweep.md)
-    n_train = max(2 * global_batch, args.batch * args.steps_per_epoch)
+    # rank's batch, at least one global minibatch.  Every rank holds the
+    # whole set (the global shuffle may hand any sample to any rank), so the
+    # per-rank HBM it takes is fixed up to N = steps_per_epoch (16: 32768
+    # images, 5 GB at b2048) and grows linearly past it; an epoch of one or
+    # two steps measured as cheap as sixteen (152.9k vs 154.3k img/s at
+    # b2048, profiles/r4/alexnet_batch_sweep.md)
+    n_train = max(global_batch, args.batch * args.steps_per_epoch)
     launcher = DummyLauncher()
     launcher.dp_ = dp
     wf = StandardWorkflow(
@@ -107,6 +117,7 @@ def main():
         # buffer sets, one graph each, so each set needs its passes
         graph_warmup=_graph_warmup(args.warmup))
     wf.initialize(device=device)
+    wd = _watchdog(wf, dp)
 
     def sync():
         if backend == "hip":
@@ -114,6 +125,7 @@ def main():
 
     wf.run_steps(args.warmup)
     sync()
+    _stall_for_test(dp)
     store = getattr(wf, "param_store_", None)
     if store is not None:
         store.comm_report()   # drop the warmup steps' events
@@ -147,7 +159,7 @@ def main():
         with graphs.suspended():
             wf.run_steps(args.stats_steps)
         sync()
-    dp_info = dp_report(dp, store, backend)
+    dp_info = dp_report(dp, store, backend, wf)
     if dp.rank == 0:
         base = None
         try:
@@ -186,7 +198,49 @@ def main():
                          wf.get_unit_run_time_stats()]
                 json.dump({"result": out, "unit_stats": stats}, f, indent=1)
     dp.barrier()
+    if wd is not None:
+        wd.stop()
     dp.shutdown()
+    return 0
+
+
+def _spawn(args):
+    """--gpus N without a launcher: one child rank per GPU (the driver's
+    torch.distributed.run contract: RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / a free MASTER_PORT), rank 0's JSON line on this
+    process's stdout.  This parent never touches the GPU."""
+    from veles_amd.parallel.launch import spawn_ranks
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    code = spawn_ranks(list(range(args.gpus)), cmd)
+    if code:
+        print("bench.py: rank group exited with %s" % code, file=sys.stderr)
+    return code
+
+
+def _watchdog(wf, dp):
+    """At N > 1: exit 124 with a [watchdog] line when this rank's step
+    makes no progress (decision runs) for VELES_AMD_BENCH_WATCHDOG_S s - a
+    hung collective ends the run instead of holding the node."""
+    if dp.world_size <= 1:
+        return None
+    from veles_amd.parallel.faults import Watchdog
+    timeout = float(os.environ.get("VELES_AMD_BENCH_WATCHDOG_S", "600"))
+
+    def expire():
+        print("[watchdog] bench.py rank %d: no training step finished for "
+              "%.0f s (a collective waiting on a peer?); exiting 124" %
+              (dp.rank, timeout), file=sys.stderr, flush=True)
+        os._exit(124)
+    return Watchdog(timeout, on_expire=expire).install(wf)
+
+
+def _stall_for_test(dp):
+    """VELES_AMD_BENCH_STALL_RANK=r (tests only): rank r stops making
+    progress after the warmup, as a rank stuck in a collective would."""
+    r = os.environ.get("VELES_AMD_BENCH_STALL_RANK")
+    if r is not None and int(r) == dp.rank and dp.world_size > 1:
+        while True:
+            time.sleep(1.0)
 
 
 def _graph_warmup(warmup):
@@ -197,7 +251,7 @@ def _graph_warmup(warmup):
     return max(0, min(2, per - 1))
 
 
-def dp_report(dp, store, backend):
+def dp_report(dp, store, backend, wf=None):
     """What the multi-rank step did, for reading an N > 1 result
     (docs/PARALLEL.md): ranks seen by the process group, RCCL version,
     gradient bucket layout and wire dtype, and the compute stream's exposed
@@ -226,6 +280,7 @@ def dp_report(dp, store, backend):
         tl = store.timeline_report()
         if tl is not None:
             info["bucket_timeline"] = tl
+    info["per_rank_graphs"] = _per_rank_graphs(dp, store, backend, wf)
     ms = torch.tensor([rep["mean_ms"] if rep else -1.0], dtype=torch.float64)
     if dp.world_size > 1:
         if backend == "hip":
@@ -241,5 +296,24 @@ def dp_report(dp, store, backend):
     return info
 
 
+def _per_rank_graphs(dp, store, backend, wf):
+    """[rank, graph_backward, forward captures, forward replays, backward
+    captures, backward replays] of every rank (all-gathered)."""
+    import torch
+    import torch.distributed as dist
+    segs = {s.name: s for s in getattr(wf, "graph_segments_", [])} \
+        if wf is not None else {}
+    row = [dp.rank, int(bool(store.graph_safe())) if store else 0]
+    for name in ("forward", "backward"):
+        s = segs.get(name)
+        row += [s.captures, s.replays] if s is not None else [0, 0]
+    t = torch.tensor(row, dtype=torch.int64)
+    if backend == "hip":
+        t = t.cuda()
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[int(v) for v in o.cpu()] for o in out]
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -110,3 +110,52 @@ def test_diamond_branches_on_streams(graph):
         root.common.engine.parallel_fanout = old
     assert torch.equal(outs[False], outs[True])
     assert float(outs[True].float().abs().sum()) > 0
+
+
+def test_dead_end_branch_rejoins_for_capture():
+    """A branch that never reaches a join (here: the end point links from
+    branch a only, b is a dead end) is joined back when the outermost
+    scheduler drain ends (_Branches.join_all), so a capture of the pass ends
+    cleanly and the replay computes b's output too."""
+    dev = Device(backend="hip")
+    old = root.common.engine.parallel_fanout
+    try:
+        root.common.engine.parallel_fanout = True
+        g = torch.Generator(device="cuda").manual_seed(5)
+        x = (torch.rand(2048, 2048, generator=g, device="cuda") - 0.5).to(
+            torch.bfloat16)
+        wa = ((torch.rand(2048, 2048, generator=g, device="cuda") - 0.5) /
+              16).to(torch.bfloat16)
+        wb = ((torch.rand(2048, 2048, generator=g, device="cuda") - 0.5) /
+              16).to(torch.bfloat16)
+        wf = DummyWorkflow(dev)
+        fork = TrivialUnit(wf)
+        fork.link_from(wf.start_point)
+        a = _Branch(wf, x, wa, name="branch_a")
+        b = _Branch(wf, x, wb, name="branch_b")
+        a.link_from(fork)
+        b.link_from(fork)
+        wf.end_point.unlink_from(wf.start_point)
+        wf.end_point.link_from(a)
+        wf.initialize(device=dev)
+        wf.run()
+        torch.cuda.synchronize()
+        ref = b.output.devmem.clone()
+        for u in wf:
+            u.stopped = False
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            graph.capture_begin()
+            with _Scheduler() as sched:
+                wf.start_point.run_dependent()
+                sched.drain()
+            graph.capture_end()
+        b.output.devmem.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert a.stream_seen != b.stream_seen
+        assert torch.equal(b.output.devmem, ref)
+    finally:
+        root.common.engine.parallel_fanout = old

@@ -148,8 +148,8 @@ class Main(object):
             trace_events=args.trace_events or None, log_id=args.log_id,
             snapshot_file=args.snapshot or None)
         if args.snapshot:
-            from veles_amd.snapshotter import SnapshotterToFile
-            wf = SnapshotterToFile.import_(args.snapshot)
+            from veles_amd.snapshotter import import_snapshot
+            wf = import_snapshot(args.snapshot)
             wf.workflow = self.launcher
             self.launcher.add_ref(wf)
             if args.test and hasattr(wf, "switch_to_testing"):

@@ -38,8 +38,10 @@ any such unit in a segment keeps that segment eager.  A capture that fails
 (an op that synchronises, an unsupported call) re-runs the pass eagerly and
 pins that key to eager mode; host state that the discarded capture
 advanced (the parameter store's step counters, the fp8 history step) is
-restored first (``state_hooks``).  Multi-rank workflows over RCCL capture
-the backward too, collectives included: the bucketed all-reduces are
+restored first (``state_hooks``).  Multi-rank workflows over RCCL can
+capture the backward too, collectives included (default on a one-rank
+group; at N > 1 opt-in with ``root.common.engine.dp.graph_backward =
+True`` or ``VELES_AMD_DP_GRAPH_BACKWARD=1`` until a multi-GPU parity run): the bucketed all-reduces are
 enqueued by the GD units in the same order at every rank and RCCL
 collectives are stream-capturable, so the graph holds the compute stream's
 kernels, each bucket's all-reduce on the process group's stream (forked
@@ -47,8 +49,7 @@ from and joined back into the capture by events) and the per-bucket updates
 on the update stream - N = 1 and N > 1 replay the same kind of step.  A
 backward whose collectives block the host (gloo) or that accumulates
 gradients over micro-steps stays eager (``graph_safe`` of the parameter
-store); ``root.common.engine.dp.graph_backward = False`` (or
-``VELES_AMD_DP_GRAPH_BACKWARD=0``) keeps the multi-rank backward eager.
+store).
 :func:`suspended` runs passes eagerly for a while (per-bucket timing events
 of the instrumented steps cannot be captured).  Disable graphs with
 ``root.common.engine.graphs = False`` or ``VELES_AMD_GRAPHS=0``.
@@ -188,6 +189,8 @@ class _HipCapture(object):
     def __exit__(self, *exc):
         ok = False
         try:
+            from veles_amd.units import _Branches
+            _Branches.join_all()   # unjoined branch streams end the capture
             self.graph.capture_end()
             ok = True
         finally:

@@ -104,8 +104,14 @@ class Launcher(Logger):
         """Every rank of a resumed data-parallel job must have restored the
         same snapshot bytes: replicas that resume different epochs / loader
         positions / momenta diverge and deadlock at the next epoch end."""
+        import hashlib
+        import os
         from veles_amd.parallel.launch import snapshot_digest
-        mine = snapshot_digest(self.snapshot_file)
+        if os.path.isfile(self.snapshot_file):
+            mine = snapshot_digest(self.snapshot_file)
+        else:   # sqlite:// or http(s):// (import_snapshot): the spec itself
+            mine = (0, hashlib.sha1(
+                self.snapshot_file.encode()).hexdigest())
         allv = self.dp_.all_gather_object(mine)
         if any(v != allv[0] for v in allv):
             raise RuntimeError(

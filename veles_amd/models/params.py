@@ -636,8 +636,14 @@ class ParameterStore(object):
         if not self._multi():
             return True
         from veles_amd.utils.config import root, get
+        # default: captured only on a one-rank (solo) RCCL group, where it
+        # was measured against dp1; with real peers the backward stays eager
+        # (RCCL collectives under graph capture have no multi-GPU parity
+        # run yet; the eager step is GPU-bound, so it costs no throughput)
+        # until engine.dp.graph_backward / VELES_AMD_DP_GRAPH_BACKWARD=1
+        default = bool(getattr(self.dp, "solo", False))
         on = os.environ.get("VELES_AMD_DP_GRAPH_BACKWARD", "1" if get(
-            root.common.engine.dp.graph_backward, True) else "0") != "0"
+            root.common.engine.dp.graph_backward, default) else "0") != "0"
         return on and not getattr(self.dp, "host_blocking_wait", True)
 
     def _multi(self):

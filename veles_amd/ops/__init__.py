@@ -497,7 +497,18 @@ def _nhwc(x):
 _WS = {}
 
 
+def _branch_key():
+    """The branch stream's id while a fan-out branch runs (units._Branches):
+    concurrent branches must not share scratch buffers."""
+    from veles_amd.units import _Branches
+    br = _Branches.current()
+    return None if br is None else id(br[0])
+
+
 def _workspace(key, shape, dtype, device, zero=False):
+    bk = _branch_key()
+    if bk is not None:
+        key = (key, "branch", bk)
     t = _WS.get(key)
     if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or \
             t.device != device:

@@ -133,6 +133,15 @@ class _Registry(object):
 _REGISTRIES = {}
 
 
+def release_dp(dp):
+    """Forget ``dp`` in every registry (DataParallel.shutdown): a later
+    workflow in the same process must not prime through a destroyed
+    process group."""
+    for r in _REGISTRIES.values():
+        if r.dp is dp:
+            r.dp = None
+
+
 def registry(device):
     device = torch.device(device)
     key = (device.type, device.index)
@@ -181,9 +190,10 @@ class Scaler(object):
             st[:HIST] = x.float().abs().max()
             st[HIST] = 0
         dp = self.registry.dp
-        if dp is not None and getattr(dp, "multi", False):
+        import torch.distributed as dist
+        if dp is not None and getattr(dp, "multi", False) and \
+                dist.is_initialized():
             # the first scale of every rank from the GLOBAL batch's amax
-            import torch.distributed as dist
             dist.all_reduce(st, op=dist.ReduceOp.MAX)
 
 

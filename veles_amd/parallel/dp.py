@@ -126,6 +126,8 @@ class DataParallel(object):
         return out
 
     def shutdown(self):
+        from veles_amd.ops import fp8
+        fp8.release_dp(self)
         if self.multi and dist.is_initialized():
             dist.destroy_process_group()
 

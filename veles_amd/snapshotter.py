@@ -145,7 +145,7 @@ class SnapshotterBase(Unit, metaclass=SnapshotterRegistry):
 
     @staticmethod
     def import_(file_name):
-        return SnapshotterToFile.import_(file_name)
+        return import_snapshot(file_name)
 
 
 class SnapshotterToFile(SnapshotterBase):
@@ -265,3 +265,61 @@ class SnapshotterToDB(SnapshotterBase):
         c.close()
         with gzip.GzipFile(fileobj=io.BytesIO(row[0])) as f:
             return pickle.load(f)
+
+
+def _split_sqlite(spec):
+    """sqlite://<database file>[/<table>[/<row id>]] (SnapshotterToDB's
+    destination string) -> (database, table, row id or None)."""
+    rest = spec[len("sqlite://"):]
+    parts = rest.split("/")
+    for i in range(len(parts), 0, -1):
+        db = "/".join(parts[:i])
+        if db and os.path.isfile(db):
+            tail = [t for t in parts[i:] if t]
+            if len(tail) > 2:
+                break
+            table = tail[0] if tail else "veles"
+            rid = int(tail[1]) if len(tail) > 1 else None
+            return db, table, rid
+    raise FileNotFoundError("no SQLite snapshot database in %r" % spec)
+
+
+def _fetch(url, directory=None):
+    """Download an http(s) snapshot into the snapshot directory (the name
+    keeps its codec extension) and return the local path."""
+    import urllib.parse
+    import urllib.request
+    directory = directory or get(root.common.dirs.snapshots, ".")
+    os.makedirs(directory, exist_ok=True)
+    name = os.path.basename(urllib.parse.urlparse(url).path) or \
+        "downloaded.pickle"
+    dst = os.path.join(directory, name)
+    tmp = dst + ".part"
+    with urllib.request.urlopen(url, timeout=60) as r, open(tmp, "wb") as f:
+        while True:
+            chunk = r.read(1 << 20)
+            if not chunk:
+                break
+            f.write(chunk)
+    os.replace(tmp, dst)
+    return dst
+
+
+def import_snapshot(spec):
+    """``-w`` for every sink (reference veles/__main__.py:539-589): a file
+    path, ``sqlite://db[/table[/id]]`` (SnapshotterToDB; newest row when
+    the id is omitted) or an ``http(s)://`` URL (fetched into
+    root.common.dirs.snapshots first)."""
+    spec = spec.strip()
+    if spec.startswith("sqlite://"):
+        db, table, rid = _split_sqlite(spec)
+        logging.getLogger("Snapshotter").info(
+            "Reading %s table %s row %s", db, table,
+            "newest" if rid is None else rid)
+        return SnapshotterToDB.import_from(db, table, rid)
+    if spec.startswith(("http://", "https://")):
+        return SnapshotterToFile.import_(_fetch(spec))
+    if spec.startswith("odbc://"):
+        raise ValueError("odbc:// snapshots: use the SQLite sink "
+                         "(sqlite://<file>[/<table>[/<id>]])")
+    return SnapshotterToFile.import_(spec)

@@ -101,6 +101,10 @@ class _Scheduler(object):
 
     def __exit__(self, *exc):
         self._tls.stack.pop()
+        if not self._tls.stack:
+            # the outermost drain is over: branches that never reached a
+            # join (dead ends, end_point from one parent) rejoin here
+            _Branches.join_all()
         return False
 
     def drain(self):
@@ -165,11 +169,39 @@ class _Branches(object):
         while len(pool) < need:
             pool.append(torch.cuda.Stream(device))
         out = []
+        forked = cls._forked()
         for i in range(n):
             st = pool[d * cls.PER_FORK + i % cls.PER_FORK]
             st.wait_stream(base)
             out.append((st, parent, base))
+            forked[id(st)] = st
         return out
+
+    @classmethod
+    def _forked(cls):
+        f = getattr(cls._tls, "forked", None)
+        if f is None:
+            f = cls._tls.forked = {}
+        return f
+
+    @classmethod
+    def join_all(cls):
+        """Make the current stream wait on every branch stream forked since
+        the last call.  A join unit only waits on its own parents, so a
+        branch that ends anywhere else would otherwise still run while the
+        next step's kernels on the compute stream overwrite its inputs, and
+        a capture would end with that stream unjoined.  Called when the
+        outermost scheduler drain ends and before a HIP graph capture ends
+        (graphs._HipCapture)."""
+        forked = getattr(cls._tls, "forked", None)
+        if not forked:
+            return
+        import torch
+        cls._tls.forked = {}
+        cur = torch.cuda.current_stream()
+        for st in forked.values():
+            if st.cuda_stream != cur.cuda_stream:
+                cur.wait_stream(st)
 
 
 _ROCTX = [None, False]
