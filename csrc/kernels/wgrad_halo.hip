@@ -1,0 +1,478 @@
+// wgrad_halo.hip - convolution weight gradient with the input window of a
+// pixel step staged ONCE in LDS and shared by every tap ("halo" wgrad).
+//
+//   dW[oc][kh][kw][c] (+)= sum_p dY[p][oc] * X[n(p)][oh(p)+kh-pt][ow(p)+kw-pl][c]
+//
+// Why (round 5, VERDICT r4 "next" #1): the GEMM formulation of the weight
+// gradient (gemm_core.h ConvWgradB, T4) stages im2col(X) = KH*KW shifted
+// copies of the same pixels through LDS-DMA every K step.  The DMA pieces,
+// not the MFMAs, bound those loops (profiles/r4/t4_ablation/README.md:
+// without the main-loop DMA +62-73 % on the weight gradients).  Here a
+// workgroup owns an output tile of MT output channels x (KHT*KW taps x NP
+// 16-channel planes) and loops over a range of pixels in steps of 64; per
+// step it DMAs
+//   * A = dY[64 pixels][MT channels]  (MN-major, 64 x MT bf16), and
+//   * the input WINDOW those 64 pixels touch: the image rows they span plus
+//     the kh halo, all columns plus the kw halo, NP x 16 channels -
+// and every tap reads its B fragments out of the same window at a constant
+// offset (kh * Wp + kw slots).  Per step that is ~30 KiB for 64 x MT x
+// (KHT*KW*16*NP) MACs: 3x3, MT 128, NP 2 -> 0.0058 operand bytes per FLOP
+// against 0.013 for the T4 loop and 0.0156 for the 128-row loop.
+//
+// Window layout (per plane, 32-B slots of 16 bf16 channels): slot
+// rs * Wp + cs holds input pixel (row of window row rs, column cs - pl).
+// Wp = OW + 8 is congruent to OW mod 8, so 8 consecutive output pixels -
+// across an output-row wrap too - map to 8 slots that are distinct mod 8:
+// the ds_read_b64_tr_b16 lane groups (8 pixels x 32 B) hit every bank once.
+// Window row rs of a step starting at output row oh0 of image n0 is input
+// row oh0 + kh0 - pt + rs of image n0 while rs < OH - oh0 + KHT - 1, and
+// input row rs - (OH - oh0) - (KHT - 1) + kh0 - pt of image n0 + 1 after
+// that (the second image's rows shifted by the halo so the images never
+// share a slot).  A step spans at most two images (OH * OW >= 64), and one
+// when OH * OW is a multiple of 64 (the window then has no second image).
+//
+// K order.  MFMA 16x16x32 k labels map to pixels pi(l) = (l & 4 ? 16 : 0) +
+// (l >> 3) * 4 + (l & 3) (+32 per half step) on BOTH operands, so each
+// 32-lane group of a transposed read covers 8 consecutive pixels (the
+// conflict-free shape above).  The sum over pixels is order-independent
+// up to f32 rounding: results match the 128-row loop to rounding, not bits.
+//
+// Split over pixels: each workgroup stores its f32 tile into its own slice
+// of a [splits][OC][KK] workspace (no atomics), and hvk_wgrad_finish adds
+// the slices in split order into dW - deterministic.  The bias gradient
+// comes from extra MFMAs against an all-ones operand in the workgroups of
+// tap group 0 / channel chunk 0 (slices [splits][OC]).
+//
+// Reference counterpart: the GD units' err x input matmuls through OCLBLAS
+// (/root/reference/veles/ocl_blas.py:187-236); SURVEY §2.4 row 1.
+#include "conv_geom.h"
+
+using namespace hvk;
+
+namespace {
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct HaloGeom {
+  int N, H, W, C, OH, OW, OC, Cg, OCg, KH, KW, pt, pl;
+  int P;    // N * OH * OW
+  int KK;   // KH * KW * Cg
+  int Wp;   // window slots per row (OW + 8)
+  int WR;   // window rows
+  FastDiv fOW;
+};
+
+// XOR of the 32-B block index of A image row r (MT / 16 blocks per row):
+// 8 consecutive rows (one 32-lane transposed read) hit every bank once
+template <int MT>
+__device__ __forceinline__ int a_sw(int r) {
+  if constexpr (MT == 128) return r & 7;
+  else if constexpr (MT == 96) return (r >> 2) & 1;
+  else return (r >> 1) & 3;   // 64, 192
+}
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+// two transposed 8-B reads (k rows of this lane's pixel, +16 pixels) ->
+// one 16x16x32 operand fragment; o0 / o1 are LDS byte offsets
+__device__ __forceinline__ bf16x8 tr_read(lds_u8* sm, uint32_t o0,
+                                          uint32_t o1) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sm + o0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sm + o1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// MT: output channels per tile; NP: 16-channel planes; KHT: kh rows per tap
+// group; KW: taps per kh row; NJW: n-tiles (16 columns) per wave column;
+// PB: LDS bytes per window plane; BIAS: fold the bias gradient
+template <int MT, int NP, int KHT, int KW, int NJW, int PB>
+__global__ void __launch_bounds__(256, 2)
+wgrad_halo_kernel(const uint16_t* __restrict__ x,
+                  const uint16_t* __restrict__ dy, float* __restrict__ ws,
+                  float* __restrict__ wsb, HaloGeom g, int mtiles,
+                  int cchunks, int kgroups, int tiles, int kspan,
+                  int bias) {
+  constexpr int NJ = KHT * KW * NP;          // n-tiles of the workgroup
+  static_assert(2 * NJW >= NJ, "two wave columns cover the n-tiles");
+  constexpr int MI = MT / 32;                // m-tiles per wave (2 x 2 waves)
+  constexpr int AP = MT * 2;                 // A image row pitch (bytes)
+  constexpr int ABYTES = 64 * AP;
+  constexpr int NA = ABYTES / 1024;          // A DMA pieces per step
+  static_assert(NA % 4 == 0, "A pieces divide over the four waves");
+  constexpr int NAW = NA / 4;
+  constexpr int BBYTES = NP * PB;
+  constexpr int NB = (BBYTES + 1023) / 1024; // window DMA pieces per step
+  constexpr int NBW = (NB + 3) / 4;
+  constexpr int STAGE = ABYTES + NB * 1024;
+  static_assert(2 * 2 * STAGE <= 160 * 1024, "two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+  const int wgid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wgid % tiles;
+  const int split = wgid / tiles;
+  int tt = tile;
+  const int kg = tt % kgroups; tt /= kgroups;
+  const int cc = tt % cchunks; tt /= cchunks;
+  const int mt = tt % mtiles;
+  const int gi = tt / mtiles;
+  const int pbeg = split * kspan;
+  const int pend = min(g.P, pbeg + kspan);
+  if (pbeg >= pend) return;   // the host sizes splits so this never happens
+  const int coff_y = gi * g.OCg + mt * MT;
+  const int coff_x = gi * g.Cg + cc * 16 * NP;
+  const int kh0 = kg * KHT;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int trq = fr >> 2, trp = fr & 3;
+  const int q = fq * 4 + trq;   // this lane's pixel (+16 h + 32 ks)
+
+  lds_u8* sm = (lds_u8*)smem;
+  const __amdgpu_buffer_rsrc_t ra = dma_rsrc(dy);
+  const __amdgpu_buffer_rsrc_t rb = dma_rsrc(x);
+
+  // ---- A DMA slots: image byte -> (row r, logical 8-channel chunk)
+  uint32_t a_off[NAW];
+  int a_row[NAW];
+#pragma unroll
+  for (int i = 0; i < NAW; ++i) {
+    const int ib = (w * NAW + i) * 1024 + 16 * lane;
+    const int r = ib / AP;
+    const int pc = (ib - r * AP) >> 4;
+    const int lb = (pc >> 1) ^ a_sw<MT>(r);
+    const int m = lb * 16 + (pc & 1) * 8;
+    a_row[i] = r;
+    a_off[i] = (uint32_t)(r * g.OC + coff_y + m) * 2u;
+  }
+  // ---- window DMA slots: image byte -> (plane, window row, column, half)
+  const int WS = g.WR * g.Wp;
+  int b_rs[NBW];
+  uint32_t b_col[NBW];
+  uint32_t b_ok[NBW];
+#pragma unroll
+  for (int i = 0; i < NBW; ++i) {
+    const int pi = w + 4 * i;
+    const int ib = pi * 1024 + 16 * lane;
+    const int plane = ib / PB;
+    const int wb = ib - plane * PB;
+    const int slot = wb >> 5;
+    const int half = (wb >> 4) & 1;
+    const int rs = slot / g.Wp;
+    const int cs = slot - rs * g.Wp;
+    const int iw = cs - g.pl;
+    b_rs[i] = rs;
+    b_ok[i] = (pi < NB && plane < NP && slot < WS && cs < g.OW + g.KW - 1 &&
+               iw >= 0 && iw < g.W) ? 1u : 0u;
+    b_col[i] = (uint32_t)(iw * g.C + coff_x + plane * 16 + half * 8) * 2u;
+  }
+  const uint32_t rowbytes = (uint32_t)g.W * g.C * 2u;
+
+  // ---- A fragment offsets (bytes in the A image) of this lane's m-tiles
+  const int mrow0 = wr * (MT / 2);
+  int a_frag[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mb = mrow0 / 16 + i;
+    a_frag[i] = q * AP + ((mb ^ a_sw<MT>(q)) << 5) + trp * 8;
+  }
+
+  f32x4 acc[MI][NJW];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
+                       (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
+
+  // step decode (wave-uniform): first pixel's image / row / column
+  int p0 = pbeg;
+  uint32_t n0, rem, oh0, ow0;
+  {
+    uint32_t ohw = (uint32_t)g.OH * g.OW;
+    n0 = (uint32_t)p0 / ohw;
+    rem = (uint32_t)p0 - n0 * ohw;
+    oh0 = fdiv(rem, g.fOW);
+    ow0 = rem - oh0 * g.OW;
+  }
+
+  // DMA of the step at pixel p (decoded n, oh, ow) into stage st
+  auto issue = [&](int p, int n, int oh, uint8_t* st) {
+    const uint32_t pa = (uint32_t)p * (uint32_t)g.OC * 2u;
+#pragma unroll
+    for (int i = 0; i < NAW; ++i) {
+      const uint32_t v = (p + a_row[i] < pend) ? pa + a_off[i] : kBufOOB;
+      dma16(ra, st + (w * NAW + i) * 1024, v);
+    }
+    // window rows: image n up to row slot rc, image n + 1 after it
+    const int rc = g.OH - oh + KHT - 1;
+    const int ih_a = oh + kh0 - g.pt;
+    const int ih_b = kh0 - g.pt - rc;
+    const int gr_a = n * g.H + ih_a;
+    const int gr_b = (n + 1) * g.H + ih_b;
+    const bool n1ok = n + 1 < g.N;
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      if (w + 4 * i < NB) {   // wave-uniform
+        const int rs = b_rs[i];
+        const bool first = rs < rc;
+        const int ih = (first ? ih_a : ih_b) + rs;
+        const int gr = (first ? gr_a : gr_b) + rs;
+        const bool ok = b_ok[i] && (unsigned)ih < (unsigned)g.H &&
+                        (first || n1ok);
+        const uint32_t v = ok ? (uint32_t)gr * rowbytes + b_col[i] : kBufOOB;
+        dma16(rb, st + ABYTES + (w + 4 * i) * 1024, v);
+      }
+    }
+  };
+  auto advance = [&](int& p, uint32_t& n, uint32_t& oh, uint32_t& ow) {
+    p += 64;
+    ow += 64;
+    while (ow >= (uint32_t)g.OW) {   // scalar: at most 64 / OW + 1 turns
+      ow -= g.OW;
+      if (++oh == (uint32_t)g.OH) { oh = 0; ++n; }
+    }
+  };
+
+  const int nk = (pend - pbeg + 63) >> 6;
+  issue(p0, n0, oh0, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  int pn = p0;
+  uint32_t nn = n0, ohn = oh0, own = ow0;
+  advance(pn, nn, ohn, own);
+
+  const bool bwave = bias && kg == 0 && cc == 0 && wc == 0;
+
+  auto main_loop = [&](auto wcc, auto with_bias) {
+    constexpr int WC = decltype(wcc)::value;
+    constexpr bool WB = decltype(with_bias)::value;
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint32_t cur = (kt & 1) * STAGE;
+      if (kt + 1 < nk) issue(pn, nn, ohn, smem + ((kt + 1) & 1) * STAGE);
+      // B fragment bases (LDS bytes) of this lane's 4 pixels (q + 16 i)
+      // for every kh of the tap group
+      uint32_t bb[4][KHT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t ow = ow0 + q + 16 * i;
+        const uint32_t gr = fdiv(ow, g.fOW);
+        const int owr = (int)(ow - gr * (uint32_t)g.OW);
+        const int rs = (int)gr + ((oh0 + gr >= (uint32_t)g.OH) ? KHT - 1 : 0);
+        const uint32_t base = cur + ABYTES + (rs * g.Wp + owr) * 32 + trp * 8;
+#pragma unroll
+        for (int kh = 0; kh < KHT; ++kh) bb[i][kh] = base + kh * g.Wp * 32;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 a[MI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const uint32_t oa = cur + a_frag[i] + ks * 32 * AP;
+          a[i] = tr_read(sm, oa, oa + 16 * AP);
+        }
+#pragma unroll
+        for (int j = 0; j < NJW; ++j) {
+          const int jg = WC * NJW + j;
+          if (jg < NJ) {   // compile-time after unrolling (WC constant)
+            const int tl = jg / NP, pl_ = jg - (jg / NP) * NP;
+            const int khl = tl / KW, kwl = tl - (tl / KW) * KW;
+            const uint32_t off = kwl * 32 + pl_ * PB;   // bytes
+            const bf16x8 b = tr_read(sm, bb[2 * ks][khl] + off,
+                                     bb[2 * ks + 1][khl] + off);
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  b, a[i], acc[i][j], 0, 0, 0);
+          }
+        }
+        if constexpr (WB) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+            accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a[i],
+                                                              accb[i], 0, 0, 0);
+        }
+      }
+      // step kt + 1 landed; every read of step kt done
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      ow0 = own; oh0 = ohn; n0 = nn;
+      advance(pn, nn, ohn, own);
+    }
+  };
+  if (wc == 0) {
+    if (bwave) main_loop(std::integral_constant<int, 0>{}, std::true_type{});
+    else main_loop(std::integral_constant<int, 0>{}, std::false_type{});
+  } else {
+    main_loop(std::integral_constant<int, 1>{}, std::false_type{});
+  }
+
+  // ---- epilogue: D[n][m] quads (4 consecutive n of one m) -> slice
+  const long long sbase = (long long)split * g.OC;
+#pragma unroll
+  for (int j = 0; j < NJW; ++j) {
+    const int jg = wc * NJW + j;
+    if (jg >= NJ) continue;
+    const int tl = jg / NP, pl_ = jg - (jg / NP) * NP;
+    const int khg = kh0 + tl / KW, kwl = tl - (tl / KW) * KW;
+    const int ng = (khg * g.KW + kwl) * g.Cg + cc * 16 * NP + pl_ * 16 + fq * 4;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int mg = coff_y + mrow0 + i * 16 + fr;
+      *(float4*)(ws + (sbase + mg) * g.KK + ng) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+  if (bwave && fq == 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+      wsb[sbase + coff_y + mrow0 + i * 16 + fr] = accb[i][0];
+  }
+}
+
+// dW[e] += sum_s ws[s][e] (e < n, float4), dbias[m] += sum_s wsb[s][m]
+__global__ void __launch_bounds__(256)
+wgrad_finish_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                    long long n4, int splits, const float* __restrict__ wsb,
+                    float* __restrict__ db, int oc) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n4;
+       e += stride) {
+    float4 s = ((const float4*)ws)[e];
+    for (int k = 1; k < splits; ++k) {
+      const float4 v = ((const float4*)ws)[(long long)k * n4 + e];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float4 d = ((float4*)dw)[e];
+    d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
+    ((float4*)dw)[e] = d;
+  }
+  if (db != nullptr && blockIdx.x == 0) {
+    for (int m = threadIdx.x; m < oc; m += blockDim.x) {
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k) s += wsb[(long long)k * oc + m];
+      db[m] += s;
+    }
+  }
+}
+
+struct Plan {
+  int var;        // 0: unsupported
+  int MT, NP, KHT, PB;
+  int tiles, mtiles, cchunks, kgroups;
+  int splits, kspan;
+  HaloGeom g;
+};
+
+constexpr int kSlots = 512;   // workgroups resident at two per CU
+
+Plan make_plan(int N, int H, int W, int C, int OC, int KH, int KW, int pt,
+               int pl, int OH, int OW, int groups, int splits) {
+  Plan p{};
+  const int Cg = C / groups, OCg = OC / groups;
+  HaloGeom& g = p.g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.OH = OH; g.OW = OW; g.OC = OC;
+  g.Cg = Cg; g.OCg = OCg; g.KH = KH; g.KW = KW; g.pt = pt; g.pl = pl;
+  g.P = N * OH * OW;
+  g.KK = KH * KW * Cg;
+  g.Wp = OW + 8;
+  g.fOW = make_fastdiv(OW);
+  if (OH * OW < 64 || KW > 9 || C % 8 != 0 || OC % 8 != 0) return p;
+  if ((long long)N * H * W * C * 2 >= kBufMaxBytes ||
+      (long long)g.P * OC * 2 >= kBufMaxBytes)
+    return p;
+  const int span = (OW - 1 + 63) / OW + 1;   // output rows of 64 pixels
+  // with OH * OW a multiple of 64 no step crosses an image (steps start at
+  // multiples of 64): no second image's rows in the window
+  const int cross = (OH * OW) % 64 != 0 ? 2 : 1;
+  struct Cand { int var, MT, NP, KHT, KW, PB; };
+  const Cand cands[] = {
+      {1, 128, 2, 3, 3, 7168},
+      {2, 96, 2, 3, 3, 7168},
+      {3, 128, 3, 1, 5, 5120},
+      {4, 128, 2, 3, 3, 10240},   // VGG-16 28 / 56-wide layers
+  };
+  for (const Cand& c : cands) {
+    if (KW != c.KW || KH % c.KHT || OCg % c.MT || Cg % (16 * c.NP)) continue;
+    const int WR = span + cross * (c.KHT - 1);
+    if (WR * g.Wp * 32 > c.PB) continue;
+    p.var = c.var; p.MT = c.MT; p.NP = c.NP; p.KHT = c.KHT; p.PB = c.PB;
+    g.WR = WR;
+    break;
+  }
+  if (!p.var) return p;
+  p.mtiles = OCg / p.MT;
+  p.cchunks = Cg / (16 * p.NP);
+  p.kgroups = KH / p.KHT;
+  p.tiles = groups * p.mtiles * p.cchunks * p.kgroups;
+  const int steps = (g.P + 63) / 64;
+  // at most one round of workgroups: a 513th workgroup would run alone in
+  // a second round (AlexNet at ceil(512 / tiles) splits: 0.7-0.9x)
+  int s = splits > 0 ? splits : kSlots / p.tiles;
+  s = max(1, min(s, steps));
+  const int ks = (steps + s - 1) / s;
+  p.kspan = ks * 64;
+  p.splits = (g.P + p.kspan - 1) / p.kspan;   // every split non-empty
+  return p;
+}
+
+}  // namespace
+
+// Weight gradient through the halo kernel.  ws == nullptr: plan only,
+// returns the f32 workspace elements needed ([splits][OC][KK] + [splits]
+// [OC]) or -1 when the shape does not take this kernel (the caller uses
+// hvk_conv_wgrad).  Else launches the kernel and the finishing pass
+// (dW / dbias accumulate) and returns 0, or a HIP error code.
+HVK_API long long hvk_conv_wgrad_halo(const void* X, const void* dY, float* dW,
+                                      float* dbias, float* ws, int N, int H,
+                                      int W, int C, int OC, int KH, int KW,
+                                      int pt, int pl, int OH, int OW,
+                                      int groups, int splits, hipStream_t s) {
+  Plan p = make_plan(N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, splits);
+  if (!p.var) return -1;
+  const long long kk = (long long)KH * KW * (C / groups);
+  const long long need = (long long)p.splits * OC * kk + (long long)p.splits * OC;
+  if (ws == nullptr) return need;
+  if (((uintptr_t)X & 15) || ((uintptr_t)dY & 15)) return -1;
+  float* wsb = ws + (long long)p.splits * OC * kk;
+  dim3 grid((unsigned)(p.tiles * p.splits)), blk(256);
+  const int bias = dbias != nullptr;
+  const uint16_t* x = (const uint16_t*)X;
+  const uint16_t* dy = (const uint16_t*)dY;
+#define HALO_GO(MT, NP, KHT, KW, NJW, PB)                                      \
+  hipLaunchKernelGGL((wgrad_halo_kernel<MT, NP, KHT, KW, NJW, PB>), grid, blk, \
+                     0, s, x, dy, ws, wsb, p.g, p.mtiles, p.cchunks,           \
+                     p.kgroups, p.tiles, p.kspan, bias)
+  switch (p.var) {
+    case 1: HALO_GO(128, 2, 3, 3, 9, 7168); break;
+    case 2: HALO_GO(96, 2, 3, 3, 9, 7168); break;
+    case 3: HALO_GO(128, 3, 1, 5, 8, 5120); break;
+    case 4: HALO_GO(128, 2, 3, 3, 9, 10240); break;
+    default: return -1;
+  }
+#undef HALO_GO
+  hipError_t e = launch_status(s);
+  if (e != hipSuccess) return (long long)e;
+  const long long n4 = (long long)OC * kk / 4;
+  const int fb = (int)min(2048ll, (n4 + 255) / 256);
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3(max(fb, 1)), dim3(256), 0, s,
+                     ws, dW, n4, p.splits, wsb, dbias, OC);
+  return (long long)launch_status(s);
+}
+
+// the plan's split count (tests / autotune logging)
+HVK_API int hvk_conv_wgrad_halo_splits(int N, int H, int W, int C, int OC,
+                                       int KH, int KW, int pt, int pl, int OH,
+                                       int OW, int groups, int splits) {
+  Plan p = make_plan(N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, splits);
+  return p.var ? p.splits : -1;
+}

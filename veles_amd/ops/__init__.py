@@ -518,6 +518,25 @@ def _workspace(key, shape, dtype, device, zero=False):
     return t
 
 
+_GROWN = {}
+_RETIRED = []
+
+
+def _grow_ws(name, n, dtype, device):
+    """A scratch buffer of at least n elements shared by every call with this
+    name (per device and fan-out branch), grown geometrically.  A buffer it
+    outgrows stays allocated: a HIP graph captured earlier may still write
+    into it on replay."""
+    key = (name, str(device), dtype, _branch_key())
+    t = _GROWN.get(key)
+    if t is None or t.numel() < n:
+        if t is not None:
+            _RETIRED.append(t)
+        size = max(n, 0 if t is None else t.numel() * 3 // 2)
+        t = _GROWN[key] = torch.empty(size, dtype=dtype, device=device)
+    return t[:n]
+
+
 def needs_im2col(C, groups):
     """Small-channel convs (C/groups % 8 != 0, e.g. RGB input) run as an
     explicit bf16 im2col + dense MFMA GEMM instead of per-element gathers."""
@@ -1080,6 +1099,10 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
                       N, H, W, C, OC, KH, KW, sy, sx, pt, pl, OH, OW,
                       int(sp), _s(x))
             return dw
+        if (sy, sx) == (1, 1) and _halo_wgrad(x, dy, dw, dbias, N, H, W, C,
+                                               OC, KH, KW, pt, pl, OH, OW,
+                                               groups):
+            return dw
         if splits is None:
             splits = _wgrad_splits_for(
                 x, dy, dw, sliding, padding, groups,
@@ -1095,6 +1118,39 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
     if dbias is not None:
         dbias += dy.float().reshape(-1, OC).sum(0)
     return dw
+
+
+_HALO_WGRAD = os.environ.get("VELES_AMD_HALO_WGRAD", "1") != "0"
+
+
+def set_halo_wgrad(on):
+    """A/B knob of the halo weight-gradient kernel (env
+    VELES_AMD_HALO_WGRAD)."""
+    global _HALO_WGRAD
+    _HALO_WGRAD = bool(on)
+
+
+def _halo_wgrad(x, dy, dw, dbias, N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
+                groups):
+    """Stride-1 weight gradient on the halo kernel (csrc/kernels/
+    wgrad_halo.hip) when the shape takes it: the input window of each
+    64-pixel step is staged once and read by every tap; split over pixels
+    into workspace slices that a finishing pass adds into dw / dbias in
+    split order (deterministic).  False: the caller uses hvk_conv_wgrad."""
+    if not _HALO_WGRAD or x.dtype != torch.bfloat16 or \
+            dy.dtype != torch.bfloat16 or not dw.is_contiguous() or \
+            not x.is_contiguous() or not dy.is_contiguous():
+        return False
+    from veles_amd.ops import _lib
+    fn = _lib.lib().hvk_conv_wgrad_halo
+    geo = (N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, 0)
+    need = fn(_p(x), _p(dy), _p(dw), _p(dbias), None, *geo, _s(x))
+    if need < 0:
+        return False
+    ws = _grow_ws("wgrad_halo_ws", int(need), torch.float32, x.device)
+    rc = fn(_p(x), _p(dy), _p(dw), _p(dbias), _p(ws), *geo, _s(x))
+    _lib.check(int(rc), "hvk_conv_wgrad_halo")
+    return True
 
 
 # 512 blocks (2 per CU) measured best on AlexNet b512 (72.7k img/s vs 71.6k

@@ -104,13 +104,18 @@ _SIGS = {
     "hvk_conv_dgrad_fp8": [P, P, P] + [I] * 14 + [P, I, I, I, P, P, I, F, F,
                            P, P, P, F, I, P],
     "hvk_conv_wgrad_fp8": [P, P, P, P] + [I] * 17 + [P, P, I, F, F, P],
+    # halo weight gradient (csrc/kernels/wgrad_halo.hip): (X, dY, dW,
+    # dbias, ws, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, splits, s)
+    "hvk_conv_wgrad_halo": [P, P, P, P, P] + [I] * 13 + [P],
+    "hvk_conv_wgrad_halo_splits": [I] * 13,
     "hvk_take_last_error": [],
     "hvk_end_stream_capture": [P],
     "hvk_stream_create": [],
 }
 _OPTIONAL = {}
-# functions returning a pointer (every other one returns int)
+# functions returning a pointer / a 64-bit int (every other one returns int)
 _PTR_RET = {"hvk_stream_create"}
+_LL_RET = {"hvk_conv_wgrad_halo"}
 
 
 def _load():
@@ -128,7 +133,8 @@ def _load():
                                            "-m veles_amd.ops.build" %
                                            (LIB_PATH, name))
             fn.argtypes = sig
-            fn.restype = ctypes.c_void_p if name in _PTR_RET else ctypes.c_int
+            fn.restype = ctypes.c_void_p if name in _PTR_RET else \
+                ctypes.c_longlong if name in _LL_RET else ctypes.c_int
         # A/B schedule selectors for whole-run experiments (bench.py under
         # an environment setting; tests and tools call the setters directly)
         for env, fn in (("VELES_AMD_GEMM_VARIANT", "hvk_set_gemm_variant"),
