@@ -55,11 +55,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 struct HaloGeom {
   int N, H, W, C, OH, OW, OC, Cg, OCg, KH, KW, pt, pl;
-  int P;    // N * OH * OW
-  int KK;   // KH * KW * Cg
-  int Wp;   // window slots per row (OW + 8)
-  int WR;   // window rows
-  FastDiv fOW;
+  int P;     // N * OH * OW
+  int OHW;   // OH * OW
+  int KK;    // KH * KW * Cg
+  int Wp;    // pixel-slot row pitch (OW + 8)
+  int WR;    // full-row window: rows
+  int SEGP;  // segment window: slots per kh segment
+  int spi;   // segment window: 64-pixel steps per image
+  FastDiv fOW, fWp;
 };
 
 // XOR of the 32-B block index of A image row r (MT / 16 blocks per row):
@@ -86,8 +89,15 @@ __device__ __forceinline__ bf16x8 tr_read(lds_u8* sm, uint32_t o0,
 
 // MT: output channels per tile; NP: 16-channel planes; KHT: kh rows per tap
 // group; KW: taps per kh row; NJW: n-tiles (16 columns) per wave column;
-// PB: LDS bytes per window plane; BIAS: fold the bias gradient
-template <int MT, int NP, int KHT, int KW, int NJW, int PB>
+// PB: LDS bytes per window plane.
+// SEG: the segment window for wide images (64 pixels cover a sliver of two
+// rows): steps are image-aligned (a step never crosses an image; the last
+// one of an image is partial) and each kh has its own SEGP-slot segment,
+// slot kh * SEGP + d + kw for the pixel at slot distance d = (oh - oh0) *
+// Wp + ow - ow0 from the step's first pixel - the same "pixel base + tap
+// offset" read with the tap row pitch SEGP instead of Wp.  kspan counts
+// steps then, pixels otherwise.
+template <int MT, int NP, int KHT, int KW, int NJW, int PB, bool SEG>
 __global__ void __launch_bounds__(256, 2)
 wgrad_halo_kernel(const uint16_t* __restrict__ x,
                   const uint16_t* __restrict__ dy, float* __restrict__ ws,
@@ -117,8 +127,10 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
   const int cc = tt % cchunks; tt /= cchunks;
   const int mt = tt % mtiles;
   const int gi = tt / mtiles;
+  // pixel range (full-row window) or step range (segment window)
+  const int total = SEG ? g.N * g.spi : g.P;
   const int pbeg = split * kspan;
-  const int pend = min(g.P, pbeg + kspan);
+  const int pend = min(total, pbeg + kspan);
   if (pbeg >= pend) return;   // the host sizes splits so this never happens
   const int coff_y = gi * g.OCg + mt * MT;
   const int coff_x = gi * g.Cg + cc * 16 * NP;
@@ -149,10 +161,12 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
     a_off[i] = (uint32_t)(r * g.OC + coff_y + m) * 2u;
   }
   // ---- window DMA slots: image byte -> (plane, window row, column, half)
-  const int WS = g.WR * g.Wp;
+  // (full-row) or (plane, kh segment, segment slot, half) (SEG)
+  const int WS = SEG ? KHT * g.SEGP : g.WR * g.Wp;
   int b_rs[NBW];
   uint32_t b_col[NBW];
   uint32_t b_ok[NBW];
+  int b_j[NBW];
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
     const int pi = w + 4 * i;
@@ -161,15 +175,25 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
     const int wb = ib - plane * PB;
     const int slot = wb >> 5;
     const int half = (wb >> 4) & 1;
-    const int rs = slot / g.Wp;
-    const int cs = slot - rs * g.Wp;
-    const int iw = cs - g.pl;
-    b_rs[i] = rs;
-    b_ok[i] = (pi < NB && plane < NP && slot < WS && cs < g.OW + g.KW - 1 &&
-               iw >= 0 && iw < g.W) ? 1u : 0u;
-    b_col[i] = (uint32_t)(iw * g.C + coff_x + plane * 16 + half * 8) * 2u;
+    if constexpr (SEG) {
+      const int khs = slot / g.SEGP;
+      b_rs[i] = khs;   // the segment's kh
+      b_j[i] = slot - khs * g.SEGP;
+      b_ok[i] = (pi < NB && plane < NP && slot < WS) ? 1u : 0u;
+      b_col[i] = (uint32_t)(coff_x + plane * 16 + half * 8) * 2u;
+    } else {
+      const int rs = slot / g.Wp;
+      const int cs = slot - rs * g.Wp;
+      const int iw = cs - g.pl;
+      b_rs[i] = rs;
+      b_j[i] = 0;
+      b_ok[i] = (pi < NB && plane < NP && slot < WS &&
+                 cs < g.OW + g.KW - 1 && iw >= 0 && iw < g.W) ? 1u : 0u;
+      b_col[i] = (uint32_t)(iw * g.C + coff_x + plane * 16 + half * 8) * 2u;
+    }
   }
   const uint32_t rowbytes = (uint32_t)g.W * g.C * 2u;
+  const uint32_t pixbytes = (uint32_t)g.C * 2u;
 
   // ---- A fragment offsets (bytes in the A image) of this lane's m-tiles
   const int mrow0 = wr * (MT / 2);
@@ -191,24 +215,52 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
   const bf16x8 ones = {(__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f,
                        (__bf16)1.f, (__bf16)1.f, (__bf16)1.f, (__bf16)1.f};
 
-  // step decode (wave-uniform): first pixel's image / row / column
-  int p0 = pbeg;
-  uint32_t n0, rem, oh0, ow0;
-  {
-    uint32_t ohw = (uint32_t)g.OH * g.OW;
-    n0 = (uint32_t)p0 / ohw;
-    rem = (uint32_t)p0 - n0 * ohw;
-    oh0 = fdiv(rem, g.fOW);
-    ow0 = rem - oh0 * g.OW;
+  // step decode (wave-uniform): the first pixel's image n, its index pin
+  // in the image, row and column
+  uint32_t n0, pin0, oh0, ow0;
+  if constexpr (SEG) {
+    n0 = (uint32_t)pbeg / (uint32_t)g.spi;
+    pin0 = ((uint32_t)pbeg - n0 * g.spi) * 64u;
+  } else {
+    n0 = (uint32_t)pbeg / (uint32_t)g.OHW;
+    pin0 = (uint32_t)pbeg - n0 * g.OHW;
   }
+  oh0 = fdiv(pin0, g.fOW);
+  ow0 = pin0 - oh0 * g.OW;
 
-  // DMA of the step at pixel p (decoded n, oh, ow) into stage st
-  auto issue = [&](int p, int n, int oh, uint8_t* st) {
+  // DMA of the step at (n, pin, oh, ow) into stage st
+  auto issue = [&](int n, int pin, int oh, int ow, uint8_t* st) {
+    const int p = n * g.OHW + pin;
     const uint32_t pa = (uint32_t)p * (uint32_t)g.OC * 2u;
+    const int plim = SEG ? g.OHW - pin : pend - p;   // valid rows < plim
 #pragma unroll
     for (int i = 0; i < NAW; ++i) {
-      const uint32_t v = (p + a_row[i] < pend) ? pa + a_off[i] : kBufOOB;
+      const uint32_t v = (a_row[i] < plim) ? pa + a_off[i] : kBufOOB;
       dma16(ra, st + (w * NAW + i) * 1024, v);
+    }
+    if constexpr (SEG) {
+      // segment kh, slot j: input row oh + (ow + j) / Wp + kh0 + kh - pt,
+      // column (ow + j) % Wp - pl
+      const int ihb = oh + kh0 - g.pt;
+      const uint32_t nrow = (uint32_t)n * g.H;
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        if (w + 4 * i < NB) {   // wave-uniform
+          const uint32_t sj = (uint32_t)(ow + b_j[i]);
+          const uint32_t rr = fdiv(sj, g.fWp);
+          const int col = (int)(sj - rr * (uint32_t)g.Wp);
+          const int ih = ihb + (int)rr + b_rs[i];
+          const int iw = col - g.pl;
+          const bool ok = b_ok[i] && col < g.OW + g.KW - 1 &&
+                          (unsigned)iw < (unsigned)g.W &&
+                          (unsigned)ih < (unsigned)g.H;
+          const uint32_t v = ok ? (nrow + (uint32_t)ih) * rowbytes +
+                                      (uint32_t)iw * pixbytes + b_col[i]
+                                : kBufOOB;
+          dma16(rb, st + ABYTES + (w + 4 * i) * 1024, v);
+        }
+      }
+      return;
     }
     // window rows: image n up to row slot rc, image n + 1 after it
     const int rc = g.OH - oh + KHT - 1;
@@ -231,8 +283,14 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
       }
     }
   };
-  auto advance = [&](int& p, uint32_t& n, uint32_t& oh, uint32_t& ow) {
-    p += 64;
+  auto advance = [&](uint32_t& n, uint32_t& pin, uint32_t& oh,
+                     uint32_t& ow) {
+    pin += 64;
+    if (SEG && pin >= (uint32_t)g.OHW) {   // the next image's first step
+      pin = 0; oh = 0; ow = 0; ++n;
+      return;
+    }
+    if (!SEG && pin >= (uint32_t)g.OHW) pin -= g.OHW;
     ow += 64;
     while (ow >= (uint32_t)g.OW) {   // scalar: at most 64 / OW + 1 turns
       ow -= g.OW;
@@ -240,15 +298,14 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
     }
   };
 
-  const int nk = (pend - pbeg + 63) >> 6;
-  issue(p0, n0, oh0, smem);
+  const int nk = SEG ? pend - pbeg : (pend - pbeg + 63) >> 6;
+  issue(n0, pin0, oh0, ow0, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  int pn = p0;
-  uint32_t nn = n0, ohn = oh0, own = ow0;
-  advance(pn, nn, ohn, own);
+  uint32_t nn = n0, pinn = pin0, ohn = oh0, own = ow0;
+  advance(nn, pinn, ohn, own);
 
   const bool bwave = bias && kg == 0 && cc == 0 && wc == 0;
 
@@ -257,19 +314,30 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
     constexpr bool WB = decltype(with_bias)::value;
     for (int kt = 0; kt < nk; ++kt) {
       const uint32_t cur = (kt & 1) * STAGE;
-      if (kt + 1 < nk) issue(pn, nn, ohn, smem + ((kt + 1) & 1) * STAGE);
+      if (kt + 1 < nk)
+        issue(nn, pinn, ohn, own, smem + ((kt + 1) & 1) * STAGE);
       // B fragment bases (LDS bytes) of this lane's 4 pixels (q + 16 i)
       // for every kh of the tap group
       uint32_t bb[4][KHT];
+      const int kp = SEG ? g.SEGP : g.Wp;   // slots per kh
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t ow = ow0 + q + 16 * i;
         const uint32_t gr = fdiv(ow, g.fOW);
         const int owr = (int)(ow - gr * (uint32_t)g.OW);
-        const int rs = (int)gr + ((oh0 + gr >= (uint32_t)g.OH) ? KHT - 1 : 0);
-        const uint32_t base = cur + ABYTES + (rs * g.Wp + owr) * 32 + trp * 8;
+        int slot;
+        if constexpr (SEG) {
+          // pixels past the image end (A rows zero) read slot 0 of the
+          // stage: finite data, never the other stage's unwritten LDS
+          slot = pin0 + q + 16 * i < (uint32_t)g.OHW
+                     ? (int)gr * g.Wp + owr - (int)ow0 : 0;
+        } else {
+          slot = ((int)gr + ((oh0 + gr >= (uint32_t)g.OH) ? KHT - 1 : 0)) *
+                     g.Wp + owr;
+        }
+        const uint32_t base = cur + ABYTES + slot * 32 + trp * 8;
 #pragma unroll
-        for (int kh = 0; kh < KHT; ++kh) bb[i][kh] = base + kh * g.Wp * 32;
+        for (int kh = 0; kh < KHT; ++kh) bb[i][kh] = base + kh * kp * 32;
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -305,8 +373,8 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      ow0 = own; oh0 = ohn; n0 = nn;
-      advance(pn, nn, ohn, own);
+      ow0 = own; oh0 = ohn; n0 = nn; pin0 = pinn;
+      advance(nn, pinn, ohn, own);
     }
   };
   if (wc == 0) {
@@ -339,29 +407,63 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
   }
 }
 
-// dW[e] += sum_s ws[s][e] (e < n, float4), dbias[m] += sum_s wsb[s][m]
+// dW[e] += sum_s ws[s][e] (e < n4 float4 elements), dbias[m] += sum_s
+// wsb[s][m]: R threads per element sum the splits k = r, r + R, ... and
+// their partials are added in r order (deterministic).  R > 1 when the
+// splits outnumber the elements' parallelism (AlexNet conv1: one tile, 512
+// splits: one thread per element took 0.24 ms).  Blocks past nmain reduce
+// the bias.
+template <int R>
 __global__ void __launch_bounds__(256)
 wgrad_finish_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                     long long n4, int splits, const float* __restrict__ wsb,
-                    float* __restrict__ db, int oc) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n4;
-       e += stride) {
-    float4 s = ((const float4*)ws)[e];
-    for (int k = 1; k < splits; ++k) {
-      const float4 v = ((const float4*)ws)[(long long)k * n4 + e];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+                    float* __restrict__ db, int oc, int nmain) {
+  constexpr int EPB = 256 / R;
+  __shared__ float4 red[256];
+  const int r = threadIdx.x % R, el = threadIdx.x / R;
+  if ((int)blockIdx.x < nmain) {
+    const long long e = (long long)blockIdx.x * EPB + el;
+    float4 sacc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < n4)
+      for (int k = r; k < splits; k += R) {
+        const float4 v = ((const float4*)ws)[(long long)k * n4 + e];
+        sacc.x += v.x; sacc.y += v.y; sacc.z += v.z; sacc.w += v.w;
+      }
+    if constexpr (R == 1) {
+      if (e < n4) {
+        float4 d = ((float4*)dw)[e];
+        d.x += sacc.x; d.y += sacc.y; d.z += sacc.z; d.w += sacc.w;
+        ((float4*)dw)[e] = d;
+      }
+      return;
     }
-    float4 d = ((float4*)dw)[e];
-    d.x += s.x; d.y += s.y; d.z += s.z; d.w += s.w;
-    ((float4*)dw)[e] = d;
+    red[threadIdx.x] = sacc;
+    __syncthreads();
+    if (r == 0 && e < n4) {
+      float4 t = red[el * R];
+#pragma unroll
+      for (int i = 1; i < R; ++i) {
+        const float4 v = red[el * R + i];
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+      }
+      float4 d = ((float4*)dw)[e];
+      d.x += t.x; d.y += t.y; d.z += t.z; d.w += t.w;
+      ((float4*)dw)[e] = d;
+    }
+    return;
   }
-  if (db != nullptr && blockIdx.x == 0) {
-    for (int m = threadIdx.x; m < oc; m += blockDim.x) {
-      float s = 0.f;
-      for (int k = 0; k < splits; ++k) s += wsb[(long long)k * oc + m];
-      db[m] += s;
-    }
+  if (db == nullptr) return;
+  const int m = ((int)blockIdx.x - nmain) * EPB + el;
+  float sb = 0.f;
+  if (m < oc)
+    for (int k = r; k < splits; k += R) sb += wsb[(long long)k * oc + m];
+  float* rf = (float*)red;
+  rf[threadIdx.x] = sb;
+  __syncthreads();
+  if (r == 0 && m < oc) {
+    float t = rf[el * R];
+    for (int i = 1; i < R; ++i) t += rf[el * R + i];
+    db[m] += t;
   }
 }
 
@@ -390,23 +492,50 @@ Plan make_plan(int N, int H, int W, int C, int OC, int KH, int KW, int pt,
   if ((long long)N * H * W * C * 2 >= kBufMaxBytes ||
       (long long)g.P * OC * 2 >= kBufMaxBytes)
     return p;
+  g.OHW = OH * OW;
+  g.fWp = make_fastdiv(g.Wp);
   const int span = (OW - 1 + 63) / OW + 1;   // output rows of 64 pixels
   // with OH * OW a multiple of 64 no step crosses an image (steps start at
   // multiples of 64): no second image's rows in the window
   const int cross = (OH * OW) % 64 != 0 ? 2 : 1;
-  struct Cand { int var, MT, NP, KHT, KW, PB; };
+  // segment window: slots a kh segment needs, over the image-aligned steps
+  // (the last pixel's distance from the first, plus the kw halo)
+  const int spi = (g.OHW + 63) / 64;
+  int dmax = 0;
+  for (int st = 0; st < spi; ++st) {
+    const int pin = 64 * st, last = min(pin + 63, g.OHW - 1);
+    const int d = (last / OW - pin / OW) * g.Wp + last % OW - pin % OW;
+    dmax = max(dmax, d);
+  }
+  struct Cand { int var, MT, NP, KHT, KW, PB, seg; };
+  // in order of preference (the first that fits is taken)
   const Cand cands[] = {
-      {1, 128, 2, 3, 3, 7168},
-      {2, 96, 2, 3, 3, 7168},
-      {3, 128, 3, 1, 5, 5120},
-      {4, 128, 2, 3, 3, 10240},   // VGG-16 28 / 56-wide layers
+      {1, 128, 2, 3, 3, 7168, 0},    // AlexNet conv3 / conv5, VGG 14-wide
+      {5, 128, 2, 3, 3, 7168, 1},    // VGG 56 / 112-wide (segments)
+      {4, 128, 2, 3, 3, 10240, 0},   // VGG 28-wide
+      {2, 96, 2, 3, 3, 7168, 0},     // AlexNet conv4
+      {7, 96, 3, 3, 3, 8192, 1},     // AlexNet conv1 (space-to-depth)
+      {6, 64, 4, 3, 3, 7168, 1},     // VGG conv1_2 (224-wide, 64 channels)
+      {3, 128, 3, 1, 5, 5120, 0},    // AlexNet conv2 (5 x 5)
   };
   for (const Cand& c : cands) {
     if (KW != c.KW || KH % c.KHT || OCg % c.MT || Cg % (16 * c.NP)) continue;
-    const int WR = span + cross * (c.KHT - 1);
-    if (WR * g.Wp * 32 > c.PB) continue;
+    if (c.seg) {
+      // image-aligned steps waste the tail of each image's last step
+      if (spi * 64 * 100 > g.OHW * 103) continue;
+      const int segp = dmax + KW;
+      if (c.KHT * segp * 32 > c.PB) continue;
+      g.SEGP = segp;
+      g.spi = spi;
+      g.WR = 0;
+    } else {
+      const int WR = span + cross * (c.KHT - 1);
+      if (WR * g.Wp * 32 > c.PB) continue;
+      g.WR = WR;
+      g.SEGP = 0;
+      g.spi = 0;
+    }
     p.var = c.var; p.MT = c.MT; p.NP = c.NP; p.KHT = c.KHT; p.PB = c.PB;
-    g.WR = WR;
     break;
   }
   if (!p.var) return p;
@@ -414,14 +543,17 @@ Plan make_plan(int N, int H, int W, int C, int OC, int KH, int KW, int pt,
   p.cchunks = Cg / (16 * p.NP);
   p.kgroups = KH / p.KHT;
   p.tiles = groups * p.mtiles * p.cchunks * p.kgroups;
-  const int steps = (g.P + 63) / 64;
+  // step units: 64 pixels (full-row window: kspan in pixels), image-aligned
+  // steps (segment window: kspan in steps)
+  const bool seg = g.SEGP > 0;
+  const int steps = seg ? N * spi : (g.P + 63) / 64;
   // at most one round of workgroups: a 513th workgroup would run alone in
   // a second round (AlexNet at ceil(512 / tiles) splits: 0.7-0.9x)
   int s = splits > 0 ? splits : kSlots / p.tiles;
   s = max(1, min(s, steps));
   const int ks = (steps + s - 1) / s;
-  p.kspan = ks * 64;
-  p.splits = (g.P + p.kspan - 1) / p.kspan;   // every split non-empty
+  p.kspan = seg ? ks : ks * 64;
+  p.splits = (steps + ks - 1) / ks;   // every split non-empty
   return p;
 }
 
@@ -448,24 +580,34 @@ HVK_API long long hvk_conv_wgrad_halo(const void* X, const void* dY, float* dW,
   const int bias = dbias != nullptr;
   const uint16_t* x = (const uint16_t*)X;
   const uint16_t* dy = (const uint16_t*)dY;
-#define HALO_GO(MT, NP, KHT, KW, NJW, PB)                                      \
-  hipLaunchKernelGGL((wgrad_halo_kernel<MT, NP, KHT, KW, NJW, PB>), grid, blk, \
-                     0, s, x, dy, ws, wsb, p.g, p.mtiles, p.cchunks,           \
+#define HALO_GO(MT, NP, KHT, KW, NJW, PB, SEG)                                \
+  hipLaunchKernelGGL((wgrad_halo_kernel<MT, NP, KHT, KW, NJW, PB, SEG>), grid, \
+                     blk, 0, s, x, dy, ws, wsb, p.g, p.mtiles, p.cchunks,      \
                      p.kgroups, p.tiles, p.kspan, bias)
   switch (p.var) {
-    case 1: HALO_GO(128, 2, 3, 3, 9, 7168); break;
-    case 2: HALO_GO(96, 2, 3, 3, 9, 7168); break;
-    case 3: HALO_GO(128, 3, 1, 5, 8, 5120); break;
-    case 4: HALO_GO(128, 2, 3, 3, 9, 10240); break;
+    case 1: HALO_GO(128, 2, 3, 3, 9, 7168, false); break;
+    case 2: HALO_GO(96, 2, 3, 3, 9, 7168, false); break;
+    case 3: HALO_GO(128, 3, 1, 5, 8, 5120, false); break;
+    case 4: HALO_GO(128, 2, 3, 3, 9, 10240, false); break;
+    case 5: HALO_GO(128, 2, 3, 3, 9, 7168, true); break;
+    case 6: HALO_GO(64, 4, 3, 3, 18, 7168, true); break;
+    case 7: HALO_GO(96, 3, 3, 3, 14, 8192, true); break;
     default: return -1;
   }
 #undef HALO_GO
   hipError_t e = launch_status(s);
   if (e != hipSuccess) return (long long)e;
   const long long n4 = (long long)OC * kk / 4;
-  const int fb = (int)min(2048ll, (n4 + 255) / 256);
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3(max(fb, 1)), dim3(256), 0, s,
-                     ws, dW, n4, p.splits, wsb, dbias, OC);
+  // threads per element: enough workgroups for the chip, <= 32 splits each
+  const int R = (p.splits >= 64 && n4 < (1 << 17)) ? 16
+              : (p.splits >= 16 && n4 < (1 << 19)) ? 4 : 1;
+  const int epb = 256 / R;
+  const int nmain = (int)((n4 + epb - 1) / epb);
+  const int nb = dbias ? (OC + epb - 1) / epb : 0;
+  auto fk = R == 16 ? wgrad_finish_kernel<16>
+          : R == 4 ? wgrad_finish_kernel<4> : wgrad_finish_kernel<1>;
+  hipLaunchKernelGGL(fk, dim3(nmain + nb), dim3(256), 0, s, ws, dW, n4,
+                     p.splits, wsb, dbias, OC, nmain);
   return (long long)launch_status(s);
 }
 

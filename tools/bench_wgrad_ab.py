@@ -33,13 +33,14 @@ def timeit(fn, n=8, w=2):
     return e0.elapsed_time(e1) / n * 1e-3
 
 
-def case(N, H, W, C, OC, k, p, g):
+def case(N, H, W, C, OC, k, p, g, st=1):
+    OH, OW = ops.conv_out_size(H, W, k, k, (st, st), (p, p, p, p))
     x = (torch.rand(N, H, W, C, device="cuda") * 2 - 1).to(BF)
-    dy = (torch.rand(N, H, W, OC, device="cuda") * 2 - 1).to(BF)
+    dy = (torch.rand(N, OH, OW, OC, device="cuda") * 2 - 1).to(BF)
     dw = torch.zeros(OC, k, k, C // g, device="cuda")
     db = torch.zeros(OC, device="cuda")
-    fl = 2.0 * N * H * W * OC * k * k * (C // g)
-    return fl, lambda: ops.conv_wgrad(x, dy, dw, (1, 1), (p, p, p, p), g,
+    fl = 2.0 * N * OH * OW * OC * k * k * (C // g)
+    return fl, lambda: ops.conv_wgrad(x, dy, dw, (st, st), (p, p, p, p), g,
                                       dbias=db)
 
 
@@ -47,12 +48,15 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     VB = int(sys.argv[3]) if len(sys.argv) > 3 else 0
-    cases = [("alex_conv2", (B, 27, 27, 96, 256, 5, 2, 2)),
+    cases = [("alex_conv1", (B, 227, 227, 3, 96, 11, 0, 1, 4)),
+             ("alex_conv2", (B, 27, 27, 96, 256, 5, 2, 2)),
              ("alex_conv3", (B, 13, 13, 256, 384, 3, 1, 1)),
              ("alex_conv4", (B, 13, 13, 384, 384, 3, 1, 2)),
              ("alex_conv5", (B, 13, 13, 384, 256, 3, 1, 2))]
     if VB:
-        cases += [("vgg_conv3_2", (VB, 56, 56, 256, 256, 3, 1, 1)),
+        cases += [("vgg_conv1_2", (VB // 4, 224, 224, 64, 64, 3, 1, 1)),
+                  ("vgg_conv2_2", (VB // 2, 112, 112, 128, 128, 3, 1, 1)),
+                  ("vgg_conv3_2", (VB, 56, 56, 256, 256, 3, 1, 1)),
                   ("vgg_conv4_2", (VB, 28, 28, 512, 512, 3, 1, 1)),
                   ("vgg_conv5_2", (VB, 14, 14, 512, 512, 3, 1, 1))]
     out = {}

@@ -1047,14 +1047,17 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             # self-clearing workspace: zeroed once, cleared again by the fold
             dw2 = _workspace(("s2dg", dw.data_ptr()), (OC, KH2, KW2, C2),
                              torch.float32, dw.device, zero=True)
-            # logged with the logical image shape: the autotuner replays
-            # the call on a plain image (the s2d data has C2 channels)
-            sp = splits or _wgrad_splits_for(
-                (N, H, W, C), dy, dw, sliding, padding, groups,
-                (N * OH * OW, OC, KH2 * KW2 * C2 + 1, 1))
-            _lib_call("hvk_conv_wgrad", _p(x2), _p(dy), _p(dw2), N, H2, W2,
-                      C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1, int(sp),
-                      _p(dbias), _s(x))
+            if not _halo_wgrad(x2, dy, dw2, dbias, N, H2, W2, C2, OC, KH2,
+                               KW2, 0, 0, OH, OW, 1):
+                # logged with the logical image shape: the autotuner
+                # replays the call on a plain image (the s2d data has C2
+                # channels)
+                sp = splits or _wgrad_splits_for(
+                    (N, H, W, C), dy, dw, sliding, padding, groups,
+                    (N * OH * OW, OC, KH2 * KW2 * C2 + 1, 1))
+                _lib_call("hvk_conv_wgrad", _p(x2), _p(dy), _p(dw2), N, H2,
+                          W2, C2, OC, KH2, KW2, 1, 1, 0, 0, OH, OW, 1,
+                          int(sp), _p(dbias), _s(x))
             if dw.is_contiguous():
                 _lib_call("hvk_s2d_grad_fold", _p(dw2), _p(dw), OC, KH, KW, C,
                           s2, 1, _s(x))
