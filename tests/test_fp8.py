@@ -268,6 +268,12 @@ WGRAD8 = CONVS8 + [
     (4, 28, 28, 64, 128, 3, 3, (1, 1), (1, 1, 1, 1), 1),
     (8, 14, 14, 256, 160, 3, 3, (1, 1), (1, 1, 1, 1), 1),
     (16, 7, 7, 48, 32, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    # the fp8 halo kernel (wgrad_halo.hip): full-row windows with steps
+    # across images (13 / 56-wide), segment windows (112 / 224-wide)
+    (3, 13, 13, 256, 384, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (2, 56, 56, 64, 128, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (1, 112, 112, 64, 128, 3, 3, (1, 1), (1, 1, 1, 1), 1),
+    (1, 224, 224, 64, 64, 3, 3, (1, 1), (1, 1, 1, 1), 1),
 ]
 
 
@@ -619,3 +625,32 @@ def test_fp8_fc_dgrad_transposed_weights():
     close(out, ref, 1e-2)
     assert torch.equal(gd.wt8_.view(torch.uint8).cpu(),
                        fwd.w8_.view(torch.uint8).t().cpu())
+
+
+@pytest.mark.gpu
+def test_conv_wgrad_fp8_halo_taken_and_matches_gemm_kernel():
+    """VGG-like stride-1 shapes take the fp8 halo weight gradient; it equals
+    the wgrad_fp8.hip kernel's result to f32 rounding (same fp8 operands,
+    same scales)"""
+    N, H, W, C, OC = 2, 56, 56, 128, 128
+    x8, sx, _, _ = _pair(rnd(N, H, W, C))
+    d8, sd, _, _ = _pair(rnd(N, H, W, OC, seed=2, scale=1e-2), fp8.E5M2)
+    geo = (N, H, W, C, OC, 3, 3, 1, 1, H, W, 1, 0, sx.fmt, sd.fmt,
+           sx.state.data_ptr(), sd.state.data_ptr(), fp8.HIST,
+           float(sx.fmax_eff), float(sd.fmax_eff), 0)
+    assert ops._lib.lib().hvk_conv_wgrad_halo_fp8(
+        x8.data_ptr(), d8.data_ptr(), 0, 0, None, *geo) > 0
+    res = {}
+    try:
+        for on in (True, False):
+            ops.set_halo_wgrad(on)
+            got = torch.zeros(OC, 3, 3, C, device=DEV)
+            gotb = torch.zeros(OC, device=DEV)
+            fp8.conv_wgrad(x8, sx, d8, sd, got, (1, 1), (1, 1, 1, 1), 1,
+                           dbias=gotb)
+            res[on] = (got, gotb)
+    finally:
+        ops.set_halo_wgrad(True)
+    torch.cuda.synchronize()
+    close(res[True][0], res[False][0], 1e-5)
+    close(res[True][1], res[False][1], 1e-5)

@@ -108,6 +108,8 @@ _SIGS = {
     # dbias, ws, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, splits, s)
     "hvk_conv_wgrad_halo": [P, P, P, P, P] + [I] * 13 + [P],
     "hvk_conv_wgrad_halo_splits": [I] * 13,
+    "hvk_conv_wgrad_halo_fp8": [P, P, P, P, P] + [I] * 15 + [P, P, I, F, F,
+                                                            P],
     "hvk_take_last_error": [],
     "hvk_end_stream_capture": [P],
     "hvk_stream_create": [],
@@ -115,7 +117,7 @@ _SIGS = {
 _OPTIONAL = {}
 # functions returning a pointer / a 64-bit int (every other one returns int)
 _PTR_RET = {"hvk_stream_create"}
-_LL_RET = {"hvk_conv_wgrad_halo"}
+_LL_RET = {"hvk_conv_wgrad_halo", "hvk_conv_wgrad_halo_fp8"}
 
 
 def _load():

@@ -363,6 +363,34 @@ def conv_dgrad(dy8, sdy, w8, sw, x_shape, sliding=(1, 1),
     return dx
 
 
+def _halo_wgrad8(x8, sx, dy8, sdy, dw, dbias, pt, pl, OH, OW, groups,
+                 splits):
+    """Stride-1 fp8 weight gradient on the halo kernel (csrc/kernels/
+    wgrad_halo.hip wgrad_halo8_kernel) when the shape takes it; False
+    leaves the call to hvk_conv_wgrad_fp8."""
+    from veles_amd import ops
+    if not ops._HALO_WGRAD or not dw.is_contiguous() or \
+            not x8.is_contiguous() or not dy8.is_contiguous():
+        return False
+    N, H, W, C = x8.shape
+    OC = dy8.shape[3]
+    KH, KW = dw.shape[1], dw.shape[2]
+    fn = ops._lib.lib().hvk_conv_wgrad_halo_fp8
+    geo = (N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+           int(splits) if splits else 0, sx.fmt, sdy.fmt,
+           sx.state.data_ptr(), sdy.state.data_ptr(), HIST,
+           float(sx.fmax_eff), float(sdy.fmax_eff), _s(x8))
+    db = None if dbias is None else dbias.data_ptr()
+    need = fn(x8.data_ptr(), dy8.data_ptr(), dw.data_ptr(), db, None, *geo)
+    if need < 0:
+        return False
+    ws = ops._grow_ws("wgrad_halo_ws", int(need), torch.float32, x8.device)
+    rc = fn(x8.data_ptr(), dy8.data_ptr(), dw.data_ptr(), db, ws.data_ptr(),
+            *geo)
+    ops._lib.check(int(rc), "hvk_conv_wgrad_halo_fp8")
+    return True
+
+
 def conv_wgrad(x8, sx, dy8, sdy, dw, sliding=(1, 1), padding=(0, 0, 0, 0),
                groups=1, splits=None, dbias=None):
     """dw (float32 [OC][KH][KW][C/g]) += conv weight gradient of deq(x8)
@@ -381,6 +409,10 @@ def conv_wgrad(x8, sx, dy8, sdy, dw, sliding=(1, 1), padding=(0, 0, 0, 0),
         # a sum over pixels: image chunks (32-bit buffer offsets) accumulate
         for n0, n1 in ops._image_chunks(N, x8, dy8):
             n = n1 - n0
+            if (syy, sxx) == (1, 1) and _halo_wgrad8(
+                    x8[n0:n1], sx, dy8[n0:n1], sdy, dw, dbias, pt, pl, OH,
+                    OW, groups, splits):
+                continue
             sp = splits if splits is not None else ops.wgrad_splits(
                 n * OH * OW, OC // groups, KH * KW * Cg, groups)
             _call("hvk_conv_wgrad_fp8", x8[n0:n1].data_ptr(),
