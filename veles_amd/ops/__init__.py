@@ -752,6 +752,18 @@ _HALO = os.environ.get("VELES_AMD_HALO", "1") != "0"
 _HALO_DGRAD = os.environ.get("VELES_AMD_HALO_DGRAD", "0") != "0"
 
 
+# weight-stationary stride-1 convs (csrc/kernels/conv_ws.hip): AlexNet conv1
+# (s2d) / conv2 forward, VGG conv1_2 forward and backward-data.  Opt-in
+# until it beats the implicit GEMM (profiles/r5/ab_conv_ws.log)
+_CONV_WS = os.environ.get("VELES_AMD_CONV_WS", "0") != "0"
+
+
+def set_conv_ws(on):
+    """A/B knob of the weight-stationary conv kernels."""
+    global _CONV_WS
+    _CONV_WS = bool(on)
+
+
 def set_conv_halo(on, dgrad=None):
     """Enable / disable the LDS-halo stride-1 conv kernels (A/B runs);
     ``dgrad`` sets the backward-data kernel separately (default: same as
@@ -781,6 +793,15 @@ def _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
         return fused
     sfx = "" if q8 is None else "_q8"
     extra = [] if q8 is None else list(q8)
+    if _CONV_WS and q8 is None and sy == 1 and sx == 1 and \
+            out.is_contiguous() and x.dtype == torch.bfloat16:
+        rc = _lib.lib().hvk_conv_fwd_ws(
+            _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
+            OH, OW, groups, act, stream)
+        if rc == 0:
+            return False
+        if rc != -2:
+            _lib.check(rc, "hvk_conv_fwd_ws")
     if _HALO and sy == 1 and sx == 1 and out.is_contiguous():
         rc = getattr(_lib.lib(), "hvk_conv_fwd_halo" + sfx)(
             _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
@@ -921,6 +942,16 @@ def _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out, fq):
 
 def _dgrad_call(dy, wt, out, aux, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
                 OH, OW, groups, aux_act):
+    if _CONV_WS and sx == 1 and sy == 1 and out.is_contiguous() and \
+            dy.dtype == torch.bfloat16 and \
+            (aux is None or aux.is_contiguous()):
+        rc = _lib.lib().hvk_conv_dgrad_ws(
+            _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
+            groups, _p(aux), aux_act, _s(dy))
+        if rc == 0:
+            return
+        if rc != -2:
+            _lib.check(rc, "hvk_conv_dgrad_ws")
     if _HALO_DGRAD and sx == 1 and sy == 1 and out.is_contiguous():
         rc = _lib.lib().hvk_conv_dgrad_halo(
             _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH,

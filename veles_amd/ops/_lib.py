@@ -110,6 +110,9 @@ _SIGS = {
     "hvk_conv_wgrad_halo_splits": [I] * 13,
     "hvk_conv_wgrad_halo_fp8": [P, P, P, P, P] + [I] * 15 + [P, P, I, F, F,
                                                             P],
+    # weight-stationary convs (csrc/kernels/conv_ws.hip)
+    "hvk_conv_fwd_ws": [P, P, P, P] + [I] * 13 + [P],
+    "hvk_conv_dgrad_ws": [P, P, P] + [I] * 12 + [P, I, P],
     "hvk_take_last_error": [],
     "hvk_end_stream_capture": [P],
     "hvk_stream_create": [],
