@@ -36,9 +36,13 @@
 // Window forms (as wgrad_halo.hip): full rows with steps that may span two
 // images (narrow images), or per-kh segments with image-aligned tiles (wide
 // images: VGG 224).
-#include <cstdlib>
-
 #include "conv_geom.h"
+
+// diagnostic builds only (wrong results by design): 1 no window DMA, 2 no
+// epilogue stores, 4 no MFMAs
+#ifndef HVK_WS_ABL
+#define HVK_WS_ABL 0
+#endif
 
 using namespace hvk;
 
@@ -56,8 +60,6 @@ struct WsGeom {
   int P, OHW;
   int Wp, WR, SEGP, spi, PB;   // PB: window bytes
   int pairs, wpp, tiles;   // (group, n-tile) pairs, WGs per pair, tiles
-  int abl;                 // diagnostics (HVK_WS_ABL, wrong results): 1 no
-                           // window DMA, 2 no epilogue stores, 4 no MFMAs
   FastDiv fOW, fWp, fOHW, fSPI;
 };
 
@@ -195,7 +197,7 @@ conv_ws_kernel(const uint16_t* __restrict__ src,
               (ok ? 0x80000000u : 0u);
   }
   auto issue = [&](int tl, int stage) {
-    if (g.abl & 1) return;
+    if constexpr ((HVK_WS_ABL & 1) != 0) return;
     int n, pin, oh, ow;
     decode(tl, n, pin, oh, ow);
     uint8_t* dst = smem + stage * WIN;
@@ -286,7 +288,7 @@ conv_ws_kernel(const uint16_t* __restrict__ src,
               *(lds_bf16x8*)(sm + bb[i] + ofs[s + PD]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (!(g.abl & 4)) {
+      if constexpr ((HVK_WS_ABL & 4) == 0) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -322,7 +324,7 @@ conv_ws_kernel(const uint16_t* __restrict__ src,
         pg = (long long)tl * TPX + m;
         ok = pg < g.P;
       }
-      if (!ok || ((g.abl & 2) && acc[i][0][0] != 1234.5f)) continue;
+      if (!ok || ((HVK_WS_ABL & 2) && acc[i][0][0] != 1234.5f)) continue;
 #pragma unroll
       for (int j = 0; j < NJW; ++j) {
         const int oc = gi * g.OCg + nt * NOUT + (wn * NJW + j) * 16 + fq * 4;
@@ -412,8 +414,6 @@ WsPlan ws_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   g.fOHW = make_fastdiv(g.OHW);
   g.fSPI = make_fastdiv(seg ? spi : 1);
   p.grid = g.pairs * g.wpp;
-  static const int abl = getenv("HVK_WS_ABL") ? atoi(getenv("HVK_WS_ABL")) : 0;
-  g.abl = abl;
   p.var = c->var * 2 + (seg ? 1 : 0);
   return p;
 }

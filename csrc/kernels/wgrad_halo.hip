@@ -46,6 +46,12 @@
 // Reference counterpart: the GD units' err x input matmuls through OCLBLAS
 // (/root/reference/veles/ocl_blas.py:187-236); SURVEY §2.4 row 1.
 #include "conv_geom.h"
+
+// diagnostic builds only (wrong results by design): 1 no window DMA, 2 no
+// epilogue stores, 4 no MFMAs
+#ifndef HVK_HALO_ABL
+#define HVK_HALO_ABL 0
+#endif
 #include "fp8_common.h"
 
 using namespace hvk;
@@ -231,6 +237,7 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
 
   // DMA of the step at (n, pin, oh, ow) into stage st
   auto issue = [&](int n, int pin, int oh, int ow, uint8_t* st) {
+    if constexpr ((HVK_HALO_ABL & 1) != 0) return;
     const int p = n * g.OHW + pin;
     const uint32_t pa = (uint32_t)p * (uint32_t)g.OC * 2u;
     const int plim = SEG ? g.OHW - pin : pend - p;   // valid rows < plim
@@ -357,10 +364,14 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
             const uint32_t off = kwl * 32 + pl_ * PB;   // bytes
             const bf16x8 b = tr_read(sm, bb[2 * ks][khl] + off,
                                      bb[2 * ks + 1][khl] + off);
+            if constexpr ((HVK_HALO_ABL & 4) != 0) {
+              acc[0][j][0] += (float)b[0] + (float)a[0][0];
+            } else {
 #pragma unroll
-            for (int i = 0; i < MI; ++i)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  b, a[i], acc[i][j], 0, 0, 0);
+              for (int i = 0; i < MI; ++i)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    b, a[i], acc[i][j], 0, 0, 0);
+            }
           }
         }
         if constexpr (WB) {
@@ -390,7 +401,7 @@ wgrad_halo_kernel(const uint16_t* __restrict__ x,
 #pragma unroll
   for (int j = 0; j < NJW; ++j) {
     const int jg = wc * NJW + j;
-    if (jg >= NJ) continue;
+    if (jg >= NJ || ((HVK_HALO_ABL & 2) && acc[0][j][0] != 1234.5f)) continue;
     const int tl = jg / NP, pl_ = jg - (jg / NP) * NP;
     const int khg = kh0 + tl / KW, kwl = tl - (tl / KW) * KW;
     const int ng = (khg * g.KW + kwl) * g.Cg + cc * 16 * NP + pl_ * 16 + fq * 4;

@@ -6,3 +6,8 @@ for a in 0 1 2 4 3; do
   HVK_WS_ABL=$a timeout -k 10 300 python -u tools/bench_conv_ab.py 2048 3 128 > gpurun_out/ws_abl_$a.log 2>&1 || { tail gpurun_out/ws_abl_$a.log; exit 1; }
   grep -v amdgpu.ids gpurun_out/ws_abl_$a.log
 done
+for a in 0 1 2 4; do
+  echo "== HVK_HALO_ABL=$a"
+  HVK_HALO_ABL=$a timeout -k 10 300 python -u tools/bench_wgrad_ab.py 2048 3 > gpurun_out/halo_abl_$a.log 2>&1 || { tail gpurun_out/halo_abl_$a.log; exit 1; }
+  grep -v amdgpu.ids gpurun_out/halo_abl_$a.log
+done
