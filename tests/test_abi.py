@@ -15,7 +15,8 @@ def _decls():
     out = {}
     for f in glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")):
         src = open(f).read()
-        for m in re.finditer(r"HVK_API\s+(int|void\s*\*)\s*(hvk_\w+)\s*"
+        for m in re.finditer(r"HVK_API\s+(int|void\s*\*|long\s+long|void)\s*"
+                             r"(hvk_\w+)\s*"
                              r"\(([^)]*)\)", src):
             out[m.group(2)] = (m.group(1).replace(" ", ""),
                                [a.strip() for a in m.group(3).split(",")
@@ -46,6 +47,9 @@ def test_every_binding_matches_its_declaration():
         ret, args = decls[name]
         # a pointer result read back as a C int would be truncated
         assert (ret == "void*") == (name in _lib._PTR_RET), \
+            "%s returns %s" % (name, ret)
+        # a 64-bit result read back as a C int would be truncated too
+        assert (ret == "longlong") == (name in _lib._LL_RET), \
             "%s returns %s" % (name, ret)
         want = [_kind(a) for a in args]
         assert len(sig) == len(want), "%s: %d args bound, %d declared" % (

@@ -1,0 +1,126 @@
+"""Channel-chunked halo convolutions (csrc/kernels/conv_hc.hip) against the
+float32 PyTorch references (F.conv2d / torch.nn.grad.conv2d_input on the
+same bf16 values) and against the kernels they replace
+(ops.set_conv_hc(False)): every AlexNet conv forward (conv1 through the
+space-to-depth image) and the stride-1 backward-data shapes, partial last
+tiles, tiles spanning several images, and batches large enough that every
+persistent workgroup walks several items."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from veles_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return ((torch.rand(*shape, generator=g, device="cuda") - 0.5) *
+            scale).to(torch.bfloat16)
+
+
+def _both(fn):
+    out = {}
+    try:
+        for on in (True, False):
+            ops.set_conv_hc(on, -1)
+            out[on] = fn()
+            torch.cuda.synchronize()
+    finally:
+        ops.set_conv_hc(False, -1)
+    return out
+
+
+def _close(a, b, tol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    assert err <= tol * (b.abs().max().item() + 1e-6), err
+
+
+FWD = [
+    # N, H, W, C, OC, K, stride, pad, groups
+    (2, 227, 227, 3, 96, 11, 4, 0, 1),     # conv1 (space-to-depth)
+    (3, 27, 27, 96, 256, 5, 1, 2, 2),      # conv2
+    (3, 13, 13, 256, 384, 3, 1, 1, 1),     # conv3
+    (3, 13, 13, 384, 384, 3, 1, 1, 2),     # conv4
+    (3, 13, 13, 384, 256, 3, 1, 1, 2),     # conv5
+    (384, 13, 13, 384, 384, 3, 1, 1, 2),   # conv4, many items per workgroup
+    (1, 56, 56, 64, 64, 3, 1, 1, 1),       # VGG-16 64-channel layer
+]
+
+
+@pytest.mark.parametrize("shape", FWD)
+def test_conv_hc_forward(shape):
+    N, H, W, C, OC, K, st, pad, g = shape
+    x = _r(N, H, W, C, scale=2.0, seed=1)
+    w = _r(OC, K, K, C // g, scale=0.2, seed=2)
+    b = torch.randn(OC, device="cuda") * 0.1
+    res = _both(lambda: ops.conv_fwd(x, w, b, (st, st), (pad,) * 4, g,
+                                     act="str"))
+    ref = F.conv2d(F.pad(x.permute(0, 3, 1, 2).float(), (pad,) * 4),
+                   w.permute(0, 3, 1, 2).float(), b, stride=st,
+                   groups=g).clamp_min(0).permute(0, 2, 3, 1)
+    _close(res[True], ref, 1e-2)
+    _close(res[True], res[False], 1e-2)
+
+
+DGRAD = [
+    (3, 27, 27, 96, 256, 5, 2, 2),         # conv2
+    (3, 13, 13, 256, 384, 3, 1, 1),        # conv3
+    (3, 13, 13, 384, 384, 3, 1, 2),        # conv4
+    (3, 13, 13, 384, 256, 3, 1, 2),        # conv5
+    (200, 27, 27, 96, 256, 5, 2, 2),       # conv2, many items per workgroup
+]
+
+
+@pytest.mark.parametrize("shape", DGRAD)
+def test_conv_hc_dgrad(shape):
+    N, H, W, C, OC, K, pad, g = shape
+    dy = _r(N, H, W, OC, scale=1.0, seed=3)
+    w = _r(OC, K, K, C // g, scale=0.2, seed=4)
+    aux = _r(N, H, W, C, scale=2.0, seed=5)   # the layer below's ReLU output
+    res = _both(lambda: ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1),
+                                       (pad,) * 4, g, aux=aux,
+                                       aux_act="str"))
+    ref = torch.nn.grad.conv2d_input(
+        (N, C, H, W), w.permute(0, 3, 1, 2).float(),
+        dy.permute(0, 3, 1, 2).float(), padding=pad,
+        groups=g).permute(0, 2, 3, 1)
+    ref = ref * (aux.float() > 0)
+    _close(res[True], ref, 1e-2)
+    _close(res[True], res[False], 1e-2)
+
+
+def test_conv_hc_taken_and_forced_variants():
+    from veles_amd.ops import _lib
+    lib = _lib.lib()
+    x = _r(3, 13, 13, 384, scale=1.0, seed=1)
+    w = _r(384, 3, 3, 192, scale=0.1, seed=2)
+    ref = None
+    try:
+        # conv4 fits the 128-, 96- and 64-channel tiles: every forced
+        # configuration gives the same sums up to rounding
+        for var in (-1, 2, 3):
+            lib.hvk_hc_variant(var)
+            y = torch.empty(3, 13, 13, 384, dtype=torch.bfloat16,
+                            device="cuda")
+            rc = lib.hvk_conv_fwd_hc(
+                x.data_ptr(), w.data_ptr(), None, y.data_ptr(), 3, 13, 13,
+                384, 384, 3, 3, 1, 1, 13, 13, 2, 0,
+                torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, var
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = y
+            else:
+                _close(y, ref, 4e-3)
+        # a configuration for another kernel size is not taken
+        lib.hvk_hc_variant(4)
+        rc = lib.hvk_conv_fwd_hc(
+            x.data_ptr(), w.data_ptr(), None, ref.data_ptr(), 3, 13, 13, 384,
+            384, 3, 3, 1, 1, 13, 13, 2, 0,
+            torch.cuda.current_stream().cuda_stream)
+        assert rc == -2
+    finally:
+        lib.hvk_hc_variant(-1)

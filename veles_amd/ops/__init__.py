@@ -764,6 +764,21 @@ def set_conv_ws(on):
     _CONV_WS = bool(on)
 
 
+# channel-chunked halo convs (csrc/kernels/conv_hc.hip): stride-1 3 x 3 and
+# 5 x 5 forward / backward-data with a per-chunk input window shared by
+# every tap
+_CONV_HC = os.environ.get("VELES_AMD_CONV_HC", "0") != "0"
+
+
+def set_conv_hc(on, variant=None):
+    """A/B knob of the channel-chunked halo conv kernels; ``variant`` forces
+    one configuration of conv_hc.hip's table (-1: automatic)."""
+    global _CONV_HC
+    _CONV_HC = bool(on)
+    if variant is not None and _lib.available():
+        _lib.lib().hvk_hc_variant(int(variant))
+
+
 def set_conv_halo(on, dgrad=None):
     """Enable / disable the LDS-halo stride-1 conv kernels (A/B runs);
     ``dgrad`` sets the backward-data kernel separately (default: same as
@@ -802,6 +817,15 @@ def _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
             return False
         if rc != -2:
             _lib.check(rc, "hvk_conv_fwd_ws")
+    if _CONV_HC and q8 is None and sy == 1 and sx == 1 and \
+            out.is_contiguous() and x.dtype == torch.bfloat16:
+        rc = _lib.lib().hvk_conv_fwd_hc(
+            _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
+            OH, OW, groups, act, stream)
+        if rc == 0:
+            return False
+        if rc != -2:
+            _lib.check(rc, "hvk_conv_fwd_hc")
     if _HALO and sy == 1 and sx == 1 and out.is_contiguous():
         rc = getattr(_lib.lib(), "hvk_conv_fwd_halo" + sfx)(
             _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
@@ -952,6 +976,16 @@ def _dgrad_call(dy, wt, out, aux, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
             return
         if rc != -2:
             _lib.check(rc, "hvk_conv_dgrad_ws")
+    if _CONV_HC and sx == 1 and sy == 1 and out.is_contiguous() and \
+            dy.dtype == torch.bfloat16 and \
+            (aux is None or aux.is_contiguous()):
+        rc = _lib.lib().hvk_conv_dgrad_hc(
+            _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
+            groups, _p(aux), aux_act, _s(dy))
+        if rc == 0:
+            return
+        if rc != -2:
+            _lib.check(rc, "hvk_conv_dgrad_hc")
     if _HALO_DGRAD and sx == 1 and sy == 1 and out.is_contiguous():
         rc = _lib.lib().hvk_conv_dgrad_halo(
             _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH,

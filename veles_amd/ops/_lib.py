@@ -113,6 +113,10 @@ _SIGS = {
     # weight-stationary convs (csrc/kernels/conv_ws.hip)
     "hvk_conv_fwd_ws": [P, P, P, P] + [I] * 13 + [P],
     "hvk_conv_dgrad_ws": [P, P, P] + [I] * 12 + [P, I, P],
+    # channel-chunked halo convs (csrc/kernels/conv_hc.hip)
+    "hvk_conv_fwd_hc": [P, P, P, P] + [I] * 13 + [P],
+    "hvk_conv_dgrad_hc": [P, P, P] + [I] * 12 + [P, I, P],
+    "hvk_hc_variant": [I],
     "hvk_take_last_error": [],
     "hvk_end_stream_capture": [P],
     "hvk_stream_create": [],
