@@ -58,11 +58,6 @@
 
 #include "conv_geom.h"
 
-// diagnostic builds only (wrong results by design): 1 no DMA, 2 no epilogue
-// stores, 4 no MFMAs
-#ifndef HVK_HC_ABL
-#define HVK_HC_ABL 0
-#endif
 
 using namespace hvk;
 
@@ -70,6 +65,8 @@ namespace {
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 struct HcGeom {
   int N, H, W, C;     // window source (x or dY), NHWC, C channels in total
@@ -85,8 +82,11 @@ struct HcGeom {
 };
 
 // KH x KW taps; WM x WN = 8 waves, each 64 pixels x NJW * 16 channels;
-// NBW: window DMA pieces per wave (upper bound, the plan checks)
-template <int KH, int KW, int WM, int WN, int NJW, int NBW>
+// NBW: window DMA pieces per wave (upper bound, the plan checks).
+// ABL: diagnostic instantiations only (wrong results by design; compile-time
+// so that the production loop carries no test): 1 no DMA after the first
+// stage, 2 no epilogue stores, 4 no MFMAs, 8 no stage wait / barrier
+template <int KH, int KW, int WM, int WN, int NJW, int NBW, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 conv_hc_kernel(const uint16_t* __restrict__ src,
                const uint16_t* __restrict__ wts, const float* __restrict__ bias,
@@ -103,9 +103,18 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   constexpr int WB = BN * TP * 32;           // weight bytes per stage
   constexpr int NWP = (WB + 1023) / 1024;    // weight DMA pieces
   constexpr int NWW = (NWP + NWV - 1) / NWV;
+  // n-tiles per store group: the weight rows are permuted so that a lane's
+  // accumulators of NG consecutive n-tiles are 4 * NG consecutive output
+  // channels (16- or 24-B stores, 16 * NG channels per pixel and group of 4
+  // lanes; 128 B for NG 4) instead of 8-B pieces of 16-channel tiles
+  constexpr int NG = NJW % 4 == 0 ? 4 : NJW % 3 == 0 ? 3 : NJW % 2 == 0 ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   lds_u8* sm = (lds_u8*)smem;
-  const uint32_t STAGE = (uint32_t)g.WIN + NWP * 1024;
+  // stage: window | weights | bias block (1 KiB: one DMA piece, the BN
+  // output channels' bias of the item's last chunk, wide tiles only)
+  constexpr int BIASB = NJW <= 4 ? 0 : 1024;
+  const uint32_t STAGE_B = (uint32_t)g.WIN + NWP * 1024;
+  const uint32_t STAGE = STAGE_B + BIASB;
   const int NBP = g.WIN >> 10;               // window pieces per stage
   const int NC = g.CG >> 4;                  // chunks (K stages) per item
   const int KT = T * g.CG;                   // weight row length (elements)
@@ -115,32 +124,22 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   const int wm = w % WM, wn = w / WM;
   const int fr = lane & 15, fq = lane >> 4;
 
-  // ---- weight DMA: this lane's 16-B chunk of each of its pieces ->
-  // (row n, granule tp, half); pad granules and rows read zeros
-  uint32_t wq[NWW];
-#pragma unroll
-  for (int i = 0; i < NWW; ++i) {
-    const int pi = w + NWV * i;
+  // ---- weight DMA: this lane's 16-B chunk of piece pi -> byte offset in
+  // the filter bank (row n, granule tp, half), or kBufOOB for pad granules
+  // and rows (recomputed per issue: registers, not time, are short here)
+  auto wq = [&](int pi) __attribute__((always_inline)) -> uint32_t {
     const int ib = pi * 1024 + 16 * lane;
     const int n = ib / (TP * 32);
     const int rem = ib - n * (TP * 32);
     const int tp = rem >> 5, half = (rem >> 4) & 1;
-    const bool ok = pi < NWP && n < BN && tp < T;
     const int tap = g.flip ? T - 1 - tp : tp;
-    wq[i] = ok ? (uint32_t)(n * KT + tap * g.CG + half * 8) * 2u : kBufOOB;
-  }
-  // ---- window DMA: (window row, column, half) of this lane's chunks
-  uint32_t pw[NBW];
-#pragma unroll
-  for (int i = 0; i < NBW; ++i) {
-    const int pi = w + NWV * i;
-    const uint32_t slot = (uint32_t)(pi * 1024 + 16 * lane) >> 5;
-    const uint32_t r = fdiv(slot, g.fWp);
-    const uint32_t cs = slot - r * (uint32_t)g.Wp;
-    const bool ok = pi < NBP && (int)cs < g.OW + KW - 1;
-    pw[i] = r | (cs << 10) | ((uint32_t)(lane & 1) << 30) |
-            (ok ? 0x80000000u : 0u);
-  }
+    // LDS row n = 16 J + 4 f + r (n-tile J, lane group f) holds channel
+    // 16 NG (J / NG) + 4 NG f + 4 (J % NG) + r
+    const int J = n >> 4, f = (n >> 2) & 3, r = n & 3;
+    const int ch = 16 * NG * (J / NG) + 4 * NG * f + 4 * (J % NG) + r;
+    return (n < BN && tp < T)
+               ? (uint32_t)(ch * KT + tap * g.CG + half * 8) * 2u : kBufOOB;
+  };
   // ---- A fragment tap offsets per k-step (k-group fq: tap 2s + fq / 2,
   // channel half fq % 2); the pad tap reads tap 0 (finite, zero weight)
   uint32_t ofs[NKS];
@@ -163,26 +162,35 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   const uint32_t pixbytes = (uint32_t)g.C * 2u;
 
   // item -> (pixel tile, group, n-tile), n-tile fastest
-  auto decode = [&](int it, int& ptl, int& gi, int& nt) {
+  auto decode = [&](int it, int& ptl, int& gi, int& nt) __attribute__((always_inline)) {
     nt = it % g.NT;
     const int r = it / g.NT;
     gi = r % g.G;
     ptl = r / g.G;
   };
-  auto issue = [&](int it, int c, uint32_t stb) {
-    if constexpr ((HVK_HC_ABL & 1) != 0) return;
+  // The DMA of one chunk, prepared by prepare() and issued slot by slot:
+  // per wave NBW window slots, NWW weight slots and one bias slot.
+  // window source byte offsets of this lane's chunks for the item being
+  // loaded (chunk 0; chunk c adds 32 c), computed at its first chunk
+  uint32_t pwb[NBW];
+  uint32_t d_cofs = 0, d_wofs = 0, d_bofs = 0;
+  bool d_bias = false;
+  auto prepare = [&](int it, int c) __attribute__((always_inline)) {
     int ptl, gi, nt;
     decode(it, ptl, gi, nt);
-    const uint32_t p0 = (uint32_t)ptl * TPX;
-    const uint32_t n0 = fdiv(p0, g.fOHW);
-    const uint32_t oh0 = fdiv(p0 - n0 * (uint32_t)g.OHW, g.fOW);
-    const int rc = g.OH - (int)oh0 + KH - 1;
-    const uint32_t cofs = (uint32_t)(gi * g.CG + c * 16) * 2u;
+    if (c == 0) {   // wave-uniform
+      const uint32_t p0 = (uint32_t)ptl * TPX;
+      const uint32_t n0 = fdiv(p0, g.fOHW);
+      const uint32_t oh0 = fdiv(p0 - n0 * (uint32_t)g.OHW, g.fOW);
+      const int rc = g.OH - (int)oh0 + KH - 1;
+      const uint32_t gofs = (uint32_t)(gi * g.CG) * 2u;
 #pragma unroll
-    for (int i = 0; i < NBW; ++i) {
-      if (w + NWV * i < NBP) {   // wave-uniform
-        const int r = (int)(pw[i] & 1023u);
-        const int cs = (int)((pw[i] >> 10) & 0xfffffu);
+      for (int i = 0; i < NBW; ++i) {
+        // this lane's chunk of window piece w + 8 i: (window row, column)
+        const uint32_t slot =
+            (uint32_t)((w + NWV * i) * 1024 + 16 * lane) >> 5;
+        const int r = (int)fdiv(slot, g.fWp);
+        const int cs = (int)slot - r * g.Wp;
         int j, lr;
         if (r < rc) {
           j = 0;
@@ -194,27 +202,44 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
         }
         const int ih = lr - g.pt, iw = cs - g.pl;
         const uint32_t n = n0 + (uint32_t)j;
-        const bool ok = (pw[i] >> 31) && (unsigned)ih < (unsigned)g.H &&
+        const bool ok = w + NWV * i < NBP && r < 1024 &&
+                        cs < g.OW + KW - 1 && (unsigned)ih < (unsigned)g.H &&
                         (unsigned)iw < (unsigned)g.W && n < (uint32_t)g.N;
-        const uint32_t v = ok ? (n * (uint32_t)g.H + (uint32_t)ih) * rowbytes +
-                                    (uint32_t)iw * pixbytes + cofs +
-                                    ((pw[i] >> 30) & 1u) * 16u
-                              : kBufOOB;
-        dma16(rs, smem + stb + (w + NWV * i) * 1024, v);
+        pwb[i] = ok ? (n * (uint32_t)g.H + (uint32_t)ih) * rowbytes +
+                          (uint32_t)iw * pixbytes + gofs +
+                          (uint32_t)(lane & 1) * 16u
+                    : kBufOOB;
       }
     }
-    const uint32_t wofs =
-        ((uint32_t)(gi * g.OCg + nt * BN) * (uint32_t)KT + c * 16) * 2u;
-#pragma unroll
-    for (int i = 0; i < NWW; ++i) {
-      if (w + NWV * i < NWP)   // wave-uniform
+    d_cofs = (uint32_t)c * 32u;
+    d_wofs = ((uint32_t)(gi * g.OCg + nt * BN) * (uint32_t)KT + c * 16) * 2u;
+    d_bias = BIASB && bias && c == NC - 1 && w == 0;
+    d_bofs = lane < BN / 4 ? (uint32_t)(gi * g.OCg + nt * BN + 4 * lane) * 4u
+                           : kBufOOB;
+  };
+  constexpr int NSLOT = NBW + NWW + (BIASB ? 1 : 0);
+  const __amdgpu_buffer_rsrc_t rbias = dma_rsrc(bias);
+  auto issue_slot = [&](int q, uint32_t stb) __attribute__((always_inline)) {
+    if (q < NBW) {
+      if (w + NWV * q < NBP)   // wave-uniform
+        dma16(rs, smem + stb + (w + NWV * q) * 1024,
+              pwb[q] >= kBufOOB ? kBufOOB : pwb[q] + d_cofs);
+    } else if (q < NBW + NWW) {
+      const int i = q - NBW;
+      if (w + NWV * i < NWP) {   // wave-uniform
+        const uint32_t o = wq(w + NWV * i);
         dma16(rw, smem + stb + g.WIN + (w + NWV * i) * 1024,
-              wq[i] >= kBufOOB ? kBufOOB : wq[i] + wofs);
+              o >= kBufOOB ? kBufOOB : o + d_wofs);
+      }
+    } else if (d_bias) {
+      // the item's bias block (natural channel order; lanes past BN / 4
+      // read zeros)
+      dma16(rbias, smem + stb + STAGE_B, d_bofs);
     }
   };
   // window slot bytes of this lane's pixels (fr of each m-tile)
   uint32_t bb[MI];
-  auto slots = [&](int it) {
+  auto slots = [&](int it) __attribute__((always_inline)) {
     int ptl, gi, nt;
     decode(it, ptl, gi, nt);
     const uint32_t p0 = (uint32_t)ptl * TPX;
@@ -241,11 +266,25 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   const int nwg = gridDim.x;
   int item = xcd_remap(blockIdx.x, nwg);
   if (item >= g.items) return;
-  issue(item, 0, 0);
+  const __amdgpu_buffer_rsrc_t ro = dma_rsrc(out);
+  auto next = [&](int& it, int& c) __attribute__((always_inline)) {
+    if (++c == NC) {
+      c = 0;
+      it += nwg;
+    }
+  };
+  prepare(item, 0);
+#pragma unroll
+  for (int q = 0; q < NSLOT; ++q) issue_slot(q, 0);
   slots(item);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  // (it1, c1): the chunk DMA'd into the other stage during this one
+  int it1 = item, c1 = 0;
+  next(it1, c1);
+  bool more1 = it1 < g.items;
+  if (more1) prepare(it1, c1);
 
   f32x4 acc[MI][NJW];
 #pragma unroll
@@ -253,17 +292,53 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 #pragma unroll
     for (int j = 0; j < NJW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // The next chunk's DMA slots are spread over the first ~2/3 of this
+  // chunk's k-steps (a burst at the chunk start stalls both waves of a SIMD
+  // at once: the barrier aligns them).  The bias and the derivative operand
+  // of narrow tiles (NJW <= 4) are loaded into registers at the start of the
+  // item's last chunk; wide tiles read the bias from the stage's bias block
+  // (DMA'd with the last chunk) and the derivative operand from memory.
+  constexpr int NKSD = NKS > 2 ? (2 * NKS + 2) / 3 : NKS;
+  constexpr bool PFA = NJW <= 4;
+  float4 bpre[PFA ? NJW : 1];
+  uint2 apre[PFA ? MI : 1][PFA ? NJW : 1];
   int c = 0;
   uint32_t cur = 0;
   for (;;) {
-    int nitem = item, nc = c + 1;
-    if (nc == NC) {
-      nc = 0;
-      nitem += nwg;
+    const bool last = c == NC - 1;
+    int ptl, gi, nt;
+    decode(item, ptl, gi, nt);
+    const uint32_t p0 = (uint32_t)ptl * TPX;
+    // lane's first channel of store group u (within the n-tile): + 16 NG u
+    const int chl = 16 * NG * wn * (NJW / NG) + 4 * NG * fq;
+    const int chb = gi * g.OCg + nt * BN + chl;
+    if constexpr (PFA) {
+      if (last) {
+        if (bias) {
+#pragma unroll
+          for (int j = 0; j < NJW; ++j)
+            bpre[j] = *(const float4*)(bias + chb + 16 * NG * (j / NG) +
+                                       4 * (j % NG));
+        }
+        if (aux) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const uint32_t p =
+                min(p0 + wm * 64 + i * 16 + fr, (uint32_t)g.P - 1);
+#pragma unroll
+            for (int j = 0; j < NJW; ++j)
+              apre[i][j] = *(const uint2*)(aux + (long long)p * g.OCT + chb +
+                                           16 * NG * (j / NG) + 4 * (j % NG));
+          }
+        }
+      }
     }
-    const bool more = nitem < g.items;
-    if (more) issue(nitem, nc, cur ^ STAGE);
+    const uint32_t nxt = cur ^ STAGE;
     const uint32_t wb = cur + (uint32_t)g.WIN;
+    // opaque per chunk: otherwise the MI x NKS window addresses bb + ofs
+    // are hoisted out of the chunk loop into as many live registers
+#pragma unroll
+    for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(bb[i]));
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
       bf16x8 a[MI], b[NJW];
@@ -273,7 +348,7 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 #pragma unroll
       for (int j = 0; j < NJW; ++j)
         b[j] = *(lds_bf16x8*)(sm + wb + bq[j] + s * 64);
-      if constexpr ((HVK_HC_ABL & 4) == 0) {
+      if constexpr ((ABL & 4) == 0) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -285,56 +360,107 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
         for (int i = 0; i < MI; ++i)
           acc[i][0][0] += (float)a[i][0] + (float)b[0][0];
       }
+      if constexpr ((ABL & 1) == 0) {
+        if (more1) {
+#pragma unroll
+          for (int q = 0; q < NSLOT; ++q)
+            if (q * NKSD / NSLOT == s) issue_slot(q, nxt);
+        }
+      }
+      // >= 24 accumulator tiles: no reads of the next k-step hoisted above
+      // these MFMAs (double-buffered fragments would not fit the 256
+      // registers of two waves per SIMD; the other wave hides the latency)
+      if constexpr (MI * NJW >= 24) __builtin_amdgcn_sched_barrier(0);
     }
-    // the next chunk landed; every read of this one done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (c == NC - 1) {
-      // epilogue (lane: D[n = fq * 4 + r][m = fr], 4 consecutive output
-      // channels of one pixel): bias, activation, derivative of the layer
-      // below, bf16, one 8-B store per (m-tile, n-tile)
-      int ptl, gi, nt;
-      decode(item, ptl, gi, nt);
-      const uint32_t p0 = (uint32_t)ptl * TPX;
+    // chunk (it1, c1) landed; every read of (item, c) done
+    if constexpr ((ABL & 8) == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (last) {
+      // lane: D[n = fq * 4 + r][m = fr] of each n-tile; with the row
+      // permutation 4 NG consecutive output channels of one pixel per store
+      // group: bias, activation, derivative of the layer below, bf16.
+      // Buffer stores: pixels past the end go to the out-of-range offset
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const uint32_t p = p0 + wm * 64 + i * 16 + fr;
-        if (p >= (uint32_t)g.P ||
-            ((HVK_HC_ABL & 2) && acc[i][0][0] != 1234.5f))
-          continue;
+        const uint32_t pa = min(p, (uint32_t)g.P - 1);
+        const bool ok = p < (uint32_t)g.P &&
+                        !((ABL & 2) && acc[i][0][0] != 1234.5f);
+        const uint32_t ob = (uint32_t)(((long long)p * g.OCT + chb) * 2);
 #pragma unroll
-        for (int j = 0; j < NJW; ++j) {
-          const int oc = gi * g.OCg + nt * BN + (wn * NJW + j) * 16 + fq * 4;
-          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2],
-                        acc[i][j][3]};
-          if (bias) {
-            const float4 bv = *(const float4*)(bias + oc);
-            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+        for (int u = 0; u < NJW / NG; ++u) {
+          float v[4 * NG];
+#pragma unroll
+          for (int e = 0; e < NG; ++e) {
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (bias) {
+              if constexpr (PFA) {
+                bv = bpre[NG * u + e];
+              } else {
+                const f32x4 lb = *(const __attribute__((address_space(3)))
+                                        f32x4*)(sm + cur + STAGE_B +
+                                                (chl + 16 * NG * u + 4 * e) *
+                                                    4);
+                bv = make_float4(lb[0], lb[1], lb[2], lb[3]);
+              }
+            }
+            v[4 * e] = acc[i][NG * u + e][0] + bv.x;
+            v[4 * e + 1] = acc[i][NG * u + e][1] + bv.y;
+            v[4 * e + 2] = acc[i][NG * u + e][2] + bv.z;
+            v[4 * e + 3] = acc[i][NG * u + e][3] + bv.w;
           }
-          act_fwd_n<4>(v, act);
-          const long long oi = (long long)p * g.OCT + oc;
+          act_fwd_n<4 * NG>(v, act);
           if (aux) {
-            const uint2 av = *(const uint2*)(aux + oi);
-            const float y[4] = {__uint_as_float(av.x << 16),
-                                __uint_as_float(av.x & 0xffff0000u),
-                                __uint_as_float(av.y << 16),
-                                __uint_as_float(av.y & 0xffff0000u)};
-            act_bwd_mul_n<4>(v, y, aux_act);
+            float y[4 * NG];
+#pragma unroll
+            for (int e = 0; e < NG; ++e) {
+              uint2 av;
+              if constexpr (PFA)
+                av = apre[i][NG * u + e];
+              else
+                av = *(const uint2*)(aux + (long long)pa * g.OCT + chb +
+                                     16 * NG * u + 4 * e);
+              y[4 * e] = __uint_as_float(av.x << 16);
+              y[4 * e + 1] = __uint_as_float(av.x & 0xffff0000u);
+              y[4 * e + 2] = __uint_as_float(av.y << 16);
+              y[4 * e + 3] = __uint_as_float(av.y & 0xffff0000u);
+            }
+            act_bwd_mul_n<4 * NG>(v, y, aux_act);
           }
-          *(uint2*)(out + oi) = make_uint2(pack_bf16x2(v[0], v[1]),
-                                           pack_bf16x2(v[2], v[3]));
+          const uint32_t o = ob + 32 * NG * u;
+          if constexpr (NG % 2 == 0) {   // 16-B aligned: 8 NG * 2 B apart
+#pragma unroll
+            for (int e = 0; e < NG; e += 2) {
+              const uint4 q = pack_bf16x8(v + 4 * e);
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  u32x4{q.x, q.y, q.z, q.w}, ro, ok ? o + 8 * e : kBufOOB,
+                  0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < NG; ++e)
+              __builtin_amdgcn_raw_buffer_store_b64(
+                  u32x2{pack_bf16x2(v[4 * e], v[4 * e + 1]),
+                        pack_bf16x2(v[4 * e + 2], v[4 * e + 3])},
+                  ro, ok ? o + 8 * e : kBufOOB, 0, 0);
+          }
         }
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (more) slots(nitem);
+      if (more1) slots(it1);
     }
-    if (!more) break;
-    item = nitem;
-    c = nc;
+    if (!more1) break;
+    item = it1;
+    c = c1;
+    next(it1, c1);
+    more1 = it1 < g.items;
+    if (more1) prepare(it1, c1);
     cur ^= STAGE;
   }
 }
@@ -349,22 +475,26 @@ struct HcPlan {
 constexpr int kCUs = 256;
 constexpr int kNBW = 8;   // window pieces per wave: 64 KiB windows at most
 int g_hc_variant = -1;    // -1 automatic, 0 off, > 0 forced configuration
+int g_hc_abl = 0;         // diagnostic instantiation (configurations 5, 6)
 
-struct HcCand { int var, KH, KW, WM, WN, NJW; };
+struct HcCand { int var, KH, KW, WM, WN, NJW, NBW; };
 // per kernel size, in order of preference (the first whose n-tile divides
 // the group's outputs and whose two stages fit the LDS)
 constexpr HcCand kHcCands[] = {
-    {1, 3, 3, 4, 2, 4},   // 256 px x 128 ch: AlexNet conv3 / conv5 fwd, conv3 dgrad
-    {2, 3, 3, 4, 2, 3},   // 256 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
-    {3, 3, 3, 8, 1, 4},   // 512 px x 64 ch: VGG-16 64-channel layers
-    {4, 5, 5, 4, 2, 2},   // 256 px x 64 ch: AlexNet conv2 fwd
-    {5, 5, 5, 8, 1, 3},   // 512 px x 48 ch: AlexNet conv2 dgrad
+    {6, 3, 3, 8, 1, 8, 5},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
+    {7, 3, 3, 8, 1, 6, 5},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
+    {1, 3, 3, 4, 2, 4, 8},   // 256 px x 128 ch
+    {2, 3, 3, 4, 2, 3, 8},   // 256 px x 96 ch
+    {3, 3, 3, 8, 1, 4, 8},   // 512 px x 64 ch: VGG-16 64-channel layers
+    {4, 5, 5, 4, 2, 2, 8},   // 256 px x 64 ch: AlexNet conv2 fwd
+    {5, 5, 5, 8, 1, 3, 8},   // 512 px x 48 ch: AlexNet conv2 dgrad
 };
 
+// weight (+ bias block) bytes of one stage
 int hc_nbytes_w(const HcCand& k) {
   const int T = k.KH * k.KW, TP = 2 * ((T + 1) / 2) + 1;
   const int BN = k.WN * k.NJW * 16;
-  return (BN * TP * 32 + 1023) / 1024 * 1024;
+  return (BN * TP * 32 + 1023) / 1024 * 1024 + (k.NJW <= 4 ? 0 : 1024);
 }
 
 HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
@@ -375,7 +505,7 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   const int CG = C / groups, OCg = OCT / groups;
   if (CG % 16 || OCg % 16 || OCT % 4) return p;
   if ((long long)N * H * W * C * 2 >= kBufMaxBytes) return p;
-  if ((long long)N * OH * OW >= (1ll << 31)) return p;
+  if ((long long)N * OH * OW * OCT * 2 >= kBufMaxBytes) return p;
   g.N = N; g.H = H; g.W = W; g.C = C; g.OH = OH; g.OW = OW; g.OCT = OCT;
   g.OCg = OCg; g.CG = CG; g.pt = pt; g.pl = pl; g.G = groups;
   g.P = N * OH * OW;
@@ -407,7 +537,7 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
     }
     if (wr >= 1024) continue;
     g.WIN = (wr * g.Wp * 32 + 1023) / 1024 * 1024;
-    if (g.WIN / 1024 > 8 * kNBW) continue;
+    if (g.WIN / 1024 > 8 * k.NBW) continue;
     const size_t lds = 2 * (size_t)(g.WIN + hc_nbytes_w(k));
     if (lds > 160 * 1024) continue;
     g.NT = OCg / BN;
@@ -424,11 +554,13 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   return p;
 }
 
-template <int KH, int KW, int WM, int WN, int NJW>
+template <int KH, int KW, int WM, int WN, int NJW, int ABL = 0,
+          int NBW = kNBW>
 hipError_t go_hc(const HcPlan& p, const void* src, const void* wts,
                  const float* bias, void* out, const void* aux, int act,
                  int aux_act, hipStream_t s) {
-  auto kern = conv_hc_kernel<KH, KW, WM, WN, NJW, kNBW>;
+  if (p.g.WIN / 1024 > 8 * NBW) return hipErrorInvalidValue;
+  auto kern = conv_hc_kernel<KH, KW, WM, WN, NJW, NBW, ABL>;
   static bool attr = false;   // once per instantiation, before any capture
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(
@@ -443,6 +575,21 @@ hipError_t go_hc(const HcPlan& p, const void* src, const void* wts,
   return launch_status(s);
 }
 
+template <int KH, int KW, int WM, int WN, int NJW, int NBW = kNBW>
+hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
+                     const float* bias, void* out, const void* aux, int act,
+                     int aux_act, hipStream_t s) {
+  switch (g_hc_abl) {
+#define HC_ABL(A) \
+    case A: return go_hc<KH, KW, WM, WN, NJW, A, NBW>(p, src, wts, bias, out, \
+                                                      aux, act, aux_act, s);
+    HC_ABL(1) HC_ABL(2) HC_ABL(4) HC_ABL(8) HC_ABL(3) HC_ABL(9)
+#undef HC_ABL
+    default: return go_hc<KH, KW, WM, WN, NJW, 0, NBW>(p, src, wts, bias, out,
+                                                       aux, act, aux_act, s);
+  }
+}
+
 hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
                      const float* bias, void* out, const void* aux, int act,
                      int aux_act, hipStream_t s) {
@@ -455,8 +602,12 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
                                         aux_act, s);
     case 4: return go_hc<5, 5, 4, 2, 2>(p, src, wts, bias, out, aux, act,
                                         aux_act, s);
-    case 5: return go_hc<5, 5, 8, 1, 3>(p, src, wts, bias, out, aux, act,
-                                        aux_act, s);
+    case 5: return go_hc_abl<5, 5, 8, 1, 3>(p, src, wts, bias, out, aux,
+                                            act, aux_act, s);
+    case 6: return go_hc_abl<3, 3, 8, 1, 8, 5>(p, src, wts, bias, out, aux,
+                                               act, aux_act, s);
+    case 7: return go_hc<3, 3, 8, 1, 6, 0, 5>(p, src, wts, bias, out, aux,
+                                              act, aux_act, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -465,6 +616,9 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
 
 // Force a configuration (kHcCands var), 0 = off, -1 = automatic.
 HVK_API void hvk_hc_variant(int v) { g_hc_variant = v; }
+// Diagnostic ablation builds of configurations 5 and 6 (see conv_hc_kernel's
+// ABL); 0 = the production kernel.
+HVK_API void hvk_hc_ablation(int a) { g_hc_abl = a; }
 
 // Forward: Y[N][OH][OW][OC] = act(conv(X, W) + bias), stride 1, X bf16 NHWC,
 // W [OC][KH][KW][C/g].  Returns 0, -2 when the shape does not take this

@@ -1,0 +1,49 @@
+"""Ablation of the channel-chunked halo conv kernel (conv_hc.hip): times the
+diagnostic instantiations (hvk_hc_ablation: 1 no DMA, 2 no epilogue
+stores, 4 no MFMAs, 8 no stage wait / barrier; wrong results by design)
+against the production kernel, interleaved in one process, on AlexNet
+conv3 forward (configuration 6) and conv2 backward-data (configuration 5).
+
+    python tools/ablate_conv_hc.py [batch] [rounds]"""
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+import veles_amd.ops as ops  # noqa: E402
+from veles_amd.ops import _lib  # noqa: E402
+
+sys.path.insert(0, "tools")
+from bench_conv_hc_ab import case, timeit  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    lib = _lib.lib()
+    ops.set_conv_hc(True, -1)
+    cases = [("conv3_fwd v6", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
+             ("conv2_dgrad v5", ("dgrad", B, 27, 27, 96, 256, 5, 1, 2, 2))]
+    abls = [0, 1, 2, 4, 8, 3, 9]
+    try:
+        for name, shp in cases:
+            fl, fn = case(*shp)
+            res = {a: [] for a in abls}
+            for _ in range(rounds):
+                for a in abls:
+                    lib.hvk_hc_ablation(a)
+                    res[a].append(timeit(fn) * 1e3)
+            med = {a: statistics.median(v) for a, v in res.items()}
+            print("%-15s " % name + "  ".join(
+                "abl%d %.3f ms (%.0f TF)" % (a, med[a], fl / med[a] / 1e9)
+                for a in abls), flush=True)
+            del fn
+            torch.cuda.empty_cache()
+    finally:
+        lib.hvk_hc_ablation(0)
+        ops.set_conv_hc(False, -1)
+
+
+if __name__ == "__main__":
+    main()
