@@ -474,7 +474,9 @@ struct HcPlan {
 
 constexpr int kCUs = 256;
 constexpr int kNBW = 8;   // window pieces per wave: 64 KiB windows at most
-int g_hc_variant = -1;    // -1 automatic, 0 off, > 0 forced configuration
+// -2 automatic on the shapes where it beats the implicit-GEMM kernels, -1 on
+// every shape it supports, 0 off, > 0 one forced configuration
+int g_hc_variant = -2;
 int g_hc_abl = 0;         // diagnostic instantiation (configurations 5, 6)
 
 struct HcCand { int var, KH, KW, WM, WN, NJW, NBW; };
@@ -504,6 +506,16 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   if (g_hc_variant == 0) return p;
   const int CG = C / groups, OCg = OCT / groups;
   if (CG % 16 || OCg % 16 || OCT % 4) return p;
+  // automatic: the shapes measured faster than the T4 / 256x256 / 128-row
+  // implicit GEMM in one process (profiles/r5/ab_conv_hc_*.log): 5 x 5
+  // (AlexNet conv2 1.03-1.08x forward, 1.37x backward-data), narrow-source
+  // forwards (conv1 through space-to-depth 1.14x, VGG conv1_2 1.06x) and
+  // the 56-wide 256-channel layers (VGG conv3_x 1.07x both ways).  The
+  // 13-wide AlexNet conv3-5, VGG conv2_2 / conv4_2 and conv1_2
+  // backward-data run at parity or below and stay on the GEMM
+  if (g_hc_variant == -2 &&
+      !(KH == 5 || (!flip && CG <= 64) || (OW >= 56 && CG >= 256)))
+    return p;
   if ((long long)N * H * W * C * 2 >= kBufMaxBytes) return p;
   if ((long long)N * OH * OW * OCT * 2 >= kBufMaxBytes) return p;
   g.N = N; g.H = H; g.W = W; g.C = C; g.OH = OH; g.OW = OW; g.OCT = OCT;
@@ -614,7 +626,8 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
 
 }  // namespace
 
-// Force a configuration (kHcCands var), 0 = off, -1 = automatic.
+// -2 automatic (the measured winners), -1 every supported shape, 0 off,
+// > 0 one forced configuration (kHcCands var).
 HVK_API void hvk_hc_variant(int v) { g_hc_variant = v; }
 // Diagnostic ablation builds of configurations 5 and 6 (see conv_hc_kernel's
 // ABL); 0 = the production kernel.

@@ -22,13 +22,14 @@ def _r(*shape, scale=1.0, seed=0):
 
 def _both(fn):
     out = {}
+    prev = ops._CONV_HC
     try:
         for on in (True, False):
-            ops.set_conv_hc(on, -1)
+            ops.set_conv_hc(on, -1)   # every supported shape
             out[on] = fn()
             torch.cuda.synchronize()
     finally:
-        ops.set_conv_hc(False, -1)
+        ops.set_conv_hc(prev, -2)
     return out
 
 
@@ -115,6 +116,13 @@ def test_conv_hc_taken_and_forced_variants():
                 ref = y
             else:
                 _close(y, ref, 4e-3)
+        # the automatic policy leaves the 13-wide AlexNet layers to the GEMM
+        lib.hvk_hc_variant(-2)
+        rc = lib.hvk_conv_fwd_hc(
+            x.data_ptr(), w.data_ptr(), None, ref.data_ptr(), 3, 13, 13, 384,
+            384, 3, 3, 1, 1, 13, 13, 2, 0,
+            torch.cuda.current_stream().cuda_stream)
+        assert rc == -2
         # a configuration for another kernel size is not taken
         lib.hvk_hc_variant(4)
         rc = lib.hvk_conv_fwd_hc(
@@ -123,4 +131,4 @@ def test_conv_hc_taken_and_forced_variants():
             torch.cuda.current_stream().cuda_stream)
         assert rc == -2
     finally:
-        lib.hvk_hc_variant(-1)
+        lib.hvk_hc_variant(-2)

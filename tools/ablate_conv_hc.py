@@ -42,7 +42,7 @@ def main():
             torch.cuda.empty_cache()
     finally:
         lib.hvk_hc_ablation(0)
-        ops.set_conv_hc(False, -1)
+        ops.set_conv_hc(True, -2)
 
 
 if __name__ == "__main__":

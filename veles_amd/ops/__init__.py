@@ -766,13 +766,15 @@ def set_conv_ws(on):
 
 # channel-chunked halo convs (csrc/kernels/conv_hc.hip): stride-1 3 x 3 and
 # 5 x 5 forward / backward-data with a per-chunk input window shared by
-# every tap
-_CONV_HC = os.environ.get("VELES_AMD_CONV_HC", "0") != "0"
+# every tap; on by default for the shapes where it measured faster
+# (conv_hc.hip hc_plan, profiles/r5/ab_conv_hc_*.log)
+_CONV_HC = os.environ.get("VELES_AMD_CONV_HC", "1") != "0"
 
 
 def set_conv_hc(on, variant=None):
-    """A/B knob of the channel-chunked halo conv kernels; ``variant`` forces
-    one configuration of conv_hc.hip's table (-1: automatic)."""
+    """A/B knob of the channel-chunked halo conv kernels; ``variant``: -2
+    the automatic shape policy (default), -1 every supported shape, > 0 one
+    forced configuration of conv_hc.hip's table."""
     global _CONV_HC
     _CONV_HC = bool(on)
     if variant is not None and _lib.available():
