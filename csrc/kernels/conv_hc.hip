@@ -81,27 +81,36 @@ struct HcGeom {
   FastDiv fOW, fOHW, fHPd, fWp;
 };
 
-// KH x KW taps; WM x WN = 8 waves, each 64 pixels x NJW * 16 channels;
-// NBW: window DMA pieces per wave (upper bound, the plan checks).
+// KH x KW taps, KHS kh rows per K stage (a 5 x 5 splits into 3 + 2 rows:
+// half the weights per stage, so a 512 x 64 tile fits two stages); WM x WN
+// = 8 waves, each 64 pixels x NJW * 16 channels; NBW: window DMA pieces per
+// wave (upper bound, the plan checks).
 // ABL: diagnostic instantiations only (wrong results by design; compile-time
 // so that the production loop carries no test): 1 no DMA after the first
 // stage, 2 no epilogue stores, 4 no MFMAs, 8 no stage wait / barrier
-template <int KH, int KW, int WM, int WN, int NJW, int NBW, int ABL = 0>
+template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW,
+          int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 conv_hc_kernel(const uint16_t* __restrict__ src,
                const uint16_t* __restrict__ wts, const float* __restrict__ bias,
                uint16_t* __restrict__ out, const uint16_t* __restrict__ aux,
                int act, int aux_act, HcGeom g) {
   constexpr int T = KH * KW;
-  constexpr int NKS = (T + 1) / 2;           // MFMA k-steps per chunk
-  constexpr int TP = 2 * NKS + 1;            // granules per weight row (odd)
+  constexpr int NH = (KH + KHS - 1) / KHS;   // stages per 16-channel chunk
+  static_assert(NH <= 2, "at most two kh groups");
+  // kh group h: rows h KHS .. + RH(h), T_h taps, NKS_h MFMA k-steps, TP_h
+  // (odd) 32-B granules per weight row in LDS
+  constexpr int RH0 = KHS, RH1 = KH - KHS;
+  constexpr int T0 = RH0 * KW, T1 = RH1 * KW;
+  constexpr int NKS0 = (T0 + 1) / 2, NKS1 = (T1 + 1) / 2;
+  constexpr int TP0 = 2 * NKS0 + 1, TP1 = 2 * NKS1 + 1;
   constexpr int NWV = WM * WN;
   static_assert(NWV == 8, "eight waves");
   constexpr int MI = 4;                      // 64 pixels per wave
   constexpr int TPX = WM * 64;
   constexpr int BN = WN * NJW * 16;
-  constexpr int WB = BN * TP * 32;           // weight bytes per stage
-  constexpr int NWP = (WB + 1023) / 1024;    // weight DMA pieces
+  constexpr int WB = BN * TP0 * 32;          // weight bytes per stage
+  constexpr int NWP = (WB + 1023) / 1024;    // weight DMA pieces (at most)
   constexpr int NWW = (NWP + NWV - 1) / NWV;
   // n-tiles per store group: the weight rows are permuted so that a lane's
   // accumulators of NG consecutive n-tiles are 4 * NG consecutive output
@@ -111,12 +120,12 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   lds_u8* sm = (lds_u8*)smem;
   // stage: window | weights | bias block (1 KiB: one DMA piece, the BN
-  // output channels' bias of the item's last chunk, wide tiles only)
-  constexpr int BIASB = NJW <= 4 ? 0 : 1024;
+  // output channels' bias of the item's last stage, wide tiles only)
+  constexpr int BIASB = NJW <= 3 ? 0 : 1024;
   const uint32_t STAGE_B = (uint32_t)g.WIN + NWP * 1024;
   const uint32_t STAGE = STAGE_B + BIASB;
   const int NBP = g.WIN >> 10;               // window pieces per stage
-  const int NC = g.CG >> 4;                  // chunks (K stages) per item
+  const int NQ = (g.CG >> 4) * NH;           // K stages per item
   const int KT = T * g.CG;                   // weight row length (elements)
 
   const int t = threadIdx.x, lane = t & 63;
@@ -124,37 +133,45 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   const int wm = w % WM, wn = w / WM;
   const int fr = lane & 15, fq = lane >> 4;
 
-  // ---- weight DMA: this lane's 16-B chunk of piece pi -> byte offset in
-  // the filter bank (row n, granule tp, half), or kBufOOB for pad granules
-  // and rows (recomputed per issue: registers, not time, are short here)
-  auto wq = [&](int pi) __attribute__((always_inline)) -> uint32_t {
+  // ---- weight DMA of kh group H: this lane's 16-B chunk of piece pi ->
+  // byte offset in the filter bank (row n, granule tp, half), or kBufOOB
+  // for pad granules and rows (recomputed per issue: registers, not time,
+  // are short here)
+  auto wq = [&](auto hc, int pi) __attribute__((always_inline)) -> uint32_t {
+    constexpr int H = decltype(hc)::value;
+    constexpr int TPH = H ? TP1 : TP0, TH = H ? T1 : T0;
     const int ib = pi * 1024 + 16 * lane;
-    const int n = ib / (TP * 32);
-    const int rem = ib - n * (TP * 32);
+    const int n = ib / (TPH * 32);
+    const int rem = ib - n * (TPH * 32);
     const int tp = rem >> 5, half = (rem >> 4) & 1;
-    const int tap = g.flip ? T - 1 - tp : tp;
+    const int tap0 = H * KHS * KW + tp;
+    const int tap = g.flip ? T - 1 - tap0 : tap0;
     // LDS row n = 16 J + 4 f + r (n-tile J, lane group f) holds channel
     // 16 NG (J / NG) + 4 NG f + 4 (J % NG) + r
     const int J = n >> 4, f = (n >> 2) & 3, r = n & 3;
     const int ch = 16 * NG * (J / NG) + 4 * NG * f + 4 * (J % NG) + r;
-    return (n < BN && tp < T)
+    return (n < BN && tp < TH && pi * 1024 < BN * TPH * 32)
                ? (uint32_t)(ch * KT + tap * g.CG + half * 8) * 2u : kBufOOB;
   };
-  // ---- A fragment tap offsets per k-step (k-group fq: tap 2s + fq / 2,
-  // channel half fq % 2); the pad tap reads tap 0 (finite, zero weight)
-  uint32_t ofs[NKS];
+  // ---- A fragment tap offsets per k-step of each kh group (k-group fq:
+  // tap 2s + fq / 2 of the group, channel half fq % 2); the pad tap reads
+  // tap 0 (finite, zero weight).  Window rows of a stage start at its
+  // group's first kh, so the offsets use the kh within the group
+  uint32_t ofs0[NKS0], ofs1[NKS1 > 0 ? NKS1 : 1];
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) {
+  for (int s = 0; s < NKS0; ++s) {
     int tp = 2 * s + (fq >> 1);
-    if (tp >= T) tp = 0;
+    if (tp >= T0) tp = 0;
     const int kh = tp / KW, kw = tp - (tp / KW) * KW;
-    ofs[s] = (uint32_t)((kh * g.Wp + kw) * 32 + (fq & 1) * 16);
+    ofs0[s] = (uint32_t)((kh * g.Wp + kw) * 32 + (fq & 1) * 16);
   }
-  // ---- B fragment row bases (weights: row n, k-group fq)
-  uint32_t bq[NJW];
 #pragma unroll
-  for (int j = 0; j < NJW; ++j)
-    bq[j] = (uint32_t)(((wn * NJW + j) * 16 + fr) * (TP * 32) + fq * 16);
+  for (int s = 0; s < NKS1; ++s) {
+    int tp = 2 * s + (fq >> 1);
+    if (tp >= T1) tp = 0;
+    const int kh = tp / KW, kw = tp - (tp / KW) * KW;
+    ofs1[s] = (uint32_t)((kh * g.Wp + kw) * 32 + (fq & 1) * 16);
+  }
 
   const __amdgpu_buffer_rsrc_t rs = dma_rsrc(src);
   const __amdgpu_buffer_rsrc_t rw = dma_rsrc(wts);
@@ -162,23 +179,26 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   const uint32_t pixbytes = (uint32_t)g.C * 2u;
 
   // item -> (pixel tile, group, n-tile), n-tile fastest
-  auto decode = [&](int it, int& ptl, int& gi, int& nt) __attribute__((always_inline)) {
+  auto decode = [&](int it, int& ptl, int& gi, int& nt)
+                    __attribute__((always_inline)) {
     nt = it % g.NT;
     const int r = it / g.NT;
     gi = r % g.G;
     ptl = r / g.G;
   };
-  // The DMA of one chunk, prepared by prepare() and issued slot by slot:
+  // The DMA of one stage, prepared by prepare() and issued slot by slot:
   // per wave NBW window slots, NWW weight slots and one bias slot.
-  // window source byte offsets of this lane's chunks for the item being
-  // loaded (chunk 0; chunk c adds 32 c), computed at its first chunk
+  // window source byte offsets of this lane's chunks (channel chunk 0; chunk
+  // c adds 32 c) for the stage being loaded
   uint32_t pwb[NBW];
   uint32_t d_cofs = 0, d_wofs = 0, d_bofs = 0;
+  int d_h = 0;
   bool d_bias = false;
-  auto prepare = [&](int it, int c) __attribute__((always_inline)) {
+  auto prepare = [&](int it, int q) __attribute__((always_inline)) {
     int ptl, gi, nt;
     decode(it, ptl, gi, nt);
-    if (c == 0) {   // wave-uniform
+    const int c = q / NH, h = q - (q / NH) * NH;
+    if (NH > 1 || c == 0) {   // wave-uniform: a new item or kh group
       const uint32_t p0 = (uint32_t)ptl * TPX;
       const uint32_t n0 = fdiv(p0, g.fOHW);
       const uint32_t oh0 = fdiv(p0 - n0 * (uint32_t)g.OHW, g.fOW);
@@ -186,23 +206,25 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
       const uint32_t gofs = (uint32_t)(gi * g.CG) * 2u;
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
-        // this lane's chunk of window piece w + 8 i: (window row, column)
+        // this lane's chunk of window piece w + 8 i: (window row, column);
+        // window row r of kh group h is row r + h KHS of the full layout
         const uint32_t slot =
             (uint32_t)((w + NWV * i) * 1024 + 16 * lane) >> 5;
-        const int r = (int)fdiv(slot, g.fWp);
-        const int cs = (int)slot - r * g.Wp;
+        const int rw_ = (int)fdiv(slot, g.fWp);
+        const int cs = (int)slot - rw_ * g.Wp;
+        const int r = rw_ + h * KHS;
         int j, lr;
         if (r < rc) {
           j = 0;
           lr = (int)oh0 + r;
         } else {
-          const int q = (int)fdiv((uint32_t)(r - rc), g.fHPd);
-          j = 1 + q;
-          lr = r - rc - q * g.HPd;
+          const int qq = (int)fdiv((uint32_t)(r - rc), g.fHPd);
+          j = 1 + qq;
+          lr = r - rc - qq * g.HPd;
         }
         const int ih = lr - g.pt, iw = cs - g.pl;
         const uint32_t n = n0 + (uint32_t)j;
-        const bool ok = w + NWV * i < NBP && r < 1024 &&
+        const bool ok = w + NWV * i < NBP && rw_ < 1024 &&
                         cs < g.OW + KW - 1 && (unsigned)ih < (unsigned)g.H &&
                         (unsigned)iw < (unsigned)g.W && n < (uint32_t)g.N;
         pwb[i] = ok ? (n * (uint32_t)g.H + (uint32_t)ih) * rowbytes +
@@ -211,9 +233,10 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
                     : kBufOOB;
       }
     }
+    d_h = h;
     d_cofs = (uint32_t)c * 32u;
     d_wofs = ((uint32_t)(gi * g.OCg + nt * BN) * (uint32_t)KT + c * 16) * 2u;
-    d_bias = BIASB && bias && c == NC - 1 && w == 0;
+    d_bias = BIASB && bias && q == NQ - 1 && w == 0;
     d_bofs = lane < BN / 4 ? (uint32_t)(gi * g.OCg + nt * BN + 4 * lane) * 4u
                            : kBufOOB;
   };
@@ -227,7 +250,9 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
     } else if (q < NBW + NWW) {
       const int i = q - NBW;
       if (w + NWV * i < NWP) {   // wave-uniform
-        const uint32_t o = wq(w + NWV * i);
+        const uint32_t o =
+            (NH > 1 && d_h) ? wq(std::integral_constant<int, 1>{}, w + NWV * i)
+                            : wq(std::integral_constant<int, 0>{}, w + NWV * i);
         dma16(rw, smem + stb + g.WIN + (w + NWV * i) * 1024,
               o >= kBufOOB ? kBufOOB : o + d_wofs);
       }
@@ -267,9 +292,9 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   int item = xcd_remap(blockIdx.x, nwg);
   if (item >= g.items) return;
   const __amdgpu_buffer_rsrc_t ro = dma_rsrc(out);
-  auto next = [&](int& it, int& c) __attribute__((always_inline)) {
-    if (++c == NC) {
-      c = 0;
+  auto next = [&](int& it, int& q) __attribute__((always_inline)) {
+    if (++q == NQ) {
+      q = 0;
       it += nwg;
     }
   };
@@ -280,11 +305,11 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  // (it1, c1): the chunk DMA'd into the other stage during this one
-  int it1 = item, c1 = 0;
-  next(it1, c1);
+  // (it1, q1): the stage DMA'd into the other buffer during this one
+  int it1 = item, q1 = 0;
+  next(it1, q1);
   bool more1 = it1 < g.items;
-  if (more1) prepare(it1, c1);
+  if (more1) prepare(it1, q1);
 
   f32x4 acc[MI][NJW];
 #pragma unroll
@@ -292,20 +317,64 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 #pragma unroll
     for (int j = 0; j < NJW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // The next chunk's DMA slots are spread over the first ~2/3 of this
-  // chunk's k-steps (a burst at the chunk start stalls both waves of a SIMD
+  // The next stage's DMA slots are spread over the first ~2/3 of this
+  // stage's k-steps (a burst at the stage start stalls both waves of a SIMD
   // at once: the barrier aligns them).  The bias and the derivative operand
-  // of narrow tiles (NJW <= 4) are loaded into registers at the start of the
-  // item's last chunk; wide tiles read the bias from the stage's bias block
-  // (DMA'd with the last chunk) and the derivative operand from memory.
-  constexpr int NKSD = NKS > 2 ? (2 * NKS + 2) / 3 : NKS;
-  constexpr bool PFA = NJW <= 4;
+  // of narrow tiles (NJW <= 3) are loaded into registers at the start of the
+  // item's last stage; wide tiles read the bias from the stage's bias block
+  // (DMA'd with the last stage) and the derivative operand from memory.
+  constexpr bool PFA = NJW <= 3;
   float4 bpre[PFA ? NJW : 1];
   uint2 apre[PFA ? MI : 1][PFA ? NJW : 1];
-  int c = 0;
+  int q = 0;
   uint32_t cur = 0;
+  // the k-steps of kh group H on the stage in buffer cur, interleaved with
+  // the DMA of the next stage into nxt
+  auto kloop = [&](auto hc, uint32_t nxt) __attribute__((always_inline)) {
+    constexpr int H = decltype(hc)::value;
+    constexpr int NKSH = H ? NKS1 : NKS0, TPH = H ? TP1 : TP0;
+    constexpr int NKSD = NKSH > 2 ? (2 * NKSH + 2) / 3 : NKSH;
+    const uint32_t wb = cur + (uint32_t)g.WIN +
+                        (uint32_t)(((wn * NJW) * 16 + fr) * (TPH * 32) +
+                                   fq * 16);
+#pragma unroll
+    for (int s = 0; s < NKSH; ++s) {
+      bf16x8 a[MI], b[NJW];
+      const uint32_t os = H ? ofs1[H ? s : 0] : ofs0[s];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        a[i] = *(lds_bf16x8*)(sm + cur + bb[i] + os);
+#pragma unroll
+      for (int j = 0; j < NJW; ++j)
+        b[j] = *(lds_bf16x8*)(sm + wb + j * 16 * (TPH * 32) + s * 64);
+      if constexpr ((ABL & 4) == 0) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJW; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                b[j], a[i], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          acc[i][0][0] += (float)a[i][0] + (float)b[0][0];
+      }
+      if constexpr ((ABL & 1) == 0) {
+        if (more1) {
+#pragma unroll
+          for (int k = 0; k < NSLOT; ++k)
+            if (k * NKSD / NSLOT == s) issue_slot(k, nxt);
+        }
+      }
+      // >= 24 accumulator tiles: no reads of the next k-step hoisted above
+      // these MFMAs (double-buffered fragments would not fit the 256
+      // registers of two waves per SIMD; the other wave hides the latency)
+      if constexpr (MI * NJW >= 24 || NH > 1)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   for (;;) {
-    const bool last = c == NC - 1;
+    const bool last = q == NQ - 1;
     int ptl, gi, nt;
     decode(item, ptl, gi, nt);
     const uint32_t p0 = (uint32_t)ptl * TPX;
@@ -333,46 +402,14 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
         }
       }
     }
-    const uint32_t nxt = cur ^ STAGE;
-    const uint32_t wb = cur + (uint32_t)g.WIN;
-    // opaque per chunk: otherwise the MI x NKS window addresses bb + ofs
-    // are hoisted out of the chunk loop into as many live registers
+    // opaque per stage: otherwise the MI x NKS window addresses bb + ofs
+    // are hoisted out of the stage loop into as many live registers
 #pragma unroll
     for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(bb[i]));
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      bf16x8 a[MI], b[NJW];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-        a[i] = *(lds_bf16x8*)(sm + cur + bb[i] + ofs[s]);
-#pragma unroll
-      for (int j = 0; j < NJW; ++j)
-        b[j] = *(lds_bf16x8*)(sm + wb + bq[j] + s * 64);
-      if constexpr ((ABL & 4) == 0) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NJW; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                b[j], a[i], acc[i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-          acc[i][0][0] += (float)a[i][0] + (float)b[0][0];
-      }
-      if constexpr ((ABL & 1) == 0) {
-        if (more1) {
-#pragma unroll
-          for (int q = 0; q < NSLOT; ++q)
-            if (q * NKSD / NSLOT == s) issue_slot(q, nxt);
-        }
-      }
-      // >= 24 accumulator tiles: no reads of the next k-step hoisted above
-      // these MFMAs (double-buffered fragments would not fit the 256
-      // registers of two waves per SIMD; the other wave hides the latency)
-      if constexpr (MI * NJW >= 24) __builtin_amdgcn_sched_barrier(0);
-    }
-    // chunk (it1, c1) landed; every read of (item, c) done
+    const uint32_t nxt = cur ^ STAGE;
+    if (NH > 1 && (q % NH) != 0) kloop(std::integral_constant<int, 1>{}, nxt);
+    else kloop(std::integral_constant<int, 0>{}, nxt);
+    // stage (it1, q1) landed; every read of (item, q) done
     if constexpr ((ABL & 8) == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -434,10 +471,10 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
           if constexpr (NG % 2 == 0) {   // 16-B aligned: 8 NG * 2 B apart
 #pragma unroll
             for (int e = 0; e < NG; e += 2) {
-              const uint4 q = pack_bf16x8(v + 4 * e);
+              const uint4 qv = pack_bf16x8(v + 4 * e);
               __builtin_amdgcn_raw_buffer_store_b128(
-                  u32x4{q.x, q.y, q.z, q.w}, ro, ok ? o + 8 * e : kBufOOB,
-                  0, 0);
+                  u32x4{qv.x, qv.y, qv.z, qv.w}, ro,
+                  ok ? o + 8 * e : kBufOOB, 0, 0);
             }
           } else {
 #pragma unroll
@@ -457,10 +494,10 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
     }
     if (!more1) break;
     item = it1;
-    c = c1;
-    next(it1, c1);
+    q = q1;
+    next(it1, q1);
     more1 = it1 < g.items;
-    if (more1) prepare(it1, c1);
+    if (more1) prepare(it1, q1);
     cur ^= STAGE;
   }
 }
@@ -479,24 +516,28 @@ constexpr int kNBW = 8;   // window pieces per wave: 64 KiB windows at most
 int g_hc_variant = -2;
 int g_hc_abl = 0;         // diagnostic instantiation (configurations 5, 6)
 
-struct HcCand { int var, KH, KW, WM, WN, NJW, NBW; };
+struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW; };
 // per kernel size, in order of preference (the first whose n-tile divides
 // the group's outputs and whose two stages fit the LDS)
 constexpr HcCand kHcCands[] = {
-    {6, 3, 3, 8, 1, 8, 5},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
-    {7, 3, 3, 8, 1, 6, 5},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
-    {1, 3, 3, 4, 2, 4, 8},   // 256 px x 128 ch
-    {2, 3, 3, 4, 2, 3, 8},   // 256 px x 96 ch
-    {3, 3, 3, 8, 1, 4, 8},   // 512 px x 64 ch: VGG-16 64-channel layers
-    {4, 5, 5, 4, 2, 2, 8},   // 256 px x 64 ch: AlexNet conv2 fwd
-    {5, 5, 5, 8, 1, 3, 8},   // 512 px x 48 ch: AlexNet conv2 dgrad
+    {6, 3, 3, 3, 8, 1, 8, 5},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
+    {7, 3, 3, 3, 8, 1, 6, 5},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
+    {1, 3, 3, 3, 4, 2, 4, 8},   // 256 px x 128 ch
+    {2, 3, 3, 3, 4, 2, 3, 8},   // 256 px x 96 ch
+    {3, 3, 3, 3, 8, 1, 4, 8},   // 512 px x 64 ch: VGG-16 64-channel layers
+    {4, 5, 5, 5, 4, 2, 2, 8},   // 256 px x 64 ch: AlexNet conv2 fwd
+    {5, 5, 5, 5, 8, 1, 3, 8},   // 512 px x 48 ch: AlexNet conv2 dgrad
+    // 512 px x 64 ch in two kh groups (3 + 2 rows per stage): half the
+    // weights per stage, but twice the window DMA and stages; AlexNet conv2
+    // forward 755 TF against 878 for configuration 4 (forced runs only)
+    {8, 5, 5, 3, 8, 1, 4, 8},
 };
 
 // weight (+ bias block) bytes of one stage
 int hc_nbytes_w(const HcCand& k) {
-  const int T = k.KH * k.KW, TP = 2 * ((T + 1) / 2) + 1;
+  const int T = k.KHS * k.KW, TP = 2 * ((T + 1) / 2) + 1;
   const int BN = k.WN * k.NJW * 16;
-  return (BN * TP * 32 + 1023) / 1024 * 1024 + (k.NJW <= 4 ? 0 : 1024);
+  return (BN * TP * 32 + 1023) / 1024 * 1024 + (k.NJW <= 3 ? 0 : 1024);
 }
 
 HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
@@ -545,7 +586,7 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
       const int rc = OH - oh0 + KH - 1;
       const int j = n1 - n0;
       const int row = j == 0 ? oh1 - oh0 : rc + (j - 1) * g.HPd + oh1;
-      wr = std::max(wr, row + KH);
+      wr = std::max(wr, row + k.KHS);   // the first kh group's rows
     }
     if (wr >= 1024) continue;
     g.WIN = (wr * g.Wp * 32 + 1023) / 1024 * 1024;
@@ -566,13 +607,13 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   return p;
 }
 
-template <int KH, int KW, int WM, int WN, int NJW, int ABL = 0,
+template <int KH, int KW, int KHS, int WM, int WN, int NJW, int ABL = 0,
           int NBW = kNBW>
 hipError_t go_hc(const HcPlan& p, const void* src, const void* wts,
                  const float* bias, void* out, const void* aux, int act,
                  int aux_act, hipStream_t s) {
   if (p.g.WIN / 1024 > 8 * NBW) return hipErrorInvalidValue;
-  auto kern = conv_hc_kernel<KH, KW, WM, WN, NJW, NBW, ABL>;
+  auto kern = conv_hc_kernel<KH, KW, KHS, WM, WN, NJW, NBW, ABL>;
   static bool attr = false;   // once per instantiation, before any capture
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(
@@ -587,18 +628,18 @@ hipError_t go_hc(const HcPlan& p, const void* src, const void* wts,
   return launch_status(s);
 }
 
-template <int KH, int KW, int WM, int WN, int NJW, int NBW = kNBW>
+template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW = kNBW>
 hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
                      const float* bias, void* out, const void* aux, int act,
                      int aux_act, hipStream_t s) {
   switch (g_hc_abl) {
 #define HC_ABL(A) \
-    case A: return go_hc<KH, KW, WM, WN, NJW, A, NBW>(p, src, wts, bias, out, \
-                                                      aux, act, aux_act, s);
+    case A: return go_hc<KH, KW, KHS, WM, WN, NJW, A, NBW>(                    \
+        p, src, wts, bias, out, aux, act, aux_act, s);
     HC_ABL(1) HC_ABL(2) HC_ABL(4) HC_ABL(8) HC_ABL(3) HC_ABL(9)
 #undef HC_ABL
-    default: return go_hc<KH, KW, WM, WN, NJW, 0, NBW>(p, src, wts, bias, out,
-                                                       aux, act, aux_act, s);
+    default: return go_hc<KH, KW, KHS, WM, WN, NJW, 0, NBW>(
+        p, src, wts, bias, out, aux, act, aux_act, s);
   }
 }
 
@@ -606,20 +647,22 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
                      const float* bias, void* out, const void* aux, int act,
                      int aux_act, hipStream_t s) {
   switch (p.var) {
-    case 1: return go_hc<3, 3, 4, 2, 4>(p, src, wts, bias, out, aux, act,
-                                        aux_act, s);
-    case 2: return go_hc<3, 3, 4, 2, 3>(p, src, wts, bias, out, aux, act,
-                                        aux_act, s);
-    case 3: return go_hc<3, 3, 8, 1, 4>(p, src, wts, bias, out, aux, act,
-                                        aux_act, s);
-    case 4: return go_hc<5, 5, 4, 2, 2>(p, src, wts, bias, out, aux, act,
-                                        aux_act, s);
-    case 5: return go_hc_abl<5, 5, 8, 1, 3>(p, src, wts, bias, out, aux,
-                                            act, aux_act, s);
-    case 6: return go_hc_abl<3, 3, 8, 1, 8, 5>(p, src, wts, bias, out, aux,
-                                               act, aux_act, s);
-    case 7: return go_hc<3, 3, 8, 1, 6, 0, 5>(p, src, wts, bias, out, aux,
-                                              act, aux_act, s);
+#define HC_GO(V, ...) \
+    case V: return go_hc<__VA_ARGS__>(p, src, wts, bias, out, aux, act, \
+                                      aux_act, s);
+#define HC_GO_ABL(V, ...) \
+    case V: return go_hc_abl<__VA_ARGS__>(p, src, wts, bias, out, aux, act, \
+                                          aux_act, s);
+    HC_GO(1, 3, 3, 3, 4, 2, 4)
+    HC_GO(2, 3, 3, 3, 4, 2, 3)
+    HC_GO(3, 3, 3, 3, 8, 1, 4)
+    HC_GO(4, 5, 5, 5, 4, 2, 2)
+    HC_GO_ABL(5, 5, 5, 5, 8, 1, 3)
+    HC_GO_ABL(6, 3, 3, 3, 8, 1, 8, 5)
+    HC_GO(7, 3, 3, 3, 8, 1, 6, 0, 5)
+    HC_GO(8, 5, 5, 3, 8, 1, 4)
+#undef HC_GO
+#undef HC_GO_ABL
     default: return hipErrorInvalidValue;
   }
 }

@@ -116,6 +116,22 @@ def test_conv_hc_taken_and_forced_variants():
                 ref = y
             else:
                 _close(y, ref, 4e-3)
+        # AlexNet conv2 on the 5 x 5 tiles with and without the kh split
+        x2 = _r(3, 27, 27, 96, scale=1.0, seed=3)
+        w2 = _r(256, 5, 5, 48, scale=0.1, seed=4)
+        outs = []
+        for var in (4, 8):
+            lib.hvk_hc_variant(var)
+            y = torch.empty(3, 27, 27, 256, dtype=torch.bfloat16,
+                            device="cuda")
+            rc = lib.hvk_conv_fwd_hc(
+                x2.data_ptr(), w2.data_ptr(), None, y.data_ptr(), 3, 27, 27,
+                96, 256, 5, 5, 2, 2, 27, 27, 2, 0,
+                torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, var
+            outs.append(y)
+        torch.cuda.synchronize()
+        _close(outs[1], outs[0], 4e-3)
         # the automatic policy leaves the 13-wide AlexNet layers to the GEMM
         lib.hvk_hc_variant(-2)
         rc = lib.hvk_conv_fwd_hc(
