@@ -85,9 +85,11 @@ struct HcGeom {
 // half the weights per stage, so a 512 x 64 tile fits two stages); WM x WN
 // = 8 waves, each 64 pixels x NJW * 16 channels; NBW: window DMA pieces per
 // wave (upper bound, the plan checks).
-// ABL: diagnostic instantiations only (wrong results by design; compile-time
-// so that the production loop carries no test): 1 no DMA after the first
-// stage, 2 no epilogue stores, 4 no MFMAs, 8 no stage wait / barrier
+// ABL: diagnostic instantiations (compile-time so that the production loop
+// carries no test): 1 no DMA after the first stage, 2 no epilogue stores,
+// 4 no MFMAs, 8 no stage wait / barrier (wrong results by design); 16 / 32
+// the DMA spread over the first third of the k-steps / issued at once
+// (correct, for A/B runs)
 template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW,
           int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
@@ -333,7 +335,12 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   auto kloop = [&](auto hc, uint32_t nxt) __attribute__((always_inline)) {
     constexpr int H = decltype(hc)::value;
     constexpr int NKSH = H ? NKS1 : NKS0, TPH = H ? TP1 : TP0;
-    constexpr int NKSD = NKSH > 2 ? (2 * NKSH + 2) / 3 : NKSH;
+    // the k-steps the next stage's DMA is spread over: the first ~2/3
+    // (ABL 16: the first third, 32: all of it at the first k-step)
+    constexpr int NKSD = (ABL & 32)   ? 1
+                         : (ABL & 16) ? (NKSH + 2) / 3
+                         : NKSH > 2   ? (2 * NKSH + 2) / 3
+                                      : NKSH;
     const uint32_t wb = cur + (uint32_t)g.WIN +
                         (uint32_t)(((wn * NJW) * 16 + fr) * (TPH * 32) +
                                    fq * 16);
@@ -636,7 +643,8 @@ hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
 #define HC_ABL(A) \
     case A: return go_hc<KH, KW, KHS, WM, WN, NJW, A, NBW>(                    \
         p, src, wts, bias, out, aux, act, aux_act, s);
-    HC_ABL(1) HC_ABL(2) HC_ABL(4) HC_ABL(8) HC_ABL(3) HC_ABL(9)
+    HC_ABL(1) HC_ABL(2) HC_ABL(4) HC_ABL(8) HC_ABL(3) HC_ABL(9) HC_ABL(16)
+    HC_ABL(32)
 #undef HC_ABL
     default: return go_hc<KH, KW, KHS, WM, WN, NJW, 0, NBW>(
         p, src, wts, bias, out, aux, act, aux_act, s);

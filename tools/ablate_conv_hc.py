@@ -4,7 +4,10 @@ stores, 4 no MFMAs, 8 no stage wait / barrier; wrong results by design)
 against the production kernel, interleaved in one process, on AlexNet
 conv3 forward (configuration 6) and conv2 backward-data (configuration 5).
 
-    python tools/ablate_conv_hc.py [batch] [rounds]"""
+    python tools/ablate_conv_hc.py [batch] [rounds] [ablations, e.g. 0,16,32]
+
+16 / 32 are correct variants (the next stage's DMA over the first third of
+the k-steps / all at the first), not ablations."""
 import statistics
 import sys
 
@@ -25,7 +28,8 @@ def main():
     ops.set_conv_hc(True, -1)
     cases = [("conv3_fwd v6", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
              ("conv2_dgrad v5", ("dgrad", B, 27, 27, 96, 256, 5, 1, 2, 2))]
-    abls = [0, 1, 2, 4, 8, 3, 9]
+    abls = [int(a) for a in sys.argv[3].split(",")] \
+        if len(sys.argv) > 3 else [0, 1, 2, 4, 8, 3, 9]
     try:
         for name, shp in cases:
             fl, fn = case(*shp)
