@@ -88,8 +88,8 @@ struct HcGeom {
 // ABL: diagnostic instantiations (compile-time so that the production loop
 // carries no test): 1 no DMA after the first stage, 2 no epilogue stores,
 // 4 no MFMAs, 8 no stage wait / barrier (wrong results by design); 16 / 32
-// the DMA spread over the first third of the k-steps / issued at once
-// (correct, for A/B runs)
+// the DMA spread over the first third of the k-steps / issued at once, 64
+// no software pipelining of the fragment reads (correct, for A/B runs)
 template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW,
           int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
@@ -344,9 +344,12 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
     const uint32_t wb = cur + (uint32_t)g.WIN +
                         (uint32_t)(((wn * NJW) * 16 + fr) * (TPH * 32) +
                                    fq * 16);
-#pragma unroll
-    for (int s = 0; s < NKSH; ++s) {
-      bf16x8 a[MI], b[NJW];
+    // narrow tiles: the fragments of k-step s + 1 are read before the MFMAs
+    // of k-step s are issued (the compiler otherwise places every read next
+    // to its MFMAs and waits out the LDS latency each k-step); wide tiles
+    // have no registers for a second set
+    constexpr bool SP = MI * NJW <= 16 && NH == 1 && (ABL & 64) == 0;
+    auto rd = [&](int s, bf16x8* a, bf16x8* b) __attribute__((always_inline)) {
       const uint32_t os = H ? ofs1[H ? s : 0] : ofs0[s];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -354,6 +357,9 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 #pragma unroll
       for (int j = 0; j < NJW; ++j)
         b[j] = *(lds_bf16x8*)(sm + wb + j * 16 * (TPH * 32) + s * 64);
+    };
+    auto mfmas = [&](const bf16x8* a, const bf16x8* b)
+                     __attribute__((always_inline)) {
       if constexpr ((ABL & 4) == 0) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
@@ -366,6 +372,8 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
         for (int i = 0; i < MI; ++i)
           acc[i][0][0] += (float)a[i][0] + (float)b[0][0];
       }
+    };
+    auto dma = [&](int s) __attribute__((always_inline)) {
       if constexpr ((ABL & 1) == 0) {
         if (more1) {
 #pragma unroll
@@ -373,11 +381,31 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
             if (k * NKSD / NSLOT == s) issue_slot(k, nxt);
         }
       }
-      // >= 24 accumulator tiles: no reads of the next k-step hoisted above
-      // these MFMAs (double-buffered fragments would not fit the 256
-      // registers of two waves per SIMD; the other wave hides the latency)
-      if constexpr (MI * NJW >= 24 || NH > 1)
+    };
+    if constexpr (SP) {
+      bf16x8 a[2][MI], b[2][NJW];
+      rd(0, a[0], b[0]);
+#pragma unroll
+      for (int s = 0; s < NKSH; ++s) {
+        if (s + 1 < NKSH) rd(s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
         __builtin_amdgcn_sched_barrier(0);
+        mfmas(a[s & 1], b[s & 1]);
+        dma(s);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NKSH; ++s) {
+        bf16x8 a[MI], b[NJW];
+        rd(s, a, b);
+        mfmas(a, b);
+        dma(s);
+        // >= 24 accumulator tiles: no reads of the next k-step hoisted above
+        // these MFMAs (double-buffered fragments would not fit the 256
+        // registers of two waves per SIMD; the other wave hides the latency)
+        if constexpr (MI * NJW >= 24 || NH > 1)
+          __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   for (;;) {
@@ -644,7 +672,7 @@ hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
     case A: return go_hc<KH, KW, KHS, WM, WN, NJW, A, NBW>(                    \
         p, src, wts, bias, out, aux, act, aux_act, s);
     HC_ABL(1) HC_ABL(2) HC_ABL(4) HC_ABL(8) HC_ABL(3) HC_ABL(9) HC_ABL(16)
-    HC_ABL(32)
+    HC_ABL(32) HC_ABL(64)
 #undef HC_ABL
     default: return go_hc<KH, KW, KHS, WM, WN, NJW, 0, NBW>(
         p, src, wts, bias, out, aux, act, aux_act, s);
