@@ -348,7 +348,7 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
     // of k-step s are issued (the compiler otherwise places every read next
     // to its MFMAs and waits out the LDS latency each k-step); wide tiles
     // have no registers for a second set
-    constexpr bool SP = MI * NJW <= 16 && NH == 1 && (ABL & 64) == 0;
+    constexpr bool SP = MI * NJW <= 24 && NH == 1 && (ABL & 64) == 0;
     auto rd = [&](int s, bf16x8* a, bf16x8* b) __attribute__((always_inline)) {
       const uint32_t os = H ? ofs1[H ? s : 0] : ofs0[s];
 #pragma unroll
