@@ -206,6 +206,30 @@ def test_single_rank_overlapped_update_matches_serial(graphs):
     assert torch.equal(st.lp, st.master.to(st.lp.dtype))
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_wgrad_side_stream_matches_serial(graphs, monkeypatch):
+    """Conv weight gradients on a branch stream (engine.wgrad_stream): they
+    run under the backward-data / LRN / pooling kernels below them, eagerly
+    and inside the captured backward, and the update waits for the stream.
+    Same trajectory as the serial step."""
+    steps = 12
+    monkeypatch.setenv("VELES_AMD_WGRAD_STREAM", "0")
+    ser = _train(graphs, steps, overlap=False)
+    monkeypatch.setenv("VELES_AMD_WGRAD_STREAM", "1")
+    side = _train(graphs, steps, overlap=False)
+    assert side.param_store_.grad_streams and \
+        not ser.param_store_.grad_streams
+    if graphs:
+        assert side.graph_segments_[1].failures == 0
+        assert side.graph_segments_[1].replays > 0
+    assert side.param_store_.steps == ser.param_store_.steps == steps
+    assert _rel(side.param_store_.master, ser.param_store_.master) < 2e-2
+    he, hs = ser.decision.history, side.decision.history
+    for a, b in zip(he, hs):
+        assert abs(a["validation_loss"] - b["validation_loss"]) < \
+            0.05 * abs(a["validation_loss"]) + 1e-3
+
+
 def _solo_run(out, solo, steps, port):
     import os
     import numpy

@@ -75,15 +75,26 @@ class GradientDescentConv(GradientDescentBase):
                     tuple(self.dy8_.shape) != tuple(err.shape):
                 self.dy8_ = fp8.quantize(err, self.fp8_sdy_, out=self.dy8_)
             self.dy8_fresh_ = False
-        if use8 and self._fp8_wgrad_ok(fwd, x):
-            fp8.conv_wgrad(fwd.x8_, fwd.fp8_sx_, self.dy8_, self.fp8_sdy_,
-                           pw.grad, fwd.sliding, fwd.padding, fwd.grouping,
-                           dbias=None if pb is None else pb.grad)
+        def wgrad():
+            if use8 and self._fp8_wgrad_ok(fwd, x):
+                fp8.conv_wgrad(fwd.x8_, fwd.fp8_sx_, self.dy8_,
+                               self.fp8_sdy_, pw.grad, fwd.sliding,
+                               fwd.padding, fwd.grouping,
+                               dbias=None if pb is None else pb.grad)
+            else:
+                # weight AND bias gradients from one implicit-GEMM launch
+                ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,
+                               fwd.grouping, col=getattr(fwd, "col_", None),
+                               dbias=None if pb is None else pb.grad)
+
+        if self._wgrad_on_side(err):
+            # the weight gradient on a branch stream: it runs under this
+            # layer's backward-data and the layers below it (LRN / pooling
+            # backward, the next backward-data) instead of before them;
+            # the parameter store's consumers wait for the stream
+            _side_stream_run(self, wgrad)
         else:
-            # weight AND bias gradients from one implicit-GEMM launch
-            ops.conv_wgrad(x, err, pw.grad, fwd.sliding, fwd.padding,
-                           fwd.grouping, col=getattr(fwd, "col_", None),
-                           dbias=None if pb is None else pb.grad)
+            wgrad()
         if self.need_err_input:
             ei = self.alloc_err_input(tuple(x.shape))
             aux, aux_act = self.aux_tensor()
@@ -110,6 +121,22 @@ class GradientDescentConv(GradientDescentBase):
         self.report_gradients()
 
 
+    def _wgrad_on_side(self, err):
+        """Weight gradient off the compute stream (engine.wgrad_stream /
+        VELES_AMD_WGRAD_STREAM, on by default: AlexNet b2048 172.7-173.6k
+        -> 175.0-175.3k img/s on one box, profiles/r5/bench_wgrad_stream_ab.md).
+        Multi-rank, the bucket collective of a layer waits for it (it is
+        launched from the compute stream after the layer's backward-data),
+        so there it overlaps that backward-data only."""
+        import os
+        from veles_amd.utils.config import root, get
+        if not err.is_cuda or os.environ.get(
+                "VELES_AMD_WGRAD_STREAM",
+                "1" if get(root.common.engine.wgrad_stream, True)
+                else "0") == "0":
+            return False
+        return self.store_ is not None
+
     @staticmethod
     def _fp8_wgrad_ok(fwd, x):
         """the fp8 weight gradient needs the forward's e4m3 input copy of
@@ -135,6 +162,25 @@ class GDStrictRELUConv(GradientDescentConv):
 
 class GDSigmoidConv(GradientDescentConv):
     MAPPING = "conv_sigmoid"
+
+
+def _side_stream_run(unit, fn):
+    """Run fn on a branch stream forked from the current one (units.
+    _Branches: its scratch buffers are the branch's own, and the scheduler
+    / HIP-graph capture joins it at the end); the stream is registered with
+    the unit's parameter store so that the update waits for it."""
+    import torch
+    from veles_amd.units import _Branches
+    (br,) = _Branches.fork(torch.cuda.current_stream().device, 1)
+    st = br[0]
+    unit.store_.grad_streams[id(st)] = st
+    prev = _Branches._tls.__dict__.get("br")
+    _Branches._tls.br = br
+    try:
+        with torch.cuda.stream(st):
+            fn()
+    finally:
+        _Branches._tls.br = prev
 
 
 def fp8_grad_consumer(unit):
