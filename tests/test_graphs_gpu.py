@@ -217,8 +217,8 @@ def test_wgrad_side_stream_matches_serial(graphs, monkeypatch):
     ser = _train(graphs, steps, overlap=False)
     monkeypatch.setenv("VELES_AMD_WGRAD_STREAM", "1")
     side = _train(graphs, steps, overlap=False)
-    assert side.param_store_.grad_streams and \
-        not ser.param_store_.grad_streams
+    assert side.param_store_.branch_grads and \
+        not ser.param_store_.branch_grads
     if graphs:
         assert side.graph_segments_[1].failures == 0
         assert side.graph_segments_[1].replays > 0

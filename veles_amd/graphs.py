@@ -187,9 +187,9 @@ class _HipCapture(object):
             ctx.__exit__(None, None, None)
 
     def __exit__(self, *exc):
+        from veles_amd.units import _Branches
         ok = False
         try:
-            from veles_amd.units import _Branches
             _Branches.join_all()   # unjoined branch streams end the capture
             self.graph.capture_end()
             ok = True
@@ -197,6 +197,10 @@ class _HipCapture(object):
             self._leave()
             if not ok:
                 self.retire_stream()
+                # branch streams forked inside the broken capture joined it:
+                # end it on them too (after the origin stream) and fork
+                # fresh ones from now on
+                _Branches.abandon_capture()
         return False
 
     @staticmethod

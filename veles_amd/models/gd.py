@@ -19,6 +19,7 @@ import torch
 from veles_amd.models.nn_units import GradientDescentBase
 from veles_amd import ops
 from veles_amd.ops import fp8
+from veles_amd.models.gd_conv import _side_stream_run, _wgrad_on_side
 
 __all__ = ["GradientDescent", "GDTanh", "GDRELU", "GDStrictRELU",
            "GDSigmoid", "GDSoftmax"]
@@ -51,28 +52,39 @@ class GradientDescent(GradientDescentBase):
         B = err.shape[0]
         e2 = err.reshape(B, -1)
         x = self.input.devmem.reshape(B, -1)
+        tmp = ()
         if x.dtype != e2.dtype:
             x = x.to(e2.dtype)
+            tmp = (x,)
         pw, pb = fwd._pw_, fwd._pb_
         bg = None if pb is None else pb.grad
         # the step's only contribution: write, not read-modify-write
         ow = self.store_.overwrite
         mode = "overwrite" if ow else True
-        if not fwd.weights_transposed and bg is not None and \
-                _bias_colsum() and e2.is_cuda:
-            # grad_b by the column-sum kernel: the ones column costs the
-            # weight-gradient GEMM one more column tile and its buffer-DMA
-            # path (engine.fc_bias_colsum)
-            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode)
-            ops.col_sum(e2, out=bg, accumulate=not ow)
-        elif not fwd.weights_transposed:
-            # grad_W and grad_b (ones column) from one GEMM
-            ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode,
-                     bias_grad=bg)
-        else:
-            ops.gemm(x, e2, trans_a=True, out=pw.grad, accumulate=mode)
-            if bg is not None:
+
+        def wgrad():
+            if not fwd.weights_transposed and bg is not None and \
+                    _bias_colsum() and e2.is_cuda:
+                # grad_b by the column-sum kernel: the ones column costs the
+                # weight-gradient GEMM one more column tile and its
+                # buffer-DMA path (engine.fc_bias_colsum)
+                ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode)
                 ops.col_sum(e2, out=bg, accumulate=not ow)
+            elif not fwd.weights_transposed:
+                # grad_W and grad_b (ones column) from one GEMM
+                ops.gemm(e2, x, trans_a=True, out=pw.grad, accumulate=mode,
+                         bias_grad=bg)
+            else:
+                ops.gemm(x, e2, trans_a=True, out=pw.grad, accumulate=mode)
+                if bg is not None:
+                    ops.col_sum(e2, out=bg, accumulate=not ow)
+
+        if _wgrad_on_side(self, e2):
+            # off the compute stream, under the backward-data chain below
+            # (gd_conv.py)
+            _side_stream_run(self, wgrad, keep=tmp)
+        else:
+            wgrad()
         if self.need_err_input:
             ei = self.alloc_err_input(self.input.devmem.shape)
             aux, aux_act = self.aux_tensor()

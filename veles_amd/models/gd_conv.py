@@ -56,8 +56,10 @@ class GradientDescentConv(GradientDescentBase):
         squeeze = not s2d and x.dim() == 3
         if squeeze:
             x = x.unsqueeze(-1)
+        tmp = ()
         if not s2d and x.dtype != err.dtype:
             x = x.to(err.dtype)
+            tmp = (x,)
         pw, pb = fwd._pw_, fwd._pb_
         if self.store_.overwrite and not all(
                 self.store_.cleared_by_update(p) for p in (pw, pb)
@@ -92,7 +94,7 @@ class GradientDescentConv(GradientDescentBase):
             # layer's backward-data and the layers below it (LRN / pooling
             # backward, the next backward-data) instead of before them;
             # the parameter store's consumers wait for the stream
-            _side_stream_run(self, wgrad)
+            _side_stream_run(self, wgrad, keep=tmp)
         else:
             wgrad()
         if self.need_err_input:
@@ -122,20 +124,7 @@ class GradientDescentConv(GradientDescentBase):
 
 
     def _wgrad_on_side(self, err):
-        """Weight gradient off the compute stream (engine.wgrad_stream /
-        VELES_AMD_WGRAD_STREAM, on by default: AlexNet b2048 172.7-173.6k
-        -> 175.0-175.3k img/s on one box, profiles/r5/bench_wgrad_stream_ab.md).
-        Multi-rank, the bucket collective of a layer waits for it (it is
-        launched from the compute stream after the layer's backward-data),
-        so there it overlaps that backward-data only."""
-        import os
-        from veles_amd.utils.config import root, get
-        if not err.is_cuda or os.environ.get(
-                "VELES_AMD_WGRAD_STREAM",
-                "1" if get(root.common.engine.wgrad_stream, True)
-                else "0") == "0":
-            return False
-        return self.store_ is not None
+        return _wgrad_on_side(self, err)
 
     @staticmethod
     def _fp8_wgrad_ok(fwd, x):
@@ -164,16 +153,39 @@ class GDSigmoidConv(GradientDescentConv):
     MAPPING = "conv_sigmoid"
 
 
-def _side_stream_run(unit, fn):
+def _wgrad_on_side(unit, err):
+    """Weight gradients (conv and fully-connected GD units) off the compute
+    stream (engine.wgrad_stream / VELES_AMD_WGRAD_STREAM, on by default:
+    AlexNet b2048 172.7-173.6k -> 175.0-175.3k img/s on one box with the
+    conv ones, profiles/r5/bench_wgrad_stream_ab.md).  Multi-rank, a
+    layer's bucket collective waits for it (it is launched from the compute
+    stream after the layer's backward-data), so there it overlaps that
+    backward-data only."""
+    import os
+    from veles_amd.utils.config import root, get
+    if not err.is_cuda or os.environ.get(
+            "VELES_AMD_WGRAD_STREAM",
+            "1" if get(root.common.engine.wgrad_stream, True) else "0") == "0":
+        return False
+    return getattr(unit, "store_", None) is not None
+
+
+def _side_stream_run(unit, fn, keep=()):
     """Run fn on a branch stream forked from the current one (units.
     _Branches: its scratch buffers are the branch's own, and the scheduler
-    / HIP-graph capture joins it at the end); the stream is registered with
-    the unit's parameter store so that the update waits for it."""
+    / HIP-graph capture joins it at the end); the unit's parameter store is
+    told, so that the update waits for the device's branch streams.
+    ``keep``:
+    temporaries made on the compute stream that fn reads (their memory
+    must not be reused before the branch is done with it)."""
     import torch
     from veles_amd.units import _Branches
     (br,) = _Branches.fork(torch.cuda.current_stream().device, 1)
     st = br[0]
-    unit.store_.grad_streams[id(st)] = st
+    unit.store_.branch_grads = True
+    for t in keep:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            t.record_stream(st)
     prev = _Branches._tls.__dict__.get("br")
     _Branches._tls.br = br
     try:

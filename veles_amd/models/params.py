@@ -88,10 +88,10 @@ class ParameterStore(object):
         self._overlap = None
         self._single = None   # single-rank overlapped update (decided once)
         self._upd_stream = None
-        # side streams that write gradients (conv weight gradients off the
-        # compute stream, gd_conv.py): everything that consumes the gradient
-        # buffer waits for them too
-        self.grad_streams = {}
+        # gradients are written on branch streams too (weight gradients off
+        # the compute stream, gd_conv.py): everything that consumes the
+        # gradient buffer then waits for the device's branch streams
+        self.branch_grads = False
         self._bucket_tables = {}
         # workgroups of a side-stream bucket update (0: the full grid); one
         # per CU measured best (profiles/dp_overlap_update_r2.md)
@@ -304,15 +304,23 @@ class ParameterStore(object):
             if all(id(p) in self._ready for p in b):
                 self._launch_bucket(i)
 
+    def _grad_streams(self):
+        """The device's branch streams (units._Branches: a capture that
+        failed replaces them, so they are looked up, not remembered)."""
+        if not self.branch_grads:
+            return []
+        from veles_amd.units import _Branches
+        return _Branches.streams(self.master.device)
+
     def _launch_bucket(self, i):
         self._launched.add(i)
-        if self.grad_streams and self.master is not None and \
+        if self.branch_grads and self.master is not None and \
                 self.master.is_cuda:
             # the collective (launched from the compute stream) must see the
             # weight gradients written on the branch streams
             import torch
             cur = torch.cuda.current_stream(self.master.device)
-            for st in self.grad_streams.values():
+            for st in self._grad_streams():
                 cur.wait_stream(st)
         if self._tl is not None:
             self._tl[1][i] = self._event()
@@ -486,7 +494,7 @@ class ParameterStore(object):
             # bucket's GD kernels); joined back in apply()
             self._upd_stream.wait_stream(
                 torch.cuda.current_stream(self.master.device))
-            for st in self.grad_streams.values():
+            for st in self._grad_streams():
                 self._upd_stream.wait_stream(st)
         # the side stream waits for this bucket's collective (which itself
         # waited for the compute stream at launch); its writes to the bf16
@@ -539,12 +547,12 @@ class ParameterStore(object):
         """Wait for the gradient all-reduces, then one fused SGD update."""
         from veles_amd import ops
         self._accum_count += 1
-        if self.grad_streams and self.master is not None and \
+        if self.branch_grads and self.master is not None and \
                 self.master.is_cuda:
             # the gradients written off the compute stream are complete
             import torch
             cur = torch.cuda.current_stream(self.master.device)
-            for st in self.grad_streams.values():
+            for st in self._grad_streams():
                 cur.wait_stream(st)
         if self._accum_count < self.accumulate:
             self._ready.clear()

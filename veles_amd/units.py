@@ -144,6 +144,7 @@ class _Branches(object):
     A branch context is (stream, enclosing context, fork stream)."""
     _tls = threading.local()
     _pools = {}
+    _abandoned = []
     PER_FORK = 4
 
     @classmethod
@@ -167,7 +168,13 @@ class _Branches(object):
         d = cls.depth(parent)
         need = (d + 1) * cls.PER_FORK
         while len(pool) < need:
-            pool.append(torch.cuda.Stream(device))
+            # the kernel library's own streams, not torch's round-robin pool:
+            # a stream that a failed capture leaves in the invalidated state
+            # must never come back as some other "new" stream
+            # (graphs._capture_stream, abandon_capture)
+            from veles_amd.graphs import _capture_stream
+            with torch.cuda.device(device):
+                pool.append(_capture_stream())
         out = []
         forked = cls._forked()
         for i in range(n):
@@ -183,6 +190,30 @@ class _Branches(object):
         if f is None:
             f = cls._tls.forked = {}
         return f
+
+    @classmethod
+    def streams(cls, device):
+        """The branch streams of the device's pool (forked so far)."""
+        return list(cls._pools.get(str(device), ()))
+
+    @classmethod
+    def abandon_capture(cls):
+        """After a HIP-graph capture that failed: the branch streams forked
+        inside it joined the (invalidated) capture.  End it on every pooled
+        branch stream and start new pools, so that no later fork hands out a
+        stream still in that state (graphs._HipCapture)."""
+        cls._tls.forked = {}
+        pools, cls._pools = cls._pools, {}
+        cls._abandoned.extend(pools.values())   # never handed out again
+        try:
+            from veles_amd.ops import _lib
+            if not _lib.available():
+                return
+            for pool in pools.values():
+                for st in pool:
+                    _lib.lib().hvk_end_stream_capture(st.cuda_stream)
+        except Exception:  # noqa: BLE001 - best effort on an error path
+            pass
 
     @classmethod
     def join_all(cls):
