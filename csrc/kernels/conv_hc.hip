@@ -582,15 +582,13 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   if (g_hc_variant == 0) return p;
   const int CG = C / groups, OCg = OCT / groups;
   if (CG % 16 || OCg % 16 || OCT % 4) return p;
-  // automatic: the shapes measured faster than the T4 / 256x256 / 128-row
-  // implicit GEMM in one process (profiles/r5/ab_conv_hc_*.log): 5 x 5
-  // (AlexNet conv2 1.03-1.08x forward, 1.37x backward-data), narrow-source
-  // forwards (conv1 through space-to-depth 1.14x, VGG conv1_2 1.06x) and
-  // the 56-wide 256-channel layers (VGG conv3_x 1.07x both ways).  The
-  // 13-wide AlexNet conv3-5, VGG conv2_2 / conv4_2 and conv1_2
-  // backward-data run at parity or below and stay on the GEMM
-  if (g_hc_variant == -2 &&
-      !(KH == 5 || (!flip && CG <= 64) || (OW >= 56 && CG >= 256)))
+  // automatic: every shape except the ones measured slower than the T4 /
+  // 256x256 / 128-row implicit GEMM in one process
+  // (profiles/r5/ab_conv_hc_alexnet_vgg_r5o.log): AlexNet conv1 1.16x,
+  // conv2 1.12x / 1.45x (forward / backward-data), conv3-5 1.02-1.05x, VGG
+  // conv1_2 forward 1.08x, conv3_2 1.06-1.07x, conv4_2 1.00-1.02x; left to
+  // the GEMM: VGG conv1_2 backward-data (0.99x) and conv2_2 (0.95x)
+  if (g_hc_variant == -2 && ((flip && CG <= 64) || (OW >= 100 && CG >= 128)))
     return p;
   if ((long long)N * H * W * C * 2 >= kBufMaxBytes) return p;
   if ((long long)N * OH * OW * OCT * 2 >= kBufMaxBytes) return p;

@@ -132,11 +132,21 @@ def test_conv_hc_taken_and_forced_variants():
             outs.append(y)
         torch.cuda.synchronize()
         _close(outs[1], outs[0], 4e-3)
-        # the automatic policy leaves the 13-wide AlexNet layers to the GEMM
+        # the automatic policy takes AlexNet conv4 and leaves VGG conv2_2
+        # (measured slower) to the GEMM
         lib.hvk_hc_variant(-2)
         rc = lib.hvk_conv_fwd_hc(
             x.data_ptr(), w.data_ptr(), None, ref.data_ptr(), 3, 13, 13, 384,
             384, 3, 3, 1, 1, 13, 13, 2, 0,
+            torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        xv = _r(1, 112, 112, 128, scale=1.0, seed=5)
+        wv = _r(128, 3, 3, 128, scale=0.1, seed=6)
+        yv = torch.empty(1, 112, 112, 128, dtype=torch.bfloat16,
+                         device="cuda")
+        rc = lib.hvk_conv_fwd_hc(
+            xv.data_ptr(), wv.data_ptr(), None, yv.data_ptr(), 1, 112, 112,
+            128, 128, 3, 3, 1, 1, 112, 112, 1, 0,
             torch.cuda.current_stream().cuda_stream)
         assert rc == -2
         # a configuration for another kernel size is not taken
