@@ -560,7 +560,8 @@ constexpr HcCand kHcCands[] = {
     {1, 3, 3, 3, 4, 2, 4, 8},   // 256 px x 128 ch
     {2, 3, 3, 3, 4, 2, 3, 8},   // 256 px x 96 ch
     {3, 3, 3, 3, 8, 1, 4, 8},   // 512 px x 64 ch: VGG-16 64-channel layers
-    {4, 5, 5, 5, 4, 2, 2, 8},   // 256 px x 64 ch: AlexNet conv2 fwd
+    {11, 5, 5, 5, 8, 1, 2, 8},  // 512 px x 32 ch: AlexNet conv2 fwd
+    {4, 5, 5, 5, 4, 2, 2, 8},   // 256 px x 64 ch
     {5, 5, 5, 5, 8, 1, 3, 8},   // 512 px x 48 ch: AlexNet conv2 dgrad
     // 512 px x 64 ch in two kh groups (3 + 2 rows per stage): half the
     // weights per stage, but twice the window DMA and stages; AlexNet conv2
@@ -695,6 +696,7 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
     HC_GO_ABL(6, 3, 3, 3, 8, 1, 8, 5)
     HC_GO(7, 3, 3, 3, 8, 1, 6, 0, 5)
     HC_GO(8, 5, 5, 3, 8, 1, 4)
+    HC_GO(11, 5, 5, 5, 8, 1, 2)
 #undef HC_GO
 #undef HC_GO_ABL
     default: return hipErrorInvalidValue;
