@@ -89,7 +89,8 @@ struct HcGeom {
 // carries no test): 1 no DMA after the first stage, 2 no epilogue stores,
 // 4 no MFMAs, 8 no stage wait / barrier (wrong results by design); 16 / 32
 // the DMA spread over the first third of the k-steps / issued at once, 64
-// no software pipelining of the fragment reads (correct, for A/B runs)
+// no software pipelining of the fragment reads (correct, for A/B runs), 256
+// no weight DMA after the first stage (wrong results)
 template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW,
           int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
@@ -107,9 +108,13 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   constexpr int NKS0 = (T0 + 1) / 2, NKS1 = (T1 + 1) / 2;
   constexpr int TP0 = 2 * NKS0 + 1, TP1 = 2 * NKS1 + 1;
   constexpr int NWV = WM * WN;
+  // eight waves (two per SIMD).  Four waves of 128 pixels (one per SIMD,
+  // 512 registers, the accumulators in the AGPR half) measured 0.25-0.79x:
+  // profiles/r5/ab_conv_hc_one_wave_per_simd_r5q.log
   static_assert(NWV == 8, "eight waves");
   constexpr int MI = 4;                      // 64 pixels per wave
-  constexpr int TPX = WM * 64;
+  constexpr int WPX = MI * 16;
+  constexpr int TPX = WM * WPX;
   constexpr int BN = WN * NJW * 16;
   constexpr int WB = BN * TP0 * 32;          // weight bytes per stage
   constexpr int NWP = (WB + 1023) / 1024;    // weight DMA pieces (at most)
@@ -118,6 +123,8 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   // accumulators of NG consecutive n-tiles are 4 * NG consecutive output
   // channels (16- or 24-B stores, 16 * NG channels per pixel and group of 4
   // lanes; 128 B for NG 4) instead of 8-B pieces of 16-channel tiles
+  // (two n-tiles per group for NJW 6 - 16-B stores - spilled inside the
+  // k-loop and measured 10-12 % slower: profiles/r5/ablate_conv_hc_r5q.log)
   constexpr int NG = NJW % 4 == 0 ? 4 : NJW % 3 == 0 ? 3 : NJW % 2 == 0 ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   lds_u8* sm = (lds_u8*)smem;
@@ -250,6 +257,9 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
         dma16(rs, smem + stb + (w + NWV * q) * 1024,
               pwb[q] >= kBufOOB ? kBufOOB : pwb[q] + d_cofs);
     } else if (q < NBW + NWW) {
+      if constexpr ((ABL & 256) != 0) {
+        if (stb != 0 || d_cofs != 0) return;
+      }
       const int i = q - NBW;
       if (w + NWV * i < NWP) {   // wave-uniform
         const uint32_t o =
@@ -275,7 +285,7 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
     const int rc = g.OH - (int)oh0 + KH - 1;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      const uint32_t p = p0 + wm * 64 + i * 16 + fr;
+      const uint32_t p = p0 + wm * WPX + i * 16 + fr;
       if (p >= (uint32_t)g.P) {   // past the last pixel: slot 0 (finite)
         bb[i] = 0;
         continue;
@@ -428,7 +438,7 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 #pragma unroll
           for (int i = 0; i < MI; ++i) {
             const uint32_t p =
-                min(p0 + wm * 64 + i * 16 + fr, (uint32_t)g.P - 1);
+                min(p0 + wm * WPX + i * 16 + fr, (uint32_t)g.P - 1);
 #pragma unroll
             for (int j = 0; j < NJW; ++j)
               apre[i][j] = *(const uint2*)(aux + (long long)p * g.OCT + chb +
@@ -457,7 +467,7 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
       // Buffer stores: pixels past the end go to the out-of-range offset
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const uint32_t p = p0 + wm * 64 + i * 16 + fr;
+        const uint32_t p = p0 + wm * WPX + i * 16 + fr;
         const uint32_t pa = min(p, (uint32_t)g.P - 1);
         const bool ok = p < (uint32_t)g.P &&
                         !((ABL & 2) && acc[i][0][0] != 1234.5f);
@@ -549,7 +559,7 @@ constexpr int kNBW = 8;   // window pieces per wave: 64 KiB windows at most
 // -2 automatic on the shapes where it beats the implicit-GEMM kernels, -1 on
 // every shape it supports, 0 off, > 0 one forced configuration
 int g_hc_variant = -2;
-int g_hc_abl = 0;         // diagnostic instantiation (configurations 5, 6)
+int g_hc_abl = 0;         // diagnostic instantiation (configurations 5-7)
 
 struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW; };
 // per kernel size, in order of preference (the first whose n-tile divides
@@ -624,7 +634,7 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
     }
     if (wr >= 1024) continue;
     g.WIN = (wr * g.Wp * 32 + 1023) / 1024 * 1024;
-    if (g.WIN / 1024 > 8 * k.NBW) continue;
+    if (g.WIN / 1024 > k.WM * k.WN * k.NBW) continue;
     const size_t lds = 2 * (size_t)(g.WIN + hc_nbytes_w(k));
     if (lds > 160 * 1024) continue;
     g.NT = OCg / BN;
@@ -646,7 +656,7 @@ template <int KH, int KW, int KHS, int WM, int WN, int NJW, int ABL = 0,
 hipError_t go_hc(const HcPlan& p, const void* src, const void* wts,
                  const float* bias, void* out, const void* aux, int act,
                  int aux_act, hipStream_t s) {
-  if (p.g.WIN / 1024 > 8 * NBW) return hipErrorInvalidValue;
+  if (p.g.WIN / 1024 > WM * WN * NBW) return hipErrorInvalidValue;
   auto kern = conv_hc_kernel<KH, KW, KHS, WM, WN, NJW, NBW, ABL>;
   static bool attr = false;   // once per instantiation, before any capture
   if (!attr) {
@@ -671,7 +681,7 @@ hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
     case A: return go_hc<KH, KW, KHS, WM, WN, NJW, A, NBW>(                    \
         p, src, wts, bias, out, aux, act, aux_act, s);
     HC_ABL(1) HC_ABL(2) HC_ABL(4) HC_ABL(8) HC_ABL(3) HC_ABL(9) HC_ABL(16)
-    HC_ABL(32) HC_ABL(64)
+    HC_ABL(32) HC_ABL(64) HC_ABL(256)
 #undef HC_ABL
     default: return go_hc<KH, KW, KHS, WM, WN, NJW, 0, NBW>(
         p, src, wts, bias, out, aux, act, aux_act, s);
@@ -694,7 +704,7 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
     HC_GO(4, 5, 5, 5, 4, 2, 2)
     HC_GO_ABL(5, 5, 5, 5, 8, 1, 3)
     HC_GO_ABL(6, 3, 3, 3, 8, 1, 8, 5)
-    HC_GO(7, 3, 3, 3, 8, 1, 6, 0, 5)
+    HC_GO_ABL(7, 3, 3, 3, 8, 1, 6, 5)
     HC_GO(8, 5, 5, 3, 8, 1, 4)
     HC_GO(11, 5, 5, 5, 8, 1, 2)
 #undef HC_GO
@@ -708,7 +718,7 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
 // -2 automatic (the measured winners), -1 every supported shape, 0 off,
 // > 0 one forced configuration (kHcCands var).
 HVK_API void hvk_hc_variant(int v) { g_hc_variant = v; }
-// Diagnostic ablation builds of configurations 5 and 6 (see conv_hc_kernel's
+// Diagnostic ablation builds of configurations 5, 6 and 7 (see conv_hc_kernel's
 // ABL); 0 = the production kernel.
 HVK_API void hvk_hc_ablation(int a) { g_hc_abl = a; }
 

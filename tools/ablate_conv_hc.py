@@ -2,7 +2,8 @@
 diagnostic instantiations (hvk_hc_ablation: 1 no DMA, 2 no epilogue
 stores, 4 no MFMAs, 8 no stage wait / barrier; wrong results by design)
 against the production kernel, interleaved in one process, on AlexNet
-conv3 forward (configuration 6) and conv2 backward-data (configuration 5).
+conv1 forward (s2d, configuration 7), conv3 forward (configuration 6) and
+conv2 backward-data (configuration 5).
 
     python tools/ablate_conv_hc.py [batch] [rounds] [ablations, e.g. 0,16,32]
 
@@ -26,7 +27,10 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     lib = _lib.lib()
     ops.set_conv_hc(True, -1)
-    cases = [("conv3_fwd v6", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
+    cases = [("conv1_fwd v7", ("fwd", B, 227, 227, 3, 96, 11, 4, 0, 1)),
+             ("conv4_fwd v7", ("fwd", B, 13, 13, 384, 384, 3, 1, 1, 2)),
+             ("conv5_dgrad v7", ("dgrad", B, 13, 13, 384, 256, 3, 1, 1, 2)),
+             ("conv3_fwd v6", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
              ("conv2_dgrad v5", ("dgrad", B, 27, 27, 96, 256, 5, 1, 2, 2))]
     abls = [int(a) for a in sys.argv[3].split(",")] \
         if len(sys.argv) > 3 else [0, 1, 2, 4, 8, 3, 9]

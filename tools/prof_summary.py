@@ -44,6 +44,17 @@ def main(trace, out, steps=None, title="", window=False):
                      % (k[0], k[1], k[2], k[3], k[4], k[5], c, d / c / 1e6,
                         d / 1e6, ("%.3f" % (d / 1e6 / steps)) if steps
                         else "-", 100.0 * d / tot))
+    if window and steps and len(rows) % steps == 0:
+        # the last timed step in dispatch order (which layer is which kernel)
+        per = len(rows) // steps
+        lines += ["", "## Last timed step in dispatch order", "",
+                  "| # | kernel | grid x | ms |", "|---|---|---|---|"]
+        for i, r in enumerate(rows[-per:]):
+            n = r["Kernel_Name"].replace("void ", "").replace(
+                "(anonymous namespace)::", "").split("(")[0][:90]
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            lines.append("| %d | %s | %s | %.3f |" % (i, n, r["Grid_Size_X"],
+                                                      d / 1e6))
     open(out, "w").write("\n".join(lines) + "\n")
 
 
