@@ -1081,6 +1081,9 @@ void lrn_pool3s2_fwd_walk_kernel(
   static_assert(half >= 1 && half <= 2, "dword halo");
   const int CV = C >> 3;
   const int total = N * S * OW * CV;
+  // 32-bit element offsets (the host checks N H W C < 2^31)
+  const uint32_t WC = (uint32_t)W * C, HWC = (uint32_t)H * WC;
+  const uint32_t lastrow = (uint32_t)(H - 1) * WC;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += gridDim.x * blockDim.x) {
     uint32_t t1, cvu, t2, owu, nu, su;
@@ -1090,10 +1093,13 @@ void lrn_pool3s2_fwd_walk_kernel(
     const int c0 = (int)cvu * 8, w0 = (int)owu * 2;
     const int oh0 = (int)su * R, oh1 = min(OH, oh0 + R);
     const bool has_lo = c0 >= 8, has_hi = c0 + 8 < C;
-    const uint16_t* img = x + (long long)nu * H * W * C;
+    const uint16_t* img = x + nu * HWC;
     const bool c1v = w0 + 1 < W, c2v = w0 + 2 < W;
     const int wc1 = c1v ? w0 + 1 : W - 1, wc2 = c2v ? w0 + 2 : W - 1;
-    auto px = [&](int h, int w) { return img + ((long long)h * W + w) * C; };
+    const uint32_t col[3] = {(uint32_t)w0 * C, (uint32_t)wc1 * C,
+                             (uint32_t)wc2 * C};
+    // pixel (row offset ro, window column j)
+    auto px = [&](uint32_t ro, int j) { return img + ro + col[j]; };
     // column max of a row: value and column (first maximum)
     auto rowmax = [&](float y0, float y1v, float y2v, float& b, int& bi) {
       b = y0;
@@ -1104,10 +1110,10 @@ void lrn_pool3s2_fwd_walk_kernel(
     float cb[8];
     int ci[8];
     {   // the strip's first window row
-      const int h = 2 * oh0;
-      const LrnPx p0 = lrn_ldpx(px(h, w0), c0, has_lo, has_hi);
-      const LrnPx p1 = lrn_ldpx(px(h, wc1), c0, has_lo, has_hi);
-      const LrnPx p2 = lrn_ldpx(px(h, wc2), c0, has_lo, has_hi);
+      const uint32_t ro = 2u * oh0 * WC;
+      const LrnPx p0 = lrn_ldpx(px(ro, 0), c0, has_lo, has_hi);
+      const LrnPx p1 = lrn_ldpx(px(ro, 1), c0, has_lo, has_hi);
+      const LrnPx p2 = lrn_ldpx(px(ro, 2), c0, has_lo, has_hi);
       f32x2v ya[8], yb[8];
       lrn_pair<half>(p0, p1, alpha, beta, k, ya);
       lrn_pair<half>(p2, p2, alpha, beta, k, yb);
@@ -1119,13 +1125,13 @@ void lrn_pool3s2_fwd_walk_kernel(
     // row indexes: always in range, masked by r1v / r2v when used)
     LrnPx a[3], b[3];
     auto load_rows = [&](int oh, LrnPx* ra, LrnPx* rb) {
-      const int hc1 = min(2 * oh + 1, H - 1), hc2 = min(2 * oh + 2, H - 1);
-      ra[0] = lrn_ldpx(px(hc1, w0), c0, has_lo, has_hi);
-      ra[1] = lrn_ldpx(px(hc1, wc1), c0, has_lo, has_hi);
-      ra[2] = lrn_ldpx(px(hc1, wc2), c0, has_lo, has_hi);
-      rb[0] = lrn_ldpx(px(hc2, w0), c0, has_lo, has_hi);
-      rb[1] = lrn_ldpx(px(hc2, wc1), c0, has_lo, has_hi);
-      rb[2] = lrn_ldpx(px(hc2, wc2), c0, has_lo, has_hi);
+      const uint32_t r1 = (uint32_t)(2 * oh + 1) * WC;
+      const uint32_t hc1 = min(r1, lastrow), hc2 = min(r1 + WC, lastrow);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        ra[j] = lrn_ldpx(px(hc1, j), c0, has_lo, has_hi);
+        rb[j] = lrn_ldpx(px(hc2, j), c0, has_lo, has_hi);
+      }
     };
     load_rows(oh0, a, b);
     for (int oh = oh0; oh < oh1; ++oh) {
@@ -1279,8 +1285,13 @@ __device__ __forceinline__ float lane_from_above(float v) {  // lane + 1
       0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
 }
 
-template <int half, bool PRE>
-__global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
+// AM: the fused activation derivative, resolved at compile time (a runtime
+// switch per pixel put a branch ladder between the four pixels of an
+// iteration): 0 none, 1 strict ReLU of x itself (aux == x, the AlexNet
+// conv -> LRN pair), 2 any (runtime aux / aux_act)
+template <int half, bool PRE, int AM = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void lrn_pool3s2_bwd_dpp_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
     const uint8_t* __restrict__ argmax, uint16_t* __restrict__ dx, int N,
     int H, int W, int C, int OH, int OW, float alpha, float beta, float k,
@@ -1294,6 +1305,10 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
   const bool aux_x = aux == x;
   const int nwv = (nblk + bpw - 1) / bpw;
   const int wstride = (gridDim.x * blockDim.x) >> 6;
+  // 32-bit element offsets (the host checks N H W C < 2^31): a handful of
+  // multiplies per iteration instead of a 64-bit chain per load
+  const uint32_t WC = (uint32_t)W * C, OWC = (uint32_t)OW * C;
+  const uint32_t HWC = (uint32_t)H * WC, OHWC = (uint32_t)OH * OWC;
   // the loop bound is wave-uniform: every lane reaches every DPP
   for (int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wv < nwv;
        wv += wstride) {
@@ -1313,26 +1328,34 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
     // window and pixel
     uint4 gvv[4], xr[4];
     uint2 avv[4];
+    // pixel p of the block: row 2 bh + (p >> 1), column 2 bw + (p & 1)
+    // (clamped into the image; 2 bh < H always)
+    const uint32_t xo = nu * HWC + c0;
+    const uint32_t xrow[2] = {2 * bhu * WC, min(2 * bhu + 1, (uint32_t)H - 1) * WC};
+    const uint32_t xcol[2] = {2 * bwu * (uint32_t)C,
+                              min(2 * bwu + 1, (uint32_t)W - 1) * (uint32_t)C};
     if constexpr (PRE) {
+      // windows (bh - 1 + a, bw - 1 + b), clamped
+      const uint32_t yo0 = nu * OHWC + c0;
+      const uint32_t yrow[2] = {(bhu > 0 ? bhu - 1 : 0) * OWC,
+                                min(bhu, (uint32_t)OH - 1) * OWC};
+      const uint32_t ycol[2] = {(bwu > 0 ? bwu - 1 : 0) * (uint32_t)C,
+                                min(bwu, (uint32_t)OW - 1) * (uint32_t)C};
+      const bool rok[2] = {bhu > 0, bhu < (uint32_t)OH};
+      const bool cok[2] = {bwu > 0, bwu < (uint32_t)OW};
 #pragma unroll
       for (int wi = 0; wi < 4; ++wi) {
         const int a = wi >> 1, b = wi & 1;
-        const int oh = (int)bhu - 1 + a, ow = (int)bwu - 1 + b;
-        const bool wv_ok = ok && oh >= 0 && ow >= 0 && oh < OH && ow < OW;
-        const long long yo = (((long long)nu * OH + min(max(oh, 0), OH - 1)) *
-                                  OW + min(max(ow, 0), OW - 1)) * C + c0;
+        const bool wv_ok = ok && rok[a] && cok[b];
+        const uint32_t yo = yo0 + yrow[a] + ycol[b];
         gvv[wi] = *(const uint4*)(dp + yo);
         const uint2 av = *(const uint2*)(argmax + yo);
         // an absent window matches no pixel (index 0xff)
         avv[wi] = wv_ok ? av : make_uint2(0xffffffffu, 0xffffffffu);
       }
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int hp = min((int)bhu * 2 + (p >> 1), H - 1);
-        const int wp = min((int)bwu * 2 + (p & 1), W - 1);
-        xr[p] = *(const uint4*)(x + (((long long)nu * H + hp) * W + wp) * C +
-                                c0);
-      }
+      for (int p = 0; p < 4; ++p)
+        xr[p] = *(const uint4*)(x + xo + xrow[p >> 1] + xcol[p & 1]);
     }
 #pragma unroll
     for (int wi = 0; wi < 4; ++wi) {
@@ -1369,12 +1392,17 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
     for (int p = 0; p < 4; ++p) {
       const int hp = (int)bhu * 2 + (p >> 1), wp = (int)bwu * 2 + (p & 1);
       const bool pv = ok && hp < H && wp < W;
-      const long long po = (((long long)nu * H + hp) * W + wp) * C + c0;
+      // (equal to the clamped offset whenever pv)
+      const uint32_t po = xo + xrow[p >> 1] + xcol[p & 1];
       float xv[8];
       if constexpr (PRE) {
+        // a pixel past the image edge (odd H / W) or of an absent block
+        // reads a clamped in-range pixel: its values reach no valid lane (the
+        // DPP halo stops at block edges, no window selects it) and it is not
+        // stored
         const uint16_t* h8 = (const uint16_t*)&xr[p];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) xv[q] = pv ? bf2f(h8[q]) : 0.f;
+        for (int q = 0; q < 8; ++q) xv[q] = bf2f(h8[q]);
       } else if (pv) {
         load8(x + po, xv);
       } else {
@@ -1391,6 +1419,21 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
       for (int i = 0; i < 4; ++i) {
         X2[i] = f32x2_t{xv[2 * i], xv[2 * i + 1]};
         G2[i] = f32x2_t{g[p][2 * i], g[p][2 * i + 1]};
+      }
+      if constexpr (AM == 1) {
+        // x is the ReLU output (>= 0): dx = 0 where x = 0 is g = 0 there
+        // (that channel's t_j = g x s^(-beta-1) is 0 anyway) - one clamped
+        // product per channel pair, min(max(x 2^126, 0), 1) = [x > 0] for
+        // every normal x, instead of a compare and a select per channel
+        // (the compiler splits a clamped vector product into two scalar
+        // v_max clamps; the packed product's clamp bit does it in one)
+        const f32x2_t BIG = {0x1p126f, 0x1p126f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x2_t m;
+          asm("v_pk_mul_f32 %0, %1, %2 clamp" : "=v"(m) : "v"(X2[i]), "v"(BIG));
+          G2[i] = G2[i] * m;
+        }
       }
       // squares of channels c0 - half .. c0 + 8 + half
       float e[8 + 2 * half];
@@ -1413,16 +1456,23 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
       for (int d = 1; d <= 2 * half; ++d) w[0] += e[d];
 #pragma unroll
       for (int q = 1; q < 8; ++q) w[q] = (w[q - 1] + e[q + 2 * half]) - e[q - 1];
-      const f32x2_t K2 = {k, k}, A2 = {alpha, alpha};
+      // Scaled by c = 2 alpha beta (> 0: the host routes alpha beta = 0 to
+      // the per-thread kernel): S = s / c, E = c s^(-beta-1) (the log2 c
+      // terms fold into one fma), so E S = s^-beta, T = c t_j and
+      // dx = g s^-beta - x sum(T) - no separate product by -2 alpha beta
+      const float cs = 2.f * alpha * beta;
+      const f32x2_t K2 = {k / cs, k / cs}, A2 = {0.5f / beta, 0.5f / beta};
       const f32x2_t NB1 = {-beta - 1.f, -beta - 1.f};
+      const float lc = -beta * __log2f(cs);
+      const f32x2_t LC2 = {lc, lc};
       f32x2_t SB2[4], T2[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const f32x2_t S2 = K2 + A2 * f32x2_t{w[2 * i], w[2 * i + 1]};
-        f32x2_t L2 = f32x2_t{__log2f(S2.x), __log2f(S2.y)} * NB1;
-        const f32x2_t E2 = {ex2(L2.x), ex2(L2.y)};  // s^(-beta-1)
+        const f32x2_t L2 = f32x2_t{__log2f(S2.x), __log2f(S2.y)} * NB1 + LC2;
+        const f32x2_t E2 = {ex2(L2.x), ex2(L2.y)};  // c s^(-beta-1)
         SB2[i] = E2 * S2;                               // s^-beta
-        T2[i] = G2[i] * X2[i] * E2;                     // t_j
+        T2[i] = G2[i] * X2[i] * E2;                     // c t_j
       }
       float tj[8 + 2 * half];
 #pragma unroll
@@ -1444,24 +1494,25 @@ __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_dpp_kernel(
 #pragma unroll
       for (int q = 1; q < 8; ++q)
         acc[q] = (acc[q - 1] + tj[q + 2 * half]) - tj[q - 1];
-      const f32x2_t M2 = {-2.f * alpha * beta, -2.f * alpha * beta};
       float v[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const f32x2_t V2 =
-            G2[i] * SB2[i] + (M2 * X2[i]) * f32x2_t{acc[2 * i], acc[2 * i + 1]};
+            G2[i] * SB2[i] - X2[i] * f32x2_t{acc[2 * i], acc[2 * i + 1]};
         v[2 * i] = V2.x;
         v[2 * i + 1] = V2.y;
       }
-      if (aux && pv) {
-        float av8[8];
-        if (aux_x) {
+      if constexpr (AM == 2) {
+        if (aux && pv) {
+          float av8[8];
+          if (aux_x) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) av8[q] = xv[q];
-        } else {
-          load8(aux + po, av8);
+            for (int q = 0; q < 8; ++q) av8[q] = xv[q];
+          } else {
+            load8(aux + po, av8);
+          }
+          act_bwd_mul8(v, av8, aux_act);
         }
-        act_bwd_mul8(v, av8, aux_act);
       }
       if (pv) *(uint4*)(dx + po) = pack_bf16x8(v);
     }
@@ -1684,21 +1735,23 @@ HVK_API int hvk_lrn_pool_bwd_u8(const void* x, const void* dp,
   const int h = n / 2;
   const int BH = (H + 1) / 2, BW = (W + 1) / 2;
   const long long tb = (long long)N * BH * BW * (C / 8);
-  if (C / 8 <= 64 && h >= 1 && h <= 4) {
+  if (C / 8 <= 64 && h >= 1 && h <= 4 && alpha * beta > 0.f && k > 0.f) {
     // whole 2 x 2 blocks per wave, their chunks on consecutive lanes
     const int CV = C / 8, bpw = 64 / CV;
     const long long nblk = (long long)N * BH * BW;
     const long long waves = (nblk + bpw - 1) / bpw;
     const long long blocks = std::min<long long>((waves + 3) / 4, 1 << 16);
     const bool pre = g_lrn_bwd_variant == 0;
-    auto kd = h == 1 ? (pre ? lrn_pool3s2_bwd_dpp_kernel<1, true>
-                            : lrn_pool3s2_bwd_dpp_kernel<1, false>)
-            : h == 2 ? (pre ? lrn_pool3s2_bwd_dpp_kernel<2, true>
-                            : lrn_pool3s2_bwd_dpp_kernel<2, false>)
-            : h == 3 ? (pre ? lrn_pool3s2_bwd_dpp_kernel<3, true>
-                            : lrn_pool3s2_bwd_dpp_kernel<3, false>)
-                     : (pre ? lrn_pool3s2_bwd_dpp_kernel<4, true>
-                            : lrn_pool3s2_bwd_dpp_kernel<4, false>);
+    // the activation derivative as a template: none, ReLU of x, any
+    const int am = !aux ? 0 : (aux == x && aux_act == ACT_STRICT_RELU) ? 1 : 2;
+#define LRN_BWD_K(H)                                                      \
+    (!pre      ? lrn_pool3s2_bwd_dpp_kernel<H, false>                     \
+     : am == 0 ? lrn_pool3s2_bwd_dpp_kernel<H, true, 0>                   \
+     : am == 1 ? lrn_pool3s2_bwd_dpp_kernel<H, true, 1>                   \
+               : lrn_pool3s2_bwd_dpp_kernel<H, true, 2>)
+    auto kd = h == 1 ? LRN_BWD_K(1) : h == 2 ? LRN_BWD_K(2)
+            : h == 3 ? LRN_BWD_K(3) : LRN_BWD_K(4);
+#undef LRN_BWD_K
     hipLaunchKernelGGL(kd, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const uint16_t*)x, (const uint16_t*)dp,
                        (const uint8_t*)argmax, (uint16_t*)dx, N, H, W, C, OH,

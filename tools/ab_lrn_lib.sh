@@ -1,0 +1,9 @@
+#!/bin/bash
+# bench_lrn.py with the committed LRN kernels (abl/libhvk_lrn_old.so, built
+# from HEAD's pool_lrn.hip) against the working tree's, alternating on one box
+set -e
+for i in 1 2; do
+  HVK_LIBRARY=abl/libhvk_lrn_old.so timeout -k 10 200 python tools/bench_lrn.py 2048 > gpurun_out/lrn_old_$i.log 2>&1
+  timeout -k 10 200 python tools/bench_lrn.py 2048 > gpurun_out/lrn_new_$i.log 2>&1
+  for v in old new; do echo "$v $i: $(grep -h "^conv. {" gpurun_out/lrn_${v}_$i.log | tr '\n' ' ')"; done
+done

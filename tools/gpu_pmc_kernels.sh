@@ -1,0 +1,20 @@
+#!/bin/bash
+# PMC passes (instruction mix, wave state, fetch / write bytes) over any
+# probe program, summarised for the kernels whose name contains $FILTER.
+#   FILTER=lrn TAG=lrn PROBE="tools/bench_lrn.py 2048" tools/gpu_pmc_kernels.sh
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-k}
+for pass in A B F W; do
+  case $pass in
+    A) ctr="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVES" ;;
+    B) ctr="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE" ;;
+    F) ctr="FETCH_SIZE" ;;
+    W) ctr="WRITE_SIZE" ;;
+  esac
+  tools/gpu_step.sh 200 gpurun_out/pmc_${T}_$pass.log timeout -s KILL 150 \
+    rocprofv3 --kernel-trace --pmc $ctr -d "$R/gpurun_out/pmc_${T}_$pass" \
+    -o run --output-format csv -- python3 $PROBE || exit 1
+done
+python3 tools/pmc_kernels_summary.py "$T" "$FILTER"
+exit 0

@@ -1,0 +1,37 @@
+"""Summary of tools/gpu_pmc_kernels.sh passes: python3 tools/pmc_kernels_summary.py TAG FILTER"""
+import csv, glob, sys, collections
+T, filt = sys.argv[1], sys.argv[2]
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+calls = collections.defaultdict(lambda: collections.defaultdict(int))
+ns = collections.defaultdict(list)
+for p in "ABFW":
+    f = glob.glob("gpurun_out/pmc_%s_%s/**/*counter_collection.csv" % (T, p), recursive=True)
+    if not f:
+        continue
+    for r in csv.DictReader(open(f[0])):
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:70] + " grid " + r.get("Grid_Size", r.get("Grid_Size_X", ""))
+        if filt not in k:
+            continue
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        calls[k][r["Counter_Name"]] += 1
+        if p == "B" and r["Counter_Name"] == "SQ_WAVE_CYCLES":
+            ns[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+for k, d in agg.items():
+    c = calls[k]
+    m = {n: d[n] / max(c[n], 1) for n in d}   # per call
+    w = max(m.get("SQ_WAVES", 1), 1)
+    print(k)
+    print("  per wave: VALU %.0f SALU %.0f VMEMrd %.0f VMEMwr %.0f LDS %.0f SMEM %.0f" % tuple(
+        m.get(x, 0) / w for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
+                                  "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_INSTS_SMEM")))
+    wc = max(m.get("SQ_WAVE_CYCLES", 1), 1)
+    bc = max(m.get("SQ_BUSY_CYCLES", 1), 1)
+    print("  wave cycles: wait %.1f%% instwait %.1f%% active %.1f%% valu-active %.1f%% salu-active %.1f%%" % (
+        100 * m.get("SQ_WAIT_ANY", 0) / wc, 100 * m.get("SQ_WAIT_INST_ANY", 0) / wc,
+        100 * m.get("SQ_ACTIVE_INST_ANY", 0) / wc, 100 * m.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+        100 * m.get("SQ_ACTIVE_INST_SCA", 0) / wc))
+    if ns[k]:
+        ms = sum(ns[k]) / len(ns[k]) / 1e6
+        fb, wb = m.get("FETCH_SIZE", 0) * 1024, m.get("WRITE_SIZE", 0) * 1024
+        print("  ms/call %.3f  fetch %.1f MB  write %.1f MB  -> %.2f TB/s" % (
+            ms, fb / 1e6, wb / 1e6, (fb + wb) / ms / 1e9))
