@@ -309,6 +309,86 @@ __global__ void pool_bwd3_kernel(const uint16_t* __restrict__ dy,
   }
 }
 
+// 3x3 / stride-2 (unpadded) max pooling backward over 2x2 input blocks, the
+// layout of lrn_pool3s2_bwd_dpp_kernel: a pixel of block (bh, bw) lies only
+// in windows (bh - 1 + a, bw - 1 + b), so one thread loads those (at most)
+// four windows' gradient + argmax once for its four pixels - the per-pixel
+// kernel above loads them once per pixel, 3.25x the bytes through L2
+// (AlexNet pool5: 13x13 -> 6x6).  An absent window's gradient is zeroed (its
+// clamped twin's argmax may name one of these pixels).
+template <int MODE>
+__global__ __launch_bounds__(256) void pool_bwd3s2_blk_kernel(
+    const uint16_t* __restrict__ dy, const int* __restrict__ argmax,
+    uint16_t* __restrict__ dx, int N, int H, int W, int C, int OH, int OW,
+    const uint16_t* aux, int aux_act, FastDiv fCV, FastDiv fBW,
+    FastDiv fBH) {
+  static_assert(MODE != POOL_AVG, "argmax-based modes");
+  const int CV = C >> 3;
+  const int BH = (H + 1) >> 1, BW = (W + 1) >> 1;
+  const uint32_t total = (uint32_t)N * BH * BW * CV;
+  const uint32_t OWC = (uint32_t)OW * C;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += gridDim.x * blockDim.x) {
+    uint32_t blk, cvu, t, bwu, nu, bhu;
+    fdivmod(e, fCV, blk, cvu);
+    fdivmod(blk, fBW, t, bwu);
+    fdivmod(t, fBH, nu, bhu);
+    const uint32_t c0 = cvu * 8;
+    const uint32_t orow[2] = {(bhu > 0 ? bhu - 1 : 0), min(bhu, (uint32_t)OH - 1)};
+    const uint32_t ocol[2] = {(bwu > 0 ? bwu - 1 : 0), min(bwu, (uint32_t)OW - 1)};
+    const bool rok[2] = {bhu > 0, bhu < (uint32_t)OH};
+    const bool cok[2] = {bwu > 0, bwu < (uint32_t)OW};
+    uint4 g[4];
+    int4 a0[4], a1[4];
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const int a = wi >> 1, b = wi & 1;
+      const uint32_t yo =
+          (nu * OH + orow[a]) * OWC + ocol[b] * (uint32_t)C + c0;
+      const uint4 gv = *(const uint4*)(dy + yo);
+      g[wi] = rok[a] && cok[b] ? gv : make_uint4(0u, 0u, 0u, 0u);
+      a0[wi] = *(const int4*)(argmax + yo);
+      a1[wi] = *(const int4*)(argmax + yo + 4);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint32_t hp = 2 * bhu + (p >> 1), wp = 2 * bwu + (p & 1);
+      const bool pv = hp < (uint32_t)H && wp < (uint32_t)W;
+      const uint32_t xoff = ((nu * H + hp) * W + wp) * C + c0;
+      float acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+#pragma unroll
+      for (int wi = 0; wi < 4; ++wi) {
+        const int a = wi >> 1, b = wi & 1;
+        // window-local row / column of pixel p in window (bh-1+a, bw-1+b)
+        const int r = 2 * (1 - a) + (p >> 1), c = 2 * (1 - b) + (p & 1);
+        if (r > 2 || c > 2) continue;
+        const uint16_t* gv = (const uint16_t*)&g[wi];
+        const int am[8] = {a0[wi].x, a0[wi].y, a0[wi].z, a0[wi].w,
+                           a1[wi].x, a1[wi].y, a1[wi].z, a1[wi].w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          acc[q] += am[q] == (int)xoff + q ? bf2f(gv[q]) : 0.f;
+      }
+      if (aux) {
+        const uint4 av4 = *(const uint4*)(aux + (pv ? xoff : c0));
+        const uint16_t* ah = (const uint16_t*)&av4;
+        float av[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) av[q] = bf2f(ah[q]);
+        act_bwd_mul8(acc, av, aux_act);
+      }
+      if (pv) *(uint4*)(dx + xoff) = pack_bf16x8(acc);
+    }
+  }
+}
+
+// backward selector for A/B runs (hvk_set_pool_bwd_variant): 0 the 2x2-block
+// kernel for unpadded 3x3 / stride-2 max pooling, 1 the per-pixel kernel
+static int g_pool_bwd_variant = 0;
+HVK_API void hvk_set_pool_bwd_variant(int v) { g_pool_bwd_variant = v; }
+
 // LRN across channels: s_c = k + alpha * sum_{|c'-c|<=n/2} x_c'^2 ;
 // y_c = x_c * s_c^-beta.  One wave per pixel; channels staged in LDS.
 constexpr int LRN_MAXC = 1024;
@@ -1094,8 +1174,10 @@ void lrn_pool3s2_fwd_walk_kernel(
     const int oh0 = (int)su * R, oh1 = min(OH, oh0 + R);
     const bool has_lo = c0 >= 8, has_hi = c0 + 8 < C;
     const uint16_t* img = x + nu * HWC;
-    const bool c1v = w0 + 1 < W, c2v = w0 + 2 < W;
-    const int wc1 = c1v ? w0 + 1 : W - 1, wc2 = c2v ? w0 + 2 : W - 1;
+    // every window lies inside the image (the host passes OH = (H - 3) / 2
+    // + 1, OW likewise): no edge masks (they held ~50 SGPRs, spilled to VGPR
+    // lanes)
+    const int wc1 = w0 + 1, wc2 = w0 + 2;
     const uint32_t col[3] = {(uint32_t)w0 * C, (uint32_t)wc1 * C,
                              (uint32_t)wc2 * C};
     // pixel (row offset ro, window column j)
@@ -1104,8 +1186,8 @@ void lrn_pool3s2_fwd_walk_kernel(
     auto rowmax = [&](float y0, float y1v, float y2v, float& b, int& bi) {
       b = y0;
       bi = 0;
-      if (c1v && y1v > b) { b = y1v; bi = 1; }
-      if (c2v && y2v > b) { b = y2v; bi = 2; }
+      if (y1v > b) { b = y1v; bi = 1; }
+      if (y2v > b) { b = y2v; bi = 2; }
     };
     float cb[8];
     int ci[8];
@@ -1135,7 +1217,6 @@ void lrn_pool3s2_fwd_walk_kernel(
     };
     load_rows(oh0, a, b);
     for (int oh = oh0; oh < oh1; ++oh) {
-      const bool r1v = 2 * oh + 1 < H, r2v = 2 * oh + 2 < H;
       LrnPx na[3], nb[3];
       if constexpr (PF) load_rows(min(oh + 1, oh1 - 1), na, nb);
       else if (oh > oh0) load_rows(oh, a, b);
@@ -1152,8 +1233,8 @@ void lrn_pool3s2_fwd_walk_kernel(
         rowmax(yc[0][q].y, yc[1][q].y, yc[2][q].y, b2, i2);
         float best = cb[q];
         int bi = ci[q];
-        if (r1v && b1 > best) { best = b1; bi = 3 + i1; }
-        if (r2v && b2 > best) { best = b2; bi = 6 + i2; }
+        if (b1 > best) { best = b1; bi = 3 + i1; }
+        if (b2 > best) { best = b2; bi = 6 + i2; }
         o[q] = f2bf(best);
         ai[q] = (uint8_t)bi;
         cb[q] = b2;   // this window's last row starts the next one
@@ -1685,7 +1766,8 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
     return -1;
   const int h = n / 2;
   const long long total = (long long)N * OH * OW * (C / 8);
-  if (h >= 1 && h <= 2 && g_lrn_fwd_variant != 1) {
+  if (h >= 1 && h <= 2 && g_lrn_fwd_variant != 1 && OH == (H - 3) / 2 + 1 &&
+      OW == (W - 3) / 2 + 1) {
     // vertical walk over strips of about 14 output rows (AlexNet: one strip
     // for conv2's 13 rows, two for conv1's 27)
     const int t = g_lrn_fwd_variant == 3 ? 5 : g_lrn_fwd_variant == 4 ? 9 : 14;
@@ -1816,6 +1898,20 @@ HVK_API int hvk_pool_bwd(const void* dy, const int* argmax, void* dx, int N,
   if (C % 8 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
       ((uintptr_t)aux & 15) == 0) {
     long long total = (long long)N * H * W * (C / 8);
+    if (ky == 3 && kx == 3 && sy == 2 && sx == 2 && pt == 0 && pl == 0 &&
+        mode != POOL_AVG && g_pool_bwd_variant == 0 &&
+        ((uintptr_t)argmax & 15) == 0 &&
+        (long long)N * H * W * C < (1ll << 31)) {
+      const long long tb = (long long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+      auto kb = mode == POOL_MAXABS ? pool_bwd3s2_blk_kernel<POOL_MAXABS>
+                                    : pool_bwd3s2_blk_kernel<POOL_MAX>;
+      hipLaunchKernelGGL(kb, dim3(grid_for(tb)), dim3(256), 0, s,
+                         (const uint16_t*)dy, argmax, (uint16_t*)dx, N, H, W,
+                         C, OH, OW, (const uint16_t*)aux, aux_act,
+                         make_fastdiv(C / 8), make_fastdiv((W + 1) / 2),
+                         make_fastdiv((H + 1) / 2));
+      return (int)launch_status(s);
+    }
     if (ky == 3 && kx == 3 && sy >= 2 && sx >= 2 &&
         ((uintptr_t)argmax & 15) == 0 &&
         (long long)N * H * W * C < (1ll << 31)) {

@@ -336,7 +336,9 @@ def test_conv_wgrad(cfg):
                                        # 4- and 2-channel lanes (LeNet)
                                        ((2, 24, 24, 20), 2, 2),
                                        ((2, 8, 8, 50), 2, 2),
-                                       ((2, 9, 9, 12), 3, 2)])
+                                       ((2, 9, 9, 12), 3, 2),
+                                       # AlexNet pool5 (2x2-block backward)
+                                       ((2, 13, 13, 256), 3, 2)])
 def test_pool(mode, shape, k, s):
     x = rnd(*shape)
     y, am = ops.pool_fwd(x, k, k, (s, s), mode)
@@ -350,6 +352,31 @@ def test_pool(mode, shape, k, s):
     dxg = ops.pool_bwd(dy.to(DEV), amg, shape, k, k, (s, s), mode,
                        aux=aux.to(DEV), aux_act=3)
     close(dxg, dx, 1e-2)
+
+
+@pytest.mark.parametrize("shape", [(3, 13, 13, 256), (2, 14, 12, 24),
+                                   (1, 27, 27, 96)])
+def test_pool_bwd_block_matches_per_pixel(shape):
+    """3x3 / stride-2 max-pool backward: the 2x2-block kernel (each window's
+    gradient and argmax loaded once per block) against the per-pixel kernel
+    (hvk_set_pool_bwd_variant 1), odd and even image sides, with a fused
+    ReLU derivative; the window sums may differ in order only."""
+    lib = ops._lib.lib()
+    x = rnd(*shape, scale=2.0).to(DEV)
+    y, am = ops.pool_fwd(x, 3, 3, (2, 2), "max")
+    dy = rnd(*y.shape, seed=7).to(DEV)
+    outs = []
+    try:
+        for v in (1, 0):
+            lib.hvk_set_pool_bwd_variant(v)
+            outs.append(ops.pool_bwd(dy, am, shape, 3, 3, (2, 2), "max",
+                                     aux=x, aux_act=3))
+            torch.cuda.synchronize()
+    finally:
+        lib.hvk_set_pool_bwd_variant(0)
+    a, b = outs[0].float().cpu(), outs[1].float().cpu()
+    assert torch.allclose(a, b, rtol=1 / 128, atol=0)
+    assert b.abs().sum().item() > 0
 
 
 @pytest.mark.parametrize("C", [96, 256, 13])
