@@ -31,11 +31,30 @@ def main(trace, out, steps=None, title="", window=False):
         a[0] += 1
         a[1] += d
     tot = sum(v[1] for v in agg.values())
+    busy = ""
+    if window and rows:
+        # the union of the dispatch intervals (concurrent streams overlap):
+        # what is left of the window is GPU idle time
+        iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                    for r in rows)
+        u, (cs, ce) = 0, iv[0]
+        for s, e in iv[1:]:
+            if s > ce:
+                u, cs, ce = u + ce - cs, s, e
+            else:
+                ce = max(ce, e)
+        u += ce - cs
+        span = iv[-1][1] - iv[0][0]
+        busy = (" Busy (union of dispatches) %.3f ms of a %.3f ms window"
+                "%s; idle %.3f ms." % (u / 1e6, span / 1e6,
+                                       (" (%.3f / %.3f ms per step)" % (
+                                           u / 1e6 / steps, span / 1e6 / steps))
+                                       if steps else "", (span - u) / 1e6))
     lines = ["# %s" % title, "",
              "Total kernel time %.3f ms over %d dispatches%s." %
              (tot / 1e6, sum(v[0] for v in agg.values()),
               ("; %.3f ms of kernel time per step" % (tot / 1e6 / steps))
-              if steps else ""), "",
+              if steps else "") + busy, "",
              "| kernel | grid (x,y,z threads) | VGPR | LDS | calls | "
              "ms/call | total ms | ms/step | % |",
              "|---|---|---|---|---|---|---|---|---|"]
