@@ -230,6 +230,28 @@ def test_wgrad_side_stream_matches_serial(graphs, monkeypatch):
             0.05 * abs(a["validation_loss"]) + 1e-3
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_tail_update_matches_serial(graphs, monkeypatch):
+    """One rank: the update of every bucket but the last on the side stream
+    beside the last layers' weight gradients (engine.tail_update), eagerly
+    and inside the captured backward - the same trajectory as one update
+    after the backward."""
+    steps = 12
+    monkeypatch.setenv("VELES_AMD_TAIL_UPDATE", "0")
+    ser = _train(graphs, steps, overlap=False, bucket_mb=0.05)
+    monkeypatch.setenv("VELES_AMD_TAIL_UPDATE", "1")
+    tail = _train(graphs, steps, overlap=False, bucket_mb=0.05)
+    assert tail.param_store_._tail and not ser.param_store_._tail
+    assert len(tail.param_store_.buckets) > 1
+    if graphs:
+        assert tail.graph_segments_[1].failures == 0
+        assert tail.graph_segments_[1].replays > 0
+    assert tail.param_store_.steps == ser.param_store_.steps == steps
+    assert _rel(tail.param_store_.master, ser.param_store_.master) < 2e-2
+    st = tail.param_store_
+    assert torch.equal(st.lp, st.master.to(st.lp.dtype))
+
+
 def _solo_run(out, solo, steps, port):
     import os
     import numpy

@@ -87,6 +87,9 @@ class ParameterStore(object):
         # multi-rank: per-bucket updates on a side stream (_overlap_update)
         self._overlap = None
         self._single = None   # single-rank overlapped update (decided once)
+        self._tail = None     # single-rank tail-overlapped update (ditto)
+        self._tail_evs = None  # branch-stream events of the tail's gradients
+        self._span_tables = {}  # (lo, hi) -> segment table of a span update
         self._upd_stream = None
         # gradients are written on branch streams too (weight gradients off
         # the compute stream, gd_conv.py): everything that consumes the
@@ -295,6 +298,19 @@ class ParameterStore(object):
                             all(id(p) in self._ready for p in b):
                         self._launched.add(i)
                         self._bucket_update(i, None)
+            elif self._tail_overlap() and self._tail_evs is None and \
+                    all(id(p) in self._ready
+                        for b in self.buckets[:-1] for p in b):
+                # every gradient but the last bucket's is enqueued: mark the
+                # branch streams here, so that the early buckets' update can
+                # later wait for exactly these weight gradients (not for the
+                # last layers', which it is to run beside)
+                import torch
+                self._tail_evs = []
+                for st in self._grad_streams():
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    self._tail_evs.append(ev)
             return
         if self._accum_count + 1 < self.accumulate:
             return
@@ -446,6 +462,60 @@ class ParameterStore(object):
                 self._single = self._solver_segs is None
         return self._single
 
+    def _tail_overlap(self):
+        """One rank on a GPU, plain SGD, no accumulation: the update of every
+        bucket but the last runs on the side stream from the moment the last
+        layers' weight gradients are enqueued (their branch streams are not
+        waited for), beside them - the memory-bound update of the classifier
+        under the MFMA-bound first-layer weight gradient at the end of the
+        backward, where the per-bucket overlap above (launched during the
+        whole backward) measured slower.  Off by default: AlexNet b2048
+        174.8-176.4k img/s with it against 180.1-180.7k without on one box
+        (the update's 256 workgroups and HBM traffic slow the persistent
+        conv1 weight gradient by more than the 0.22 ms they take off the
+        critical path; profiles/r5/ab_tail_update_r5r.log).
+        ``root.common.engine.tail_update`` / ``VELES_AMD_TAIL_UPDATE`` (0 / 1).
+        """
+        if self._tail is None:
+            from veles_amd.utils.config import root, get
+            on = os.environ.get(
+                "VELES_AMD_TAIL_UPDATE",
+                "1" if get(root.common.engine.tail_update, False) else "0")
+            gpu = self.master is not None and self.master.is_cuda
+            self._tail = (on != "0" and gpu and not self._multi() and
+                          self.accumulate == 1 and len(self.buckets) > 1 and
+                          not self._single_overlap())
+            if self._tail:
+                self._cached_segments()
+                self._tail = self._solver_segs is None
+        return self._tail
+
+    def _span_update(self, lo, hi, stream, max_blocks=None):
+        """Fused SGD over [lo, hi) of the store on ``stream``."""
+        import torch
+        from veles_amd import ops
+        segs = self._span_segs(lo, hi)
+        if not segs:
+            return
+        zf = True if not self.overwrite else max(0, self.zero_tail - lo)
+        if (lo, hi) not in self._span_tables:
+            self._span_tables[(lo, hi)] = ops.SegmentTable(self.master.device)
+        lp = self.lp[lo:hi] if self.lp is not None else None
+        with torch.cuda.stream(stream):
+            ops.sgd_update(self.master[lo:hi], self.grad[lo:hi],
+                           self.mom[lo:hi], segs, w_lp=lp, zero_grad=zf,
+                           table=self._span_tables[(lo, hi)],
+                           max_blocks=max_blocks)
+
+    def _span_segs(self, lo, hi):
+        """The update segments inside [lo, hi), span-relative."""
+        segs = []
+        for b, e, lr, d, l1, m in self._cached_segments():
+            b, e = max(b, lo), min(e, hi)
+            if b < e:
+                segs.append((b - lo, e - lo, lr, d, l1, m))
+        return segs
+
     def _bucket_span(self, i):
         """[lo, hi) of bucket i's update: from its first parameter to the
         next bucket's (the last bucket to ``total``), so the spans tile the
@@ -547,6 +617,24 @@ class ParameterStore(object):
         """Wait for the gradient all-reduces, then one fused SGD update."""
         from veles_amd import ops
         self._accum_count += 1
+        tail = (not self._multi() and gscale == 1.0 and
+                self._tail_evs is not None and self._tail_overlap())
+        if tail:
+            # the early buckets' update on the side stream, after the compute
+            # stream's work so far (the last layers' backward-data / LRN) and
+            # the weight gradients marked in grads_ready, beside the last
+            # layers' weight gradients still running on the branch streams
+            import torch
+            cur = torch.cuda.current_stream(self.master.device)
+            if self._upd_stream is None:
+                self._upd_stream = torch.cuda.Stream(device=self.master.device)
+            self._upd_stream.wait_stream(cur)
+            for ev in self._tail_evs:
+                self._upd_stream.wait_event(ev)
+            split = self.buckets[-1][0].offset
+            self._span_update(0, split, self._upd_stream,
+                              max_blocks=self._upd_blocks)
+        self._tail_evs = None
         if self.branch_grads and self.master is not None and \
                 self.master.is_cuda:
             # the gradients written off the compute stream are complete
@@ -607,7 +695,15 @@ class ParameterStore(object):
         segs = [] if overlapped else self._cached_segments()
         if segs and self._seg_table is None:
             self._seg_table = ops.SegmentTable(self.master.device)
-        if overlapped:
+        if tail:
+            # the last bucket here, then the next forward waits for the side
+            # stream's update of the others
+            import torch
+            self._span_update(self.buckets[-1][0].offset, self.total,
+                              torch.cuda.current_stream(self.master.device))
+            torch.cuda.current_stream(self.master.device).wait_stream(
+                self._upd_stream)
+        elif overlapped:
             pass  # updated bucket by bucket (``_bucket_update``)
         elif segs and self._solver_segs is not None:
             import torch
@@ -697,6 +793,8 @@ class ParameterStore(object):
             # per-bucket tables of the overlapped updates
             for i, tab in self._bucket_tables.items():
                 tab.update(ops._pack_sgd_segs(self._bucket_segs(i)))
+            for (lo, hi), tab in self._span_tables.items():
+                tab.update(ops._pack_sgd_segs(self._span_segs(lo, hi)))
 
     def replayed_step(self):
         """Host bookkeeping of one update whose kernels ran in a graph."""
@@ -715,7 +813,8 @@ class ParameterStore(object):
         re-run eagerly: graphs.py)."""
         st = {"steps": self.steps, "ready": set(self._ready),
               "works": list(self._works), "launched": set(self._launched),
-              "accum": self._accum_count, "pending": dict(self._pending)}
+              "accum": self._accum_count, "pending": dict(self._pending),
+              "tail_evs": self._tail_evs}
         if self.device is not None and getattr(self.device, "fp8", False):
             from veles_amd.ops import fp8
             st["fp8_step"] = fp8.registry(self.device.torch_device).step
@@ -728,6 +827,8 @@ class ParameterStore(object):
         self._launched = set(st["launched"])
         self._accum_count = st["accum"]
         self._pending = dict(st["pending"])
+        # events recorded inside a failed capture must not be waited for
+        self._tail_evs = st.get("tail_evs")
         if "fp8_step" in st:
             from veles_amd.ops import fp8
             fp8.registry(self.device.torch_device).step = st["fp8_step"]
