@@ -560,6 +560,11 @@ constexpr int kNBW = 8;   // window pieces per wave: 64 KiB windows at most
 // every shape it supports, 0 off, > 0 one forced configuration
 int g_hc_variant = -2;
 int g_hc_abl = 0;         // diagnostic instantiation (configurations 5-7)
+// window slot row pitch Wp = OW + pad (hvk_hc_pitch_pad; pad >= KW - 1).  8
+// keeps Wp = OW (mod 8): conflict-free A fragments across row wraps; a
+// smaller pad shrinks the window of small images (13 x 13: 21 -> 15 slots
+// per row) at the price of conflicts on the wrapping fragments
+int g_hc_pad = 8;
 
 struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW; };
 // per kernel size, in order of preference (the first whose n-tile divides
@@ -607,7 +612,7 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   g.OCg = OCg; g.CG = CG; g.pt = pt; g.pl = pl; g.G = groups;
   g.P = N * OH * OW;
   g.OHW = OH * OW;
-  g.Wp = OW + 8;
+  g.Wp = OW + std::max(g_hc_pad, KW - 1);
   g.HPd = OH + KH - 1;
   g.flip = flip ? 1 : 0;
   if (OW + KW - 1 > g.Wp || g.Wp >= (1 << 20)) return p;
@@ -721,6 +726,8 @@ HVK_API void hvk_hc_variant(int v) { g_hc_variant = v; }
 // Diagnostic ablation builds of configurations 5, 6 and 7 (see conv_hc_kernel's
 // ABL); 0 = the production kernel.
 HVK_API void hvk_hc_ablation(int a) { g_hc_abl = a; }
+// window row pitch pad (8 default; see g_hc_pad)
+HVK_API void hvk_hc_pitch_pad(int p) { g_hc_pad = p; }
 
 // Forward: Y[N][OH][OW][OC] = act(conv(X, W) + bias), stride 1, X bf16 NHWC,
 // W [OC][KH][KW][C/g].  Returns 0, -2 when the shape does not take this

@@ -117,6 +117,7 @@ _SIGS = {
     "hvk_conv_fwd_hc": [P, P, P, P] + [I] * 13 + [P],
     "hvk_conv_dgrad_hc": [P, P, P] + [I] * 12 + [P, I, P],
     "hvk_hc_variant": [I],
+    "hvk_hc_pitch_pad": [I],
     "hvk_set_pool_bwd_variant": [I],
     "hvk_hc_ablation": [I],
     "hvk_take_last_error": [],
