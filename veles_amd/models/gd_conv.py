@@ -155,7 +155,8 @@ class GDSigmoidConv(GradientDescentConv):
 
 def _wgrad_on_side(unit, err):
     """Weight gradients (conv and fully-connected GD units) off the compute
-    stream (engine.wgrad_stream / VELES_AMD_WGRAD_STREAM, on by default:
+    stream (engine.wgrad_stream / VELES_AMD_WGRAD_STREAM, on by default
+    except under an eager multi-rank backward:
     AlexNet b2048 172.7-173.6k -> 175.0-175.3k img/s on one box with the
     conv ones, profiles/r5/bench_wgrad_stream_ab.md).  Multi-rank, a
     layer's bucket collective waits for it (it is launched from the compute
@@ -163,11 +164,18 @@ def _wgrad_on_side(unit, err):
     backward-data only."""
     import os
     from veles_amd.utils.config import root, get
-    if not err.is_cuda or os.environ.get(
-            "VELES_AMD_WGRAD_STREAM",
-            "1" if get(root.common.engine.wgrad_stream, True) else "0") == "0":
+    store = getattr(unit, "store_", None)
+    env = os.environ.get("VELES_AMD_WGRAD_STREAM")
+    if not err.is_cuda or store is None or env == "0" or (
+            env is None and not get(root.common.engine.wgrad_stream, True)):
         return False
-    return getattr(unit, "store_", None) is not None
+    if env is None and store._multi() and not store.graph_safe():
+        # an eager multi-rank backward (the N > 1 default): the serial weight
+        # gradients measured faster there - one-rank RCCL group, AlexNet
+        # b2048: 173.6-173.8k img/s against 167.2-168.6k with the branch
+        # streams (profiles/r5/ab_solo_eager_wgrad_r5s.log); "1" forces them
+        return False
+    return True
 
 
 def _side_stream_run(unit, fn, keep=()):
