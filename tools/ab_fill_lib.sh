@@ -1,7 +1,7 @@
 #!/bin/bash
-# tools/probe_fill_s2d.py with HEAD's elementwise.hip (abl/libhvk_fill_old.so,
-# linked beside the other current objects) against the working tree's,
-# alternating on one box
+# tools/probe_fill_s2d.py with another revision's elementwise.hip
+# (abl/libhvk_fill_old.so: python tools/build_ab_lib.py elementwise HEAD
+# abl/libhvk_fill_old.so) against the working tree's, alternating on one box
 set -e
 for i in 1 2 3; do
   HVK_LIBRARY=abl/libhvk_fill_old.so timeout -k 10 120 python tools/probe_fill_s2d.py 2048 > gpurun_out/fill_old_$i.log 2>&1
