@@ -34,14 +34,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # 2048 per GPU (round 4 sweep, profiles/r4/alexnet_batch_sweep.md):
-    # b1024 144.9k, b2048 154.3k, b3072 156.2k, b4096 157.2k img/s on one
-    # MI355X; b2048 takes ~20 GB of the 288 GB HBM with every activation
-    # tensor under 2 GB (the 32-bit buffer offsets of the LDS-DMA loaders;
-    # b4096's conv1 output is 2.4 GB), and halves the all-reduce-to-compute
-    # ratio of b1024 for the multi-GPU points
+    # 3072 per GPU (end of round 5, profiles/r5/alexnet_batch_sweep_r5t.log:
+    # b2048 179.8-180.3k, b3072 184.5-186.0k, b4096 184.5-186.3k, b6144
+    # 185.9k img/s on one MI355X; round 4: b2048 154.3k, b3072 156.2k): the
+    # smallest batch on the plateau, ~30 GB of the 288 GB HBM with every
+    # activation tensor under 2 GB (the 32-bit buffer offsets of the LDS-DMA
+    # loaders; b4096's conv1 output is 2.4 GB and runs image-chunked, b8192
+    # passes the LRN kernels' 2^31-element limit), and 1.5x the compute per
+    # all-reduce of b2048 for the multi-GPU points
     ap.add_argument("--batch", type=int, default=None,
-                    help="per-GPU minibatch (weak scaling); default 2048, "
+                    help="per-GPU minibatch (weak scaling); default 3072, "
                          "512 for vgg16 (the fp8 and bf16 throughput "
                          "plateau: profiles/r4/vgg16_batch_sweep.md)")
     ap.add_argument("--model", default="alexnet")
@@ -60,7 +62,7 @@ def main():
                          "kernels (step-only rocprofv3 summaries)")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = 512 if args.model == "vgg16" else 2048
+        args.batch = 512 if args.model == "vgg16" else 3072
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _spawn(args)
 
@@ -95,8 +97,8 @@ def main():
     # the resident synthetic set: --steps-per-epoch minibatches of ONE
     # rank's batch, at least one global minibatch.  Every rank holds the
     # whole set (the global shuffle may hand any sample to any rank), so the
-    # per-rank HBM it takes is fixed up to N = steps_per_epoch (16: 32768
-    # images, 5 GB at b2048) and grows linearly past it; an epoch of one or
+    # per-rank HBM it takes is fixed up to N = steps_per_epoch (16: 49152
+    # images, 7.6 GB at b3072) and grows linearly past it; an epoch of one or
     # two steps measured as cheap as sixteen (152.9k vs 154.3k img/s at
     # b2048, profiles/r4/alexnet_batch_sweep.md)
     n_train = max(global_batch, args.batch * args.steps_per_epoch)
