@@ -412,11 +412,15 @@ def test_fused_quantisation_bf16_conv(cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bwd", [False, True])
-def test_fused_quantisation_pool2(bwd):
+@pytest.mark.parametrize("chunked", [False, True])
+def test_fused_quantisation_pool2(bwd, chunked, monkeypatch):
     """The 2 x 2 pooling kernels' fused fp8 copy of their result equals a
     separate quantize pass at the consumer scaler's scale; the amax reaches
-    the history at the roll."""
+    the history at the roll.  ``chunked``: one launch per image (the path
+    past 2^31 elements, threshold lowered), the amax of all of them."""
     N, H, W, C = 3, 16, 14, 32
+    if chunked:
+        monkeypatch.setattr(ops, "_CHUNK_ELEMS", H * W * C + 1)
     nxt = fp8.Scaler(DEV, fp8.E5M2 if bwd else fp8.E4M3)
     nxt.prime(torch.full((16,), 2.0, device=DEV))
     x = rnd(N, H, W, C).to(torch.bfloat16).to(DEV)

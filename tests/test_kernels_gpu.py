@@ -635,6 +635,37 @@ def test_lrn_pool_bwd_preload_matches_inline(shape, n, aux_mode):
     assert torch.allclose(a, b, rtol=1 / 128, atol=0)
 
 
+def test_pool_lrn_image_chunks_match_whole(monkeypatch):
+    """Past 2^31 elements the 2x2 pooling and the one-byte-argmax LRN-pool
+    pair run in image chunks (their kernels index with 32-bit offsets): a
+    lowered threshold (chunks of 2, 2, 1 images) against the whole-batch
+    launch, bitwise, fused ReLU derivative included."""
+    x = rnd(5, 27, 27, 96, scale=3.0).clamp_min(0.0).to(DEV)
+    N, H, W, C = x.shape
+    n, alpha, beta, k = 5, 1e-4 / 5, 0.75, 1.0
+    OH, OW = ops.pool_out_size(H, W, 3, 3, 2, 2)
+
+    def run():
+        am8 = torch.zeros(N, OH, OW, C, dtype=torch.uint8, device=DEV)
+        y, _ = ops.lrn_pool_fwd(x, n, alpha, beta, k, 3, 3, (2, 2),
+                                argmax=am8)
+        dp = rnd(*y.shape, seed=5).to(DEV)
+        dx = ops.lrn_pool_bwd(x, dp, am8, n, alpha, beta, k, 3, 3, (2, 2),
+                              aux=x, aux_act=3)
+        x2 = x[:, :26, :26].contiguous()
+        p2 = ops.pool2_fwd(x2, "max")
+        d2 = ops.pool2_bwd(x2, rnd(*p2.shape, seed=9).to(DEV), "max",
+                           aux=x2, aux_act=3)
+        torch.cuda.synchronize()
+        return [t.cpu() for t in (y, am8, dx, p2, d2)]
+
+    whole = run()
+    monkeypatch.setattr(ops, "_CHUNK_ELEMS", 2 * H * W * C + 1)
+    assert ops._n_chunks(N, H * W * C) == [(0, 2), (2, 4), (4, 5)]
+    for a, b in zip(whole, run()):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape,stride,n,aux_mode", [
     ((2, 27, 27, 96), 2, 5, "sep"), ((3, 13, 13, 16), 2, 5, "sep"),
     ((2, 55, 55, 96), 2, 5, "sep"), ((2, 55, 55, 96), 2, 5, "x"),

@@ -1479,6 +1479,33 @@ def _q8_pool_args(q8, qs):
             float(qs.fmax_eff), qs.fmt, _f8.HIST]
 
 
+# The pooling and LRN-pool kernels index with 32-bit element offsets (they
+# refuse tensors of 2^31 elements or more): larger batches run in image
+# chunks (every image is independent in these ops; NHWC slices along N stay
+# contiguous and 16-B aligned for C % 8 == 0)
+_CHUNK_ELEMS = 1 << 31
+
+
+def _n_chunks(N, per_image):
+    """[(n0, n1)] image ranges of under _CHUNK_ELEMS elements each, or
+    None when the whole batch fits."""
+    if N * per_image < _CHUNK_ELEMS:
+        return None
+    step = max(1, (_CHUNK_ELEMS - 1) // max(per_image, 1))
+    return [(n0, min(N, n0 + step)) for n0 in range(0, N, step)]
+
+
+def _sl(t, n0, n1):
+    return None if t is None else t[n0:n1]
+
+
+def _q8_sliceable(q8, N):
+    """a fused fp8 copy splits with its result (the kernels only take the
+    max of |result| into the scaler's shards: atomics, so chunks add up)"""
+    return q8 is None or (q8.dim() == 4 and q8.shape[0] == N and
+                          q8.is_contiguous())
+
+
 def pool2_fwd(x, mode="max", out=None, q8=None, q8_scaler=None):
     """2 x 2 / stride-2 NHWC pooling that writes no argmax: ``pool2_bwd``
     recomputes the window's choice from x.  ``q8`` / ``q8_scaler``: also the
@@ -1489,6 +1516,12 @@ def pool2_fwd(x, mode="max", out=None, q8=None, q8_scaler=None):
         out = torch.empty(N, H // 2, W // 2, C, dtype=x.dtype,
                           device=x.device)
     if _gpu(x):
+        ch = _n_chunks(N, H * W * C) if _q8_sliceable(q8, N) else None
+        if ch:
+            for n0, n1 in ch:
+                pool2_fwd(x[n0:n1], mode, out=out[n0:n1],
+                          q8=_sl(q8, n0, n1), q8_scaler=q8_scaler)
+            return out
         _lib_call("hvk_pool2_fwd_q8", _p(x), _p(out), N, H, W, C, m,
                   *_q8_pool_args(q8, q8_scaler), _s(x))
         return out
@@ -1507,6 +1540,13 @@ def pool2_bwd(x, dy, mode="max", aux=None, aux_act=0, out=None, q8=None,
     if out is None:
         out = torch.empty_like(x, dtype=dy.dtype)
     if _gpu(x):
+        ch = _n_chunks(N, H * W * C) if _q8_sliceable(q8, N) else None
+        if ch:
+            for n0, n1 in ch:
+                pool2_bwd(x[n0:n1], dy[n0:n1], mode, aux=_sl(aux, n0, n1),
+                          aux_act=aux_act, out=out[n0:n1],
+                          q8=_sl(q8, n0, n1), q8_scaler=q8_scaler)
+            return out
         _lib_call("hvk_pool2_bwd_q8", _p(x), _p(dy), _p(out), N, H, W, C, m,
                   _p(aux), aux_act, *_q8_pool_args(q8, q8_scaler), _s(x))
         return out
@@ -1606,6 +1646,12 @@ def lrn_pool_fwd(x, n, alpha, beta, k, ky, kx, sliding, out=None,
     if argmax is None:
         argmax = torch.empty(N, OH, OW, C, dtype=torch.int32, device=x.device)
     if _gpu(x):
+        ch = _n_chunks(N, H * W * C) if argmax.dtype == torch.uint8 else None
+        if ch:
+            for n0, n1 in ch:
+                lrn_pool_fwd(x[n0:n1], n, alpha, beta, k, ky, kx, sliding,
+                             out=out[n0:n1], argmax=argmax[n0:n1])
+            return out, argmax
         if argmax.dtype == torch.uint8:
             if (sx, sy) != (2, 2):
                 raise ValueError("uint8 window-index argmax: stride 2 only")
@@ -1641,6 +1687,13 @@ def lrn_pool_bwd(x, dp, argmax, n, alpha, beta, k, ky, kx, sliding,
     if out is None:
         out = torch.empty_like(x)
     if _gpu(x):
+        ch = _n_chunks(N, H * W * C) if argmax.dtype == torch.uint8 else None
+        if ch:
+            for n0, n1 in ch:
+                lrn_pool_bwd(x[n0:n1], dp[n0:n1], argmax[n0:n1], n, alpha,
+                             beta, k, ky, kx, sliding, aux=_sl(aux, n0, n1),
+                             aux_act=aux_act, out=out[n0:n1])
+            return out
         if argmax.dtype == torch.uint8:
             _lib_call("hvk_lrn_pool_bwd_u8", _p(x), _p(dp), _p(argmax),
                       _p(out), N, H, W, C, OH, OW, n, float(alpha),
