@@ -153,10 +153,19 @@ class GDSigmoidConv(GradientDescentConv):
     MAPPING = "conv_sigmoid"
 
 
+# below this many multiply-adds a weight gradient stays on the compute
+# stream: a fork / join costs more than the overlap gains at small steps
+# (LeNet / CIFAR quick b100: 264-273k / 307-312k samples/s with branch
+# streams, 296k / 352k without, profiles/r5/ab_small_wgrad_stream_r5u.log);
+# every AlexNet / VGG-16 layer at the bench batches is far above it
+_SIDE_MIN_MACS = 1 << 30
+
+
 def _wgrad_on_side(unit, err):
     """Weight gradients (conv and fully-connected GD units) off the compute
     stream (engine.wgrad_stream / VELES_AMD_WGRAD_STREAM, on by default
-    except under an eager multi-rank backward:
+    for layers of at least _SIDE_MIN_MACS multiply-adds, except under an
+    eager multi-rank backward:
     AlexNet b2048 172.7-173.6k -> 175.0-175.3k img/s on one box with the
     conv ones, profiles/r5/bench_wgrad_stream_ab.md).  Multi-rank, a
     layer's bucket collective waits for it (it is launched from the compute
@@ -174,6 +183,11 @@ def _wgrad_on_side(unit, err):
         # gradients measured faster there - one-rank RCCL group, AlexNet
         # b2048: 173.6-173.8k img/s against 167.2-168.6k with the branch
         # streams (profiles/r5/ab_solo_eager_wgrad_r5s.log); "1" forces them
+        return False
+    pw = getattr(getattr(unit, "forward", None), "_pw_", None)
+    if env is None and pw is not None and err.dim() > 0 and \
+            err.numel() // max(err.shape[-1], 1) * pw.size < _SIDE_MIN_MACS:
+        # (output rows) x (weights): the layer's weight-gradient MACs
         return False
     return True
 
