@@ -11,8 +11,10 @@ itself (veles_amd.parallel.launch.spawn_ranks, from a parent that makes no
 GPU call) and exits with the group's code; it never reports a 1-rank result
 for --gpus N.  At N > 1 every rank runs a step watchdog
 (veles_amd.parallel.faults.Watchdog): a rank that makes no progress for
-VELES_AMD_BENCH_WATCHDOG_S seconds (default 600) - e.g. a collective whose
-peer never arrives - prints a [watchdog] line and exits 124.  Every timed step is a full training step through the veles_amd
+VELES_AMD_BENCH_WATCHDOG_S seconds (default 60) once its first step has
+finished, or that reaches no first step within
+VELES_AMD_BENCH_WATCHDOG_INIT_S seconds (default 300) - e.g. a collective
+whose peer never arrives - prints a [watchdog] line and exits 124.  Every timed step is a full training step through the veles_amd
 StandardWorkflow: device minibatch gather + normalisation, forward, softmax
 evaluator, decision, backward, bucketed gradient all-reduce, fused SGD.
 Prints ONE JSON line on rank 0.
@@ -219,21 +221,41 @@ def _spawn(args):
     return code
 
 
+# the hang bounds (seconds): per step once the first step has finished
+# (a step takes ~17 ms at b3072; the longest legitimate gap between two
+# decision runs is a warmup step with its HIP-graph capture, a few
+# seconds), and from the watchdog's start to the first finished step.
+# Both sit well below the driver's 600 s limit on the whole command, so a
+# hung collective is reported by the rank itself (reference: the master
+# drops a slave after max(mean + 3 sigma, --job-timeout),
+# veles/server.py:619-635).
+WATCHDOG_STEP_S = 60.0
+WATCHDOG_INIT_S = 300.0
+
+
 def _watchdog(wf, dp):
     """At N > 1: exit 124 with a [watchdog] line when this rank's step
-    makes no progress (decision runs) for VELES_AMD_BENCH_WATCHDOG_S s - a
-    hung collective ends the run instead of holding the node."""
+    makes no progress (decision runs) for VELES_AMD_BENCH_WATCHDOG_S s
+    (default 60) after its first step, or reaches no first step within
+    VELES_AMD_BENCH_WATCHDOG_INIT_S s (default 300) - a hung collective
+    ends the run instead of holding the node."""
     if dp.world_size <= 1:
         return None
     from veles_amd.parallel.faults import Watchdog
-    timeout = float(os.environ.get("VELES_AMD_BENCH_WATCHDOG_S", "600"))
+    timeout = float(os.environ.get("VELES_AMD_BENCH_WATCHDOG_S",
+                                   WATCHDOG_STEP_S))
+    init = float(os.environ.get("VELES_AMD_BENCH_WATCHDOG_INIT_S",
+                                WATCHDOG_INIT_S))
+    wd = None
 
     def expire():
         print("[watchdog] bench.py rank %d: no training step finished for "
-              "%.0f s (a collective waiting on a peer?); exiting 124" %
-              (dp.rank, timeout), file=sys.stderr, flush=True)
+              "%.0f s%s (a collective waiting on a peer?); exiting 124" %
+              (dp.rank, wd._limit(), "" if wd.armed else
+               " before the first step"), file=sys.stderr, flush=True)
         os._exit(124)
-    return Watchdog(timeout, on_expire=expire).install(wf)
+    wd = Watchdog(timeout, on_expire=expire, init_timeout=init)
+    return wd.install(wf)
 
 
 def _stall_for_test(dp):

@@ -105,6 +105,64 @@ def test_http_snapshot_fetched(snapmod, tmp_path):
         httpd.shutdown()
 
 
+def test_loaded_digest_names_the_restored_row(snapmod, tmp_path):
+    """the multi-rank "same snapshot" check digests the bytes a
+    rank restored, not the spec string - a sqlite:// spec without a row id
+    names whatever row is newest when the rank reads it."""
+    from veles_amd.snapshotter import (SnapshotterToDB, import_snapshot,
+                                       loaded_digest)
+    db = str(tmp_path / "d.sqlite")
+    SnapshotterToDB(_wf(snapmod, 1), database=db, prefix="c").export()
+    spec = "sqlite://%s" % db
+    assert import_snapshot(spec).count.n == 1
+    first = loaded_digest(spec)
+    assert first[2] == "row 1"
+    SnapshotterToDB(_wf(snapmod, 2), database=db, prefix="c").export()
+    assert import_snapshot(spec).count.n == 2
+    second = loaded_digest(spec)
+    assert second[2] == "row 2" and second[:2] != first[:2]
+
+
+def test_http_fetch_never_overwrites_and_is_unique(snapmod, tmp_path):
+    """a local file with the URL's basename is kept, and the
+    download lands under a new name."""
+    from veles_amd.snapshotter import (SnapshotterToFile, _fetch,
+                                       loaded_digest, import_snapshot)
+    src = tmp_path / "srv"
+    src.mkdir()
+    path = SnapshotterToFile(_wf(snapmod, 4), directory=str(src),
+                             prefix="cnt", compression="gz").export()
+    handler = functools.partial(http.server.SimpleHTTPRequestHandler,
+                                directory=str(src))
+    httpd = http.server.ThreadingHTTPServer(("127.0.0.1", 0), handler)
+    t = threading.Thread(target=httpd.serve_forever, daemon=True)
+    t.start()
+    try:
+        dl = tmp_path / "dl"
+        dl.mkdir()
+        keep = dl / os.path.basename(path)
+        keep.write_bytes(b"local file")
+        url = "http://127.0.0.1:%d/%s" % (httpd.server_address[1],
+                                          os.path.basename(path))
+        got = _fetch(url, str(dl))
+        assert keep.read_bytes() == b"local file"
+        assert got != str(keep) and got.endswith(".gz")
+        got2 = _fetch(url, str(dl))
+        assert got2 not in (got, str(keep))
+        assert not [f for f in os.listdir(dl) if f.endswith(".part")]
+        from veles_amd.utils.config import root
+        old = root.common.dirs.snapshots
+        root.common.dirs.snapshots = str(dl)
+        try:
+            assert import_snapshot(url).count.n == 4
+        finally:
+            root.common.dirs.snapshots = old
+        d = loaded_digest(url)
+        assert d is not None and d[0] == os.path.getsize(path)
+    finally:
+        httpd.shutdown()
+
+
 def test_cli_resumes_from_sqlite(snapmod, tmp_path):
     from veles_amd.__main__ import Main
     from veles_amd.snapshotter import SnapshotterToDB

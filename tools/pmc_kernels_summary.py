@@ -4,7 +4,7 @@ T, filt = sys.argv[1], sys.argv[2]
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(lambda: collections.defaultdict(int))
 ns = collections.defaultdict(list)
-for p in "ABFW":
+for p in "ABFWM":
     f = glob.glob("gpurun_out/pmc_%s_%s/**/*counter_collection.csv" % (T, p), recursive=True)
     if not f:
         continue
@@ -14,7 +14,8 @@ for p in "ABFW":
             continue
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         calls[k][r["Counter_Name"]] += 1
-        if p == "B" and r["Counter_Name"] == "SQ_WAVE_CYCLES":
+        if p in "BM" and r["Counter_Name"] in ("SQ_WAVE_CYCLES",
+                                               "GRBM_GUI_ACTIVE"):
             ns[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 for k, d in agg.items():
     c = calls[k]
@@ -35,3 +36,10 @@ for k, d in agg.items():
         fb, wb = m.get("FETCH_SIZE", 0) * 1024, m.get("WRITE_SIZE", 0) * 1024
         print("  ms/call %.3f  fetch %.1f MB  write %.1f MB  -> %.2f TB/s" % (
             ms, fb / 1e6, wb / 1e6, (fb + wb) / ms / 1e9))
+    if m.get("GRBM_GUI_ACTIVE"):
+        # MfmaUtil (rocprofiler-sdk counter_defs.yaml): busy cycles summed
+        # over the 1024 SIMDs / (GPU active cycles x SIMDs)
+        print("  MFMA busy %.1f%% of SIMD cycles (CU busy %.1f%%)" % (
+            100 * m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) /
+            (m["GRBM_GUI_ACTIVE"] * 1024),
+            100 * m.get("SQ_BUSY_CU_CYCLES", 0) / (m["GRBM_GUI_ACTIVE"] * 256)))

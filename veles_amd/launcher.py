@@ -104,14 +104,22 @@ class Launcher(Logger):
         """Every rank of a resumed data-parallel job must have restored the
         same snapshot bytes: replicas that resume different epochs / loader
         positions / momenta diverge and deadlock at the next epoch end."""
-        import hashlib
         import os
         from veles_amd.parallel.launch import snapshot_digest
-        if os.path.isfile(self.snapshot_file):
+        from veles_amd.snapshotter import loaded_digest
+        # the bytes this rank restored (import_snapshot records the row /
+        # download it loaded: a sqlite:// spec without a row id names the
+        # NEWEST row, which differs between ranks while a snapshotter
+        # writes or across nodes)
+        got = loaded_digest(self.snapshot_file)
+        if got is not None:
+            mine = tuple(got[:2])
+        elif os.path.isfile(self.snapshot_file):
             mine = snapshot_digest(self.snapshot_file)
-        else:   # sqlite:// or http(s):// (import_snapshot): the spec itself
-            mine = (0, hashlib.sha1(
-                self.snapshot_file.encode()).hexdigest())
+        else:
+            raise RuntimeError(
+                "cannot tell which snapshot bytes %r restored on rank %d" %
+                (self.snapshot_file, self.rank))
         allv = self.dp_.all_gather_object(mine)
         if any(v != allv[0] for v in allv):
             raise RuntimeError(

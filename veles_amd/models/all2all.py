@@ -67,6 +67,12 @@ class All2All(Forward):
         if self.fp8_ and self.fp8_sx_ is None:
             self.fp8_sx_ = fp8.Scaler(self.torch_device, fp8.E4M3)
             self.fp8_sw_ = fp8.Scaler(self.torch_device, fp8.E4M3)
+            fp8.restore_scaler(self, "fp8_sx_")
+            fp8.restore_scaler(self, "fp8_sw_")
+
+    def __getstate__(self):
+        fp8.save_scalers(self, ("fp8_sx_", "fp8_sw_"))
+        return super().__getstate__()
 
     def init_unpickled(self):
         super().init_unpickled()

@@ -13,7 +13,7 @@ from __future__ import annotations
 from veles_amd.accelerated_units import AcceleratedUnit
 from veles_amd.memory import Array
 from veles_amd.models.nn_units import GradientDescentBase
-from veles_amd.prng import random_generator
+from veles_amd.prng import device_seed, random_generator
 from veles_amd import ops
 
 __all__ = ["DropoutForward", "DropoutBackward"]
@@ -29,6 +29,7 @@ class DropoutForward(AcceleratedUnit):
         self.rand = kwargs.get("rand", random_generator.get())
         self.output = Array(shallow_pickle=True)
         self.seed = 0
+        self.seed_dev_saved = None
         self.forward_mode = False
         self.demand("input")
 
@@ -68,11 +69,8 @@ class DropoutForward(AcceleratedUnit):
             # the seed sequence lives on the device (seeded once from the
             # unit's reproducible generator): no host value enters the
             # kernel arguments, so a captured step replays with fresh masks
-            sd = self.seed_dev_
-            if sd is None or sd.device != x.device:
-                self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
-                self.seed_dev_ = sd = torch.tensor(
-                    [self.seed], dtype=torch.int32, device=x.device)
+            # (restored from a snapshot: device_seed.get)
+            sd = device_seed.get(self, x.device, self._draw_seed)
             ops.seed_advance(sd)
             ops.dropout(x, self.dropout_ratio, None, out=y, seed_dev=sd,
                         base=self.index_base(x))
@@ -80,6 +78,14 @@ class DropoutForward(AcceleratedUnit):
         self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
         ops.dropout(x, self.dropout_ratio, self.seed, out=y,
                     base=self.index_base(x))
+
+    def _draw_seed(self):
+        self.seed = int(self.rand.randint(0, 2 ** 31 - 1))
+        return self.seed
+
+    def __getstate__(self):
+        device_seed.save(self)   # exact resume of the device mask stream
+        return super().__getstate__()
 
     def index_base(self, x):
         """Mask index of this rank's first element (see the module doc)."""

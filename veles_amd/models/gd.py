@@ -100,6 +100,10 @@ class GradientDescent(GradientDescentBase):
         super().init_unpickled()
         self.e8_ = self.wt8_ = self.fp8_se_ = None
 
+    def __getstate__(self):
+        fp8.save_scalers(self, ("fp8_se_",))
+        return super().__getstate__()
+
     def _fp8_dgrad_ok(self, fwd):
         from veles_amd.utils.config import root, get
         return getattr(fwd, "fp8_", False) and \
@@ -112,6 +116,7 @@ class GradientDescent(GradientDescentBase):
         [in][out] image (the scale is the copy's)"""
         if self.fp8_se_ is None:
             self.fp8_se_ = fp8.Scaler(e2.device, fp8.E5M2)
+            fp8.restore_scaler(self, "fp8_se_")
         self.e8_ = fp8.quantize(e2, self.fp8_se_, out=self.e8_)
         w8 = fwd.w8_
         if self.wt8_ is None or self.wt8_.shape != (w8.shape[1], w8.shape[0]):

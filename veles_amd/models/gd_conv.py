@@ -41,6 +41,10 @@ class GradientDescentConv(GradientDescentBase):
         self.dy8_fresh_ = False
         self.q8_consumer_ = None
 
+    def __getstate__(self):
+        fp8.save_scalers(self, ("fp8_sdy_",))
+        return super().__getstate__()
+
     def fp8_grad_consumer(self):
         return fp8_grad_consumer(self)
 
@@ -71,6 +75,7 @@ class GradientDescentConv(GradientDescentBase):
         if use8:
             if self.fp8_sdy_ is None:
                 self.fp8_sdy_ = fp8.Scaler(self.torch_device, fp8.E5M2)
+                fp8.restore_scaler(self, "fp8_sdy_")
             # the e5m2 copy comes from the epilogue of the GD that produced
             # err_output when it wrote it this pass
             if not self.dy8_fresh_ or self.dy8_ is None or \

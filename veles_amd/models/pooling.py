@@ -18,7 +18,7 @@ import torch
 from veles_amd.accelerated_units import AcceleratedUnit
 from veles_amd.memory import Array
 from veles_amd.models.nn_units import GradientDescentBase
-from veles_amd.prng import random_generator
+from veles_amd.prng import device_seed, random_generator
 from veles_amd import ops
 
 __all__ = ["Pooling", "MaxPooling", "AvgPooling", "MaxAbsPooling",
@@ -163,6 +163,14 @@ class StochasticPooling(Pooling):
         super().init_unpickled()
         self.seed_dev_ = None
 
+    def _draw_seed(self):
+        self.uniform_seed = int(self.rand.randint(0, 2 ** 31 - 1))
+        return self.uniform_seed
+
+    def __getstate__(self):
+        device_seed.save(self)   # exact resume of the device draws
+        return super().__getstate__()
+
     def run(self):
         x = self._in()
         B, H, W, C = x.shape
@@ -181,11 +189,8 @@ class StochasticPooling(Pooling):
         train = not bool(getattr(self.workflow, "testing", False))
         if x.is_cuda:
             # device-resident seed sequence (graph-safe, like dropout)
-            sd = self.seed_dev_
-            if sd is None or sd.device != x.device:
-                self.uniform_seed = int(self.rand.randint(0, 2 ** 31 - 1))
-                self.seed_dev_ = sd = torch.tensor(
-                    [self.uniform_seed], dtype=torch.int32, device=x.device)
+            # (restored from a snapshot: device_seed.get)
+            sd = device_seed.get(self, x.device, self._draw_seed)
             if train:
                 ops.seed_advance(sd)
             ops.stochastic_pool(x, self.ky, self.kx, self.sliding,

@@ -1115,7 +1115,7 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             dw2 = _workspace(("s2dg", dw.data_ptr()), (OC, KH2, KW2, C2),
                              torch.float32, dw.device, zero=True)
             if not _halo_wgrad(x2, dy, dw2, dbias, N, H2, W2, C2, OC, KH2,
-                               KW2, 0, 0, OH, OW, 1):
+                               KW2, 0, 0, OH, OW, 1, splits):
                 # logged with the logical image shape: the autotuner
                 # replays the call on a plain image (the s2d data has C2
                 # channels)
@@ -1171,7 +1171,7 @@ def conv_wgrad(x, dy, dw, sliding=(1, 1), padding=(0, 0, 0, 0), groups=1,
             return dw
         if (sy, sx) == (1, 1) and _halo_wgrad(x, dy, dw, dbias, N, H, W, C,
                                                OC, KH, KW, pt, pl, OH, OW,
-                                               groups):
+                                               groups, splits):
             return dw
         if splits is None:
             splits = _wgrad_splits_for(
@@ -1201,19 +1201,25 @@ def set_halo_wgrad(on):
 
 
 def _halo_wgrad(x, dy, dw, dbias, N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
-                groups):
+                groups, splits=None):
     """Stride-1 weight gradient on the halo kernel (csrc/kernels/
     wgrad_halo.hip) when the shape takes it: the input window of each
     64-pixel step is staged once and read by every tap; split over pixels
     into workspace slices that a finishing pass adds into dw / dbias in
-    split order (deterministic).  False: the caller uses hvk_conv_wgrad."""
+    split order (deterministic).  ``splits``: the caller's pixel split
+    count (None: the kernel's plan).  False: the caller uses
+    hvk_conv_wgrad."""
+    # the LDS-DMA loads need 16-B aligned X / dY: refuse misaligned views
+    # here (the launch would fail after a plan-only call that said yes)
     if not _HALO_WGRAD or x.dtype != torch.bfloat16 or \
             dy.dtype != torch.bfloat16 or not dw.is_contiguous() or \
-            not x.is_contiguous() or not dy.is_contiguous():
+            not x.is_contiguous() or not dy.is_contiguous() or \
+            x.data_ptr() % 16 or dy.data_ptr() % 16:
         return False
     from veles_amd.ops import _lib
     fn = _lib.lib().hvk_conv_wgrad_halo
-    geo = (N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, 0)
+    geo = (N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+           int(splits) if splits else 0)
     need = fn(_p(x), _p(dy), _p(dw), _p(dbias), None, *geo, _s(x))
     if need < 0:
         return False

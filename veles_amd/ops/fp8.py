@@ -30,6 +30,7 @@ import torch
 from veles_amd.ops import _lib
 
 __all__ = ["E4M3", "E5M2", "Scaler", "registry", "quantize", "gemm",
+           "save_scalers", "restore_scaler",
            "conv_fwd", "conv_dgrad", "conv_wgrad", "permute_for_dgrad",
            "transpose", "dequantize", "HIST"]
 
@@ -129,6 +130,13 @@ class _Registry(object):
             gpu_step.add_(1)
         self.step += 1
 
+    def set_step(self, step):
+        """Restore the roll counter (the history slot the next roll writes)
+        from a snapshot, host and device mirror alike."""
+        self.step = int(step)
+        if self.step_dev is not None:
+            self.step_dev.fill_(self.step)
+
 
 _REGISTRIES = {}
 
@@ -174,6 +182,28 @@ class Scaler(object):
         m = self.state[:HIST].max()
         return torch.where(m > 0, self.fmax_eff / m, torch.ones_like(m))
 
+    def state_dict(self):
+        """Host copy of the scaling state for a snapshot: amax history and
+        current amax, the epilogues' amax shards, the primed flag and the
+        registry's roll counter (exact resume)."""
+        if self.state.is_cuda:
+            torch.cuda.synchronize(self.state.device)
+        return {"fmt": self.fmt, "margin": self.margin,
+                "primed": bool(self.primed),
+                "state": self.state.detach().cpu().numpy().copy(),
+                "shard": self.shard.detach().cpu().numpy().copy(),
+                "step": int(self.registry.step)}
+
+    def load_state_dict(self, d):
+        if int(d["fmt"]) != self.fmt:
+            raise ValueError("fp8 scaler snapshot of format %s restored into "
+                             "a %s scaler" % (d["fmt"], self.fmt))
+        self.margin = d.get("margin", self.margin)
+        self.primed = bool(d["primed"])
+        self.state.copy_(torch.as_tensor(d["state"]))
+        self.shard.copy_(torch.as_tensor(d["shard"]))
+        self.registry.set_step(d["step"])
+
     def prime(self, x):
         if self.primed:
             return
@@ -195,6 +225,25 @@ class Scaler(object):
                 dist.is_initialized():
             # the first scale of every rank from the GLOBAL batch's amax
             dist.all_reduce(st, op=dist.ReduceOp.MAX)
+
+
+def save_scalers(unit, names):
+    """``__getstate__`` helper: the unit's live scalers (attributes
+    ``names``, transient ``*_``) as host dicts in the pickled
+    ``fp8_saved``."""
+    saved = {n: getattr(unit, n).state_dict() for n in names
+             if getattr(unit, n, None) is not None}
+    if saved or getattr(unit, "fp8_saved", None) is None:
+        unit.fp8_saved = saved or None
+
+
+def restore_scaler(unit, name):
+    """Load the snapshot state of scaler ``name`` (just created by the
+    restored unit) once: the resumed run scales exactly as the
+    uninterrupted one would have."""
+    saved = getattr(unit, "fp8_saved", None)
+    if saved and name in saved and getattr(unit, name, None) is not None:
+        getattr(unit, name).load_state_dict(saved.pop(name))
 
 
 def quantize(x, scaler, out=None, record=True):
@@ -369,8 +418,11 @@ def _halo_wgrad8(x8, sx, dy8, sdy, dw, dbias, pt, pl, OH, OW, groups,
     wgrad_halo.hip wgrad_halo8_kernel) when the shape takes it; False
     leaves the call to hvk_conv_wgrad_fp8."""
     from veles_amd import ops
+    # the kernel's LDS-DMA needs 16-B aligned operands: refuse here (the
+    # launch would return -1, an error, after a plan that said yes)
     if not ops._HALO_WGRAD or not dw.is_contiguous() or \
-            not x8.is_contiguous() or not dy8.is_contiguous():
+            not x8.is_contiguous() or not dy8.is_contiguous() or \
+            x8.data_ptr() % 16 or dy8.data_ptr() % 16:
         return False
     N, H, W, C = x8.shape
     OC = dy8.shape[3]

@@ -254,16 +254,23 @@ class SnapshotterToDB(SnapshotterBase):
         return self._destination
 
     @staticmethod
-    def import_from(database, table="veles", row_id=None):
+    def import_from(database, table="veles", row_id=None, spec=None):
         c = sqlite3.connect(database)
         if row_id is None:
-            row = c.execute("SELECT data FROM %s ORDER BY id DESC LIMIT 1" %
-                            table).fetchone()
+            row = c.execute("SELECT id, data FROM %s ORDER BY id DESC LIMIT "
+                            "1" % table).fetchone()
         else:
-            row = c.execute("SELECT data FROM %s WHERE id=?" % table,
+            row = c.execute("SELECT id, data FROM %s WHERE id=?" % table,
                             (row_id,)).fetchone()
         c.close()
-        with gzip.GzipFile(fileobj=io.BytesIO(row[0])) as f:
+        if row is None:
+            raise LookupError("no snapshot row %s in %s table %s" % (
+                "newest" if row_id is None else row_id, database, table))
+        if spec is not None:
+            import hashlib
+            _record_loaded(spec, (len(row[1]), hashlib.sha1(
+                row[1]).hexdigest(), "row %d" % row[0]))
+        with gzip.GzipFile(fileobj=io.BytesIO(row[1])) as f:
             return pickle.load(f)
 
 
@@ -285,8 +292,13 @@ def _split_sqlite(spec):
 
 
 def _fetch(url, directory=None):
-    """Download an http(s) snapshot into the snapshot directory (the name
-    keeps its codec extension) and return the local path."""
+    """Download an http(s) snapshot into the snapshot directory and return
+    the local path.  The name keeps its codec extension; a file of that
+    name already there is never overwritten (the reference's
+    ``wget.download`` picks a new name too): the download gets a
+    process-unique one instead.  The partial file is process-unique as
+    well, so ranks of one node that fetch the same URL at once never write
+    into each other's file."""
     import urllib.parse
     import urllib.request
     directory = directory or get(root.common.dirs.snapshots, ".")
@@ -294,32 +306,61 @@ def _fetch(url, directory=None):
     name = os.path.basename(urllib.parse.urlparse(url).path) or \
         "downloaded.pickle"
     dst = os.path.join(directory, name)
-    tmp = dst + ".part"
-    with urllib.request.urlopen(url, timeout=60) as r, open(tmp, "wb") as f:
-        while True:
-            chunk = r.read(1 << 20)
-            if not chunk:
-                break
-            f.write(chunk)
-    os.replace(tmp, dst)
+    n = 0
+    while os.path.exists(dst):
+        n += 1
+        dst = os.path.join(directory, "dl%d-%d-%s" % (os.getpid(), n, name))
+    tmp = "%s.%d.part" % (dst, os.getpid())
+    try:
+        with urllib.request.urlopen(url, timeout=60) as r, \
+                open(tmp, "wb") as f:
+            while True:
+                chunk = r.read(1 << 20)
+                if not chunk:
+                    break
+                f.write(chunk)
+        os.replace(tmp, dst)
+    finally:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
     return dst
+
+
+# spec -> (size, sha1, source) of the bytes import_snapshot actually loaded
+_LOADED = {}
+
+
+def _record_loaded(spec, digest):
+    _LOADED[spec.strip()] = digest
+
+
+def loaded_digest(spec):
+    """(size, sha1 of the snapshot bytes, where they came from) that
+    ``import_snapshot(spec)`` loaded in this process, or None.  For
+    ``sqlite://`` and ``http(s)://`` specs the spec string alone does not
+    say which bytes a rank restored (the newest row, a re-fetched URL):
+    the launcher compares these digests across ranks instead."""
+    return _LOADED.get(spec.strip())
 
 
 def import_snapshot(spec):
     """``-w`` for every sink (reference veles/__main__.py:539-589): a file
     path, ``sqlite://db[/table[/id]]`` (SnapshotterToDB; newest row when
     the id is omitted) or an ``http(s)://`` URL (fetched into
-    root.common.dirs.snapshots first)."""
+    root.common.dirs.snapshots first).  What was loaded is recorded for
+    ``loaded_digest``."""
     spec = spec.strip()
     if spec.startswith("sqlite://"):
         db, table, rid = _split_sqlite(spec)
         logging.getLogger("Snapshotter").info(
             "Reading %s table %s row %s", db, table,
             "newest" if rid is None else rid)
-        return SnapshotterToDB.import_from(db, table, rid)
-    if spec.startswith(("http://", "https://")):
-        return SnapshotterToFile.import_(_fetch(spec))
+        return SnapshotterToDB.import_from(db, table, rid, spec=spec)
     if spec.startswith("odbc://"):
         raise ValueError("odbc:// snapshots: use the SQLite sink "
                          "(sqlite://<file>[/<table>[/<id>]])")
-    return SnapshotterToFile.import_(spec)
+    path = _fetch(spec) if spec.startswith(("http://", "https://")) else spec
+    from veles_amd.parallel.launch import snapshot_digest
+    if os.path.isfile(path):
+        _record_loaded(spec, snapshot_digest(path) + (path,))
+    return SnapshotterToFile.import_(path)
