@@ -38,8 +38,11 @@ for k, d in agg.items():
             ms, fb / 1e6, wb / 1e6, (fb + wb) / ms / 1e9))
     if m.get("GRBM_GUI_ACTIVE"):
         # MfmaUtil (rocprofiler-sdk counter_defs.yaml): busy cycles summed
-        # over the 1024 SIMDs / (GPU active cycles x SIMDs)
+        # over the 1024 SIMDs / (max over instances of GPU active cycles x
+        # SIMDs).  The csv sums GRBM_GUI_ACTIVE over its 8 XCD instances, so
+        # one instance is the sum / 8 (checked: the 1.16 PF conv3 forward
+        # reads 48 % = 1.16 / 2.5 PF including its pad-tap MFMAs)
+        act = m["GRBM_GUI_ACTIVE"] / 8.0
         print("  MFMA busy %.1f%% of SIMD cycles (CU busy %.1f%%)" % (
-            100 * m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) /
-            (m["GRBM_GUI_ACTIVE"] * 1024),
-            100 * m.get("SQ_BUSY_CU_CYCLES", 0) / (m["GRBM_GUI_ACTIVE"] * 256)))
+            100 * m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (act * 1024),
+            100 * m.get("SQ_BUSY_CU_CYCLES", 0) / (act * 256)))

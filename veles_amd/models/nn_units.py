@@ -60,6 +60,17 @@ def get_param_store(unit):
     return store
 
 
+
+def _sync_device(t):
+    """Wait for ALL streams of ``t``'s device before a host read for a
+    snapshot: the update may have run on the compute stream of the
+    workflow (or inside a replayed HIP graph launched there) or on the
+    update side stream, and ``Tensor.cpu()`` orders only against the
+    CURRENT stream, which outside a workflow run is another one."""
+    if t is not None and getattr(t, "is_cuda", False):
+        import torch
+        torch.cuda.synchronize(t.device)
+
 class Forward(AcceleratedUnit):
     """Base forward layer."""
     hide_from_registry = True
@@ -144,6 +155,7 @@ class Forward(AcceleratedUnit):
         return self._pb_.master
 
     def sync_params_to_host(self):
+        _sync_device(getattr(self._pw_, "master", None))
         if self._pw_ is not None and self._pw_.master is not None:
             self.weights.reset(self._pw_.master.detach().float().cpu().numpy()
                                .reshape(self.weights.mem.shape))
@@ -321,6 +333,7 @@ class GradientDescentBase(AcceleratedUnit):
     def __getstate__(self):
         fwd = getattr(self, "forward_unit", None)
         pw = getattr(fwd, "_pw_", None)  # parameterless layers: pooling...
+        _sync_device(getattr(pw, "mom", None))
         if pw is not None and pw.mom is not None:
             self.accumulated_gradient_weights.reset(
                 pw.mom.detach().float().cpu().numpy())

@@ -126,10 +126,28 @@ class DataParallel(object):
         return out
 
     def shutdown(self):
+        """Destroy the process group while the interpreter is fully alive.
+
+        ``self.group`` held the WORLD ProcessGroup object: with it alive,
+        destroy_process_group() did not destroy the gloo group, whose
+        worker threads then outlived ``main``.  A worker that was still
+        releasing its last work item at interpreter exit (the item's tensors
+        carry Python objects, so the release takes the GIL) hit the
+        finalizing interpreter, which ends such a thread with pthread_exit;
+        the forced unwind through the C++ thread function aborted the rank
+        with "terminate called without an active exception" (backtrace:
+        ProcessGroupGloo::runLoop -> TensorImpl::decref_pyobject ->
+        PyEval_AcquireThread -> pthread_exit; about 1 run in 40 of
+        test_dp_snapshotter_decision_is_collective under load,
+        docs/PARALLEL.md).  Dropping the reference and collecting lets the
+        group's destructor join its threads here instead."""
         from veles_amd.ops import fp8
         fp8.release_dp(self)
+        self.group = None
         if self.multi and dist.is_initialized():
             dist.destroy_process_group()
+        import gc
+        gc.collect()
 
     def __getstate__(self):
         raise TypeError("DataParallel groups are not picklable")
