@@ -547,11 +547,384 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   }
 }
 
+// ---------------------------------------------------------------------------
+// conv_hc32: the same persistent window / chunk pipeline on the 32x32x16
+// bf16 MFMA, where one K step is ONE tap x 16 channels (round 6, VERDICT r5
+// "next" #1): a 3 x 3 stage is 9 MFMA k-steps instead of 5 two-tap 16x16x32
+// steps of which one pads a zero-weight tap - 10 % of the MFMA issue and
+// 2 of 11 weight granules per row (18 % of the stage's weight DMA) go away;
+// a 5 x 5 stage loses 1 of 13 steps.  The 32x32 tile keeps the LDS-read /
+// MFMA ratio of the 16x16 tiles (a 64 x 128 wave tile reads 2 window and 4
+// weight fragments per 256 MFMA cycles).
+//
+// Lanes: B operand (pixels) lane l holds pixel l & 31 of the m-tile, k
+// (channels) 8 (l >> 5) .. + 7 of the tap; A operand (weights) lane l holds
+// LDS weight row l & 31 of the n-tile at the same k.  D[row][col] =
+// D[oc][pixel]: lane l keeps rows (r & 3) + 8 (r >> 2) + 4 (l >> 5) of
+// pixel l & 31; the weight rows are permuted so that these are the 16
+// consecutive output channels 16 (l >> 5) + r of the n-tile (two 16-B
+// stores per pixel and n-tile).
+//
+// Bank conflicts (ds_read_b128 lane groups {0-3,12-15,20-27}, ...): weight
+// rows are T (odd) 32-B granules apart, so 8 consecutive rows sit on 8
+// distinct even 16-B slots; the two 16-B halves of a granule are stored
+// swapped on rows with bit 3 set, which puts rows r and r + 24 / r + 12
+// and r + 20 of a lane group on distinct slots.  Window slots get the same
+// half swap on slots with bit 3 set: 16 consecutive pixels then hit 16
+// distinct bank slots (pixels that straddle a row wrap can still pair up).
+// The DMA writes LDS linearly, so both swaps are applied to the SOURCE
+// address and undone on the read (the same involution on both sides).
+// ABL (diagnostic builds only, -DHVK_HC_ABL; tools/ablate_conv_hc.py): 1 no
+// DMA after the first stage, 2 the next stage's DMA all at the first k-step,
+// 4 no MFMAs, 8 no stage-end DMA wait, 16 the DMA spread over every k-step,
+// 32 no epilogue stores (1, 4, 8, 32 give wrong results by design)
+template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0>
+__global__ void __launch_bounds__(512, 1)
+conv_hc32_kernel(const uint16_t* __restrict__ src,
+                 const uint16_t* __restrict__ wts,
+                 const float* __restrict__ bias, uint16_t* __restrict__ out,
+                 const uint16_t* __restrict__ aux, int act, int aux_act,
+                 HcGeom g) {
+  constexpr int T = KH * KW;
+  static_assert(T % 2 == 1, "odd tap count: conflict-free weight rows");
+  constexpr int NWV = WM * WN;
+  static_assert(NWV == 8, "eight waves");
+  constexpr int MI = 2;                      // 32-pixel m-tiles per wave
+  constexpr int WPX = MI * 32;
+  constexpr int TPX = WM * WPX;
+  constexpr int BN = WN * NJ * 32;
+  constexpr int RB = T * 32;                 // weight row bytes in LDS
+  constexpr int WB = BN * RB;                // weight bytes per stage
+  constexpr int NWP = (WB + 1023) / 1024;
+  constexpr int NWW = (NWP + NWV - 1) / NWV;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  lds_u8* sm = (lds_u8*)smem;
+  // stage: window | weights | bias block (1 KiB, the item's BN output
+  // channels' bias, DMA'd with its last stage)
+  const uint32_t STAGE_B = (uint32_t)g.WIN + NWP * 1024;
+  const uint32_t STAGE = STAGE_B + 1024;
+  const int NBP = g.WIN >> 10;
+  const int NQ = g.CG >> 4;                  // K stages per item
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w % WM, wn = w / WM;
+  const int l31 = lane & 31, lh = lane >> 5;
+
+  // weight DMA: the stage's weights are one contiguous block of the packed
+  // filter bank (hc32_pack_kernel: permuted rows, flipped taps and swapped
+  // halves already in place), so a piece is a linear 1-KiB copy
+  auto wq = [&](int pi) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t ib = (uint32_t)(pi * 1024 + 16 * lane);
+    return ib < (uint32_t)WB ? ib : kBufOOB;
+  };
+
+  const __amdgpu_buffer_rsrc_t rs = dma_rsrc(src);
+  const __amdgpu_buffer_rsrc_t rw = dma_rsrc(wts);
+  const uint32_t rowbytes = (uint32_t)g.W * g.C * 2u;
+  const uint32_t pixbytes = (uint32_t)g.C * 2u;
+
+  auto decode = [&](int it, int& ptl, int& gi, int& nt)
+                    __attribute__((always_inline)) {
+    nt = it % g.NT;
+    const int r = it / g.NT;
+    gi = r % g.G;
+    ptl = r / g.G;
+  };
+  uint32_t pwb[NBW];
+  uint32_t d_cofs = 0, d_wofs = 0, d_bofs = 0;
+  bool d_bias = false;
+  auto prepare = [&](int it, int q) __attribute__((always_inline)) {
+    int ptl, gi, nt;
+    decode(it, ptl, gi, nt);
+    if (q == 0) {   // wave-uniform: a new item
+      const uint32_t p0 = (uint32_t)ptl * TPX;
+      const uint32_t n0 = fdiv(p0, g.fOHW);
+      const uint32_t oh0 = fdiv(p0 - n0 * (uint32_t)g.OHW, g.fOW);
+      const int rc = g.OH - (int)oh0 + KH - 1;
+      const uint32_t gofs = (uint32_t)(gi * g.CG) * 2u;
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        const uint32_t slot =
+            (uint32_t)((w + NWV * i) * 1024 + 16 * lane) >> 5;
+        const int r = (int)fdiv(slot, g.fWp);
+        const int cs = (int)slot - r * g.Wp;
+        int j, lr;
+        if (r < rc) {
+          j = 0;
+          lr = (int)oh0 + r;
+        } else {
+          const int qq = (int)fdiv((uint32_t)(r - rc), g.fHPd);
+          j = 1 + qq;
+          lr = r - rc - qq * g.HPd;
+        }
+        const int ih = lr - g.pt, iw = cs - g.pl;
+        const uint32_t n = n0 + (uint32_t)j;
+        const bool ok = w + NWV * i < NBP && r < 1024 &&
+                        cs < g.OW + KW - 1 && (unsigned)ih < (unsigned)g.H &&
+                        (unsigned)iw < (unsigned)g.W && n < (uint32_t)g.N;
+        // stored half (lane & 1) swapped on slots with bit 3 set
+        const uint32_t half = (uint32_t)((lane & 1) ^ ((slot >> 3) & 1));
+        pwb[i] = ok ? (n * (uint32_t)g.H + (uint32_t)ih) * rowbytes +
+                          (uint32_t)iw * pixbytes + gofs + half * 16u
+                    : kBufOOB;
+      }
+    }
+    d_cofs = (uint32_t)q * 32u;
+    d_wofs = (uint32_t)(((gi * g.NT + nt) * NQ + q) * WB);
+    d_bias = bias && q == NQ - 1 && w == 0;
+    d_bofs = lane < BN / 4 ? (uint32_t)(gi * g.OCg + nt * BN + 4 * lane) * 4u
+                           : kBufOOB;
+  };
+  constexpr int NSLOT = NBW + NWW + 1;
+  const __amdgpu_buffer_rsrc_t rbias = dma_rsrc(bias);
+  auto issue_slot = [&](int q, uint32_t stb) __attribute__((always_inline)) {
+    if (q < NBW) {
+      if (w + NWV * q < NBP)   // wave-uniform
+        dma16(rs, smem + stb + (w + NWV * q) * 1024,
+              pwb[q] >= kBufOOB ? kBufOOB : pwb[q] + d_cofs);
+    } else if (q < NBW + NWW) {
+      const int i = q - NBW;
+      if (w + NWV * i < NWP) {   // wave-uniform
+        const uint32_t o = wq(w + NWV * i);
+        dma16(rw, smem + stb + g.WIN + (w + NWV * i) * 1024,
+              o >= kBufOOB ? kBufOOB : o + d_wofs);
+      }
+    } else if (d_bias) {
+      dma16(rbias, smem + stb + STAGE_B, d_bofs);
+    }
+  };
+  // window slot bytes of this lane's pixel in each m-tile
+  uint32_t bb[MI];
+  auto slots = [&](int it) __attribute__((always_inline)) {
+    int ptl, gi, nt;
+    decode(it, ptl, gi, nt);
+    const uint32_t p0 = (uint32_t)ptl * TPX;
+    const uint32_t n0 = fdiv(p0, g.fOHW);
+    const uint32_t oh0 = fdiv(p0 - n0 * (uint32_t)g.OHW, g.fOW);
+    const int rc = g.OH - (int)oh0 + KH - 1;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const uint32_t p = p0 + wm * WPX + i * 32 + l31;
+      if (p >= (uint32_t)g.P) {   // past the last pixel: slot 0 (finite)
+        bb[i] = 16u * lh;
+        continue;
+      }
+      const uint32_t n = fdiv(p, g.fOHW);
+      const uint32_t pin = p - n * (uint32_t)g.OHW;
+      const uint32_t oh = fdiv(pin, g.fOW);
+      const int ow = (int)(pin - oh * (uint32_t)g.OW);
+      const int j = (int)(n - n0);
+      const int row = j == 0 ? (int)(oh - oh0) : rc + (j - 1) * g.HPd + (int)oh;
+      bb[i] = (uint32_t)(row * g.Wp + ow) * 32u + 16u * lh;
+    }
+  };
+
+  const int nwg = gridDim.x;
+  int item = xcd_remap(blockIdx.x, nwg);
+  if (item >= g.items) return;
+  const __amdgpu_buffer_rsrc_t ro = dma_rsrc(out);
+  auto next = [&](int& it, int& q) __attribute__((always_inline)) {
+    if (++q == NQ) {
+      q = 0;
+      it += nwg;
+    }
+  };
+  prepare(item, 0);
+#pragma unroll
+  for (int q = 0; q < NSLOT; ++q) issue_slot(q, 0);
+  slots(item);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int it1 = item, q1 = 0;
+  next(it1, q1);
+  bool more1 = it1 < g.items;
+  if (more1) prepare(it1, q1);
+
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const uint32_t wrow = (uint32_t)((wn * NJ * 32 + l31) * RB +
+                                   16 * (lh ^ ((l31 >> 3) & 1)));
+  const uint32_t wp32 = (uint32_t)g.Wp * 32u;
+  int q = 0;
+  uint32_t cur = 0;
+  for (;;) {
+    const bool last = q == NQ - 1;
+    int ptl, gi, nt;
+    decode(item, ptl, gi, nt);
+    const uint32_t p0 = (uint32_t)ptl * TPX;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(bb[i]));
+    const uint32_t nxt = cur ^ STAGE;
+    const uint32_t wb = cur + (uint32_t)g.WIN + wrow;
+    // the k-steps (taps) of this stage; the next stage's DMA slots spread
+    // over the first ~2/3 of them
+    constexpr int NKSD = (ABL & 2) ? 1 : (ABL & 16) ? T : (2 * T + 2) / 3;
+    auto rd = [&](int s, bf16x8* a, bf16x8* b) __attribute__((always_inline)) {
+      const uint32_t ofs = (uint32_t)(s / KW) * wp32 + (uint32_t)(s % KW) * 32u;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const uint32_t aa = bb[i] + ofs;
+        b[i] = *(lds_bf16x8*)(sm + cur + (aa ^ ((aa >> 4) & 16u)));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        a[j] = *(lds_bf16x8*)(sm + wb + j * 32 * RB + s * 32);
+    };
+    bf16x8 fa[2][NJ], fb[2][MI];
+    rd(0, fa[0], fb[0]);
+#pragma unroll
+    for (int s = 0; s < T; ++s) {
+      if (s + 1 < T) rd(s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((ABL & 4) == 0) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                fa[s & 1][j], fb[s & 1][i], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          acc[i][0][0] += (float)fb[s & 1][i][0] + (float)fa[s & 1][0][0];
+      }
+      if (more1 && (ABL & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k)
+          if (k * NKSD / NSLOT == s) issue_slot(k, nxt);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // stage (it1, q1) landed; every read of (item, q) done
+    if constexpr ((ABL & 8) == 0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (last) {
+      // lane: pixel l31 of each m-tile, output channels 16 lh + r of each
+      // n-tile (the row permutation): bias, activation, derivative of the
+      // layer below, two 16-B bf16 stores; pixels past the end go to the
+      // out-of-range offset
+      const int chl = wn * NJ * 32 + 16 * lh;   // within the item's BN
+      const int chb = gi * g.OCg + nt * BN + chl;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const uint32_t p = p0 + wm * WPX + i * 32 + l31;
+        const uint32_t pa = min(p, (uint32_t)g.P - 1);
+        const bool ok = p < (uint32_t)g.P;
+        const uint32_t ob = (uint32_t)(((long long)p * g.OCT + chb) * 2);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          float v[16];
+#pragma unroll
+          for (int e = 0; e < 16; e += 4) {
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (bias) {
+              const f32x4 lb = *(const __attribute__((address_space(3)))
+                                      f32x4*)(sm + cur + STAGE_B +
+                                              (chl + 32 * j + e) * 4);
+              bv = make_float4(lb[0], lb[1], lb[2], lb[3]);
+            }
+            v[e] = acc[i][j][e] + bv.x;
+            v[e + 1] = acc[i][j][e + 1] + bv.y;
+            v[e + 2] = acc[i][j][e + 2] + bv.z;
+            v[e + 3] = acc[i][j][e + 3] + bv.w;
+          }
+          act_fwd_n<16>(v, act);
+          if (aux) {
+            float y[16];
+            const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
+            const uint4 a0 = *(const uint4*)ap, a1 = *(const uint4*)(ap + 8);
+            const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w,
+                                    a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              y[2 * e] = __uint_as_float(av[e] << 16);
+              y[2 * e + 1] = __uint_as_float(av[e] & 0xffff0000u);
+            }
+            act_bwd_mul_n<16>(v, y, aux_act);
+          }
+          const uint32_t o = ob + 64 * j;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint4 qv = pack_bf16x8(v + 8 * e);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u32x4{qv.x, qv.y, qv.z, qv.w}, ro,
+                ok && !((ABL & 32) && v[0] != 1234.5f) ? o + 16 * e : kBufOOB,
+                0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      if (more1) slots(it1);
+    }
+    if (!more1) break;
+    item = it1;
+    q = q1;
+    next(it1, q1);
+    more1 = it1 < g.items;
+    if (more1) prepare(it1, q1);
+    cur ^= STAGE;
+  }
+}
+
+// Stage-major filter bank of conv_hc32: packed[g][nt][c][n][t][16] holds,
+// for n-tile nt of group g and 16-channel chunk c, LDS weight row n (output
+// channel g OCg + nt BN + perm(n), the epilogue's row permutation), tap t
+// (flipped for backward-data) and source channels 16 c .. + 15, with the two
+// 8-channel halves swapped on rows with bit 3 set - exactly the stage's LDS
+// image, so the kernel's weight DMA is a contiguous copy.  The per-(row,
+// tap) 32-B gather it replaces touched one 128-B line per 32 B in L2.
+// src: [OCT][T][CG] (the forward filter bank, or backward-data's permutation
+// wt[g][c][kh][kw][oc], which has the same shape for the transposed conv).
+__global__ void hc32_pack_kernel(const uint16_t* __restrict__ src,
+                                 uint16_t* __restrict__ dst, int T, int CG,
+                                 int OCg, int BN, int flip,
+                                 long long pieces) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= pieces) return;
+  const int hs = (int)(q & 1);
+  long long r = q >> 1;
+  const int tp = (int)(r % T);
+  r /= T;
+  const int n = (int)(r % BN);
+  r /= BN;
+  const int NQ = CG >> 4;
+  const int c = (int)(r % NQ);
+  r /= NQ;
+  const int NT = OCg / BN;
+  const int nt = (int)(r % NT);
+  const int gi = (int)(r / NT);
+  const int rr = n & 31;
+  const int o = gi * OCg + nt * BN + (n & ~31) + 16 * ((rr >> 2) & 1) +
+                4 * (rr >> 3) + (rr & 3);
+  const int half = hs ^ ((n >> 3) & 1);
+  const int tap = flip ? T - 1 - tp : tp;
+  const uint4 v = *(const uint4*)(src + ((long long)o * T + tap) * CG +
+                                  c * 16 + half * 8);
+  *(uint4*)(dst + q * 8) = v;
+}
+
 struct HcPlan {
   int var;      // 0: not taken
   size_t lds;
   int grid;
   HcGeom g;
+  int KH, KW;
+  void* wpack;  // conv_hc32: the stage-major filter bank workspace
 };
 
 constexpr int kCUs = 256;
@@ -566,33 +939,46 @@ int g_hc_abl = 0;         // diagnostic instantiation (configurations 5-7)
 // per row) at the price of conflicts on the wrapping fragments
 int g_hc_pad = 8;
 
-struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW; };
+// m32: conv_hc32_kernel (32x32x16 MFMA, NJW = 32-channel n-tiles per
+// wave), else conv_hc_kernel (16x16x32, NJW = 16-channel n-tiles)
+struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW, m32; };
+// conv_hc32 candidates on (hvk_hc32; default on), else only conv_hc_kernel
+int g_hc32 = 1;
+int g_hc_last = 0;   // configuration of the last conv_hc launch (tests)
 // per kernel size, in order of preference (the first whose n-tile divides
 // the group's outputs and whose two stages fit the LDS)
 constexpr HcCand kHcCands[] = {
-    {6, 3, 3, 3, 8, 1, 8, 5},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
-    {7, 3, 3, 3, 8, 1, 6, 5},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
-    {1, 3, 3, 3, 4, 2, 4, 8},   // 256 px x 128 ch
-    {2, 3, 3, 3, 4, 2, 3, 8},   // 256 px x 96 ch
-    {3, 3, 3, 3, 8, 1, 4, 8},   // 512 px x 64 ch: VGG-16 64-channel layers
-    {11, 5, 5, 5, 8, 1, 2, 8},  // 512 px x 32 ch: AlexNet conv2 fwd
-    {4, 5, 5, 5, 4, 2, 2, 8},   // 256 px x 64 ch
-    {5, 5, 5, 5, 8, 1, 3, 8},   // 512 px x 48 ch: AlexNet conv2 dgrad
+    // conv_hc32: one tap x 16 channels per MFMA k-step
+    {21, 3, 3, 3, 8, 1, 4, 5, 1},   // 512 px x 128 ch
+    {22, 3, 3, 3, 8, 1, 3, 5, 1},   // 512 px x 96 ch
+    {23, 3, 3, 3, 8, 1, 2, 8, 1},   // 512 px x 64 ch
+    {6, 3, 3, 3, 8, 1, 8, 5, 0},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
+    {7, 3, 3, 3, 8, 1, 6, 5, 0},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
+    {1, 3, 3, 3, 4, 2, 4, 8, 0},   // 256 px x 128 ch
+    {2, 3, 3, 3, 4, 2, 3, 8, 0},   // 256 px x 96 ch
+    {3, 3, 3, 3, 8, 1, 4, 8, 0},   // 512 px x 64 ch: VGG-16 64-channel layers
+    {11, 5, 5, 5, 8, 1, 2, 8, 0},  // 512 px x 32 ch: AlexNet conv2 fwd
+    {4, 5, 5, 5, 4, 2, 2, 8, 0},   // 256 px x 64 ch
+    {5, 5, 5, 5, 8, 1, 3, 8, 0},   // 512 px x 48 ch: AlexNet conv2 dgrad
     // 512 px x 64 ch in two kh groups (3 + 2 rows per stage): half the
     // weights per stage, but twice the window DMA and stages; AlexNet conv2
     // forward 755 TF against 878 for configuration 4 (forced runs only)
-    {8, 5, 5, 3, 8, 1, 4, 8},
+    {8, 5, 5, 3, 8, 1, 4, 8, 0},
 };
+
+int hc_bn(const HcCand& k) { return k.WN * k.NJW * (k.m32 ? 32 : 16); }
 
 // weight (+ bias block) bytes of one stage
 int hc_nbytes_w(const HcCand& k) {
-  const int T = k.KHS * k.KW, TP = 2 * ((T + 1) / 2) + 1;
+  const int T = k.KHS * k.KW;
+  if (k.m32) return (hc_bn(k) * T * 32 + 1023) / 1024 * 1024 + 1024;
+  const int TP = 2 * ((T + 1) / 2) + 1;
   const int BN = k.WN * k.NJW * 16;
   return (BN * TP * 32 + 1023) / 1024 * 1024 + (k.NJW <= 3 ? 0 : 1024);
 }
 
 HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
-               int KW, int pt, int pl, int groups, bool flip) {
+               int KW, int pt, int pl, int groups, bool flip, bool al16) {
   HcPlan p{};
   HcGeom& g = p.g;
   if (g_hc_variant == 0) return p;
@@ -619,7 +1005,13 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   for (const HcCand& k : kHcCands) {
     if (k.KH != KH || k.KW != KW) continue;
     if (g_hc_variant > 0 && k.var != g_hc_variant) continue;
-    const int BN = k.WN * k.NJW * 16, TPX = k.WM * 64;
+    // conv_hc32: 16-B stores / derivative loads, and at least three K
+    // stages per item (its bias block lives in the stage buffers: with
+    // fewer, a fast wave's bias DMA for the next item could overwrite the
+    // block a slow wave still reads in its epilogue)
+    if (k.m32 && (!g_hc32 || !al16 || CG < 48 || OCT % 8)) continue;
+    if (!k.m32 && k.NJW > 3 && CG < 48) continue;
+    const int BN = hc_bn(k), TPX = k.WM * 64;
     if (OCg % BN) continue;
     // window rows: the most any tile needs (the pattern of tile starts
     // repeats with the image, so one period of starts covers every tile)
@@ -651,6 +1043,8 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
     p.lds = lds;
     p.grid = std::min(g.items, kCUs);
     p.var = k.var;
+    p.KH = KH;
+    p.KW = KW;
     return p;
   }
   return p;
@@ -677,6 +1071,71 @@ hipError_t go_hc(const HcPlan& p, const void* src, const void* wts,
   return launch_status(s);
 }
 
+// packed filter-bank bytes of a conv_hc32 plan (0: not a conv_hc32 plan)
+long long hc32_wpack_bytes(const HcPlan& p) {
+  if (p.var < 21) return 0;
+  const int KH = p.KH, KW = p.KW;
+  return (long long)p.g.G * p.g.OCg * KH * KW * p.g.CG * 2;
+}
+
+template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0>
+hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
+                   const float* bias, void* out, const void* aux, int act,
+                   int aux_act, hipStream_t s) {
+  if (p.g.WIN / 1024 > WM * WN * NBW) return hipErrorInvalidValue;
+  if (p.wpack == nullptr) return hipErrorInvalidValue;
+  {   // the stage-major filter bank, stream-ordered before the conv
+    const long long pieces = hc32_wpack_bytes(p) / 16;
+    hipLaunchKernelGGL(hc32_pack_kernel, dim3((unsigned)((pieces + 255) / 256)),
+                       dim3(256), 0, s, (const uint16_t*)wts,
+                       (uint16_t*)p.wpack, KH * KW, p.g.CG, p.g.OCg,
+                       WN * NJ * 32, p.g.flip, pieces);
+    wts = p.wpack;
+  }
+  auto kern = conv_hc32_kernel<KH, KW, WM, WN, NJ, NBW, ABL>;
+  static bool attr = false;   // once per instantiation, before any capture
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(
+        (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+        160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)p.grid), dim3(512), p.lds, s,
+                     (const uint16_t*)src, (const uint16_t*)wts, bias,
+                     (uint16_t*)out, (const uint16_t*)aux, act, aux_act, p.g);
+  return launch_status(s);
+}
+
+#ifdef HVK_HC_ABL
+template <int KH, int KW, int WM, int WN, int NJ, int NBW>
+hipError_t go_hc32_abl(const HcPlan& p, const void* src, const void* wts,
+                       const float* bias, void* out, const void* aux, int act,
+                       int aux_act, hipStream_t s) {
+  switch (g_hc_abl) {
+#define HC32_ABL(A) \
+    case A: return go_hc32<KH, KW, WM, WN, NJ, NBW, A>(                       \
+        p, src, wts, bias, out, aux, act, aux_act, s);
+    HC32_ABL(1) HC32_ABL(2) HC32_ABL(4) HC32_ABL(8) HC32_ABL(16) HC32_ABL(32)
+    HC32_ABL(9)
+#undef HC32_ABL
+    default: return go_hc32<KH, KW, WM, WN, NJ, NBW, 0>(
+        p, src, wts, bias, out, aux, act, aux_act, s);
+  }
+}
+#endif
+
+// a production launch with an explicit NBW (go_hc's seventh parameter is
+// the ablation selector)
+template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW = kNBW>
+hipError_t go_hc_nbw(const HcPlan& p, const void* src, const void* wts,
+                     const float* bias, void* out, const void* aux, int act,
+                     int aux_act, hipStream_t s) {
+  return go_hc<KH, KW, KHS, WM, WN, NJW, 0, NBW>(p, src, wts, bias, out, aux,
+                                                  act, aux_act, s);
+}
+
+#ifdef HVK_HC_ABL
 template <int KH, int KW, int KHS, int WM, int WN, int NJW, int NBW = kNBW>
 hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
                      const float* bias, void* out, const void* aux, int act,
@@ -693,6 +1152,8 @@ hipError_t go_hc_abl(const HcPlan& p, const void* src, const void* wts,
   }
 }
 
+#endif  // HVK_HC_ABL
+
 hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
                      const float* bias, void* out, const void* aux, int act,
                      int aux_act, hipStream_t s) {
@@ -700,9 +1161,21 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
 #define HC_GO(V, ...) \
     case V: return go_hc<__VA_ARGS__>(p, src, wts, bias, out, aux, act, \
                                       aux_act, s);
+#ifdef HVK_HC_ABL
 #define HC_GO_ABL(V, ...) \
     case V: return go_hc_abl<__VA_ARGS__>(p, src, wts, bias, out, aux, act, \
                                           aux_act, s);
+#define HC32(V, ...) \
+    case V: return go_hc32_abl<__VA_ARGS__>(p, src, wts, bias, out, aux, \
+                                            act, aux_act, s);
+#else
+#define HC_GO_ABL(V, ...) \
+    case V: return go_hc_nbw<__VA_ARGS__>(p, src, wts, bias, out, aux, act, \
+                                          aux_act, s);
+#define HC32(V, ...) \
+    case V: return go_hc32<__VA_ARGS__>(p, src, wts, bias, out, aux, act, \
+                                        aux_act, s);
+#endif
     HC_GO(1, 3, 3, 3, 4, 2, 4)
     HC_GO(2, 3, 3, 3, 4, 2, 3)
     HC_GO(3, 3, 3, 3, 8, 1, 4)
@@ -712,8 +1185,12 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
     HC_GO_ABL(7, 3, 3, 3, 8, 1, 6, 5)
     HC_GO(8, 5, 5, 3, 8, 1, 4)
     HC_GO(11, 5, 5, 5, 8, 1, 2)
-#undef HC_GO
+    HC32(21, 3, 3, 8, 1, 4, 5)
+    HC32(22, 3, 3, 8, 1, 3, 5)
+    HC32(23, 3, 3, 8, 1, 2, 8)
+#undef HC32
 #undef HC_GO_ABL
+#undef HC_GO
     default: return hipErrorInvalidValue;
   }
 }
@@ -728,19 +1205,58 @@ HVK_API void hvk_hc_variant(int v) { g_hc_variant = v; }
 HVK_API void hvk_hc_ablation(int a) { g_hc_abl = a; }
 // window row pitch pad (8 default; see g_hc_pad)
 HVK_API void hvk_hc_pitch_pad(int p) { g_hc_pad = p; }
+// conv_hc32 candidates (32x32x16 MFMA, one tap per k-step): 1 on (default),
+// 0 only the 16x16x32 kernel
+HVK_API void hvk_hc32(int on) { g_hc32 = on; }
+// configuration (kHcCands var) of the last hvk_conv_{fwd,dgrad}_hc launch
+HVK_API int hvk_hc_last_variant() { return g_hc_last; }
 
 // Forward: Y[N][OH][OW][OC] = act(conv(X, W) + bias), stride 1, X bf16 NHWC,
 // W [OC][KH][KW][C/g].  Returns 0, -2 when the shape does not take this
 // kernel (the caller falls back), or a HIP error.
+namespace {
+HcPlan hc_plan_fwd(int N, int H, int W, int C, int OC, int KH, int KW, int pt,
+                   int pl, int OH, int OW, int groups, bool al16) {
+  return hc_plan(N, H, W, C, OH, OW, OC, KH, KW, pt, pl, groups, false, al16);
+}
+// the window source is dY (OH x OW, OC channels), the output dX (H x W, C
+// channels), origin KH - 1 - pt / KW - 1 - pl
+HcPlan hc_plan_dgrad(int N, int H, int W, int C, int OC, int KH, int KW,
+                     int pt, int pl, int OH, int OW, int groups, bool al16) {
+  return hc_plan(N, OH, OW, OC, H, W, C, KH, KW, KH - 1 - pt, KW - 1 - pl,
+                 groups, true, al16);
+}
+}  // namespace
+
+// Bytes of the conv_hc32 packed filter-bank workspace the call with this
+// geometry needs (0: it does not take conv_hc32).  dgrad: the backward-data
+// geometry (hvk_conv_dgrad_hc's arguments); aligned: the output (and the
+// derivative operand) are 16-B aligned.
+HVK_API long long hvk_conv_hc_wpack_bytes(int dgrad, int N, int H, int W,
+                                          int C, int OC, int KH, int KW,
+                                          int pt, int pl, int OH, int OW,
+                                          int groups, int aligned) {
+  HcPlan p = dgrad ? hc_plan_dgrad(N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
+                                   groups, aligned != 0)
+                   : hc_plan_fwd(N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
+                                 groups, aligned != 0);
+  return p.var ? hc32_wpack_bytes(p) : 0;
+}
+
+// wpack: the packed filter-bank workspace (hvk_conv_hc_wpack_bytes; may be
+// null when that is 0)
 HVK_API int hvk_conv_fwd_hc(const void* X, const void* Wt, const float* bias,
                             void* Y, int N, int H, int W, int C, int OC,
                             int KH, int KW, int pt, int pl, int OH, int OW,
-                            int groups, int act, hipStream_t s) {
+                            int groups, int act, void* wpack, hipStream_t s) {
   if (((uintptr_t)X & 15) || ((uintptr_t)Wt & 15) || ((uintptr_t)Y & 7) ||
-      ((uintptr_t)bias & 15))
+      ((uintptr_t)bias & 15) || ((uintptr_t)wpack & 15))
     return -2;
-  HcPlan p = hc_plan(N, H, W, C, OH, OW, OC, KH, KW, pt, pl, groups, false);
-  if (!p.var) return -2;
+  HcPlan p = hc_plan_fwd(N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+                         ((uintptr_t)Y & 15) == 0);
+  if (!p.var || (hc32_wpack_bytes(p) && !wpack)) return -2;
+  p.wpack = wpack;
+  g_hc_last = p.var;
   return (int)hc_launch(p, X, Wt, bias, Y, nullptr, act, 0, s);
 }
 
@@ -749,14 +1265,16 @@ HVK_API int hvk_conv_fwd_hc(const void* X, const void* Wt, const float* bias,
 HVK_API int hvk_conv_dgrad_hc(const void* dY, const void* Wt, void* dX, int N,
                               int H, int W, int C, int OC, int KH, int KW,
                               int pt, int pl, int OH, int OW, int groups,
-                              const void* aux, int aux_act, hipStream_t s) {
+                              const void* aux, int aux_act, void* wpack,
+                              hipStream_t s) {
   if (((uintptr_t)dY & 15) || ((uintptr_t)Wt & 15) || ((uintptr_t)dX & 7) ||
-      ((uintptr_t)aux & 7))
+      ((uintptr_t)aux & 7) || ((uintptr_t)wpack & 15))
     return -2;
-  // the window source is dY (OH x OW, OC channels), the output dX (H x W, C
-  // channels), origin KH - 1 - pt / KW - 1 - pl
-  HcPlan p = hc_plan(N, OH, OW, OC, H, W, C, KH, KW, KH - 1 - pt,
-                     KW - 1 - pl, groups, true);
-  if (!p.var) return -2;
+  HcPlan p = hc_plan_dgrad(N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+                           ((uintptr_t)dX & 15) == 0 &&
+                               ((uintptr_t)aux & 15) == 0);
+  if (!p.var || (hc32_wpack_bytes(p) && !wpack)) return -2;
+  p.wpack = wpack;
+  g_hc_last = p.var;
   return (int)hc_launch(p, dY, Wt, nullptr, dX, aux, 0, aux_act, s);
 }

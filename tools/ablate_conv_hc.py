@@ -1,14 +1,14 @@
-"""Ablation of the channel-chunked halo conv kernel (conv_hc.hip): times the
-diagnostic instantiations (hvk_hc_ablation: 1 no DMA, 2 no epilogue
-stores, 4 no MFMAs, 8 no stage wait / barrier; wrong results by design)
-against the production kernel, interleaved in one process, on AlexNet
-conv1 forward (s2d, configuration 7), conv3 forward (configuration 6) and
-conv2 backward-data (configuration 5).
+"""Ablation of the channel-chunked halo conv kernels (conv_hc.hip): times the
+diagnostic instantiations against the production kernel, interleaved in one
+process.  They exist only in the -DHVK_HC_ABL build
+(``python tools/build_abl.py hc``; run with
+HVK_LIBRARY=build/hcabl/libhvk_hcabl.so).  conv_hc32 (configurations 21 /
+22): 1 no DMA after the first stage, 2 the DMA at the first k-step, 4 no
+MFMAs, 8 no stage-end DMA wait, 16 the DMA over every k-step, 32 no
+epilogue stores; conv_hc_kernel (configuration 5): its own table.
 
-    python tools/ablate_conv_hc.py [batch] [rounds] [ablations, e.g. 0,16,32]
-
-16 / 32 are correct variants (the next stage's DMA over the first third of
-the k-steps / all at the first), not ablations."""
+    HVK_LIBRARY=build/hcabl/libhvk_hcabl.so \
+        python tools/ablate_conv_hc.py [batch] [rounds] [ablations]"""
 import statistics
 import sys
 
@@ -27,13 +27,13 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     lib = _lib.lib()
     ops.set_conv_hc(True, -1)
-    cases = [("conv1_fwd v7", ("fwd", B, 227, 227, 3, 96, 11, 4, 0, 1)),
-             ("conv4_fwd v7", ("fwd", B, 13, 13, 384, 384, 3, 1, 1, 2)),
-             ("conv5_dgrad v7", ("dgrad", B, 13, 13, 384, 256, 3, 1, 1, 2)),
-             ("conv3_fwd v6", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
+    cases = [("conv3_fwd v21", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
+             ("conv4_fwd v22", ("fwd", B, 13, 13, 384, 384, 3, 1, 1, 2)),
+             ("conv5_dgrad v22", ("dgrad", B, 13, 13, 384, 256, 3, 1, 1, 2)),
+             ("conv1_fwd v22", ("fwd", B, 227, 227, 3, 96, 11, 4, 0, 1)),
              ("conv2_dgrad v5", ("dgrad", B, 27, 27, 96, 256, 5, 1, 2, 2))]
     abls = [int(a) for a in sys.argv[3].split(",")] \
-        if len(sys.argv) > 3 else [0, 1, 2, 4, 8, 3, 9]
+        if len(sys.argv) > 3 else [0, 1, 2, 4, 8, 16, 32, 9]
     try:
         for name, shp in cases:
             fl, fn = case(*shp)

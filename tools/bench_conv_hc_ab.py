@@ -82,22 +82,32 @@ def main():
                                        1)),
                   ("vgg_conv3_2_dgrad", ("dgrad", VB, 56, 56, 256, 256, 3, 1,
                                          1, 1))]
-    settings = [("hc", True, -1), ("base", False, -2)] + \
-        [("hc%d" % v, True, v) for v in variants]
+    # hc: the automatic policy (conv_hc32 where it applies); hc16: the same
+    # with the 32x32x16 configurations off; base: no halo conv at all
+    settings = [("hc", True, -2, True), ("hc16", True, -2, False),
+                ("base", False, -2, True)] + \
+        [("hc%d" % v, True, v, True) for v in variants]
     out = {}
     for name, shp in cases:
         fl, fn = case(*shp)
-        res = {k: [] for k, _, _ in settings}
+        res = {k: [] for k, _, _, _ in settings}
+        taken = {}
         for _ in range(rounds):
-            for key, on, var in settings:
+            for key, on, var, m32 in settings:
                 ops.set_conv_hc(on, var)
+                ops.set_conv_hc32(m32)
                 res[key].append(fl / timeit(fn) / 1e12)
+                taken[key] = ops.conv_hc_last_variant() if on else 0
         ops.set_conv_hc(True, -2)
+        ops.set_conv_hc32(True)
         med = {k: statistics.median(v) for k, v in res.items()}
-        out[name] = {"shape": shp, "tflops": med, "runs": res}
+        out[name] = {"shape": shp, "tflops": med, "runs": res,
+                     "variant": taken}
         print("%-18s " % name + "  ".join(
-            "%s %7.1f TF" % (k, med[k]) for k, _, _ in settings) +
-            "  (hc/base %.2fx)" % (med["hc"] / med["base"]), flush=True)
+            "%s %7.1f TF" % (k, med[k]) for k, _, _, _ in settings) +
+            "  (hc/hc16 %.2fx, hc/base %.2fx; hc var %d)" % (
+                med["hc"] / med["hc16"], med["hc"] / med["base"],
+                taken["hc"]), flush=True)
         del fn
         torch.cuda.empty_cache()
     os.makedirs("gpurun_out", exist_ok=True)

@@ -6,13 +6,24 @@ lands in build/abl/libhvk_abl<N>.so and is selected at run time with
 HVK_LIBRARY=<path> (veles_amd/ops/_lib.py), e.g. by
 tools/bench_gemm_ab.py under ``gpu_job.sh benv:HVK_LIBRARY=...``.
 
-    python tools/build_abl.py 1 2 4"""
+    python tools/build_abl.py 1 2 4
+    python tools/build_abl.py hc     # conv_hc.hip: build/hcabl/libhvk_hcabl.so"""
 import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                 ".."))
 from veles_amd.ops import build as B  # noqa: E402
+
+
+def build_hc():
+    """The conv_hc.hip ablation instantiations (-DHVK_HC_ABL, selected at
+    run time by hvk_hc_ablation) in build/hcabl/libhvk_hcabl.so: the
+    production library carries none of them."""
+    B.FLAGS = list(B.FLAGS) + ["-DHVK_HC_ABL"]
+    B.BUILD = os.path.join(B.REPO, "build", "hcabl", "obj")
+    B.LIB = os.path.join(B.REPO, "build", "hcabl", "libhvk_hcabl.so")
+    B.build(verbose=True)
 
 
 def main(levels):
@@ -25,4 +36,7 @@ def main(levels):
 
 
 if __name__ == "__main__":
-    main([int(a) for a in sys.argv[1:]] or [1, 2, 4])
+    if sys.argv[1:] == ["hc"]:
+        build_hc()
+    else:
+        main([int(a) for a in sys.argv[1:]] or [1, 2, 4])

@@ -4,7 +4,7 @@ T, filt = sys.argv[1], sys.argv[2]
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(lambda: collections.defaultdict(int))
 ns = collections.defaultdict(list)
-for p in "ABFWM":
+for p in "ABFWML":
     f = glob.glob("gpurun_out/pmc_%s_%s/**/*counter_collection.csv" % (T, p), recursive=True)
     if not f:
         continue
@@ -36,6 +36,12 @@ for k, d in agg.items():
         fb, wb = m.get("FETCH_SIZE", 0) * 1024, m.get("WRITE_SIZE", 0) * 1024
         print("  ms/call %.3f  fetch %.1f MB  write %.1f MB  -> %.2f TB/s" % (
             ms, fb / 1e6, wb / 1e6, (fb + wb) / ms / 1e9))
+    if "TCC_HIT_sum" in m:
+        hit, miss = m.get("TCC_HIT_sum", 0), m.get("TCC_MISS_sum", 0)
+        print("  L2 hit %.1f%%  L1->L2 read requests %.3g  L1 accesses %.3g"
+              % (100 * hit / max(hit + miss, 1), m.get(
+                  "TCP_TCC_READ_REQ_sum", 0), m.get(
+                  "TCP_TOTAL_CACHE_ACCESSES_sum", 0)))
     if m.get("GRBM_GUI_ACTIVE"):
         # MfmaUtil (rocprofiler-sdk counter_defs.yaml): busy cycles summed
         # over the 1024 SIMDs / (max over instances of GPU active cycles x

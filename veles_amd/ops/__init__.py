@@ -752,18 +752,6 @@ _HALO = os.environ.get("VELES_AMD_HALO", "1") != "0"
 _HALO_DGRAD = os.environ.get("VELES_AMD_HALO_DGRAD", "0") != "0"
 
 
-# weight-stationary stride-1 convs (csrc/kernels/conv_ws.hip): AlexNet conv1
-# (s2d) / conv2 forward, VGG conv1_2 forward and backward-data.  Opt-in
-# until it beats the implicit GEMM (profiles/r5/ab_conv_ws.log)
-_CONV_WS = os.environ.get("VELES_AMD_CONV_WS", "0") != "0"
-
-
-def set_conv_ws(on):
-    """A/B knob of the weight-stationary conv kernels."""
-    global _CONV_WS
-    _CONV_WS = bool(on)
-
-
 # channel-chunked halo convs (csrc/kernels/conv_hc.hip): stride-1 3 x 3 and
 # 5 x 5 forward / backward-data with a per-chunk input window shared by
 # every tap; on by default for the shapes where it measured faster
@@ -779,6 +767,33 @@ def set_conv_hc(on, variant=None):
     _CONV_HC = bool(on)
     if variant is not None and _lib.available():
         _lib.lib().hvk_hc_variant(int(variant))
+
+
+def _hc_wpack(dgrad, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, out,
+              aux, device):
+    """The stage-major filter-bank workspace a conv_hc32 launch packs its
+    weights into (csrc/kernels/conv_hc.hip hc32_pack_kernel), or None when
+    the call does not take conv_hc32.  One buffer per device and fan-out
+    branch, shared by the layers: each launch packs right before its conv
+    on the same stream."""
+    al = out.data_ptr() % 16 == 0 and (aux is None or aux.data_ptr() % 16 == 0)
+    need = int(_lib.lib().hvk_conv_hc_wpack_bytes(
+        dgrad, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, int(al)))
+    if need <= 0:
+        return None
+    return _grow_ws("hc32_wpack", need // 2, torch.bfloat16, device)
+
+
+def set_conv_hc32(on):
+    """A/B knob of conv_hc.hip's 32x32x16-MFMA configurations (one tap per
+    k-step; default on): off leaves the 16x16x32 two-taps-per-step kernel."""
+    if _lib.available():
+        _lib.lib().hvk_hc32(int(bool(on)))
+
+
+def conv_hc_last_variant():
+    """conv_hc.hip configuration of the last halo conv launch (tests)."""
+    return int(_lib.lib().hvk_hc_last_variant())
 
 
 def set_conv_halo(on, dgrad=None):
@@ -810,20 +825,13 @@ def _conv_fwd_call(x, w, bias, out, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
         return fused
     sfx = "" if q8 is None else "_q8"
     extra = [] if q8 is None else list(q8)
-    if _CONV_WS and q8 is None and sy == 1 and sx == 1 and \
-            out.is_contiguous() and x.dtype == torch.bfloat16:
-        rc = _lib.lib().hvk_conv_fwd_ws(
-            _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
-            OH, OW, groups, act, stream)
-        if rc == 0:
-            return False
-        if rc != -2:
-            _lib.check(rc, "hvk_conv_fwd_ws")
     if _CONV_HC and q8 is None and sy == 1 and sx == 1 and \
             out.is_contiguous() and x.dtype == torch.bfloat16:
+        wp = _hc_wpack(0, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+                       out, None, x.device)
         rc = _lib.lib().hvk_conv_fwd_hc(
             _p(x), _p(w), _p(bias), _p(out), N, H, W, C, OC, KH, KW, pt, pl,
-            OH, OW, groups, act, stream)
+            OH, OW, groups, act, _p(wp), stream)
         if rc == 0:
             return False
         if rc != -2:
@@ -968,22 +976,14 @@ def _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out, fq):
 
 def _dgrad_call(dy, wt, out, aux, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
                 OH, OW, groups, aux_act):
-    if _CONV_WS and sx == 1 and sy == 1 and out.is_contiguous() and \
-            dy.dtype == torch.bfloat16 and \
-            (aux is None or aux.is_contiguous()):
-        rc = _lib.lib().hvk_conv_dgrad_ws(
-            _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
-            groups, _p(aux), aux_act, _s(dy))
-        if rc == 0:
-            return
-        if rc != -2:
-            _lib.check(rc, "hvk_conv_dgrad_ws")
     if _CONV_HC and sx == 1 and sy == 1 and out.is_contiguous() and \
             dy.dtype == torch.bfloat16 and \
             (aux is None or aux.is_contiguous()):
+        wp = _hc_wpack(1, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+                       out, aux, dy.device)
         rc = _lib.lib().hvk_conv_dgrad_hc(
             _p(dy), _p(wt), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
-            groups, _p(aux), aux_act, _s(dy))
+            groups, _p(aux), aux_act, _p(wp), _s(dy))
         if rc == 0:
             return
         if rc != -2:

@@ -110,14 +110,14 @@ _SIGS = {
     "hvk_conv_wgrad_halo_splits": [I] * 13,
     "hvk_conv_wgrad_halo_fp8": [P, P, P, P, P] + [I] * 15 + [P, P, I, F, F,
                                                             P],
-    # weight-stationary convs (csrc/kernels/conv_ws.hip)
-    "hvk_conv_fwd_ws": [P, P, P, P] + [I] * 13 + [P],
-    "hvk_conv_dgrad_ws": [P, P, P] + [I] * 12 + [P, I, P],
     # channel-chunked halo convs (csrc/kernels/conv_hc.hip)
-    "hvk_conv_fwd_hc": [P, P, P, P] + [I] * 13 + [P],
-    "hvk_conv_dgrad_hc": [P, P, P] + [I] * 12 + [P, I, P],
+    "hvk_conv_fwd_hc": [P, P, P, P] + [I] * 13 + [P, P],
+    "hvk_conv_dgrad_hc": [P, P, P] + [I] * 12 + [P, I, P, P],
+    "hvk_conv_hc_wpack_bytes": [I] * 14,
     "hvk_hc_variant": [I],
     "hvk_hc_pitch_pad": [I],
+    "hvk_hc32": [I],
+    "hvk_hc_last_variant": [],
     "hvk_set_pool_bwd_variant": [I],
     "hvk_hc_ablation": [I],
     "hvk_take_last_error": [],
@@ -127,7 +127,8 @@ _SIGS = {
 _OPTIONAL = {}
 # functions returning a pointer / a 64-bit int (every other one returns int)
 _PTR_RET = {"hvk_stream_create"}
-_LL_RET = {"hvk_conv_wgrad_halo", "hvk_conv_wgrad_halo_fp8"}
+_LL_RET = {"hvk_conv_wgrad_halo", "hvk_conv_wgrad_halo_fp8",
+           "hvk_conv_hc_wpack_bytes"}
 
 
 def _load():
