@@ -300,6 +300,14 @@ def dp_report(dp, store, backend, wf=None):
         info["grad_dtype"] = store.grad_dtype
         info["overlapped_update"] = bool(store._overlap_update())
         info["graph_backward"] = bool(store.graph_safe())
+        info["graph_backward_mode"] = store.graph_backward_mode()
+        segs = {sg.name: sg for sg in getattr(wf, "graph_segments_", [])} \
+            if wf is not None else {}
+        bw = segs.get("backward")
+        if bw is not None and bw.validations:
+            # each key's first captured pass against the eager pass
+            # (models/params.py CaptureValidator): True = kept
+            info["capture_validated"] = list(bw.validations)
         rep = store.comm_report()
         tl = store.timeline_report()
         if tl is not None:

@@ -578,8 +578,16 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 // DMA after the first stage, 2 the next stage's DMA all at the first k-step,
 // 4 no MFMAs, 8 no stage-end DMA wait, 16 the DMA spread over every k-step,
 // 32 no epilogue stores (1, 4, 8, 32 give wrong results by design)
-template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0>
-__global__ void __launch_bounds__(512, 1)
+// MI: 32-pixel m-tiles per wave.  MI 2 with 8 waves (two per SIMD, 64 x
+// NJ * 32 wave tiles).  MI 4 with 4 waves (one per SIMD, 128 x 128 wave
+// tiles, accumulators in the AGPR half: a third less LDS read traffic per
+// MFMA) compiles with 248 VGPRs spilled (hipcc, ROCm 7.2) and is not
+// instantiated.
+template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0,
+          int MI = 2>
+__global__ void __attribute__((
+    amdgpu_flat_work_group_size(64 * WM * WN, 64 * WM * WN),
+    amdgpu_waves_per_eu(WM * WN / 4, WM * WN / 4)))
 conv_hc32_kernel(const uint16_t* __restrict__ src,
                  const uint16_t* __restrict__ wts,
                  const float* __restrict__ bias, uint16_t* __restrict__ out,
@@ -588,8 +596,7 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
   constexpr int T = KH * KW;
   static_assert(T % 2 == 1, "odd tap count: conflict-free weight rows");
   constexpr int NWV = WM * WN;
-  static_assert(NWV == 8, "eight waves");
-  constexpr int MI = 2;                      // 32-pixel m-tiles per wave
+  static_assert(NWV == 8 || NWV == 4, "eight or four waves");
   constexpr int WPX = MI * 32;
   constexpr int TPX = WM * WPX;
   constexpr int BN = WN * NJ * 32;
@@ -941,7 +948,7 @@ int g_hc_pad = 8;
 
 // m32: conv_hc32_kernel (32x32x16 MFMA, NJW = 32-channel n-tiles per
 // wave), else conv_hc_kernel (16x16x32, NJW = 16-channel n-tiles)
-struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW, m32; };
+struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW, m32, mi = 2; };
 // conv_hc32 candidates on (hvk_hc32; default on), else only conv_hc_kernel
 int g_hc32 = 1;
 int g_hc_last = 0;   // configuration of the last conv_hc launch (tests)
@@ -1011,7 +1018,7 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
     // block a slow wave still reads in its epilogue)
     if (k.m32 && (!g_hc32 || !al16 || CG < 48 || OCT % 8)) continue;
     if (!k.m32 && k.NJW > 3 && CG < 48) continue;
-    const int BN = hc_bn(k), TPX = k.WM * 64;
+    const int BN = hc_bn(k), TPX = k.WM * (k.m32 ? 32 * k.mi : 64);
     if (OCg % BN) continue;
     // window rows: the most any tile needs (the pattern of tile starts
     // repeats with the image, so one period of starts covers every tile)
@@ -1078,7 +1085,8 @@ long long hc32_wpack_bytes(const HcPlan& p) {
   return (long long)p.g.G * p.g.OCg * KH * KW * p.g.CG * 2;
 }
 
-template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0>
+template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0,
+          int MI = 2>
 hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
                    const float* bias, void* out, const void* aux, int act,
                    int aux_act, hipStream_t s) {
@@ -1092,7 +1100,7 @@ hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
                        WN * NJ * 32, p.g.flip, pieces);
     wts = p.wpack;
   }
-  auto kern = conv_hc32_kernel<KH, KW, WM, WN, NJ, NBW, ABL>;
+  auto kern = conv_hc32_kernel<KH, KW, WM, WN, NJ, NBW, ABL, MI>;
   static bool attr = false;   // once per instantiation, before any capture
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(
@@ -1101,7 +1109,7 @@ hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)p.grid), dim3(512), p.lds, s,
+  hipLaunchKernelGGL(kern, dim3((unsigned)p.grid), dim3(64 * WM * WN), p.lds, s,
                      (const uint16_t*)src, (const uint16_t*)wts, bias,
                      (uint16_t*)out, (const uint16_t*)aux, act, aux_act, p.g);
   return launch_status(s);

@@ -259,3 +259,144 @@ def test_gradient_buckets_keep_a_small_tail():
     assert sum(p.size for p in st.buckets[-1]) * 4 <= 2 << 20
     assert [p for b in st.buckets for p in b] == sorted(
         st.params, key=lambda p: p.offset)
+
+
+# -------------------------------------------------- validated capture
+class _Val(object):
+    """Validator double: device state = the units' counter dict."""
+
+    def __init__(self, dev, ok=True):
+        self.dev = dev
+        self.ok = ok
+        self.calls = []
+
+    def wanted(self):
+        return True
+
+    def save(self):
+        return dict(self.dev)
+
+    def restore(self, snap):
+        self.dev.clear()
+        self.dev.update(snap)
+
+    def result(self):
+        return dict(self.dev)
+
+    def compare(self, snap, got, ref):
+        self.calls.append((snap, got, ref))
+        return self.ok and got == ref
+
+    def agree(self, ok):
+        return ok
+
+
+@pytest.mark.parametrize("ok", [True, False])
+def test_validated_capture_keeps_or_pins(ok):
+    """The first captured pass is compared with an eager re-run of the same
+    pass from the same state: kept on a match, pinned eager on a mismatch;
+    the device state after the pass is the eager pass's either way (one
+    pass worth of work, not two)."""
+    log, dev = [], {}
+    units = [U("a", log, dev), U("b", log, dev)]
+    key = [("train", 8)]
+    v = _Val(dev, ok)
+    seg = Recording("t", units, lambda: key[0], warmup=1, validator=v)
+    _pass(seg)                      # eager warmup
+    assert dev == {"a": 1, "b": 1}
+    _pass(seg)                      # capture + replay, then the eager check
+    assert seg.validations == [ok] and len(v.calls) == 1
+    snap, got, ref = v.calls[0]
+    assert snap == {"a": 1, "b": 1} and got == ref == {"a": 2, "b": 2}
+    assert dev == {"a": 2, "b": 2}
+    _pass(seg)
+    assert dev == {"a": 3, "b": 3}
+    if ok:
+        assert seg.replays == 1 and key[0] not in seg.eager_keys
+    else:
+        assert seg.replays == 0 and key[0] in seg.eager_keys
+
+
+def _validate_rank(rank, port, fail_rank, q):
+    import os
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": "2",
+                       "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    if fail_rank is not None:
+        os.environ["VELES_AMD_DP_VALIDATE_FAIL_RANK"] = str(fail_rank)
+    import torch
+    from veles_amd.models.params import CaptureValidator
+    from veles_amd.parallel.dp import DataParallel
+    dp = DataParallel(backend="gloo", timeout_s=60)
+
+    class Store(object):
+        pass
+    st = Store()
+    st.dp = dp
+    st.master = torch.zeros(8)
+    st.params = []
+    val = CaptureValidator(st)
+    log, dev = [], {}
+    units = [U("a", log, dev), U("b", log, dev)]
+    seg = Recording("t", units, lambda: "k", warmup=1, validator=val)
+    val.wanted = lambda: True
+    val.save = lambda: {"master": st.master.clone()}
+    val.restore = lambda snap: None
+    for _ in range(3):
+        _pass(seg)
+    q.put((rank, seg.validations, "k" in seg.eager_keys, seg.replays))
+    dp.shutdown()
+
+
+@pytest.mark.parametrize("fail_rank", [None, 1])
+def test_validated_capture_agrees_over_gloo(fail_rank):
+    """Two gloo ranks: a mismatch forced on rank 1 alone
+    (VELES_AMD_DP_VALIDATE_FAIL_RANK) pins the key to eager mode on BOTH
+    ranks; with no mismatch both keep their graph."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_validate_rank, args=(r, port, fail_rank, q))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert [p.exitcode for p in ps] == [0, 0]
+    for rank, vals, pinned, replays in res:
+        if fail_rank is None:
+            assert vals == [True] and not pinned and replays == 1
+        else:
+            assert vals == [False] and pinned and replays == 0
+
+
+def test_capture_validator_compares_updates_per_tensor():
+    """A wrong update of one small tensor is caught although the weights
+    themselves differ by ~1e-4 of their size (the comparison is on the
+    updates, tensor by tensor)."""
+    from veles_amd.models.params import CaptureValidator
+
+    class P(object):
+        def __init__(self, name, offset, size):
+            self.owner, self.name = None, name
+            self.offset, self.size = offset, size
+
+    class Store(object):
+        dp = None
+        params = [P("big", 0, 1000), P("small", 1000, 10)]
+    v = CaptureValidator(Store())
+    before = torch.ones(1010)
+    upd = torch.randn(1010) * 1e-4
+    ref = before + upd
+    assert v.compare({"master": before}, ref.clone(), ref)
+    got = ref.clone()
+    got[1000:] = before[1000:] - upd[1000:]    # the small tensor's sign flipped
+    assert not v.compare({"master": before}, got, ref)
+    noisy = ref + torch.randn(1010) * 1e-9       # f32-atomic noise level
+    assert v.compare({"master": before}, noisy, ref)

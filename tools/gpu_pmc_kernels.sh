@@ -13,6 +13,8 @@ for pass in ${PASSES:-A B F W M}; do
     W) ctr="WRITE_SIZE" ;;
     M) ctr="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16" ;;
     L) ctr="TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" ;;
+    D) ctr="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_LDS SQ_INST_LEVEL_LDS SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE" ;;
+    X) ctr="SQ_VALU_MFMA_COEXEC_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" ;;
   esac
   tools/gpu_step.sh 200 gpurun_out/pmc_${T}_$pass.log timeout -s KILL 150 \
     rocprofv3 --kernel-trace --pmc $ctr -d "$R/gpurun_out/pmc_${T}_$pass" \

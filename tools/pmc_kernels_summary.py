@@ -4,7 +4,7 @@ T, filt = sys.argv[1], sys.argv[2]
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(lambda: collections.defaultdict(int))
 ns = collections.defaultdict(list)
-for p in "ABFWML":
+for p in "ABFWMLDX":
     f = glob.glob("gpurun_out/pmc_%s_%s/**/*counter_collection.csv" % (T, p), recursive=True)
     if not f:
         continue
@@ -36,6 +36,24 @@ for k, d in agg.items():
         fb, wb = m.get("FETCH_SIZE", 0) * 1024, m.get("WRITE_SIZE", 0) * 1024
         print("  ms/call %.3f  fetch %.1f MB  write %.1f MB  -> %.2f TB/s" % (
             ms, fb / 1e6, wb / 1e6, (fb + wb) / ms / 1e9))
+    if "SQ_LDS_IDX_ACTIVE" in m and m.get("GRBM_GUI_ACTIVE"):
+        # LDS busy: index-active cycles summed over the CUs (per-SIMD
+        # counters sum over 4 SIMDs) against the GPU-active cycles
+        act = m["GRBM_GUI_ACTIVE"] / 8.0
+        print("  LDS active %.1f%% of CU cycles, bank conflicts %.1f%% of "
+              "them, LDS wait %.1f%% of wave cycles" % (
+                  100 * m["SQ_LDS_IDX_ACTIVE"] / (act * 256 * 4),
+                  100 * m.get("SQ_LDS_BANK_CONFLICT", 0) /
+                  max(m["SQ_LDS_IDX_ACTIVE"], 1),
+                  100 * m.get("SQ_WAIT_INST_LDS", 0) /
+                  max(m.get("SQ_WAVE_CYCLES", 1), 1)))
+    if "SQ_VALU_MFMA_COEXEC_CYCLES" in m and m.get("GRBM_GUI_ACTIVE"):
+        act = m["GRBM_GUI_ACTIVE"] / 8.0
+        print("  MFMA busy %.1f%%, MFMA+VALU co-exec %.1f%% of SIMD cycles; "
+              "MFMA / wave %.0f" % (
+                  100 * m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (act * 1024),
+                  100 * m["SQ_VALU_MFMA_COEXEC_CYCLES"] / (act * 1024),
+                  m.get("SQ_INSTS_MFMA", 0) / max(m.get("SQ_WAVES", 1), 1)))
     if "TCC_HIT_sum" in m:
         hit, miss = m.get("TCC_HIT_sum", 0), m.get("TCC_MISS_sum", 0)
         print("  L2 hit %.1f%%  L1->L2 read requests %.3g  L1 accesses %.3g"

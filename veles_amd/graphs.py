@@ -238,8 +238,15 @@ class GraphSegment(object):
     MAX_GRAPHS = 8
 
     def __init__(self, name, units, key_fn, inputs_fn=None, warmup=2,
-                 pre_hooks=(), replay_hooks=(), state_hooks=()):
+                 pre_hooks=(), replay_hooks=(), state_hooks=(),
+                 validator=None):
         self.name = name
+        # validator (optional): checks a key's first captured pass against
+        # an eager re-run of the same pass from the same state before the
+        # graph is kept (the multi-rank backward, :meth:`_validate`)
+        self.validator = validator
+        self.validations = []
+        self._vsnap = None
         self.units = list(units)
         self.head = self.units[0]
         self.tail = self.units[-1]
@@ -333,6 +340,8 @@ class GraphSegment(object):
         self.cur = _Captured(graph, key, [(a, a._devmem)
                                           for a in self.inputs_fn()])
         self._saved = [save() for save, _ in self.state_hooks]
+        v = self.validator
+        self._vsnap = v.save() if v is not None and v.wanted() else None
         self.ctx = ctx
         self.ctx.__enter__()
         self.mode = "capture"
@@ -374,12 +383,41 @@ class GraphSegment(object):
                 self._restore_state()
                 self._rerun_eager(len(self.units))
                 return
-            self._saved = None
+            saved, self._saved = self._saved, None
             self._record(cur)
             self.graphs[cur.key] = cur
             self.captures += 1
             cur.graph.replay()  # capture records; this pass still has to run
+            if self._vsnap is not None:
+                self._validate(cur, saved)
         self.mode = None
+
+    def _validate(self, cur, saved):
+        """The key's first captured pass against the same pass run eagerly:
+        the replayed result is kept aside, the host state (``state_hooks``)
+        and the validator's device state are put back to what they were
+        before the pass, the units run eagerly (collectives included: every
+        rank does the same), and the validator compares the two results and
+        agrees on the verdict across ranks.  A mismatch on any rank pins
+        the key to eager mode everywhere; the eager pass's state stands
+        either way.  Costs one extra pass, once per key."""
+        v, snap = self.validator, self._vsnap
+        self._vsnap = None
+        got = v.result()
+        self._saved = saved
+        self._restore_state()
+        v.restore(snap)
+        self.mode = "eager"
+        self._rerun_eager(len(self.units))
+        ok = bool(v.agree(v.compare(snap, got, v.result())))
+        self.validations.append(ok)
+        if not ok:
+            self.failures += 1
+            self._pin_eager(cur.key, RuntimeError(
+                "the captured pass differs from the eager pass"))
+        else:
+            _log.info("%s: captured pass of %r matches the eager pass",
+                      self.name, cur.key)
 
     def _record(self, cur):
         import torch
@@ -501,6 +539,7 @@ def install_step_graphs(wf, warmup=2):
             "backward", gds, bkey, inputs, warmup=warmup,
             pre_hooks=[store.refresh_table],
             replay_hooks=[store.replayed_step],
-            state_hooks=[(store.host_state, store.restore_host_state)]))
+            state_hooks=[(store.host_state, store.restore_host_state)],
+            validator=store.capture_validator()))
     wf.graph_segments_ = segs
     return segs

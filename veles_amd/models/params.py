@@ -16,6 +16,7 @@ Master weights are float32; the compute copy is the device compute dtype
 """
 from __future__ import annotations
 
+import logging
 import os
 
 import numpy
@@ -35,6 +36,8 @@ def _cover(segs, total):
     if pos < total:
         out.append((pos, total, 0.0, 0.0, 0.0, 0.0))
     return out
+
+_log = logging.getLogger("params")
 
 
 class Param(object):
@@ -760,16 +763,32 @@ class ParameterStore(object):
             return False
         if not self._multi():
             return True
+        return self.graph_backward_mode() != "eager" and \
+            not getattr(self.dp, "host_blocking_wait", True)
+
+    def graph_backward_mode(self):
+        """How a multi-rank backward runs (``engine.dp.graph_backward`` /
+        VELES_AMD_DP_GRAPH_BACKWARD): "eager" (0 / False), "capture" (1 /
+        True) or "validate" - captured, but each key's first captured pass
+        is checked against the same pass run eagerly from the same state on
+        every rank, and kept only if all ranks agree (:class:`
+        CaptureValidator`).  Default: "capture" on a one-rank (solo) RCCL
+        group, where it was measured against dp1; "eager" with real peers
+        (no multi-GPU run of the captured collectives yet)."""
         from veles_amd.utils.config import root, get
-        # default: captured only on a one-rank (solo) RCCL group, where it
-        # was measured against dp1; with real peers the backward stays eager
-        # (RCCL collectives under graph capture have no multi-GPU parity
-        # run yet; the eager step is GPU-bound, so it costs no throughput)
-        # until engine.dp.graph_backward / VELES_AMD_DP_GRAPH_BACKWARD=1
-        default = bool(getattr(self.dp, "solo", False))
-        on = os.environ.get("VELES_AMD_DP_GRAPH_BACKWARD", "1" if get(
-            root.common.engine.dp.graph_backward, default) else "0") != "0"
-        return on and not getattr(self.dp, "host_blocking_wait", True)
+        default = "capture" if getattr(self.dp, "solo", False) else "eager"
+        v = os.environ.get("VELES_AMD_DP_GRAPH_BACKWARD")
+        if v is None:
+            v = get(root.common.engine.dp.graph_backward, default)
+        v = str(v).lower()
+        if v in ("0", "false", "eager", "none", ""):
+            return "eager"
+        if v in ("validate", "validated", "auto"):
+            return "validate"
+        return "capture"
+
+    def capture_validator(self):
+        return CaptureValidator(self)
 
     def _multi(self):
         """Gradients go through collectives (``DataParallel.multi``)."""
@@ -856,3 +875,100 @@ class ParameterStore(object):
         if self.lp is not None:
             self.lp.copy_(self.master)
         self.steps = st.get("steps", 0)
+
+
+class CaptureValidator(object):
+    """Checks a multi-rank backward's first captured pass (graphs.py
+    ``GraphSegment._validate``): the device state the backward advances -
+    master weights, momentum (and the second solver state), the bf16
+    compute copy, the gradient buffer, the fp8 scaler rows and roll counter
+    - is snapshotted before the pass and restored for the eager re-run; the
+    two passes' weight UPDATES (not the weights: one step moves a weight by
+    ~1e-4 of itself, a wrong gradient would hide under a weight tolerance)
+    must agree per parameter tensor to ``rtol`` (f32-atomic split-K sums
+    make the kernels' results differ in the last bits from run to run), and
+    every rank must agree (one MAX all-reduce of a mismatch flag)."""
+
+    rtol = 1e-3
+
+    def __init__(self, store):
+        self.store = store
+
+    def wanted(self):
+        st = self.store
+        return st._multi() and (
+            st.graph_backward_mode() == "validate" or
+            os.environ.get("VELES_AMD_DP_VALIDATE_CAPTURE", "0") != "0")
+
+    def _fp8(self):
+        dev = getattr(self.store, "device", None)
+        if dev is None or not getattr(dev, "fp8", False):
+            return None
+        from veles_amd.ops import fp8
+        return fp8.registry(dev.torch_device)
+
+    def save(self):
+        st = self.store
+        snap = {k: getattr(st, k).clone() for k in
+                ("master", "mom", "mom2", "lp", "grad")
+                if getattr(st, k, None) is not None}
+        reg = self._fp8()
+        if reg is not None:
+            snap["fp8"] = ([b.clone() for b in reg.blocks],
+                           [b.clone() for b in reg.shard_blocks], reg.step)
+        return snap
+
+    def restore(self, snap):
+        st = self.store
+        for k, v in snap.items():
+            if k != "fp8":
+                getattr(st, k).copy_(v)
+        if "fp8" in snap:
+            reg = self._fp8()
+            blocks, shards, step = snap["fp8"]
+            for b, v in zip(reg.blocks, blocks):
+                b.copy_(v)
+            for b, v in zip(reg.shard_blocks, shards):
+                b.copy_(v)
+            reg.set_step(step)
+
+    def result(self):
+        return self.store.master.clone()
+
+    def compare(self, snap, got, ref):
+        """True when the captured pass's update matches the eager pass's,
+        tensor by tensor (``forced mismatch``: VELES_AMD_DP_VALIDATE_FAIL_RANK
+        = r makes rank r report one, for tests)."""
+        import torch
+        r = os.environ.get("VELES_AMD_DP_VALIDATE_FAIL_RANK")
+        if r is not None and int(r) == int(getattr(self.store.dp, "rank", 0)):
+            return False
+        before = snap["master"]
+        dg, de = got - before, ref - before
+        for p in self.store.params:
+            if p.offset is None:
+                continue
+            a = dg[p.offset:p.offset + p.size]
+            b = de[p.offset:p.offset + p.size]
+            d = float(torch.linalg.vector_norm((a - b).float()))
+            n = float(torch.linalg.vector_norm(b.float()))
+            if not d <= self.rtol * n + 1e-12:
+                _log.warning("captured backward differs from the eager one "
+                             "at %s: |d update| %.3g vs |update| %.3g",
+                             "%s.%s" % (getattr(p.owner, "name", "?"),
+                                        p.name), d, n)
+                return False
+        return True
+
+    def agree(self, ok):
+        """True only if every rank's pass matched."""
+        import torch
+        dp = self.store.dp
+        if dp is None or getattr(dp, "world_size", 1) <= 1:
+            return ok
+        dev = self.store.master.device if dp.backend == "nccl" else "cpu"
+        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float32,
+                         device=dev)
+        dp.all_reduce_max(t)
+        return float(t.cpu()[0]) == 0.0
+
