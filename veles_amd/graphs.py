@@ -39,9 +39,11 @@ any such unit in a segment keeps that segment eager.  A capture that fails
 pins that key to eager mode; host state that the discarded capture
 advanced (the parameter store's step counters, the fp8 history step) is
 restored first (``state_hooks``).  Multi-rank workflows over RCCL can
-capture the backward too, collectives included (default on a one-rank
-group; at N > 1 opt-in with ``root.common.engine.dp.graph_backward =
-True`` or ``VELES_AMD_DP_GRAPH_BACKWARD=1`` until a multi-GPU parity run): the bucketed all-reduces are
+capture the backward too, collectives included (``engine.dp.graph_backward``:
+captured on a one-rank group; at N > 1 "validate" - the first captured
+pass of a key is checked against an eager re-run of the same pass on every
+rank before the graph is kept, :meth:`GraphSegment._validate`): the
+bucketed all-reduces are
 enqueued by the GD units in the same order at every rank and RCCL
 collectives are stream-capturable, so the graph holds the compute stream's
 kernels, each bucket's all-reduce on the process group's stream (forked

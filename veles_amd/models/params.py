@@ -764,7 +764,8 @@ class ParameterStore(object):
         if not self._multi():
             return True
         return self.graph_backward_mode() != "eager" and \
-            not getattr(self.dp, "host_blocking_wait", True)
+            not getattr(self.dp, "host_blocking_wait", True) and \
+            not getattr(self, "capture_rejected_", False)
 
     def graph_backward_mode(self):
         """How a multi-rank backward runs (``engine.dp.graph_backward`` /
@@ -773,10 +774,14 @@ class ParameterStore(object):
         is checked against the same pass run eagerly from the same state on
         every rank, and kept only if all ranks agree (:class:`
         CaptureValidator`).  Default: "capture" on a one-rank (solo) RCCL
-        group, where it was measured against dp1; "eager" with real peers
-        (no multi-GPU run of the captured collectives yet)."""
+        group, "validate" with real peers.  Through a one-rank RCCL group at
+        AlexNet b3072 (profiles/r6/n1_path_b3072_r6d.md): dp1 185.7-186.6k
+        img/s, eager 181.6-182.5k (-2.2 %; with branch-stream weight
+        gradients 175.3-175.7k), captured 185.3-186.1k, validated capture
+        186.3-186.5k with the validation passing."""
         from veles_amd.utils.config import root, get
-        default = "capture" if getattr(self.dp, "solo", False) else "eager"
+        default = "capture" if getattr(self.dp, "solo", False) else \
+            "validate"
         v = os.environ.get("VELES_AMD_DP_GRAPH_BACKWARD")
         if v is None:
             v = get(root.common.engine.dp.graph_backward, default)
@@ -961,14 +966,19 @@ class CaptureValidator(object):
         return True
 
     def agree(self, ok):
-        """True only if every rank's pass matched."""
+        """True only if every rank's pass matched.  A rejection turns the
+        store's multi-rank backward eager for good (``graph_safe``), and
+        with it the branch-stream weight gradients, which measured slower
+        in an eager multi-rank step."""
         import torch
         dp = self.store.dp
-        if dp is None or getattr(dp, "world_size", 1) <= 1:
-            return ok
-        dev = self.store.master.device if dp.backend == "nccl" else "cpu"
-        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float32,
-                         device=dev)
-        dp.all_reduce_max(t)
-        return float(t.cpu()[0]) == 0.0
+        if dp is not None and getattr(dp, "world_size", 1) > 1:
+            dev = self.store.master.device if dp.backend == "nccl" else "cpu"
+            t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float32,
+                             device=dev)
+            dp.all_reduce_max(t)
+            ok = float(t.cpu()[0]) == 0.0
+        if not ok:
+            self.store.capture_rejected_ = True
+        return ok
 
