@@ -6,9 +6,9 @@ continues the same trajectory).
 A workflow trains k steps, is pickled exactly as the snapshotter pickles it
 (``pickle.dumps(workflow)``), restored into a fresh workflow object,
 re-initialised on the device and trained m more steps.  Its master weights
-must equal those of an uninterrupted k + m run: bit for bit when two
-uninterrupted runs agree bit for bit (the kernels of these nets are
-deterministic), else within the spread of two uninterrupted runs.  The
+must equal those of an uninterrupted k + m run bit for bit, in the
+deterministic mode (``ops.set_deterministic``: no f32-atomic reductions;
+two uninterrupted runs are checked to be bit-identical first).  The
 device-resident state that transient attributes used to drop is covered:
 
 * the dropout / stochastic-pooling seed sequence (``seed_dev_``, advanced on
@@ -136,23 +136,31 @@ def _resumed(layers, dataset, backend, batch, k, m, n_classes=None,
 
 def _check(layers, dataset, backend, batch, k, m, n_classes=None,
            control=True):
-    ref = _master(_run_through(layers, dataset, backend, batch, k + m,
+    # deterministic mode (ops.set_deterministic): no f32-atomic reductions
+    # in the gradient path, so two uninterrupted runs are bit-identical and
+    # the resumed run must be too
+    from veles_amd import ops
+    ops.set_deterministic(True)
+    try:
+        ref = _master(_run_through(layers, dataset, backend, batch, k + m,
+                                   n_classes))
+        ref2 = _master(_run_through(layers, dataset, backend, batch, k + m,
+                                    n_classes))
+        got = _master(_resumed(layers, dataset, backend, batch, k, m,
                                n_classes))
-    ref2 = _master(_run_through(layers, dataset, backend, batch, k + m,
-                                n_classes))
-    got = _master(_resumed(layers, dataset, backend, batch, k, m, n_classes))
+        bad = _master(_resumed(layers, dataset, backend, batch, k, m,
+                               n_classes, drop_seed=True)) if control \
+            else None
+    finally:
+        ops.set_deterministic(False)
     spread = float((ref2 - ref).norm())
     diff = float((got - ref).norm())
     scale = float(ref.norm())
     assert torch.isfinite(got).all()
-    if spread == 0.0:
-        assert torch.equal(got, ref), \
-            "resumed run differs from the uninterrupted one: %g" % diff
-    else:
-        assert diff <= 2.0 * spread + 1e-7 * scale, (diff, spread)
+    assert spread == 0.0, "deterministic mode is not: run-to-run %g" % spread
+    assert torch.equal(got, ref), \
+        "resumed run differs from the uninterrupted one: %g" % diff
     if control:
-        bad = _master(_resumed(layers, dataset, backend, batch, k, m,
-                               n_classes, drop_seed=True))
         lost = float((bad - ref).norm())
         assert lost > 100.0 * max(diff, spread, 1e-9 * scale), \
             "control without the device seed is not distinguishable: " \

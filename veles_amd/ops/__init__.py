@@ -277,7 +277,9 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
         atomic = 2 if overwrite else (1 if accumulate else 0)
         if splits > 1 and not accumulate:
             raise ValueError("split-K requires accumulate=True")
-        if accumulate and splits == 1:
+        if deterministic():
+            splits = 1
+        elif accumulate and splits == 1:
             # a weight gradient with a handful of output tiles and a long K
             # (CIFAR quick fc2: 10 x 64 over a 4096 batch, ONE workgroup
             # for 0.27 ms): split K over f32 atomics; an overwrite is then a
@@ -341,6 +343,26 @@ def gemm(a, b, *, trans_a=False, trans_b=False, out=None, out_dtype=None,
 
 
 _DMA_PAD_MIN = 1 << 24   # M*N*K above which padding pays for its copies
+
+# Deterministic mode (engine.deterministic / VELES_AMD_DETERMINISTIC=1):
+# no f32-atomic reductions in the gradient path - GEMM weight gradients
+# and GEMM-path conv weight gradients unsplit (one tile sums its whole K),
+# column sums through torch's fixed-order reduction; the halo weight
+# gradient and the workspace split-K GEMM are deterministic already.
+# Two runs of the same step are then bit-identical (exact-resume tests);
+# it costs the split-K parallelism of small weight gradients.
+_DETERMINISTIC = os.environ.get("VELES_AMD_DETERMINISTIC", "0") != "0"
+
+
+def set_deterministic(on):
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(on)
+
+
+def deterministic():
+    from veles_amd.utils.config import root, get
+    return _DETERMINISTIC or bool(get(root.common.engine.deterministic,
+                                      False))
 
 
 def _dma_padded(a, b, trans_a, trans_b, M, N, K, bias, aux, bias_mode=1):
@@ -1244,12 +1266,17 @@ def _wgrad_splits_for(x, dy, dw, sliding, padding, groups, shape):
         "sliding": tuple(sliding), "padding": tuple(padding),
         "groups": groups, "default": default})
     t = autotune.lookup("wgrad", *shape)
+    if deterministic():
+        return 1
     return default if t is None else max(1, t)
 
 
 def wgrad_splits(P, M, N, groups, target_blocks=None):
     """Pixel (K) splits of a weight-gradient GEMM: enough blocks to fill the
-    256 CUs, few enough that the f32 atomic reduction stays small."""
+    256 CUs, few enough that the f32 atomic reduction stays small (1 in
+    deterministic mode: no atomics)."""
+    if deterministic():
+        return 1
     target_blocks = target_blocks or _WGRAD_BLOCKS
     tiles = ((M + 127) // 128) * ((N + 127) // 128) * groups
     splits = max(1, min(target_blocks // max(tiles, 1), P // 256))
@@ -1264,7 +1291,7 @@ def col_sum(x2d, out=None, scale=1.0, accumulate=False):
         out = torch.zeros(C, dtype=torch.float32, device=x2d.device)
     elif not accumulate:
         out.zero_()
-    if _gpu(x2d):
+    if _gpu(x2d) and not deterministic():
         _lib_call("hvk_col_sum", _p(x2d), DT[x2d.dtype], R, C, _p(out),
                   float(scale), _s(x2d))
         return out
