@@ -583,6 +583,12 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 // tiles, accumulators in the AGPR half: a third less LDS read traffic per
 // MFMA) compiles with 248 VGPRs spilled (hipcc, ROCm 7.2) and is not
 // instantiated.
+// Schedule variants measured and dropped (forced configurations, same
+// process; profiles/r6/ab_hc32_schedule_variants_r6d.log,
+// ab_hc32_branch_free_r6g.log): the SIMD partners (waves 4-7) walking each
+// stage's taps rotated by T / 2 (0.1-0.9x: the doubled k-loop); s_setprio 1
+// on them (+-2 %); a branch-free DMA issue with idle slots sent to a scratch
+// piece (0.95-0.99x: the extra DMAs cost more than the branches).
 template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0,
           int MI = 2>
 __global__ void __attribute__((
@@ -685,7 +691,9 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
   };
   constexpr int NSLOT = NBW + NWW + 1;
   const __amdgpu_buffer_rsrc_t rbias = dma_rsrc(bias);
-  auto issue_slot = [&](int q, uint32_t stb) __attribute__((always_inline)) {
+  auto issue_slot = [&](int q, uint32_t stb, bool live)
+                        __attribute__((always_inline)) {
+    if (!live) return;
     if (q < NBW) {
       if (w + NWV * q < NBP)   // wave-uniform
         dma16(rs, smem + stb + (w + NWV * q) * 1024,
@@ -730,6 +738,7 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
   const int nwg = gridDim.x;
   int item = xcd_remap(blockIdx.x, nwg);
   if (item >= g.items) return;
+
   const __amdgpu_buffer_rsrc_t ro = dma_rsrc(out);
   auto next = [&](int& it, int& q) __attribute__((always_inline)) {
     if (++q == NQ) {
@@ -739,7 +748,7 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
   };
   prepare(item, 0);
 #pragma unroll
-  for (int q = 0; q < NSLOT; ++q) issue_slot(q, 0);
+  for (int q = 0; q < NSLOT; ++q) issue_slot(q, 0, true);
   slots(item);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -785,31 +794,39 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
       for (int j = 0; j < NJ; ++j)
         a[j] = *(lds_bf16x8*)(sm + wb + j * 32 * RB + s * 32);
     };
-    bf16x8 fa[2][NJ], fb[2][MI];
-    rd(0, fa[0], fb[0]);
+    // the stage's k-steps, taps in the order R, R + 1, ... (mod T)
+    auto kloop = [&](auto rc) __attribute__((always_inline)) {
+      constexpr int R = decltype(rc)::value;
+      bf16x8 fa[2][NJ], fb[2][MI];
+      rd(R % T, fa[0], fb[0]);
 #pragma unroll
-    for (int s = 0; s < T; ++s) {
-      if (s + 1 < T) rd(s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((ABL & 4) == 0) {
+      for (int s = 0; s < T; ++s) {
+        if (s + 1 < T)
+          rd((s + 1 + R) % T, fa[(s + 1) & 1], fb[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((ABL & 4) == 0) {
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                fa[s & 1][j], fb[s & 1][i], acc[i][j], 0, 0, 0);
-      } else {
+            for (int j = 0; j < NJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                  fa[s & 1][j], fb[s & 1][i], acc[i][j], 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
-          acc[i][0][0] += (float)fb[s & 1][i][0] + (float)fa[s & 1][0][0];
+          for (int i = 0; i < MI; ++i)
+            acc[i][0][0] += (float)fb[s & 1][i][0] + (float)fa[s & 1][0][0];
+        }
+        if constexpr ((ABL & 1) == 0) {
+          if (more1) {
+#pragma unroll
+            for (int k = 0; k < NSLOT; ++k)
+              if (k * NKSD / NSLOT == s) issue_slot(k, nxt, true);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (more1 && (ABL & 1) == 0) {
-#pragma unroll
-        for (int k = 0; k < NSLOT; ++k)
-          if (k * NKSD / NSLOT == s) issue_slot(k, nxt);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    };
+    kloop(std::integral_constant<int, 0>{});
     // stage (it1, q1) landed; every read of (item, q) done
     if constexpr ((ABL & 8) == 0)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -959,6 +976,7 @@ constexpr HcCand kHcCands[] = {
     {21, 3, 3, 3, 8, 1, 4, 5, 1},   // 512 px x 128 ch
     {22, 3, 3, 3, 8, 1, 3, 5, 1},   // 512 px x 96 ch
     {23, 3, 3, 3, 8, 1, 2, 8, 1},   // 512 px x 64 ch
+
     {6, 3, 3, 3, 8, 1, 8, 5, 0},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
     {7, 3, 3, 3, 8, 1, 6, 5, 0},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
     {1, 3, 3, 3, 4, 2, 4, 8, 0},   // 256 px x 128 ch
@@ -1196,6 +1214,7 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
     HC32(21, 3, 3, 8, 1, 4, 5)
     HC32(22, 3, 3, 8, 1, 3, 5)
     HC32(23, 3, 3, 8, 1, 2, 8)
+
 #undef HC32
 #undef HC_GO_ABL
 #undef HC_GO

@@ -12,5 +12,6 @@ for i in 1 2; do
   VELES_AMD_DP_SOLO_COLLECTIVES=1 tools/gpu_step.sh 300 gpurun_out/${T}_solo_graph_$i.log python3 bench.py || exit 1
   VELES_AMD_DP_SOLO_COLLECTIVES=1 VELES_AMD_DP_GRAPH_BACKWARD=validate tools/gpu_step.sh 300 gpurun_out/${T}_solo_validate_$i.log python3 bench.py || exit 1
 done
+tools/gpu_step.sh 400 gpurun_out/${T}_ab_opt.log python3 -u tools/bench_conv_hc_ab.py 2048 3 0 26,27,28,29 || exit 1
 FILTER=conv_hc TAG=${T}pmc PASSES="B D X" PROBE="tools/bench_conv_vendor.py --probe 2048" \
   tools/gpu_pmc_kernels.sh > gpurun_out/${T}_pmc.txt 2>&1 || exit 1
