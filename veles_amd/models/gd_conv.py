@@ -1,8 +1,13 @@
 """Backward units of the convolutional layers (Znicz ``gd_conv``).
 
-grad_W += wgrad(x, err)   implicit-GEMM MFMA, split over pixels, f32 atomics
-grad_b += colsum(err)
-err_input = dgrad(err, W) [* f'(below.output)]  implicit transposed-conv GEMM
+grad_W (+)= wgrad(x, err)  stride 1: the halo kernel (wgrad_halo.hip), split
+                         over pixels into workspace slices summed in split
+                         order (deterministic); else the implicit-GEMM loop,
+                         split over pixels with f32 atomics
+grad_b (+)= the pixel sums of err, from the same launch (ones operand)
+err_input = dgrad(err, W) [* f'(below.output)]  stride 1: the halo conv
+                         (conv_hc.hip, conv_hc32 / conv_hc); else the
+                         implicit transposed-conv GEMM
 
 When the forward layer runs in fp8 both GEMMs take the e5m2 copy of err:
 backward-data against the e4m3 weights, the weight gradient against the
