@@ -577,7 +577,8 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 // ABL (diagnostic builds only, -DHVK_HC_ABL; tools/ablate_conv_hc.py): 1 no
 // DMA after the first stage, 2 the next stage's DMA all at the first k-step,
 // 4 no MFMAs, 8 no stage-end DMA wait, 16 the DMA spread over every k-step,
-// 32 no epilogue stores (1, 4, 8, 32 give wrong results by design)
+// 32 no epilogue stores, 64 no epilogue at all (1, 4, 8, 32, 64 give wrong
+// results by design)
 // MI: 32-pixel m-tiles per wave.  MI 2 with 8 waves (two per SIMD, 64 x
 // NJ * 32 wave tiles).  MI 4 with 4 waves (one per SIMD, 128 x 128 wave
 // tiles, accumulators in the AGPR half: a third less LDS read traffic per
@@ -691,26 +692,39 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
   };
   constexpr int NSLOT = NBW + NWW + 1;
   const __amdgpu_buffer_rsrc_t rbias = dma_rsrc(bias);
+  // this wave's window / weight pieces (one scalar each instead of a
+  // wave-uniform mask per slot: those spilled to VGPR lanes)
+  const int nb_live = (NBP - w + NWV - 1) / NWV;
+  const int nw_live = (NWP - w + NWV - 1) / NWV;
   auto issue_slot = [&](int q, uint32_t stb, bool live)
                         __attribute__((always_inline)) {
     if (!live) return;
+    // an out-of-range piece (kBufOOB = 2^31) plus a stage offset (< 2^31)
+    // stays in [2^31, 2^32): still past the descriptor's records, no select
+    // (opaque here: else the compiler hoists one 64-bit mask per slot)
     if (q < NBW) {
-      if (w + NWV * q < NBP)   // wave-uniform
-        dma16(rs, smem + stb + (w + NWV * q) * 1024,
-              pwb[q] >= kBufOOB ? kBufOOB : pwb[q] + d_cofs);
+      int nb = nb_live;
+      asm volatile("" : "+s"(nb));
+      if (q < nb)   // wave-uniform
+        dma16(rs, smem + stb + (w + NWV * q) * 1024, pwb[q] + d_cofs);
     } else if (q < NBW + NWW) {
       const int i = q - NBW;
-      if (w + NWV * i < NWP) {   // wave-uniform
-        const uint32_t o = wq(w + NWV * i);
+      int nw = nw_live;
+      asm volatile("" : "+s"(nw));
+      if (i < nw)   // wave-uniform
         dma16(rw, smem + stb + g.WIN + (w + NWV * i) * 1024,
-              o >= kBufOOB ? kBufOOB : o + d_wofs);
-      }
+              wq(w + NWV * i) + d_wofs);
     } else if (d_bias) {
       dma16(rbias, smem + stb + STAGE_B, d_bofs);
     }
   };
   // window slot bytes of this lane's pixel in each m-tile
   uint32_t bb[MI];
+  // the swizzled window byte offset of every (m-tile, tap) read, once per
+  // item (MI * T VGPRs) instead of an add / shift / and / xor per read and
+  // k-step (conv_hc32 loops +0-5 %, profiles/r6/ab_hc32_lean_loop_r6k.log)
+  uint32_t ra[MI][T];
+  const uint32_t wp32 = (uint32_t)g.Wp * 32u;
   auto slots = [&](int it) __attribute__((always_inline)) {
     int ptl, gi, nt;
     decode(it, ptl, gi, nt);
@@ -733,6 +747,14 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
       const int row = j == 0 ? (int)(oh - oh0) : rc + (j - 1) * g.HPd + (int)oh;
       bb[i] = (uint32_t)(row * g.Wp + ow) * 32u + 16u * lh;
     }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int s = 0; s < T; ++s) {
+        const uint32_t aa = bb[i] + (uint32_t)(s / KW) * wp32 +
+                            (uint32_t)(s % KW) * 32u;
+        ra[i][s] = aa ^ ((aa >> 4) & 16u);
+      }
   };
 
   const int nwg = gridDim.x;
@@ -768,7 +790,6 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
 
   const uint32_t wrow = (uint32_t)((wn * NJ * 32 + l31) * RB +
                                    16 * (lh ^ ((l31 >> 3) & 1)));
-  const uint32_t wp32 = (uint32_t)g.Wp * 32u;
   int q = 0;
   uint32_t cur = 0;
   for (;;) {
@@ -777,19 +798,18 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
     decode(item, ptl, gi, nt);
     const uint32_t p0 = (uint32_t)ptl * TPX;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(bb[i]));
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int s = 0; s < T; ++s) asm volatile("" : "+v"(ra[i][s]));
     const uint32_t nxt = cur ^ STAGE;
     const uint32_t wb = cur + (uint32_t)g.WIN + wrow;
     // the k-steps (taps) of this stage; the next stage's DMA slots spread
     // over the first ~2/3 of them
     constexpr int NKSD = (ABL & 2) ? 1 : (ABL & 16) ? T : (2 * T + 2) / 3;
     auto rd = [&](int s, bf16x8* a, bf16x8* b) __attribute__((always_inline)) {
-      const uint32_t ofs = (uint32_t)(s / KW) * wp32 + (uint32_t)(s % KW) * 32u;
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const uint32_t aa = bb[i] + ofs;
-        b[i] = *(lds_bf16x8*)(sm + cur + (aa ^ ((aa >> 4) & 16u)));
-      }
+      for (int i = 0; i < MI; ++i)
+        b[i] = *(lds_bf16x8*)(sm + cur + ra[i][s]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         a[j] = *(lds_bf16x8*)(sm + wb + j * 32 * RB + s * 32);
@@ -839,54 +859,98 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
       // out-of-range offset
       const int chl = wn * NJ * 32 + 16 * lh;   // within the item's BN
       const int chb = gi * g.OCg + nt * BN + chl;
+      if constexpr ((ABL & 64) != 0) {   // keeps the MFMAs live
+        float z = 0.f;
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const uint32_t p = p0 + wm * WPX + i * 32 + l31;
-        const uint32_t pa = min(p, (uint32_t)g.P - 1);
-        const bool ok = p < (uint32_t)g.P;
-        const uint32_t ob = (uint32_t)(((long long)p * g.OCT + chb) * 2);
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          float v[16];
+          for (int j = 0; j < NJ; ++j) z += acc[i][j][0];
+        if (z == 1234.5f) out[t] = 0;
+      }
+      // EM 1: strict ReLU forward without a derivative operand, 2: linear
+      // with the strict-ReLU derivative (the AlexNet backward-data), both on
+      // the packed bf16 (relu_bf16x2 / relu_mask_bf16x2); 0: any
+      // activation in f32.  The epilogue stalls every MFMA of the CU
+      // (ablation: 8-9 % of the forward, 28 % of conv5 backward-data).
+      auto epi = [&](auto emc) __attribute__((always_inline)) {
+        constexpr int EM = decltype(emc)::value;
 #pragma unroll
-          for (int e = 0; e < 16; e += 4) {
-            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (bias) {
-              const f32x4 lb = *(const __attribute__((address_space(3)))
-                                      f32x4*)(sm + cur + STAGE_B +
-                                              (chl + 32 * j + e) * 4);
-              bv = make_float4(lb[0], lb[1], lb[2], lb[3]);
+        for (int i = 0; i < ((ABL & 64) ? 0 : MI); ++i) {
+          const uint32_t p = p0 + wm * WPX + i * 32 + l31;
+          const uint32_t pa = min(p, (uint32_t)g.P - 1);
+          const bool ok = p < (uint32_t)g.P;
+          const uint32_t ob = (uint32_t)(((long long)p * g.OCT + chb) * 2);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 16 && EM == 2; ++e) v[e] = acc[i][j][e];
+#pragma unroll
+            for (int e = 0; e < 16 && EM != 2; e += 4) {
+              float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (bias) {
+                const f32x4 lb = *(const __attribute__((address_space(3)))
+                                        f32x4*)(sm + cur + STAGE_B +
+                                                (chl + 32 * j + e) * 4);
+                bv = make_float4(lb[0], lb[1], lb[2], lb[3]);
+              }
+              v[e] = acc[i][j][e] + bv.x;
+              v[e + 1] = acc[i][j][e + 1] + bv.y;
+              v[e + 2] = acc[i][j][e + 2] + bv.z;
+              v[e + 3] = acc[i][j][e + 3] + bv.w;
             }
-            v[e] = acc[i][j][e] + bv.x;
-            v[e + 1] = acc[i][j][e + 1] + bv.y;
-            v[e + 2] = acc[i][j][e + 2] + bv.z;
-            v[e + 3] = acc[i][j][e + 3] + bv.w;
-          }
-          act_fwd_n<16>(v, act);
-          if (aux) {
-            float y[16];
-            const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
-            const uint4 a0 = *(const uint4*)ap, a1 = *(const uint4*)(ap + 8);
-            const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w,
-                                    a1.x, a1.y, a1.z, a1.w};
+            uint32_t pk[8];
+            if constexpr (EM == 0) {
+              act_fwd_n<16>(v, act);
+              if (aux) {
+                float y[16];
+                const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
+                const uint4 a0 = *(const uint4*)ap,
+                            a1 = *(const uint4*)(ap + 8);
+                const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w,
+                                        a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              y[2 * e] = __uint_as_float(av[e] << 16);
-              y[2 * e + 1] = __uint_as_float(av[e] & 0xffff0000u);
+                for (int e = 0; e < 8; ++e) {
+                  y[2 * e] = __uint_as_float(av[e] << 16);
+                  y[2 * e + 1] = __uint_as_float(av[e] & 0xffff0000u);
+                }
+                act_bwd_mul_n<16>(v, y, aux_act);
+              }
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]);
+            } else if constexpr (EM == 1) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                pk[e] = relu_bf16x2(pack_bf16x2(v[2 * e], v[2 * e + 1]));
+            } else {
+              const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
+              const uint4 a0 = *(const uint4*)ap, a1 = *(const uint4*)(ap + 8);
+              const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w,
+                                      a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]) &
+                        relu_mask_bf16x2(av[e]);
             }
-            act_bwd_mul_n<16>(v, y, aux_act);
-          }
-          const uint32_t o = ob + 64 * j;
+            const uint32_t o = ob + 64 * j;
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const uint4 qv = pack_bf16x8(v + 8 * e);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u32x4{qv.x, qv.y, qv.z, qv.w}, ro,
-                ok && !((ABL & 32) && v[0] != 1234.5f) ? o + 16 * e : kBufOOB,
-                0, 0);
+            for (int e = 0; e < 2; ++e)
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  u32x4{pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]},
+                  ro,
+                  ok && !((ABL & 32) && v[0] != 1234.5f) ? o + 16 * e
+                                                          : kBufOOB,
+                  0, 0);
           }
         }
-      }
+      };
+      if (!aux && act == ACT_STRICT_RELU)
+        epi(std::integral_constant<int, 1>{});
+      else if (aux && act == ACT_LINEAR && aux_act == ACT_STRICT_RELU && !bias)
+        epi(std::integral_constant<int, 2>{});
+      else
+        epi(std::integral_constant<int, 0>{});
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1143,7 +1207,7 @@ hipError_t go_hc32_abl(const HcPlan& p, const void* src, const void* wts,
     case A: return go_hc32<KH, KW, WM, WN, NJ, NBW, A>(                       \
         p, src, wts, bias, out, aux, act, aux_act, s);
     HC32_ABL(1) HC32_ABL(2) HC32_ABL(4) HC32_ABL(8) HC32_ABL(16) HC32_ABL(32)
-    HC32_ABL(9)
+    HC32_ABL(9) HC32_ABL(64)
 #undef HC32_ABL
     default: return go_hc32<KH, KW, WM, WN, NJ, NBW, 0>(
         p, src, wts, bias, out, aux, act, aux_act, s);

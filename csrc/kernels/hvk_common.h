@@ -57,6 +57,25 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float* v) {
   return make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
                     pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
 }
+// Strict ReLU on a packed bf16 pair as 16-bit integers: a bf16 is > 0
+// exactly when its bit pattern is a positive int16, so max(x, 0) and the
+// derivative mask (x > 0 ? 0xffff : 0) are one / three packed-i16 ops per
+// two values instead of an unpack, compare and select per value.
+// relu(bf16(x)) == bf16(relu(x)); masking gives +0 where x * 0 gave -0.
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t p) {
+  const s16x2_t z = {0, 0};
+  return __builtin_bit_cast(
+      uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, p), z));
+}
+// (0 -sat y) is negative exactly when y > 0 (y = -32768 saturates to
+// +32767); its sign spread over the lane is the mask
+__device__ __forceinline__ uint32_t relu_mask_bf16x2(uint32_t y) {
+  const s16x2_t z = {0, 0}, sh = {15, 15};
+  const s16x2_t t =
+      __builtin_elementwise_sub_sat(z, __builtin_bit_cast(s16x2_t, y));
+  return __builtin_bit_cast(uint32_t, t >> sh);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

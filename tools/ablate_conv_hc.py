@@ -5,7 +5,8 @@ process.  They exist only in the -DHVK_HC_ABL build
 HVK_LIBRARY=build/hcabl/libhvk_hcabl.so).  conv_hc32 (configurations 21 /
 22): 1 no DMA after the first stage, 2 the DMA at the first k-step, 4 no
 MFMAs, 8 no stage-end DMA wait, 16 the DMA over every k-step, 32 no
-epilogue stores; conv_hc_kernel (configuration 5): its own table.
+epilogue stores, 64 no epilogue; conv_hc_kernel (configuration 5): its own
+table.
 
     HVK_LIBRARY=build/hcabl/libhvk_hcabl.so \
         python tools/ablate_conv_hc.py [batch] [rounds] [ablations]"""
