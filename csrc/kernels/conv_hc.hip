@@ -251,22 +251,33 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
   };
   constexpr int NSLOT = NBW + NWW + (BIASB ? 1 : 0);
   const __amdgpu_buffer_rsrc_t rbias = dma_rsrc(bias);
+  // this wave's window / weight pieces, opaque at each use (else one 64-bit
+  // mask per slot is hoisted and spilled to VGPR lanes); an out-of-range
+  // offset (kBufOOB = 2^31) plus a stage offset (< 2^31) stays past the
+  // descriptor's records, so no select (conv_hc32 does the same)
+  const int nb_live = (NBP - w + NWV - 1) / NWV;
+  const int nw_live = (NWP - w + NWV - 1) / NWV;
   auto issue_slot = [&](int q, uint32_t stb) __attribute__((always_inline)) {
+    // (the wide tiles keep the hoisted masks: opaque counts push their
+    // 256-VGPR k-loop into more spills)
+    constexpr bool OPQ = NJW <= 4;
     if (q < NBW) {
-      if (w + NWV * q < NBP)   // wave-uniform
-        dma16(rs, smem + stb + (w + NWV * q) * 1024,
-              pwb[q] >= kBufOOB ? kBufOOB : pwb[q] + d_cofs);
+      int nb = nb_live;
+      if constexpr (OPQ) asm volatile("" : "+s"(nb));
+      if (q < nb)   // wave-uniform
+        dma16(rs, smem + stb + (w + NWV * q) * 1024, pwb[q] + d_cofs);
     } else if (q < NBW + NWW) {
       if constexpr ((ABL & 256) != 0) {
         if (stb != 0 || d_cofs != 0) return;
       }
       const int i = q - NBW;
-      if (w + NWV * i < NWP) {   // wave-uniform
+      int nw = nw_live;
+      if constexpr (OPQ) asm volatile("" : "+s"(nw));
+      if (i < nw) {   // wave-uniform
         const uint32_t o =
             (NH > 1 && d_h) ? wq(std::integral_constant<int, 1>{}, w + NWV * i)
                             : wq(std::integral_constant<int, 0>{}, w + NWV * i);
-        dma16(rw, smem + stb + g.WIN + (w + NWV * i) * 1024,
-              o >= kBufOOB ? kBufOOB : o + d_wofs);
+        dma16(rw, smem + stb + g.WIN + (w + NWV * i) * 1024, o + d_wofs);
       }
     } else if (d_bias) {
       // the item's bias block (natural channel order; lanes past BN / 4
