@@ -885,10 +885,44 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
       // (ablation: 8-9 % of the forward, 28 % of conv5 backward-data).
       auto epi = [&](auto emc) __attribute__((always_inline)) {
         constexpr int EM = decltype(emc)::value;
+        // every derivative operand of the epilogue loaded before its first
+        // store: the compiler cannot move a global load above a buffer store
+        // (possible alias), so per-block loads serialised the epilogue on a
+        // load and a store round trip per block (vmcnt counts both, in
+        // order).  The k-loop's fragment registers are dead here.
+        // (the 128-channel tile keeps per-block loads: hoisted, even per
+        // m-tile, they spill its 251-VGPR k-loop)
+        constexpr bool HALL = MI * NJ <= 6;
+        constexpr int AI = (EM == 1 || !HALL) ? 1 : MI;
+        constexpr int AJ = (EM == 1 || !HALL) ? 1 : NJ;
+        uint4 avs[AI][AJ][2];
+        auto ld_aux = [&](int i, int j, uint4& a0, uint4& a1)
+                          __attribute__((always_inline)) {
+          const uint32_t pa =
+              min(p0 + wm * WPX + i * 32 + l31, (uint32_t)g.P - 1);
+          const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
+          a0 = *(const uint4*)ap;
+          a1 = *(const uint4*)(ap + 8);
+        };
+        if (EM != 1 && HALL && aux) {
+#pragma unroll
+          for (int i = 0; i < ((ABL & 64) || EM == 1 ? 0 : MI); ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              ld_aux(i, j, avs[i % AI][j % AJ][0], avs[i % AI][j % AJ][1]);
+        }
+        auto get_aux = [&](int i, int j, uint4& a0, uint4& a1)
+                           __attribute__((always_inline)) {
+          if constexpr (HALL) {
+            a0 = avs[i % AI][j % AJ][0];
+            a1 = avs[i % AI][j % AJ][1];
+          } else {
+            ld_aux(i, j, a0, a1);
+          }
+        };
 #pragma unroll
         for (int i = 0; i < ((ABL & 64) ? 0 : MI); ++i) {
           const uint32_t p = p0 + wm * WPX + i * 32 + l31;
-          const uint32_t pa = min(p, (uint32_t)g.P - 1);
           const bool ok = p < (uint32_t)g.P;
           const uint32_t ob = (uint32_t)(((long long)p * g.OCT + chb) * 2);
 #pragma unroll
@@ -915,9 +949,8 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
               act_fwd_n<16>(v, act);
               if (aux) {
                 float y[16];
-                const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
-                const uint4 a0 = *(const uint4*)ap,
-                            a1 = *(const uint4*)(ap + 8);
+                uint4 a0, a1;
+                get_aux(i, j, a0, a1);
                 const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w,
                                         a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
@@ -935,8 +968,8 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
               for (int e = 0; e < 8; ++e)
                 pk[e] = relu_bf16x2(pack_bf16x2(v[2 * e], v[2 * e + 1]));
             } else {
-              const uint16_t* ap = aux + (long long)pa * g.OCT + chb + 32 * j;
-              const uint4 a0 = *(const uint4*)ap, a1 = *(const uint4*)(ap + 8);
+              uint4 a0, a1;
+              get_aux(i, j, a0, a1);
               const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w,
                                       a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
