@@ -1318,7 +1318,7 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
     HC_GO_ABL(6, 3, 3, 3, 8, 1, 8, 5)
     HC_GO_ABL(7, 3, 3, 3, 8, 1, 6, 5)
     HC_GO(8, 5, 5, 3, 8, 1, 4)
-    HC_GO(11, 5, 5, 5, 8, 1, 2)
+    HC_GO_ABL(11, 5, 5, 5, 8, 1, 2)
     HC32(21, 3, 3, 8, 1, 4, 5)
     HC32(22, 3, 3, 8, 1, 3, 5)
     HC32(23, 3, 3, 8, 1, 2, 8)

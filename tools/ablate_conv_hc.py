@@ -9,7 +9,7 @@ epilogue stores, 64 no epilogue; conv_hc_kernel (configuration 5): its own
 table.
 
     HVK_LIBRARY=build/hcabl/libhvk_hcabl.so \
-        python tools/ablate_conv_hc.py [batch] [rounds] [ablations]"""
+        python tools/ablate_conv_hc.py [batch] [rounds] [ablations] [filter]"""
 import statistics
 import sys
 
@@ -32,9 +32,12 @@ def main():
              ("conv4_fwd v22", ("fwd", B, 13, 13, 384, 384, 3, 1, 1, 2)),
              ("conv5_dgrad v22", ("dgrad", B, 13, 13, 384, 256, 3, 1, 1, 2)),
              ("conv1_fwd v22", ("fwd", B, 227, 227, 3, 96, 11, 4, 0, 1)),
+             ("conv2_fwd v11", ("fwd", B, 27, 27, 96, 256, 5, 1, 2, 2)),
              ("conv2_dgrad v5", ("dgrad", B, 27, 27, 96, 256, 5, 1, 2, 2))]
     abls = [int(a) for a in sys.argv[3].split(",")] \
         if len(sys.argv) > 3 else [0, 1, 2, 4, 8, 16, 32, 9]
+    if len(sys.argv) > 4:   # case-name filter (the bits differ per kernel)
+        cases = [c for c in cases if sys.argv[4] in c[0]]
     try:
         for name, shp in cases:
             fl, fn = case(*shp)
