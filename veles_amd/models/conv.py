@@ -87,7 +87,7 @@ class Conv(Forward):
         self.alloc_output((shape[0], OH, OW, self.n_kernels))
         self.fp8_ = bool(getattr(self.device, "fp8", False)) and \
             fp8.fp8_conv_ok(C, self.n_kernels, self.grouping, self.ky,
-                             self.kx)
+                             self.kx) and fp8.fp8_conv_pays(C, OH, OW)
         if self.fp8_ and self.fp8_sx_ is None:
             self.fp8_sx_ = fp8.Scaler(self.torch_device, fp8.E4M3)
             self.fp8_sw_ = fp8.Scaler(self.torch_device, fp8.E4M3)

@@ -321,6 +321,23 @@ def fp8_conv_ok(C, OC, groups, KH=1, KW=1):
         (OC // groups) % 16 == 0 and KH <= 32 and KW <= 32
 
 
+def fp8_conv_pays(C, OH, OW):
+    """Layers left on bf16 in an fp8 model because the bf16 kernels beat the
+    fp8 ones there: 64 input channels at >= 200 x 200 outputs (VGG-16
+    conv1_2).  Its fp8 forward (im2col T4, 256 x 64 tiles) took 3.0 ms and
+    backward-data (128-row loop, K = 576) 3.56 ms at b512 against 2.46 /
+    3.23 ms for the bf16 halo conv and GEMM, and its e4m3 input copy cost
+    the bf16 conv1_1 epilogue 0.78 ms (profiles/r6/vgg16_b512_{float8,
+    bfloat16}_step_r6w.md).  ``root.common.engine.fp8_all_convs = True``
+    (or VELES_AMD_FP8_ALL_CONVS=1) keeps every eligible conv on fp8."""
+    import os
+    from veles_amd.utils.config import root, get
+    if get(root.common.engine.fp8_all_convs, False) or \
+            os.environ.get("VELES_AMD_FP8_ALL_CONVS", "0") not in ("", "0"):
+        return True
+    return not (C <= 64 and OH * OW >= 200 * 200)
+
+
 def _q8_args(q8, qs):
     """Kernel arguments of a fused output quantisation (or none)."""
     if q8 is None:
