@@ -53,6 +53,27 @@ def test_quantize_saturates_cpu():
     assert q.float()[0].item() == 57344.0 and q.float()[1].item() == -57344.0
 
 
+def test_fp8_layer_policy_cpu(monkeypatch):
+    """The 224-wide 64-channel convs stay on bf16 in an fp8 model (the bf16
+    kernels beat the fp8 loops there, profiles/r6/vgg16_fp8_policy_ab_r6x.txt);
+    every other eligible shape, and all of them under the override, run fp8."""
+    monkeypatch.delenv("VELES_AMD_FP8_ALL_CONVS", raising=False)
+    assert not fp8.fp8_conv_pays(64, 224, 224)      # VGG conv1_2
+    assert fp8.fp8_conv_pays(64, 112, 112)          # VGG conv2_1
+    assert fp8.fp8_conv_pays(128, 224, 224)
+    assert fp8.fp8_conv_pays(512, 14, 14)
+    monkeypatch.setenv("VELES_AMD_FP8_ALL_CONVS", "1")
+    assert fp8.fp8_conv_pays(64, 224, 224)
+    monkeypatch.delenv("VELES_AMD_FP8_ALL_CONVS")
+    from veles_amd.utils.config import get
+    old = get(root.common.engine.fp8_all_convs, False)
+    root.common.engine.fp8_all_convs = True
+    try:
+        assert fp8.fp8_conv_pays(64, 224, 224)
+    finally:
+        root.common.engine.fp8_all_convs = old
+
+
 def test_fp8_gemm_close_to_fp32_cpu():
     a, b = rnd(96, 256), rnd(80, 256, seed=1)
     sa, sb = fp8.Scaler("cpu"), fp8.Scaler("cpu")
