@@ -66,6 +66,7 @@ namespace {
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 struct HcGeom {
@@ -78,6 +79,7 @@ struct HcGeom {
   int Wp, HPd, WIN;   // slot row pitch, padded rows per image, window bytes
   int NT, G, items;   // n-tiles per group, groups, (tile, group, n-tile) items
   int flip;           // backward-data: weight tap T - 1 - t
+  int ts;             // conv_hc32: epilogue stores staged through LDS
   FastDiv fOW, fOHW, fHPd, fWp;
 };
 
@@ -602,7 +604,7 @@ conv_hc_kernel(const uint16_t* __restrict__ src,
 // on them (+-2 %); a branch-free DMA issue with idle slots sent to a scratch
 // piece (0.95-0.99x: the extra DMAs cost more than the branches).
 template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0,
-          int MI = 2>
+          int MI = 2, bool TS = false>
 __global__ void __attribute__((
     amdgpu_flat_work_group_size(64 * WM * WN, 64 * WM * WN),
     amdgpu_waves_per_eu(WM * WN / 4, WM * WN / 4)))
@@ -883,6 +885,11 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
       // the packed bf16 (relu_bf16x2 / relu_mask_bf16x2); 0: any
       // activation in f32.  The epilogue stalls every MFMA of the CU
       // (ablation: 8-9 % of the forward, 28 % of conv5 backward-data).
+      // LDS staging slot of this wave in the consumed stage buffer (free
+      // until the barrier below): 32 rows of NJ * 64 B + 16 B pad (the pad
+      // spreads the rows' 16-B pieces over the banks)
+      constexpr int TSR = NJ * 64 + 16;
+      const uint32_t tsb = cur + (uint32_t)(w * 32 * TSR);
       auto epi = [&](auto emc) __attribute__((always_inline)) {
         constexpr int EM = decltype(emc)::value;
         // every derivative operand of the epilogue loaded before its first
@@ -920,8 +927,11 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
             ld_aux(i, j, a0, a1);
           }
         };
-#pragma unroll
-        for (int i = 0; i < ((ABL & 64) ? 0 : MI); ++i) {
+        // one call per m-tile (a lambda on a constant: the loop form was
+        // too large for the unroller once the staged stores were added,
+        // and a rolled loop puts the accumulators in scratch)
+        auto epi_i = [&](auto ic) __attribute__((always_inline)) {
+          constexpr int i = decltype(ic)::value;
           const uint32_t p = p0 + wm * WPX + i * 32 + l31;
           const bool ok = p < (uint32_t)g.P;
           const uint32_t ob = (uint32_t)(((long long)p * g.OCT + chb) * 2);
@@ -977,16 +987,59 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
                 pk[e] = pack_bf16x2(v[2 * e], v[2 * e + 1]) &
                         relu_mask_bf16x2(av[e]);
             }
-            const uint32_t o = ob + 64 * j;
+            if constexpr (TS) {   // stage the m-tile in LDS
 #pragma unroll
-            for (int e = 0; e < 2; ++e)
-              __builtin_amdgcn_raw_buffer_store_b128(
-                  u32x4{pk[4 * e], pk[4 * e + 1], pk[4 * e + 2], pk[4 * e + 3]},
-                  ro,
-                  ok && !((ABL & 32) && v[0] != 1234.5f) ? o + 16 * e
-                                                          : kBufOOB,
-                  0, 0);
+              for (int e = 0; e < 2; ++e)
+                *(lds_u32x4*)(sm + tsb + l31 * TSR + (32 * j + 16 * lh + 8 * e) *
+                                                         2) =
+                    u32x4{pk[4 * e], pk[4 * e + 1], pk[4 * e + 2],
+                          pk[4 * e + 3]};
+            } else {
+              const uint32_t o = ob + 64 * j;
+#pragma unroll
+              for (int e = 0; e < 2; ++e)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{pk[4 * e], pk[4 * e + 1], pk[4 * e + 2],
+                          pk[4 * e + 3]},
+                    ro,
+                    ok && !((ABL & 32) && v[0] != 1234.5f) ? o + 16 * e
+                                                            : kBufOOB,
+                    0, 0);
+            }
           }
+          if constexpr (TS) {
+            // the wave's 32 pixels x NJ * 32 channels read back as rows of
+            // 16-B chunks: lanes on consecutive chunks of a pixel's run, so
+            // a store covers runs of NJ * 64 contiguous bytes instead of 64
+            // scattered 16-B pieces (its own LDS slot: no barrier)
+            // (lane opaque here: else the chunk addresses, lane constants,
+            // are hoisted out of the item loop and spill its k-loop)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+#pragma unroll
+            for (int k = 0; k < 2 * NJ; ++k) {
+              const int c = ln + 64 * k;   // chunk of the m-tile
+              const int row = c / (4 * NJ), col = c - row * (4 * NJ);
+              const u32x4 val = *(const lds_u32x4*)(sm + tsb + row * TSR +
+                                                     col * 16);
+              const uint32_t pr = p0 + wm * WPX + i * 32 + row;
+              const uint32_t go =
+                  (uint32_t)(((long long)pr * g.OCT + chb - 16 * lh) * 2) +
+                  col * 16;
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  val, ro,
+                  pr < (uint32_t)g.P && !((ABL & 32) && val[0] == 12345u)
+                      ? go : kBufOOB,
+                  0, 0);
+            }
+          }
+        };
+        if constexpr ((ABL & 64) == 0) {
+          static_assert(MI <= 4, "m-tiles of the epilogue");
+          epi_i(std::integral_constant<int, 0>{});
+          if constexpr (MI > 1) epi_i(std::integral_constant<int, 1>{});
+          if constexpr (MI > 2) epi_i(std::integral_constant<int, 2>{});
+          if constexpr (MI > 3) epi_i(std::integral_constant<int, 3>{});
         }
       };
       if (!aux && act == ACT_STRICT_RELU)
@@ -1002,6 +1055,8 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
       if (more1) slots(it1);
+      // the staging slots lie in the buffer the next stage's DMA fills
+      if constexpr (TS) __builtin_amdgcn_s_barrier();
     }
     if (!more1) break;
     item = it1;
@@ -1077,6 +1132,7 @@ struct HcCand { int var, KH, KW, KHS, WM, WN, NJW, NBW, m32, mi = 2; };
 // conv_hc32 candidates on (hvk_hc32; default on), else only conv_hc_kernel
 int g_hc32 = 1;
 int g_hc_last = 0;   // configuration of the last conv_hc launch (tests)
+int g_hc32_ts = 1;   // conv_hc32 epilogue stores staged through LDS
 // per kernel size, in order of preference (the first whose n-tile divides
 // the group's outputs and whose two stages fit the LDS)
 constexpr HcCand kHcCands[] = {
@@ -1167,6 +1223,13 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
     if (g.WIN / 1024 > k.WM * k.WN * k.NBW) continue;
     const size_t lds = 2 * (size_t)(g.WIN + hc_nbytes_w(k));
     if (lds > 160 * 1024) continue;
+    // conv_hc32's store staging: one 32-row slot per wave in the window and
+    // weight part of a stage buffer; backward-data only (same process,
+    // profiles/r6/ab_hc32_staged_stores_r6y.log: conv3 / conv5 dgrad +3.4 /
+    // +2.8 %, the forwards -4 % (conv1) to +0.8 %)
+    g.ts = k.m32 && flip && g_hc32_ts &&
+           k.WM * k.WN * 32 * (k.NJW * 64 + 16) <=
+               g.WIN + hc_nbytes_w(k) - 1024;
     g.NT = OCg / BN;
     g.items = (int)(tiles * groups * g.NT);
     g.fOW = make_fastdiv(OW);
@@ -1212,8 +1275,8 @@ long long hc32_wpack_bytes(const HcPlan& p) {
 }
 
 template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0,
-          int MI = 2>
-hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
+          int MI = 2, bool TS = false>
+hipError_t go_hc32_ts(const HcPlan& p, const void* src, const void* wts,
                    const float* bias, void* out, const void* aux, int act,
                    int aux_act, hipStream_t s) {
   if (p.g.WIN / 1024 > WM * WN * NBW) return hipErrorInvalidValue;
@@ -1226,7 +1289,7 @@ hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
                        WN * NJ * 32, p.g.flip, pieces);
     wts = p.wpack;
   }
-  auto kern = conv_hc32_kernel<KH, KW, WM, WN, NJ, NBW, ABL, MI>;
+  auto kern = conv_hc32_kernel<KH, KW, WM, WN, NJ, NBW, ABL, MI, TS>;
   static bool attr = false;   // once per instantiation, before any capture
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(
@@ -1239,6 +1302,17 @@ hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
                      (const uint16_t*)src, (const uint16_t*)wts, bias,
                      (uint16_t*)out, (const uint16_t*)aux, act, aux_act, p.g);
   return launch_status(s);
+}
+
+template <int KH, int KW, int WM, int WN, int NJ, int NBW, int ABL = 0>
+hipError_t go_hc32(const HcPlan& p, const void* src, const void* wts,
+                   const float* bias, void* out, const void* aux, int act,
+                   int aux_act, hipStream_t s) {
+  if (p.g.ts)
+    return go_hc32_ts<KH, KW, WM, WN, NJ, NBW, ABL, 2, true>(
+        p, src, wts, bias, out, aux, act, aux_act, s);
+  return go_hc32_ts<KH, KW, WM, WN, NJ, NBW, ABL, 2, false>(
+      p, src, wts, bias, out, aux, act, aux_act, s);
 }
 
 #ifdef HVK_HC_ABL
@@ -1343,6 +1417,8 @@ HVK_API void hvk_hc_pitch_pad(int p) { g_hc_pad = p; }
 // conv_hc32 candidates (32x32x16 MFMA, one tap per k-step): 1 on (default),
 // 0 only the 16x16x32 kernel
 HVK_API void hvk_hc32(int on) { g_hc32 = on; }
+// conv_hc32 epilogue stores: 1 staged through LDS (default), 0 direct
+HVK_API void hvk_hc32_ts(int on) { g_hc32_ts = on; }
 // configuration (kHcCands var) of the last hvk_conv_{fwd,dgrad}_hc launch
 HVK_API int hvk_hc_last_variant() { return g_hc_last; }
 

@@ -19,7 +19,8 @@ def main():
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
     rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 5
     setter = getattr(_lib.lib(), knob)
-    cases = [("conv3_fwd", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
+    cases = [("conv1_fwd", ("fwd", B, 227, 227, 3, 96, 11, 4, 0, 1)),
+             ("conv3_fwd", ("fwd", B, 13, 13, 256, 384, 3, 1, 1, 1)),
              ("conv4_fwd", ("fwd", B, 13, 13, 384, 384, 3, 1, 1, 2)),
              ("conv5_fwd", ("fwd", B, 13, 13, 384, 256, 3, 1, 1, 2)),
              ("conv3_dgrad", ("dgrad", B, 13, 13, 256, 384, 3, 1, 1, 1)),
