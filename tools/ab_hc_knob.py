@@ -1,5 +1,5 @@
 """Same-process A/B of a conv_hc integer knob (an hvk_* setter taking one
-int, e.g. hvk_hc32_pa or hvk_hc_pitch_pad) on the AlexNet conv_hc shapes,
+int, e.g. hvk_hc32_ts or hvk_hc_pitch_pad) on the AlexNet conv_hc shapes,
 values interleaved round by round, median TF/s.  The knob is left at the
 first value.
 
