@@ -1140,6 +1140,9 @@ constexpr HcCand kHcCands[] = {
     {21, 3, 3, 3, 8, 1, 4, 5, 1},   // 512 px x 128 ch
     {22, 3, 3, 3, 8, 1, 3, 5, 1},   // 512 px x 96 ch
     {23, 3, 3, 3, 8, 1, 2, 8, 1},   // 512 px x 64 ch
+    // 5 x 5 (AlexNet conv2 forward), 512 px x 64 ch: 25 k-steps per stage,
+    // no pad tap; fits the LDS only with the tight window pitch (below)
+    {24, 5, 5, 5, 8, 1, 2, 4, 1},
 
     {6, 3, 3, 3, 8, 1, 8, 5, 0},   // 512 px x 128 ch: AlexNet conv3 / 5 fwd, conv3 dgrad
     {7, 3, 3, 3, 8, 1, 6, 5, 0},   // 512 px x 96 ch: conv1 (s2d), conv4 fwd, conv4 / 5 dgrad
@@ -1193,6 +1196,9 @@ HcPlan hc_plan(int N, int H, int W, int C, int OH, int OW, int OCT, int KH,
   if (OW + KW - 1 > g.Wp || g.Wp >= (1 << 20)) return p;
   for (const HcCand& k : kHcCands) {
     if (k.KH != KH || k.KW != KW) continue;
+    // the 5 x 5 conv_hc32 tile: Wp = OW + 4 (OW + 8 overflows the LDS by
+    // 6 KiB at 27 x 27; the row-wrap fragments then share some banks)
+    g.Wp = OW + ((k.m32 && k.KW == 5) ? KW - 1 : std::max(g_hc_pad, KW - 1));
     if (g_hc_variant > 0 && k.var != g_hc_variant) continue;
     // conv_hc32: 16-B stores / derivative loads, and at least three K
     // stages per item (its bias block lives in the stage buffers: with
@@ -1396,6 +1402,7 @@ hipError_t hc_launch(const HcPlan& p, const void* src, const void* wts,
     HC32(21, 3, 3, 8, 1, 4, 5)
     HC32(22, 3, 3, 8, 1, 3, 5)
     HC32(23, 3, 3, 8, 1, 2, 8)
+    HC32(24, 5, 5, 8, 1, 2, 4)
 
 #undef HC32
 #undef HC_GO_ABL
