@@ -7,7 +7,8 @@ HVK_LIBRARY=<path> (veles_amd/ops/_lib.py), e.g. by
 tools/bench_gemm_ab.py under ``gpu_job.sh benv:HVK_LIBRARY=...``.
 
     python tools/build_abl.py 1 2 4
-    python tools/build_abl.py hc     # conv_hc.hip: build/hcabl/libhvk_hcabl.so"""
+    python tools/build_abl.py hc     # conv_hc.hip: build/hcabl/libhvk_hcabl.so
+    python tools/build_abl.py halo 1 4   # wgrad_halo.hip: build/haloabl/"""
 import os
 import sys
 
@@ -35,8 +36,23 @@ def main(levels):
         B.build(verbose=True)
 
 
+def build_halo(levels):
+    """The halo weight-gradient ablations (wgrad_halo.hip HVK_HALO_ABL: 1 no
+    window DMA, 2 no epilogue stores, 4 no MFMAs): build/haloabl/
+    libhvk_halo<N>.so each."""
+    base_flags = list(B.FLAGS)
+    for n in levels:
+        B.FLAGS = base_flags + ["-DHVK_HALO_ABL=%d" % n]
+        B.BUILD = os.path.join(B.REPO, "build", "haloabl", "obj%d" % n)
+        B.LIB = os.path.join(B.REPO, "build", "haloabl",
+                             "libhvk_halo%d.so" % n)
+        B.build(verbose=True)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["hc"]:
         build_hc()
+    elif sys.argv[1:2] == ["halo"]:
+        build_halo([int(a) for a in sys.argv[2:]] or [1, 2, 4])
     else:
         main([int(a) for a in sys.argv[1:]] or [1, 2, 4])
