@@ -21,9 +21,11 @@
 //
 // Window layout (per plane, 32-B slots of 16 bf16 channels): slot
 // rs * Wp + cs holds input pixel (row of window row rs, column cs - pl).
-// Wp = OW + 8 is congruent to OW mod 8, so 8 consecutive output pixels -
+// With Wp = OW + 8 (congruent to OW mod 8) 8 consecutive output pixels -
 // across an output-row wrap too - map to 8 slots that are distinct mod 8:
 // the ds_read_b64_tr_b16 lane groups (8 pixels x 32 B) hit every bank once.
+// The default is the tight Wp = OW + KW - 1 (g_halo_pad): conflicts only on
+// the lane groups that straddle a row wrap, and fewer window bytes.
 // Window row rs of a step starting at output row oh0 of image n0 is input
 // row oh0 + kh0 - pt + rs of image n0 while rs < OH - oh0 + KHT - 1, and
 // input row rs - (OH - oh0) - (KHT - 1) + kh0 - pt of image n0 + 1 after
@@ -816,6 +818,13 @@ struct Plan {
 };
 
 constexpr int kSlots = 512;   // workgroups resident at two per CU
+// bf16 window row pitch Wp = OW + pad (hvk_halo_pitch_pad; at least
+// KW - 1).  8 keeps Wp = OW (mod 8): conflict-free transposed reads across
+// row wraps.  The tight pitch (2: Wp = OW + KW - 1) moves fewer window
+// bytes - the DMA issue, not the LDS, bounds this loop - and measured
+// +0.1-1.3 % on AlexNet conv2-5, +3.5 % on VGG conv4_2 / conv5_2, results
+// bit-identical (profiles/r6/ab_wgrad_halo_pitch_r6cc.log)
+int g_halo_pad = 2;
 
 // fp8: 1-byte elements, 128-pixel steps, 16-B slots (Wp = OW + 16) and the
 // fp8 candidate list
@@ -830,7 +839,7 @@ Plan make_plan(int N, int H, int W, int C, int OC, int KH, int KW, int pt,
   g.Cg = Cg; g.OCg = OCg; g.KH = KH; g.KW = KW; g.pt = pt; g.pl = pl;
   g.P = N * OH * OW;
   g.KK = KH * KW * Cg;
-  g.Wp = OW + (fp8 ? 16 : 8);
+  g.Wp = OW + (fp8 ? 16 : std::max(g_halo_pad, KW - 1));
   g.fOW = make_fastdiv(OW);
   if (OH * OW < STEP || KW > 9 || C % 16 != 0 || OC % 16 != 0) return p;
   if ((long long)N * H * W * C * ES >= kBufMaxBytes ||
@@ -970,6 +979,9 @@ static long long finish(float* ws, float* wsb, float* dW, float* dbias, int OC,
                      splits, wsb, dbias, OC, nmain);
   return (long long)launch_status(s);
 }
+
+// bf16 window row pitch pad (2 default; see g_halo_pad)
+HVK_API void hvk_halo_pitch_pad(int p) { g_halo_pad = p; }
 
 // the plan's split count (tests / autotune logging)
 HVK_API int hvk_conv_wgrad_halo_splits(int N, int H, int W, int C, int OC,

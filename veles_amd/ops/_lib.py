@@ -117,6 +117,7 @@ _SIGS = {
     "hvk_hc_variant": [I],
     "hvk_hc_pitch_pad": [I],
     "hvk_hc32": [I],
+    "hvk_halo_pitch_pad": [I],
     "hvk_hc32_ts": [I],
     "hvk_hc_last_variant": [],
     "hvk_set_pool_bwd_variant": [I],
