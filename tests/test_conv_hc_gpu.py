@@ -186,6 +186,10 @@ HC32 = [
     ("dgrad", 2, 28, 28, 512, 512, 3, 1, 1),
     ("fwd", 3, 14, 14, 512, 512, 3, 1, 1),       # VGG conv5_2
     ("dgrad", 3, 14, 14, 512, 512, 3, 1, 1),
+    # the 5 x 5 tile (configuration 24: 512 x 64, window pitch OW + 4):
+    # AlexNet conv2 forward, and several items per workgroup
+    ("fwd", 3, 27, 27, 96, 256, 5, 2, 2),
+    ("fwd", 40, 27, 27, 96, 256, 5, 2, 2),
 ]
 
 
