@@ -1254,6 +1254,134 @@ void lrn_pool3s2_fwd_walk_kernel(
   }
 }
 
+// The same walk with the channel halo taken from the neighbour lanes: a wave
+// holds bpw = 64 / CV whole output-column units (its lanes the consecutive
+// 8-channel chunks of one unit; the last 64 % CV lanes idle), so a pixel's
+// channels c0 - 2, c0 - 1 are the lane below's mid.w and c0 + 8, c0 + 9 the
+// lane above's mid.x: one 16-B load per pixel and two DPP moves instead of a
+// 16-B and two 4-B loads (the walk is bound by its load stream, not by its
+// log2 / exp2: profiles/r6/lrn_fwd_no_transcendentals_r6ff.txt).  Every lane
+// runs R rows (the units of a wave may end their strips at different rows:
+// rows past a unit's strip read clamped rows and store nothing), so every
+// DPP move is wave-uniform.  Bit-identical to the walk.
+__device__ __forceinline__ uint32_t dpp_from_below(uint32_t v) {  // lane - 1
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf,
+                                               true);
+}
+__device__ __forceinline__ uint32_t dpp_from_above(uint32_t v) {  // lane + 1
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf,
+                                               true);
+}
+
+template <int half>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void lrn_pool3s2_fwd_dpp_kernel(
+    const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+    uint8_t* __restrict__ argmax, int N, int H, int W, int C, int OH, int OW,
+    int R, int S, float alpha, float beta, float k, int bpw, int nunits,
+    FastDiv fOW, FastDiv fS) {
+  static_assert(half >= 1 && half <= 2, "dword halo");
+  const int CV = C >> 3;
+  const int lane = threadIdx.x & 63;
+  const int lb = lane / CV, cvu = lane - lb * CV;
+  const int c0 = cvu * 8;
+  const bool has_lo = cvu > 0, has_hi = cvu < CV - 1;
+  const uint32_t WC = (uint32_t)W * C, HWC = (uint32_t)H * WC;
+  const uint32_t lastrow = (uint32_t)(H - 1) * WC;
+  const int nwv = (nunits + bpw - 1) / bpw;
+  const int wstride = (gridDim.x * blockDim.x) >> 6;
+  // the loop bound is wave-uniform: every lane reaches every DPP move
+  for (int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wv < nwv;
+       wv += wstride) {
+    const int unit = wv * bpw + lb;
+    const bool ok = lb < bpw && unit < nunits;
+    uint32_t t2, owu, nu, su;
+    fdivmod((uint32_t)(ok ? unit : 0), fOW, t2, owu);
+    fdivmod(t2, fS, nu, su);
+    const int w0 = (int)owu * 2;
+    const int oh0 = (int)su * R, oh1 = min(OH, oh0 + R);
+    const uint16_t* img = x + nu * HWC;
+    const uint32_t col[3] = {(uint32_t)w0 * C, (uint32_t)(w0 + 1) * C,
+                             (uint32_t)(w0 + 2) * C};
+    auto ld = [&](uint32_t ro, int j) -> uint4 {
+      return *(const uint4*)(img + ro + col[j] + c0);
+    };
+    auto halo = [&](const uint4& m) {
+      LrnPx r;
+      r.mid = m;
+      const uint32_t lo = dpp_from_below(m.w), hi = dpp_from_above(m.x);
+      r.lo = has_lo ? lo : 0u;
+      r.hi = has_hi ? hi : 0u;
+      return r;
+    };
+    auto rowmax = [&](float y0, float y1v, float y2v, float& b, int& bi) {
+      b = y0;
+      bi = 0;
+      if (y1v > b) { b = y1v; bi = 1; }
+      if (y2v > b) { b = y2v; bi = 2; }
+    };
+    float cb[8];
+    int ci[8];
+    {   // the strip's first window row
+      const uint32_t ro = 2u * oh0 * WC;
+      const LrnPx p0 = halo(ld(ro, 0)), p1 = halo(ld(ro, 1)),
+                  p2 = halo(ld(ro, 2));
+      f32x2v ya[8], yb[8];
+      lrn_pair<half>(p0, p1, alpha, beta, k, ya);
+      lrn_pair<half>(p2, p2, alpha, beta, k, yb);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) rowmax(ya[q].x, ya[q].y, yb[q].x, cb[q], ci[q]);
+    }
+    uint4 a[3], b[3];
+    auto load_rows = [&](int oh, uint4* ra, uint4* rb) {
+      const uint32_t r1 = (uint32_t)(2 * oh + 1) * WC;
+      const uint32_t hc1 = min(r1, lastrow), hc2 = min(r1 + WC, lastrow);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        ra[j] = ld(hc1, j);
+        rb[j] = ld(hc2, j);
+      }
+    };
+    load_rows(min(oh0, OH - 1), a, b);
+    for (int r = 0; r < R; ++r) {
+      const int oh = oh0 + r;
+      uint4 na[3], nb[3];
+      load_rows(min(oh + 1, OH - 1), na, nb);
+      f32x2v yc[3][8];
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        lrn_pair<half>(halo(a[c]), halo(b[c]), alpha, beta, k, yc[c]);
+      uint16_t o[8];
+      uint8_t ai[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float b1, b2;
+        int i1, i2;
+        rowmax(yc[0][q].x, yc[1][q].x, yc[2][q].x, b1, i1);
+        rowmax(yc[0][q].y, yc[1][q].y, yc[2][q].y, b2, i2);
+        float best = cb[q];
+        int bi = ci[q];
+        if (b1 > best) { best = b1; bi = 3 + i1; }
+        if (b2 > best) { best = b2; bi = 6 + i2; }
+        o[q] = f2bf(best);
+        ai[q] = (uint8_t)bi;
+        cb[q] = b2;
+        ci[q] = i2;
+      }
+      if (ok && oh < oh1) {
+        const long long yo = (((long long)nu * OH + oh) * OW + owu) * C + c0;
+        *(uint4*)(y + yo) = *(const uint4*)o;
+        *(uint2*)(argmax + yo) = *(const uint2*)ai;
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        a[c] = na[c];
+        b[c] = nb[c];
+      }
+    }
+  }
+}
+
 template <int half>
 __global__ __launch_bounds__(256) void lrn_pool3s2_bwd_u8_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dp,
@@ -1743,9 +1871,10 @@ HVK_API int hvk_pool2_bwd(const void* x, const void* dy, void* dx, int N,
 }
 
 // forward kernel selector for A/B runs (hvk_set_lrn_fwd_variant): 0 the
-// vertical walk with the next row prefetched, 1 the per-output preloading
+// vertical walk with the next row prefetched and DPP channel halos (round
+// 6), 5 the same walk loading its halos, 1 the per-output preloading
 // kernel, 2 the walk without the prefetch, 3 / 4 the walk with the prefetch
-// over strips of about 5 / 9 output rows (0: about 14; AlexNet b2048,
+// over strips of about 5 / 9 output rows (0 / 5: about 14; AlexNet b2048,
 // tools/bench_lrn.py: conv2 273 -> 256 us from 9 to 14, conv1 419 / 423,
 // 5 rows 469 / 287: profiles/r4/lrn_fwd_strips_b2048.json)
 static int g_lrn_fwd_variant = 0;
@@ -1766,6 +1895,24 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
     return -1;
   const int h = n / 2;
   const long long total = (long long)N * OH * OW * (C / 8);
+  if (h >= 1 && h <= 2 && g_lrn_fwd_variant == 0 && C / 8 <= 64 &&
+      OH == (H - 3) / 2 + 1 && OW == (W - 3) / 2 + 1) {
+    // the walk with DPP channel halos (whole output-column units per wave):
+    // AlexNet b3072 conv1 611 -> 581 us, conv2 362 -> 337 us, bit-identical
+    // (tools/bench_lrn.py, profiles/r6/bench_lrn_dpp_halo_r6gg.log)
+    const int t = 14;
+    const int S = (OH + t - 1) / t, R = (OH + S - 1) / S;
+    const int CV = C / 8, bpw = 64 / CV;
+    const long long nunits = (long long)N * S * OW;
+    const long long waves = (nunits + bpw - 1) / bpw;
+    auto kd = h == 1 ? lrn_pool3s2_fwd_dpp_kernel<1>
+                     : lrn_pool3s2_fwd_dpp_kernel<2>;
+    hipLaunchKernelGGL(kd, dim3(grid_for(waves * 64)), dim3(256), 0, s,
+                       (const uint16_t*)x, (uint16_t*)y, (uint8_t*)argmax, N,
+                       H, W, C, OH, OW, R, S, alpha, beta, k, bpw,
+                       (int)nunits, make_fastdiv(OW), make_fastdiv(S));
+    return (int)launch_status(s);
+  }
   if (h >= 1 && h <= 2 && g_lrn_fwd_variant != 1 && OH == (H - 3) / 2 + 1 &&
       OW == (W - 3) / 2 + 1) {
     // vertical walk over strips of about 14 output rows (AlexNet: one strip
@@ -1773,7 +1920,7 @@ HVK_API int hvk_lrn_pool_fwd_u8(const void* x, void* y, void* argmax, int N,
     const int t = g_lrn_fwd_variant == 3 ? 5 : g_lrn_fwd_variant == 4 ? 9 : 14;
     const int S = (OH + t - 1) / t, R = (OH + S - 1) / S;
     const long long tw = (long long)N * S * OW * (C / 8);
-    const bool pf = g_lrn_fwd_variant != 2;
+    const bool pf = g_lrn_fwd_variant != 2;   // (5: this walk, prefetched)
     auto kw = h == 1 ? (pf ? lrn_pool3s2_fwd_walk_kernel<1, true>
                            : lrn_pool3s2_fwd_walk_kernel<1, false>)
                      : (pf ? lrn_pool3s2_fwd_walk_kernel<2, true>

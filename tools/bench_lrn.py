@@ -46,10 +46,11 @@ def main():
         setv = getattr(ops._lib.lib(), "hvk_set_lrn_fwd_variant", None)
         tf = None
         if setv is not None:
-            # forward A/B (interleaved, median of 5): 0 walk + prefetch (strips
-            # of ~14 rows; 3: ~5, 4: ~9),
-            # 1 per-output, 2 walk; and they must agree bit for bit
-            vs = (0, 1, 2, 3, 4)
+            # forward A/B (interleaved, median of 5): 0 walk + prefetch with
+            # DPP channel halos (the default since round 6), 5 the same walk
+            # loading its halos (strips of ~14 rows; 3: ~5, 4: ~9), 1
+            # per-output, 2 walk without prefetch; all bit-identical
+            vs = (0, 1, 2, 3, 4, 5)
             outs, ts = {}, {v: [] for v in vs}
             for v in vs:
                 setv(v)
@@ -65,13 +66,15 @@ def main():
                        torch.equal(outs[0][1], outs[v][1]) for v in vs[1:])
             med = {v: sorted(t)[2] for v, t in ts.items()}
             res.setdefault("fwd_ab", {})[name] = {
-                "walk_pf_us": round(med[0], 1), "perout_us": round(med[1], 1),
+                "walk_dpp_halo_us": round(med[0], 1), "perout_us": round(med[1], 1),
                 "walk_us": round(med[2], 1), "walk_pf_r5_us": round(med[3], 1),
-                "walk_pf_r9_us": round(med[4], 1), "bit_identical": same}
-            print(name, "fwd walk+prefetch %.1f us, per-output %.1f us, "
+                "walk_pf_r9_us": round(med[4], 1),
+                "walk_loaded_halo_us": round(med[5], 1), "bit_identical": same}
+            print(name, "fwd DPP-halo walk %.1f us, per-output %.1f us, "
                   "walk %.1f us, strips of 5 %.1f us, of 9 %.1f us, "
-                  "identical %s" % (med[0], med[1], med[2], med[3], med[4],
-                                    same), flush=True)
+                  "loaded-halo walk %.1f us, identical %s" % (
+                      med[0], med[1], med[2], med[3], med[4], med[5], same),
+                  flush=True)
             tf = med[0]
         setb = getattr(ops._lib.lib(), "hvk_set_lrn_bwd_variant", None)
         tb = None
