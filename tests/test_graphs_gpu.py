@@ -361,9 +361,10 @@ def test_solo_rccl_path_captures_backward_and_matches_dp1(tmp_path):
         numpy.testing.assert_allclose(ws[k], wp[k], rtol=1e-4, atol=1e-6)
 
 
-def _runahead_run(on, steps):
+def _runahead_run(on, steps, at="backward"):
     import os
     os.environ["VELES_AMD_LOADER_RUNAHEAD"] = "1" if on else "0"   # opt-in
+    os.environ["VELES_AMD_LOADER_RUNAHEAD_AT"] = at
     from veles_amd.backends import Device
     from veles_amd.dummy import DummyLauncher
     from veles_amd.models import StandardWorkflow
@@ -384,27 +385,32 @@ def _runahead_run(on, steps):
     wf.run_steps(steps)
     torch.cuda.synchronize()
     ld = wf.loader
+    assert ld.runahead_anchor_ is wf.gds[-1]   # the first backward unit
     w = [f.weights_master.float().cpu().clone() for f in wf.forwards
          if getattr(f, "_pw_", None) is not None]
     segs = {s.name: (s.captures, s.replays) for s in wf.graph_segments_}
     return w, ld.runahead_hits, ld.runahead_misses, segs
 
 
-def test_loader_runahead_matches_serial_gather():
+@pytest.mark.parametrize("at", ["backward", "fill"])
+def test_loader_runahead_matches_serial_gather(at):
     """The double-buffered gather (the next minibatch's fill on a side
-    stream, forward / backward graphs keyed by buffer parity) trains like
+    stream, launched as the backward starts or right after this step's
+    fill; forward / backward graphs keyed by buffer parity) trains like
     the serial gather over 3 epochs of 3 minibatches (every epoch end is a
     reshuffle: a prediction miss), with the space-to-depth conv1 input."""
     import os
-    old = os.environ.get("VELES_AMD_LOADER_RUNAHEAD")
+    names = ("VELES_AMD_LOADER_RUNAHEAD", "VELES_AMD_LOADER_RUNAHEAD_AT")
+    old = {n: os.environ.get(n) for n in names}
     try:
         ws, _, _, _ = _runahead_run(False, 9)
-        wr, hits, misses, segs = _runahead_run(True, 9)
+        wr, hits, misses, segs = _runahead_run(True, 9, at)
     finally:
-        if old is None:
-            os.environ.pop("VELES_AMD_LOADER_RUNAHEAD", None)
-        else:
-            os.environ["VELES_AMD_LOADER_RUNAHEAD"] = old
+        for n in names:
+            if old[n] is None:
+                os.environ.pop(n, None)
+            else:
+                os.environ[n] = old[n]
     assert hits >= 5 and misses >= 2, (hits, misses)
     assert segs["forward"][0] == 2, segs   # one graph per buffer set
     for a, b in zip(ws, wr):

@@ -2,7 +2,11 @@
 (hvk_fill_minibatch_s2d: uint8 227x227x3 -> normalised bf16 57x57x48) at
 batch B: HIP-event time and HBM rate (also a rocprofv3 / PMC probe).
 
-    python tools/probe_fill_s2d.py [batch] [reps]"""
+    python tools/probe_fill_s2d.py [batch] [reps] [variant ...]
+
+Variants (hvk_set_gemm_variant): -1 the default (four images per block),
+61 one image per block, 60 the per-chunk kernel; every variant's output is
+checked bit-identical to the first's."""
 import sys
 
 import torch
@@ -28,19 +32,30 @@ def main():
     dst = torch.empty(B, H2, W2, C2, dtype=torch.bfloat16, device="cuda")
     f = lambda: ops.fill_minibatch_s2d(src, shuffled, 0, B, dst, s, K, K,  # noqa
                                        pad, mean2, rdisp2)
-    for _ in range(3):
-        f()
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(True), torch.cuda.Event(True)
-    a.record()
-    for _ in range(reps):
-        f()
-    b.record()
-    b.synchronize()
-    us = a.elapsed_time(b) / reps * 1e3
-    mb = (B * H * W * C + dst.numel() * 2) / 1e6
-    print("fill_s2d b%d: %.1f us, %.0f MB -> %.2f TB/s" % (B, us, mb, mb / us))
-
+    variants = [int(v) for v in sys.argv[3:]] or [-1]
+    lib = ops._lib.lib()
+    ref = None
+    for v in variants:
+        lib.hvk_set_gemm_variant(v)
+        # a long warmup: the first variant timed after 3 calls read ~8 %
+        # slow (clocks still ramping), profiles/r6/fill_s2d_staging_r6ii.log
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = dst.clone()
+        same = torch.equal(dst, ref)
+        a, b = torch.cuda.Event(True), torch.cuda.Event(True)
+        a.record()
+        for _ in range(reps):
+            f()
+        b.record()
+        b.synchronize()
+        us = a.elapsed_time(b) / reps * 1e3
+        mb = (B * H * W * C + dst.numel() * 2) / 1e6
+        print("fill_s2d b%d variant %d: %.1f us, %.0f MB -> %.2f TB/s, "
+              "bit-identical %s" % (B, v, us, mb, mb / us, same))
+    lib.hvk_set_gemm_variant(-1)
 
 if __name__ == "__main__":
     main()

@@ -60,6 +60,11 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         self._ra_pending_ = None
         self._ra_stream_ = None
         self._ra_gen_ = 0
+        # (generation, (start, count), parity) of the next gather while it
+        # waits for the anchor unit (``runahead_anchor_``, set by
+        # StandardWorkflow: the first backward unit) to launch it
+        self._ra_deferred_ = None
+        self.runahead_anchor_ = None
         self.buffer_parity_ = 0
         self.runahead_hits = 0
         self.runahead_misses = 0
@@ -95,6 +100,7 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         from veles_amd import ops
         self._ra_bufs_ = None       # run-ahead sets follow the new buffers
         self._ra_pending_ = None
+        self._ra_deferred_ = None
         self.buffer_parity_ = 0
         n = self.local_minibatch_size
         dev = self.device
@@ -305,7 +311,11 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         graphs are keyed by ``buffer_parity_`` (graphs.py), one per buffer
         set.  Off by default: on AlexNet b1024 the side-stream gather ran
         beside conv1 (0.50 -> 0.65 ms) and the step was 0.8 % slower
-        (144.3k vs 145.4k img/s, profiles/r4/runahead_ab.md)."""
+        (144.3k vs 145.4k img/s, profiles/r4/runahead_ab.md); launched at
+        the backward instead (_defer_runahead) it measured +0.4 % on one
+        box and +0.0 % on another at b3072: the gather, dispatched first,
+        holds the CUs until it drains and the GEMM beside it waits
+        (profiles/r6/loader_runahead_placement_r6jj.txt)."""
         dev = self.device
         if dev is None or not getattr(dev, "is_gpu", False) or \
                 getattr(self, "original_targets", None) is not None:
@@ -343,6 +353,7 @@ class FullBatchLoader(Loader, IFullBatchLoader):
 
     def _fill_runahead(self, start_offset, count):
         import torch
+        self._launch_deferred()   # a gather whose anchor did not run
         cur = torch.cuda.current_stream(self.minibatch_data.devmem.device)
         key = (self._ra_gen_, start_offset, count)
         pend, self._ra_pending_ = self._ra_pending_, None
@@ -366,19 +377,53 @@ class FullBatchLoader(Loader, IFullBatchLoader):
         self.buffer_parity_ = parity
         nxt = self._peek_next()
         if nxt is not None and nxt[1] > 0:
-            # the other set's readers (the previous step) are all enqueued
-            # on the compute stream before this point
-            free = torch.cuda.Event()
-            free.record(cur)
-            side = self._ra_stream_
-            side.wait_event(free)
-            od, ol, oi = self._ra_views(parity ^ 1)
-            with torch.cuda.stream(side):
-                self._gather(nxt[0], nxt[1], od, ol, oi)
-                done = torch.cuda.Event()
-                done.record(side)
-            self._ra_pending_ = ((self._ra_gen_,) + nxt, parity ^ 1, done)
+            self._ra_deferred_ = (self._ra_gen_, nxt, parity ^ 1)
+            if not self._defer_runahead():
+                self._launch_deferred()
         return True
+
+    def _defer_runahead(self):
+        """Launch the next gather when the backward starts (the anchor unit)
+        rather than now.  Now, it runs beside conv1's forward, which streams
+        HBM as well and is a persistent kernel (its workgroups wait for the
+        gather's); at the backward it runs beside the fully-connected
+        GEMMs, which leave LDS and HBM bandwidth to spare.
+        ``VELES_AMD_LOADER_RUNAHEAD_AT=fill`` keeps the round-4 placement."""
+        import os
+        if self.__dict__.get("runahead_anchor_") is None:
+            return False
+        return os.environ.get("VELES_AMD_LOADER_RUNAHEAD_AT",
+                              "backward") != "fill"
+
+    def launch_runahead(self):
+        """The anchor unit's ``before_run_`` hook: enqueue the deferred
+        gather (not inside an open capture: the next fill launches it)."""
+        if self._ra_deferred_ is None:
+            return
+        import torch
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self._launch_deferred()
+
+    def _launch_deferred(self):
+        d, self._ra_deferred_ = self._ra_deferred_, None
+        if d is None or d[0] != self._ra_gen_:
+            return   # none, or the order changed since (a miss either way)
+        import torch
+        _, nxt, parity = d
+        cur = torch.cuda.current_stream(self.minibatch_data.devmem.device)
+        # the other set's readers (the previous step) are all enqueued on
+        # the compute stream before this point
+        od, ol, oi = self._ra_views(parity)
+        free = torch.cuda.Event()
+        free.record(cur)
+        side = self._ra_stream_
+        side.wait_event(free)
+        with torch.cuda.stream(side):
+            self._gather(nxt[0], nxt[1], od, ol, oi)
+            done = torch.cuda.Event()
+            done.record(side)
+        self._ra_pending_ = ((self._ra_gen_,) + nxt, parity, done)
 
     def fill_minibatch(self):
         """Host path used by analysis helpers: fill by minibatch_indices."""

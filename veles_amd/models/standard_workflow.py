@@ -467,6 +467,13 @@ class StandardWorkflow(LinkBuilders, AcceleratedWorkflow):
         # forward / backward HIP-graph segments (GPU only; veles_amd/graphs)
         from veles_amd.graphs import install_step_graphs
         install_step_graphs(self, warmup=self.graph_warmup)
+        # a run-ahead loader gathers the next minibatch as the backward
+        # starts (FullBatchLoader._defer_runahead)
+        gds = [g for g in reversed(getattr(self, "gds", []) or [])
+               if g is not None]
+        if gds and hasattr(ld, "launch_runahead"):
+            ld.runahead_anchor_ = gds[0]
+            gds[0].before_run_ = [ld.launch_runahead]
         return res
 
     def run_steps(self, n):

@@ -667,6 +667,12 @@ class Unit(Distributable, IUnit, IDistributable, metaclass=UnitRegistry):
         if events.enabled:
             events.record(self.name, "begin")
         rng = _roctx()
+        # work other units enqueue at this point of the step (the loader's
+        # run-ahead gather at the first backward unit, loader/fullbatch.py)
+        hooks = self.__dict__.get("before_run_")
+        if hooks:
+            for h in hooks:
+                h()
         # a unit inside a captured HIP-graph segment (veles_amd/graphs.py)
         # is dispatched by the segment: eager, captured or replayed
         seg = self.__dict__.get("graph_segment_")
