@@ -1439,6 +1439,82 @@ HVK_API int hvk_sgd(float* w, const float* grad, float* mom, void* w_lp,
   return (int)launch_status(s);
 }
 
+// out[C][R] = in[R][C]^T (bf16) and ws[R/(64 RT)][C] = the column sums of
+// each 64 RT-row slab of in (f32, in row order): the FC weight gradient's
+// dY^T for the NN GEMM (K-major A, the 256 x 128 ping-pong loop) plus its
+// bias gradient, in one pass over dY.  A block moves RT 64 x 64 tiles down
+// the rows through LDS, each column's sum kept in the four adjacent lanes
+// that hold its 16-row runs; R % (64 RT) == C % 64 == 0.
+template <int RT>
+__global__ void __launch_bounds__(256)
+transpose_colsum_bf16_kernel(const uint16_t* __restrict__ in, int R, int C,
+                             uint16_t* __restrict__ out,
+                             float* __restrict__ ws) {
+  __shared__ uint16_t tile[64][64 + 8];
+  const int c0 = blockIdx.x * 64, t = threadIdx.x;
+  const int col = t >> 2, rr = (t & 3) * 16;
+  float sum = 0.f;
+  for (int rt = 0; rt < RT; ++rt) {
+    const int r0 = (blockIdx.y * RT + rt) * 64;
+    const uint4* src =
+        (const uint4*)(in + (long long)(r0 + (t >> 2)) * C + c0 + rr);
+    const uint4 a = src[0], b = src[1];
+    if (rt) __syncthreads();   // the last tile's reads
+    *(uint4*)&tile[t >> 2][rr] = a;
+    *(uint4*)&tile[t >> 2][rr + 8] = b;
+    __syncthreads();
+    // thread: rows rr .. rr+15 of column col, a 32-B run of the output row
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint16_t lo = tile[rr + 2 * j][col], hi = tile[rr + 2 * j + 1][col];
+      sum += bf2f(lo);
+      sum += bf2f(hi);
+      w[j] = (uint32_t)lo | ((uint32_t)hi << 16);
+    }
+    uint4* dst = (uint4*)(out + (long long)(c0 + col) * R + r0 + rr);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+  // over the four lanes of the column (a fixed order: deterministic)
+  sum += __shfl_xor(sum, 1);
+  sum += __shfl_xor(sum, 2);
+  if ((t & 3) == 0) ws[(long long)blockIdx.y * C + c0 + col] = sum;
+}
+
+// colsum[c] (+)= sum over the slabs of ws[slab][c], in slab order
+__global__ void colsum_finish_kernel(const float* __restrict__ ws, int slabs,
+                                     int C, float* __restrict__ colsum,
+                                     int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sum = 0.f;
+  for (int p = 0; p < slabs; ++p) sum += ws[(long long)p * C + c];
+  colsum[c] = accumulate ? colsum[c] + sum : sum;
+}
+
+// out = in^T and colsum (+)= the column sums of in; ws holds R / 64 * C
+// floats.  -1 when a shape or alignment is off (the caller falls back).
+HVK_API int hvk_transpose_colsum(const void* in, int R, int C, void* out,
+                                 float* colsum, int accumulate, float* ws,
+                                 hipStream_t s) {
+  if (R % 64 || C % 64 || R <= 0 || C <= 0 || ((uintptr_t)in & 15) ||
+      ((uintptr_t)out & 15) || R / 64 > 65535)
+    return -1;
+  // four tiles per block where the rows allow: a quarter of the slabs for
+  // the finishing pass to add
+  const int rt = R % 256 == 0 ? 4 : 1;
+  hipLaunchKernelGGL(rt == 4 ? transpose_colsum_bf16_kernel<4>
+                             : transpose_colsum_bf16_kernel<1>,
+                     dim3(C / 64, R / (64 * rt)), dim3(256), 0, s,
+                     (const uint16_t*)in, R, C, (uint16_t*)out, ws);
+  if (colsum)
+    hipLaunchKernelGGL(colsum_finish_kernel, dim3((C + 255) / 256), dim3(256),
+                       0, s, (const float*)ws, R / (64 * rt), C, colsum,
+                       accumulate);
+  return (int)launch_status(s);
+}
+
 HVK_API int hvk_col_sum(const void* in, int dt, int R, int C, float* out,
                         float scale, hipStream_t s) {
   if (dt == DT_BF16 && C % 8 == 0 && C >= 512 &&

@@ -34,6 +34,22 @@ def _bias_colsum():
         root.common.engine.fc_bias_colsum, False) else "0") != "0"
 
 
+def _wgrad_nn(e2, x):
+    """FC weight gradient as transpose + NN GEMM (GPU bf16, batch and
+    outputs multiples of 64; root.common.engine.fc_wgrad_nn /
+    VELES_AMD_FC_WGRAD_NN, on by default: AlexNet b3072 fc6 / fc7,
+    profiles/r6/fc_wgrad_nn_r6kk.log)."""
+    if not e2.is_cuda or e2.dtype != torch.bfloat16 or \
+            x.dtype != torch.bfloat16 or e2.shape[0] % 64 or \
+            e2.shape[1] % 64 or not e2.is_contiguous() or \
+            not x.is_contiguous():
+        return False
+    import os
+    from veles_amd.utils.config import root, get
+    return os.environ.get("VELES_AMD_FC_WGRAD_NN", "1" if get(
+        root.common.engine.fc_wgrad_nn, True) else "0") != "0"
+
+
 class GradientDescent(GradientDescentBase):
     MAPPING = "all2all"
     OVERWRITES_GRADS = True  # see ParameterStore.overwrite
@@ -63,7 +79,21 @@ class GradientDescent(GradientDescentBase):
         mode = "overwrite" if ow else True
 
         def wgrad():
-            if not fwd.weights_transposed and bg is not None and \
+            if not fwd.weights_transposed and _wgrad_nn(e2, x):
+                # dY^T (and the bias gradient) in one pass, then the NN
+                # GEMM: K-major A takes the 256 x 128 ping-pong loop, which
+                # the MN-major dY of the TN form (and its ones column) miss
+                R, C = e2.shape
+                if self.e2t_ is None or self.e2t_.shape != (C, R):
+                    self.e2t_ = torch.empty(C, R, dtype=e2.dtype,
+                                            device=e2.device)
+                    self.e2t_ws_ = torch.empty(R // 64 * C,
+                                               dtype=torch.float32,
+                                               device=e2.device)
+                ops.transpose_colsum(e2, out=self.e2t_, colsum=bg,
+                                     accumulate=not ow, ws=self.e2t_ws_)
+                ops.gemm(self.e2t_, x, out=pw.grad, accumulate=mode)
+            elif not fwd.weights_transposed and bg is not None and \
                     _bias_colsum() and e2.is_cuda:
                 # grad_b by the column-sum kernel: the ones column costs the
                 # weight-gradient GEMM one more column tile and its
@@ -99,6 +129,7 @@ class GradientDescent(GradientDescentBase):
     def init_unpickled(self):
         super().init_unpickled()
         self.e8_ = self.wt8_ = self.fp8_se_ = None
+        self.e2t_ = self.e2t_ws_ = None
 
     def __getstate__(self):
         fp8.save_scalers(self, ("fp8_se_",))

@@ -1299,6 +1299,37 @@ def col_sum(x2d, out=None, scale=1.0, accumulate=False):
     return out
 
 
+def transpose_colsum(x2d, out=None, colsum=None, accumulate=False, ws=None):
+    """out[C][R] = x[R][C]^T (bf16) and colsum[c] (+)= sum_r x[r][c] (float32,
+    summed per 64-row slab, then the slabs in order: deterministic).  One
+    pass over x: the FC weight gradient's dY^T plus its bias gradient.
+    GPU: R and C multiples of 64; ws, float32 of (R / 64) * C, is the slab
+    workspace (allocated when None)."""
+    R, C = x2d.shape
+    if out is None:
+        out = torch.empty(C, R, dtype=x2d.dtype, device=x2d.device)
+    if _gpu(x2d):
+        if x2d.dtype != torch.bfloat16 or R % 64 or C % 64 or \
+                not x2d.is_contiguous() or not out.is_contiguous():
+            raise ValueError("transpose_colsum: contiguous bf16 with R, C "
+                             "multiples of 64")
+        if ws is None:
+            ws = torch.empty(R // 64 * C, dtype=torch.float32,
+                             device=x2d.device)
+        _lib_call("hvk_transpose_colsum", _p(x2d), R, C, _p(out),
+                  _p(colsum) if colsum is not None else None,
+                  int(bool(accumulate)), _p(ws), _s(x2d))
+        return out
+    out.copy_(x2d.t())
+    if colsum is not None:
+        sums = x2d.float().sum(0)
+        if accumulate:
+            colsum += sums
+        else:
+            colsum.copy_(sums)
+    return out
+
+
 def row_sum(x2d, out=None, scale=1.0):
     R, C = x2d.shape
     if out is None:

@@ -119,6 +119,8 @@ _SIGS = {
     "hvk_hc32": [I],
     "hvk_halo_pitch_pad": [I],
     "hvk_hc32_ts": [I],
+    # out = in^T and the column sums of in (csrc/kernels/elementwise.hip)
+    "hvk_transpose_colsum": [P, I, I, P, P, I, P, P],
     "hvk_hc_last_variant": [],
     "hvk_set_pool_bwd_variant": [I],
     "hvk_hc_ablation": [I],
