@@ -160,6 +160,11 @@ __global__ void mean_disp_kernel(const void* in, int in_dt, const float* mean,
 //   err[i][c] = (p[c] - (c == label)) * scale       (dL/dlogits of mean CE)
 //   probs (optional f32 output), per-row loss, argmax; block reductions of
 //   n_err and loss into metrics[0..1] (atomics, f32).
+// NV > 0: the row's C <= 64 NV logits are read once into registers (NV per
+// lane, the same lane-strided order, so the same sums: bit-identical to the
+// NV = 0 form, which reads the row three times; AlexNet's 1000 classes at
+// b3072: 42 -> 20 us, profiles/r6/softmax_ce_regs_r6ll.log)
+template <int NV>
 __global__ void softmax_ce_kernel(const void* logits, int in_dt, int B, int C,
                                   const int* labels, float scale, void* err,
                                   int err_dt, float* probs, int* max_idx,
@@ -175,9 +180,22 @@ __global__ void softmax_ce_kernel(const void* logits, int in_dt, int B, int C,
     long long base = (long long)row * C;
     float mx = -INFINITY;
     int amax = 0;
-    for (int c = lane; c < C; c += 64) {
-      float v = ld_any(logits, base + c, in_dt);
-      if (v > mx) { mx = v; amax = c; }
+    constexpr int NR = NV > 0 ? NV : 1;
+    float rv[NR];
+    if constexpr (NV > 0) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = lane + 64 * k;
+        rv[k] = c < C ? ld_any(logits, base + c, in_dt) : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        if (lane + 64 * k < C && rv[k] > mx) { mx = rv[k]; amax = lane + 64 * k; }
+    } else {
+      for (int c = lane; c < C; c += 64) {
+        float v = ld_any(logits, base + c, in_dt);
+        if (v > mx) { mx = v; amax = c; }
+      }
     }
     // wave argmax (first index on ties)
 #pragma unroll
@@ -187,18 +205,32 @@ __global__ void softmax_ce_kernel(const void* logits, int in_dt, int B, int C,
       if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
     }
     float sum = 0.f;
-    for (int c = lane; c < C; c += 64)
-      sum += __expf(ld_any(logits, base + c, in_dt) - mx);
+    if constexpr (NV > 0) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        if (lane + 64 * k < C) sum += __expf(rv[k] - mx);
+    } else {
+      for (int c = lane; c < C; c += 64)
+        sum += __expf(ld_any(logits, base + c, in_dt) - mx);
+    }
     sum = wave_sum(sum);
     float inv = 1.f / sum;
     int lab = labels ? labels[row] : -1;
-    for (int c = lane; c < C; c += 64) {
-      float p = __expf(ld_any(logits, base + c, in_dt) - mx) * inv;
+    auto emit = [&](int c, float v) {
+      float p = __expf(v - mx) * inv;
       if (probs) probs[base + c] = p;
       if (err) {
         float g = lab < 0 ? 0.f : (p - (c == lab ? 1.f : 0.f)) * scale;
         st_any(err, base + c, err_dt, g);
       }
+    };
+    if constexpr (NV > 0) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        if (lane + 64 * k < C) emit(lane + 64 * k, rv[k]);
+    } else {
+      for (int c = lane; c < C; c += 64)
+        emit(c, ld_any(logits, base + c, in_dt));
     }
     if (lane == 0) {
       if (max_idx) max_idx[row] = amax;
@@ -1370,9 +1402,19 @@ HVK_API int hvk_softmax_ce(const void* logits, int in_dt, int B, int C,
                            float* probs, int* max_idx, float* metrics,
                            int* confusion, hipStream_t s) {
   int blocks = (B + 3) / 4;
+  if (blocks < 1) blocks = 1;
+  if (C <= 64 * 16 && hvk_gemm_variant != 65) {
+    // the row in registers; one row per wave up to 4096 rows (one metric
+    // atomic per block and metric)
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(softmax_ce_kernel<16>, dim3(blocks), dim3(256), 0, s,
+                       logits, in_dt, B, C, labels, scale, err, err_dt, probs,
+                       max_idx, metrics, confusion);
+    return (int)launch_status(s);
+  }
   if (blocks > 256) blocks = 256;  // >= 4 rows per wave beyond 4096 rows
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(softmax_ce_kernel, dim3(blocks), dim3(256), 0, s,
+  hipLaunchKernelGGL(softmax_ce_kernel<0>, dim3(blocks), dim3(256), 0, s,
                      logits, in_dt, B, C, labels, scale, err, err_dt, probs,
                      max_idx, metrics, confusion);
   return (int)launch_status(s);
