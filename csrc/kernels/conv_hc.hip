@@ -1077,10 +1077,13 @@ conv_hc32_kernel(const uint16_t* __restrict__ src,
 // tap) 32-B gather it replaces touched one 128-B line per 32 B in L2.
 // src: [OCT][T][CG] (the forward filter bank, or backward-data's permutation
 // wt[g][c][kh][kw][oc], which has the same shape for the transposed conv).
+// fwd_w (backward-data only): src is the forward filter bank [G][CG][T][OCg]
+// itself, not its [G][OCg][T][CG] permutation; the pack gathers each piece's
+// 8 reduction channels at their stride (the permute pass is not needed)
 __global__ void hc32_pack_kernel(const uint16_t* __restrict__ src,
                                  uint16_t* __restrict__ dst, int T, int CG,
                                  int OCg, int BN, int flip,
-                                 long long pieces) {
+                                 long long pieces, int fwd_w) {
   const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= pieces) return;
   const int hs = (int)(q & 1);
@@ -1100,8 +1103,20 @@ __global__ void hc32_pack_kernel(const uint16_t* __restrict__ src,
                 4 * (rr >> 3) + (rr & 3);
   const int half = hs ^ ((n >> 3) & 1);
   const int tap = flip ? T - 1 - tp : tp;
-  const uint4 v = *(const uint4*)(src + ((long long)o * T + tap) * CG +
-                                  c * 16 + half * 8);
+  uint4 v;
+  if (fwd_w) {
+    const uint16_t* wp = src + ((long long)(gi * CG + c * 16 + half * 8) * T +
+                                tap) * OCg + (o - gi * OCg);
+    const long long st = (long long)T * OCg;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)wp[2 * j * st] | ((uint32_t)wp[(2 * j + 1) * st] << 16);
+    v = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    v = *(const uint4*)(src + ((long long)o * T + tap) * CG + c * 16 +
+                        half * 8);
+  }
   *(uint4*)(dst + q * 8) = v;
 }
 
@@ -1112,6 +1127,7 @@ struct HcPlan {
   HcGeom g;
   int KH, KW;
   void* wpack;  // conv_hc32: the stage-major filter bank workspace
+  int fwd_w;    // backward-data weights in the forward layout (hc32_pack)
 };
 
 constexpr int kCUs = 256;
@@ -1292,7 +1308,7 @@ hipError_t go_hc32_ts(const HcPlan& p, const void* src, const void* wts,
     hipLaunchKernelGGL(hc32_pack_kernel, dim3((unsigned)((pieces + 255) / 256)),
                        dim3(256), 0, s, (const uint16_t*)wts,
                        (uint16_t*)p.wpack, KH * KW, p.g.CG, p.g.OCg,
-                       WN * NJ * 32, p.g.flip, pieces);
+                       WN * NJ * 32, p.g.flip, pieces, p.fwd_w);
     wts = p.wpack;
   }
   auto kern = conv_hc32_kernel<KH, KW, WM, WN, NJ, NBW, ABL, MI, TS>;
@@ -1493,6 +1509,30 @@ HVK_API int hvk_conv_dgrad_hc(const void* dY, const void* Wt, void* dX, int N,
                                ((uintptr_t)aux & 15) == 0);
   if (!p.var || (hc32_wpack_bytes(p) && !wpack)) return -2;
   p.wpack = wpack;
+  p.fwd_w = 0;
   g_hc_last = p.var;
   return (int)hc_launch(p, dY, Wt, nullptr, dX, aux, 0, aux_act, s);
+}
+
+// hvk_conv_dgrad_hc with the weights in the FORWARD layout W [OC][KH][KW][Cg]:
+// the conv_hc32 plans pack them straight into their filter bank; -3 when the
+// plan is not a conv_hc32 one (the caller permutes and uses hvk_conv_dgrad_hc)
+HVK_API int hvk_conv_dgrad_hc_w(const void* dY, const void* W_, void* dX,
+                                int N, int H, int W, int C, int OC, int KH,
+                                int KW, int pt, int pl, int OH, int OW,
+                                int groups, const void* aux, int aux_act,
+                                void* wpack, hipStream_t s) {
+  if (((uintptr_t)dY & 15) || ((uintptr_t)dX & 7) || ((uintptr_t)aux & 7) ||
+      ((uintptr_t)wpack & 15))
+    return -2;
+  HcPlan p = hc_plan_dgrad(N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups,
+                           ((uintptr_t)dX & 15) == 0 &&
+                               ((uintptr_t)aux & 15) == 0);
+  if (!p.var) return -2;
+  if (!hc32_wpack_bytes(p)) return -3;
+  if (!wpack) return -2;
+  p.wpack = wpack;
+  p.fwd_w = 1;
+  g_hc_last = p.var;
+  return (int)hc_launch(p, dY, W_, nullptr, dX, aux, 0, aux_act, s);
 }

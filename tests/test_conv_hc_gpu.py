@@ -233,3 +233,39 @@ def test_conv_hc32_matches_reference_and_hc16(case):
     # no bias / no activation path of the forward, and a non-zero bias read
     # from the per-item bias block (tiles of several items per workgroup)
     assert torch.isfinite(out[True].float()).all()
+
+
+@pytest.mark.parametrize("shape", [
+    (3, 13, 13, 256, 384, 3, 1, 1),        # conv3
+    (64, 13, 13, 384, 384, 3, 1, 2),       # conv4
+    (3, 13, 13, 384, 256, 3, 1, 2),        # conv5
+    (2, 27, 27, 96, 256, 5, 2, 2),         # conv2: 16x16 kernel, -3
+])
+def test_conv_hc32_dgrad_packs_forward_layout_weights(shape):
+    """hvk_conv_dgrad_hc_w (the filter bank packed straight from the forward
+    weights [OC][KH][KW][Cg]) is bit-identical to hvk_conv_dgrad_hc on the
+    permuted [g][c][kh][kw][oc] copy, and declines (-3) the plans that are
+    not conv_hc32."""
+    from veles_amd.ops import _lib
+    lib = _lib.lib()
+    N, H, W, C, OC, K, pad, g = shape
+    dy = _r(N, H, W, OC, scale=1.0, seed=6)
+    w = _r(OC, K, K, C // g, scale=0.2, seed=7)
+    aux = _r(N, H, W, C, scale=2.0, seed=8)
+    OCg, Cg = OC // g, C // g
+    wt = w.view(g, OCg, K, K, Cg).permute(0, 4, 2, 3, 1).contiguous()
+    wp = ops._hc_wpack(1, N, H, W, C, OC, K, K, pad, pad, H, W, g, aux, aux,
+                       dy.device)
+    outs = []
+    for fn, ww in ((lib.hvk_conv_dgrad_hc, wt), (lib.hvk_conv_dgrad_hc_w, w)):
+        out = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+        rc = fn(ops._p(dy), ops._p(ww), ops._p(out), N, H, W, C, OC, K, K,
+                pad, pad, H, W, g, ops._p(aux), ops.act_code("str"),
+                ops._p(wp), ops._s(dy))
+        outs.append((rc, out))
+    torch.cuda.synchronize()
+    if wp is None:
+        assert outs[1][0] == -3 or outs[1][0] == -2
+        return
+    assert outs[0][0] == 0 and outs[1][0] == 0
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -996,6 +996,32 @@ def _conv_fwd(x, w, bias, sliding, padding, groups, act, out, col_out, fq):
     return out
 
 
+def _dgrad_hc_fwd_w(dy, w, out, aux, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
+                    OH, OW, groups, aux_act):
+    """Backward-data on conv_hc32 from the forward-layout weights: its
+    filter-bank pack reads them directly, so the [g][c][kh][kw][oc]
+    permutation pass is skipped.  False when that path does not apply (the
+    caller permutes and dispatches as before)."""
+    if not (_CONV_HC and sx == 1 and sy == 1 and out.is_contiguous() and
+            dy.dtype == torch.bfloat16 and w.is_contiguous() and
+            (aux is None or aux.is_contiguous())):
+        return False
+    chunks = list(_image_chunks(N, dy))
+    if len(chunks) != 1:
+        return False
+    wp = _hc_wpack(1, N, H, W, C, OC, KH, KW, pt, pl, OH, OW, groups, out,
+                   aux, dy.device)
+    if wp is None:
+        return False
+    rc = _lib.lib().hvk_conv_dgrad_hc_w(
+        _p(dy), _p(w), _p(out), N, H, W, C, OC, KH, KW, pt, pl, OH, OW,
+        groups, _p(aux), aux_act, _p(wp), _s(dy))
+    if rc in (-2, -3):
+        return False
+    _lib.check(rc, "hvk_conv_dgrad_hc_w")
+    return True
+
+
 def _dgrad_call(dy, wt, out, aux, N, H, W, C, OC, KH, KW, sy, sx, pt, pl,
                 OH, OW, groups, aux_act):
     if _CONV_HC and sx == 1 and sy == 1 and out.is_contiguous() and \
@@ -1062,6 +1088,9 @@ def conv_dgrad(dy, w, x_shape, sliding=(1, 1), padding=(0, 0, 0, 0),
             dyp[..., :OC].copy_(dy)
             dy, OC = dyp, OCp
         else:
+            if _dgrad_hc_fwd_w(dy, w, out, aux, N, H, W, C, OC, KH, KW, sy,
+                               sx, pt, pl, OH, OW, groups, aux_act):
+                return out
             wt = _workspace(("dgrad_wt", id(w)), (groups, Cg, KH, KW, OCg),
                             w.dtype, w.device)
             wt.copy_(w.view(groups, OCg, KH, KW, Cg).permute(0, 4, 2, 3, 1))

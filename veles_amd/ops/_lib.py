@@ -113,6 +113,7 @@ _SIGS = {
     # channel-chunked halo convs (csrc/kernels/conv_hc.hip)
     "hvk_conv_fwd_hc": [P, P, P, P] + [I] * 13 + [P, P],
     "hvk_conv_dgrad_hc": [P, P, P] + [I] * 12 + [P, I, P, P],
+    "hvk_conv_dgrad_hc_w": [P, P, P] + [I] * 12 + [P, I, P, P],
     "hvk_conv_hc_wpack_bytes": [I] * 14,
     "hvk_hc_variant": [I],
     "hvk_hc_pitch_pad": [I],
