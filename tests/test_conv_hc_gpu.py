@@ -48,6 +48,9 @@ FWD = [
     (3, 13, 13, 384, 256, 3, 1, 1, 2),     # conv5
     (384, 13, 13, 384, 384, 3, 1, 1, 2),   # conv4, many items per workgroup
     (1, 56, 56, 64, 64, 3, 1, 1, 1),       # VGG-16 64-channel layer
+    (1, 224, 224, 64, 64, 3, 1, 1, 1),     # VGG-16 conv1_2: 224-wide window
+    (2, 28, 28, 256, 512, 3, 1, 1, 1),     # VGG-16 conv4_1
+    (2, 14, 14, 512, 512, 3, 1, 1, 1),     # VGG-16 conv5_x
 ]
 
 
@@ -72,6 +75,10 @@ DGRAD = [
     (3, 13, 13, 384, 384, 3, 1, 2),        # conv4
     (3, 13, 13, 384, 256, 3, 1, 2),        # conv5
     (200, 27, 27, 96, 256, 5, 2, 2),       # conv2, many items per workgroup
+    (2, 56, 56, 128, 256, 3, 1, 1),        # VGG-16 conv3_1 backward-data
+    (2, 28, 28, 256, 512, 3, 1, 1),        # VGG-16 conv4_1
+    (2, 14, 14, 512, 512, 3, 1, 1),        # VGG-16 conv5_x
+    (1, 224, 224, 64, 64, 3, 1, 1),        # VGG-16 conv1_2: 224-wide window
 ]
 
 
